@@ -1,0 +1,128 @@
+"""ctypes binding of ``libadipose_hip.so`` (the C ABI declared in ``include/adipose_hip.h``).
+
+The shared library is built in-tree (``adipose_tissue-unet_amd/libadipose_hip.so``) and is the ONLY
+compute path of this package: there is no CPU or PyTorch fallback. ``lib()`` raises if the library
+is missing, and every wrapped call raises ``AdpError`` with ``adp_last_error()`` when the C side
+reports a failure.
+
+``torch`` is imported first on purpose: torch ships its own ``libamdhip64.so.7`` and the dynamic
+linker then resolves this library's ``libamdhip64.so.7`` dependency to that same runtime, so
+device pointers and ``hipStream_t`` handles from torch are valid here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libadipose_hip.so")
+
+F32 = 0
+BF16 = 1
+
+
+class AdpError(RuntimeError):
+    pass
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int) for n in (
+        "N", "Hs", "Ws", "CA_stride", "CB_stride", "upsample", "Ho", "Wo", "stride",
+        "kh", "kw", "dil", "pad", "Nout", "relu")] + [
+        ("dropout_rate", C.c_float), ("dropout_seed", C.c_uint),
+        ("out_stride", C.c_int), ("out_mode", C.c_int), ("shuffle_c", C.c_int),
+        ("out2_stride", C.c_int), ("split_c", C.c_int),
+        ("mask_stride", C.c_int), ("mask_scale", C.c_float),
+        ("mask2_stride", C.c_int), ("mask2_scale", C.c_float),
+        ("accum_stride", C.c_int)]
+
+
+class ConvIO(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "srcA", "srcB", "bn_scaleA", "bn_shiftA", "bn_scaleB", "bn_shiftB", "W", "bias",
+        "out", "out2", "addend", "mask", "mask2", "accum", "bn_sum", "bn_sqsum")]
+
+
+_P = C.c_void_p
+_I = C.c_int
+_F = C.c_float
+_S = C.c_size_t
+
+# name -> argtypes (restype is always c_int)
+_SIGS = {
+    "adp_abi_version": [],
+    "adp_conv_fwd": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P],
+    "adp_conv_wgrad": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P, _I, _P, _P, _P],
+    "adp_pack_weights": [_I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _P],
+    "adp_maxpool2_fwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "adp_maxpool2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _P, _P],
+    "adp_upsample2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P],
+    "adp_ew_add_mask": [_I, _S, _P, _P, _P, _F, _P, _P],
+    "adp_cast": [_I, _I, _S, _P, _P, _P],
+    "adp_fill_f32": [_S, _F, _P, _P],
+    "adp_bn_finalize": [_I, _F, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P],
+    "adp_bn_bwd_reduce": [_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "adp_bn_bwd_apply": [_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P],
+    "adp_head_softmax2_fwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "adp_head_softmax2_bwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P],
+    "adp_head_sigmoid_fwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "adp_head_sigmoid_bwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P],
+    "adp_resize_bilinear_fwd": [_I, _I, _I, _I, _I, _P, _P, _P],
+    "adp_resize_bilinear_bwd": [_I, _I, _I, _I, _I, _P, _P, _P],
+    "adp_loss_rows": [_I, _I, _I, _P, _P, _I, _F, _F, _P, _P, _P],
+    "adp_loss_select": [_I, _I, _I, _P, _I, _F, _F, _F, _P, _P, _P],
+    "adp_loss_grad": [_I, _I, _I, _P, _P, _I, _F, _F, _P, _P, _F, _I, _P, _P],
+    "adp_pixel_counts": [_S, _P, _P, _F, _P, _P],
+    "adp_adam": [_S, _P, _P, _P, _P, _F, _F, _F, _F, _I, _F, _F, _P],
+    "adp_ema": [_S, _P, _P, _F, _P],
+    "adp_prep_input": [_I, _I, _I, _I, _I, _P, _F, _F, _I, _I, _P, _P],
+    "adp_tta_merge": [_I, _I, _I, C.POINTER(C.c_int), _P, _P, _P],
+    "adp_blend_accum": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "adp_blend_finalize": [_S, _P, _P, _F, _P, _P],
+}
+
+_lib = None
+
+
+def exported_symbols():
+    return ["adp_last_error"] + list(_SIGS)
+
+
+def lib():
+    """Load (once) and return the CDLL. Raises if the HIP extension has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise AdpError(
+                f"libadipose_hip.so not found at {LIB_PATH}; run __graft_entry__.build() "
+                "(make -C adipose_tissue-unet_amd/csrc). There is no CPU fallback.")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        L.adp_last_error.restype = C.c_char_p
+        L.adp_last_error.argtypes = []
+        for name, args in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = C.c_int
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise AdpError(f"{name} failed ({rc}): {lib().adp_last_error().decode()}")
+    return rc
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())

@@ -1,0 +1,98 @@
+// Shared device/host helpers for libadipose_hip (gfx950 / CDNA4 only).
+//
+// Layout conventions used by every kernel in this library:
+//   * activations are NHWC, channel stride padded to a multiple of 8 ("group" = 8 channels
+//     = 16 B in bf16, 32 B in f32); pad channels are kept at zero by construction;
+//   * GEMM weights are stored [Npad][Kpad] (output channel major, K contiguous) with
+//     K = taps * Cin_stride, Kpad = round_up(K, 32), Npad = round_up(N, 64);
+//   * f32 is the parity dtype (exact f32 MFMA), bf16 the throughput dtype (f32 accumulate).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+#include <cmath>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define ADP_DEV __device__ __forceinline__
+
+enum AdpDtype { ADP_F32 = 0, ADP_BF16 = 1 };
+
+// 8-channel group as raw bytes: 16 B for bf16, 32 B for f32.
+template <typename T> struct Grp;
+template <> struct Grp<bf16> { uint4 v; };
+template <> struct Grp<float> { uint4 v[2]; };
+
+ADP_DEV float to_f(float x) { return x; }
+ADP_DEV float to_f(bf16 x) { return (float)x; }
+template <typename T> ADP_DEV T from_f(float x);
+template <> ADP_DEV float from_f<float>(float x) { return x; }
+template <> ADP_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+ADP_DEV void grp_zero(Grp<bf16>& g) { g.v = make_uint4(0, 0, 0, 0); }
+ADP_DEV void grp_zero(Grp<float>& g) { g.v[0] = make_uint4(0, 0, 0, 0); g.v[1] = g.v[0]; }
+ADP_DEV void grp_load(Grp<bf16>& g, const bf16* p) { g.v = *reinterpret_cast<const uint4*>(p); }
+ADP_DEV void grp_load(Grp<float>& g, const float* p) {
+  g.v[0] = reinterpret_cast<const uint4*>(p)[0];
+  g.v[1] = reinterpret_cast<const uint4*>(p)[1];
+}
+ADP_DEV void grp_store(const Grp<bf16>& g, bf16* p) { *reinterpret_cast<uint4*>(p) = g.v; }
+ADP_DEV void grp_store(const Grp<float>& g, float* p) {
+  reinterpret_cast<uint4*>(p)[0] = g.v[0];
+  reinterpret_cast<uint4*>(p)[1] = g.v[1];
+}
+ADP_DEV void grp_to_f(const Grp<bf16>& g, float* f) {
+  const bf16* e = reinterpret_cast<const bf16*>(&g.v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (float)e[j];
+}
+ADP_DEV void grp_to_f(const Grp<float>& g, float* f) {
+  const float* e = reinterpret_cast<const float*>(&g.v[0]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = e[j];
+}
+ADP_DEV void grp_from_f(Grp<bf16>& g, const float* f) {
+  bf16* e = reinterpret_cast<bf16*>(&g.v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = (bf16)f[j];
+}
+ADP_DEV void grp_from_f(Grp<float>& g, const float* f) {
+  float* e = reinterpret_cast<float*>(&g.v[0]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = f[j];
+}
+
+// Stateless counter-based RNG for dropout (lowbias32 mix of seed and element index):
+// the mask is never stored, backward derives it from the stored post-dropout activation.
+ADP_DEV uint32_t adp_hash(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+ADP_DEV float adp_uniform(uint32_t seed, uint64_t idx) {
+  uint32_t h = adp_hash(seed ^ adp_hash((uint32_t)idx ^ adp_hash((uint32_t)(idx >> 32) + 0x9e3779b9U)));
+  return (h >> 8) * (1.0f / 16777216.0f);
+}
+
+ADP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------- host side error plumbing
+#ifdef __cplusplus
+#include <string>
+namespace adp {
+void set_error(const std::string& msg);
+int check_launch(const char* what);
+}  // namespace adp
+#define ADP_REQUIRE(cond, msg)          \
+  do {                                  \
+    if (!(cond)) {                      \
+      adp::set_error(msg);              \
+      return -1;                        \
+    }                                   \
+  } while (0)
+#endif

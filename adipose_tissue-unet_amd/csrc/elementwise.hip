@@ -1,0 +1,439 @@
+// Bandwidth-bound kernels of the U-Net step: weight repacking, 2x2 max-pool (+grad), nearest
+// upsample grad, residual-add + ReLU-mask, BatchNorm statistics/backward, Adam, EMA.
+// Every activation kernel moves 8-channel groups (16 B bf16 / 32 B f32 per lane).
+//   MaxPooling2D((2,2),strides=(2,2))      Segmentation/train_adipose_unet_v3.py:670,674,678
+//   UpSampling2D((2,2)) gradient            :691,698,705
+//   Adam / AdamW (Keras defaults)           :800-806
+//   EMACallback update (ema = d*ema+(1-d)w) :455-459
+#include "common.h"
+#include "../../include/adipose_hip.h"
+
+namespace {
+
+constexpr int TPB = 256;
+inline int nblk(size_t n, int cap = 8192) {
+  size_t b = (n + TPB - 1) / TPB;
+  return (int)(b < (size_t)cap ? (b ? b : 1) : cap);
+}
+
+// ------------------------------------------------------------------------------ repacking
+// mode 0: dst[r][k] = src[r][k]; mode 1/2: dst[ci][t*Nout + co] = src[co][(taps-1-t)*Cin_s + ci]
+template <typename To>
+__global__ void pack_kernel(int mode, int taps, int Cin_s, int Nout, const float* src, int skp,
+                            To* dst, int rows, int dkp) {
+  size_t total = (size_t)rows * dkp;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int r = (int)(i / dkp), k = (int)(i - (size_t)r * dkp);
+    float v = 0.f;
+    if (mode == 0) {
+      v = k < skp ? src[(size_t)r * skp + k] : 0.f;
+    } else if (r < Cin_s && k < taps * Nout) {
+      int t = k / Nout, co = k - t * Nout;
+      v = src[(size_t)co * skp + (size_t)(taps - 1 - t) * Cin_s + r];
+    }
+    dst[i] = from_f<To>(v);
+  }
+}
+
+// ------------------------------------------------------------------------------ max-pool
+template <typename T>
+ADP_DEV void load_bn(Grp<T>& g, const T* p, const float* sc, const float* sh, int c, float* f) {
+  grp_load(g, p);
+  grp_to_f(g, f);
+  if (sc) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[c + j], sh[c + j]), 0.f);
+  }
+}
+
+template <typename T>
+__global__ void maxpool_fwd_kernel(int N, int H, int W, int C, const T* src, const float* sc,
+                                   const float* sh, T* dst) {
+  const int Ho = H >> 1, Wo = W >> 1, G = C >> 3;
+  size_t total = (size_t)N * Ho * Wo * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int g = (int)(i % G);
+    size_t pix = i / G;
+    int xo = (int)(pix % Wo);
+    size_t t = pix / Wo;
+    int yo = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    float best[8], f[8];
+    Grp<T> gr;
+    const T* base = src + (((size_t)n * H + 2 * yo) * W + 2 * xo) * C + g * 8;
+    load_bn(gr, base, sc, sh, g * 8, best);
+    const size_t off[3] = {(size_t)C, (size_t)W * C, (size_t)W * C + C};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      load_bn(gr, base + off[q], sc, sh, g * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) best[j] = f[j] > best[j] ? f[j] : best[j];
+    }
+    grp_from_f(gr, best);
+    grp_store(gr, dst + pix * C + g * 8);
+  }
+}
+
+// gradient routed to the first maximum in (0,0),(0,1),(1,0),(1,1) order (TF/cuDNN NHWC argmax)
+template <typename T>
+__global__ void maxpool_bwd_kernel(int N, int H, int W, int C, const T* src, const float* sc,
+                                   const float* sh, const T* dpool, const T* addend, const T* mask,
+                                   float mscale, T* dsrc) {
+  const int Ho = H >> 1, Wo = W >> 1, G = C >> 3;
+  size_t total = (size_t)N * Ho * Wo * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int g = (int)(i % G);
+    size_t pix = i / G;
+    int xo = (int)(pix % Wo);
+    size_t t = pix / Wo;
+    int yo = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    const size_t off[4] = {0, (size_t)C, (size_t)W * C, (size_t)W * C + C};
+    const size_t base = (((size_t)n * H + 2 * yo) * W + 2 * xo) * C + g * 8;
+    float v[4][8], best[8];
+    int arg[8];
+    Grp<T> gr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) load_bn(gr, src + base + off[q], sc, sh, g * 8, v[q]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = v[0][j]; arg[j] = 0; }
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (v[q][j] > best[j]) { best[j] = v[q][j]; arg[j] = q; }
+    float dp[8];
+    grp_load(gr, dpool + pix * C + g * 8);
+    grp_to_f(gr, dp);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float o[8], a[8], mk[8];
+      if (addend) { grp_load(gr, addend + base + off[q]); grp_to_f(gr, a); }
+      if (mask) { grp_load(gr, mask + base + off[q]); grp_to_f(gr, mk); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = (arg[j] == q ? dp[j] : 0.f) + (addend ? a[j] : 0.f);
+        if (mask) x = mk[j] > 0.f ? x * mscale : 0.f;
+        o[j] = x;
+      }
+      grp_from_f(gr, o);
+      grp_store(gr, dsrc + base + off[q]);
+    }
+  }
+}
+
+template <typename T>
+__global__ void upsample_bwd_kernel(int N, int Hs, int Ws, int C, const T* dup, const T* addend,
+                                    const T* mask, float mscale, T* dsrc) {
+  const int G = C >> 3, Wu = Ws * 2;
+  size_t total = (size_t)N * Hs * Ws * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int g = (int)(i % G);
+    size_t pix = i / G;
+    int xs = (int)(pix % Ws);
+    size_t t = pix / Ws;
+    int ys = (int)(t % Hs);
+    int n = (int)(t / Hs);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f[8];
+    Grp<T> gr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      size_t up = (((size_t)n * 2 * Hs + 2 * ys + (q >> 1)) * Wu + 2 * xs + (q & 1)) * C + g * 8;
+      grp_load(gr, dup + up);
+      grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    size_t o = pix * C + g * 8;
+    if (addend) {
+      grp_load(gr, addend + o); grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    if (mask) {
+      grp_load(gr, mask + o); grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = f[j] > 0.f ? acc[j] * mscale : 0.f;
+    }
+    grp_from_f(gr, acc);
+    grp_store(gr, dsrc + o);
+  }
+}
+
+template <typename T>
+__global__ void ew_add_mask_kernel(size_t ngrp, const T* a, const T* b, const T* mask, float ms, T* out) {
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < ngrp; i += (size_t)gridDim.x * TPB) {
+    Grp<T> gr;
+    float x[8], f[8];
+    grp_load(gr, a + i * 8); grp_to_f(gr, x);
+    if (b) {
+      grp_load(gr, b + i * 8); grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] += f[j];
+    }
+    if (mask) {
+      grp_load(gr, mask + i * 8); grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = f[j] > 0.f ? x[j] * ms : 0.f;
+    }
+    grp_from_f(gr, x);
+    grp_store(gr, out + i * 8);
+  }
+}
+
+template <typename Ti, typename To>
+__global__ void cast_kernel(size_t n, const Ti* src, To* dst) {
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB)
+    dst[i] = from_f<To>(to_f(src[i]));
+}
+
+__global__ void fill_kernel(size_t n, float v, float* dst) {
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) dst[i] = v;
+}
+
+// ------------------------------------------------------------------------------ BatchNorm
+__global__ void bn_finalize_kernel(int C, float count, const float* sum, const float* sq,
+                                   const float* gamma, const float* beta, float eps, float momentum,
+                                   float* scale, float* shift, float* mean, float* invstd,
+                                   float* rmean, float* rvar) {
+  int c = blockIdx.x * TPB + threadIdx.x;
+  if (c >= C) return;
+  // count < 0: eval mode, (sum, sq) hold the running (mean, var)
+  float mu = count > 0.f ? sum[c] / count : sum[c];
+  float var = count > 0.f ? fmaxf(sq[c] / count - mu * mu, 0.f) : sq[c];
+  float is = rsqrtf(var + eps);
+  float sc = gamma[c] * is;
+  scale[c] = sc;
+  shift[c] = beta[c] - mu * sc;
+  mean[c] = mu;
+  invstd[c] = is;
+  if (rmean && count > 0.f) {
+    float unb = count > 1.f ? var * count / (count - 1.f) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+  }
+}
+
+// per-channel sums of dBN and dBN*xhat; block = 256 threads as (pixel lane) x (channel group)
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(size_t M, int C, const T* dA, const T* z, const float* sc,
+                                     const float* sh, const float* mean, const float* invstd,
+                                     float* dgamma, float* dbeta) {
+  const int G = C >> 3;
+  const int lanes = TPB / G;           // pixels processed per block iteration
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (pl < lanes) {
+    for (size_t m = (size_t)blockIdx.x * lanes + pl; m < M; m += (size_t)gridDim.x * lanes) {
+      Grp<T> gr;
+      float d[8], zz[8];
+      grp_load(gr, dA + m * C + g * 8); grp_to_f(gr, d);
+      grp_load(gr, z + m * C + g * 8); grp_to_f(gr, zz);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        int c = g * 8 + j;
+        float a = fmaf(zz[j], sc[c], sh[c]);
+        float db = a > 0.f ? d[j] : 0.f;
+        s1[j] += db;
+        s2[j] += db * (zz[j] - mean[c]) * invstd[c];
+      }
+    }
+  }
+  __shared__ float red[2][TPB * 8 / 8 * 8];
+  // reduce over pixel lanes with the same channel group through LDS
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x * 8 + j] = s1[j];
+    red[1][threadIdx.x * 8 + j] = s2[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += TPB) {
+    int gg = c >> 3, j = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      a += red[0][(l * G + gg) * 8 + j];
+      b += red[1][(l * G + gg) * 8 + j];
+    }
+    atomicAdd(dbeta + c, a);
+    atomicAdd(dgamma + c, b);
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(size_t M, int C, const T* dA, const T* z, const float* sc,
+                                    const float* sh, const float* mean, const float* invstd,
+                                    const float* gamma, const float* dgamma, const float* dbeta,
+                                    float inv_count, T* dz) {
+  const int G = C >> 3;
+  size_t total = M * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int g = (int)(i % G);
+    Grp<T> gr;
+    float d[8], zz[8], o[8];
+    grp_load(gr, dA + i * 8); grp_to_f(gr, d);
+    grp_load(gr, z + i * 8); grp_to_f(gr, zz);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int c = g * 8 + j;
+      float a = fmaf(zz[j], sc[c], sh[c]);
+      float db = a > 0.f ? d[j] : 0.f;
+      float xh = (zz[j] - mean[c]) * invstd[c];
+      o[j] = gamma[c] * invstd[c] * (db - dbeta[c] * inv_count - xh * dgamma[c] * inv_count);
+    }
+    grp_from_f(gr, o);
+    grp_store(gr, dz + i * 8);
+  }
+}
+
+// ------------------------------------------------------------------------------ optimizer
+// Keras 2.13 Adam.update_step: alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1);
+// v += (g^2-v)(1-b2); w -= m*alpha/(sqrt(v)+eps). AdamW first applies w -= w*wd*lr.
+__global__ void adam_kernel(size_t n, float* w, const float* g, float* m, float* v, float lr,
+                            float b1, float b2, float eps, float alpha, float wd, float gs) {
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) {
+    float gi = g[i] * gs;
+    float wi = w[i];
+    if (wd != 0.f) wi -= wi * wd * lr;
+    float mi = m[i] + (gi - m[i]) * (1.f - b1);
+    float vi = v[i] + (gi * gi - v[i]) * (1.f - b2);
+    m[i] = mi;
+    v[i] = vi;
+    w[i] = wi - (mi * alpha) / (sqrtf(vi) + eps);
+  }
+}
+
+__global__ void ema_kernel(size_t n, float* ema, const float* p, float d) {
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB)
+    ema[i] = d * ema[i] + (1.f - d) * p[i];
+}
+
+}  // namespace
+
+#define DTYPE_SWITCH(dtype, T, ...)                                   \
+  do {                                                                \
+    if ((dtype) == ADP_F32) { using T = float; __VA_ARGS__; }         \
+    else if ((dtype) == ADP_BF16) { using T = bf16; __VA_ARGS__; }    \
+    else { adp::set_error("unknown dtype"); return -1; }              \
+  } while (0)
+
+extern "C" int adp_pack_weights(int dtype_out, int mode, int taps, int Cin_s, int Nout,
+                                const float* src, int src_kpad, void* dst, int dst_rows, int dst_kpad,
+                                adp_stream_t st) {
+  ADP_REQUIRE(src && dst && dst_rows > 0 && dst_kpad > 0, "adp_pack_weights: bad arguments");
+  ADP_REQUIRE(mode >= 0 && mode <= 2, "adp_pack_weights: bad mode");
+  size_t n = (size_t)dst_rows * dst_kpad;
+  DTYPE_SWITCH(dtype_out, T,
+               hipLaunchKernelGGL(pack_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, mode, taps,
+                                  Cin_s, Nout, src, src_kpad, (T*)dst, dst_rows, dst_kpad));
+  return adp::check_launch("adp_pack_weights");
+}
+
+extern "C" int adp_maxpool2_fwd(int dtype, int N, int H, int W, int C, const void* src,
+                                const float* sc, const float* sh, void* dst, adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && H % 2 == 0 && W % 2 == 0, "adp_maxpool2_fwd: need C%8==0 and even H,W");
+  size_t n = (size_t)N * (H / 2) * (W / 2) * (C / 8);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(maxpool_fwd_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W,
+                                  C, (const T*)src, sc, sh, (T*)dst));
+  return adp::check_launch("adp_maxpool2_fwd");
+}
+
+extern "C" int adp_maxpool2_bwd(int dtype, int N, int H, int W, int C, const void* src,
+                                const float* sc, const float* sh, const void* dpool, const void* addend,
+                                const void* mask, float ms, void* dsrc, adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && H % 2 == 0 && W % 2 == 0, "adp_maxpool2_bwd: need C%8==0 and even H,W");
+  size_t n = (size_t)N * (H / 2) * (W / 2) * (C / 8);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W,
+                                  C, (const T*)src, sc, sh, (const T*)dpool, (const T*)addend,
+                                  (const T*)mask, ms, (T*)dsrc));
+  return adp::check_launch("adp_maxpool2_bwd");
+}
+
+extern "C" int adp_upsample2_bwd(int dtype, int N, int Hs, int Ws, int C, const void* dup,
+                                 const void* addend, const void* mask, float ms, void* dsrc,
+                                 adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0, "adp_upsample2_bwd: need C%8==0");
+  size_t n = (size_t)N * Hs * Ws * (C / 8);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(upsample_bwd_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, Hs,
+                                  Ws, C, (const T*)dup, (const T*)addend, (const T*)mask, ms, (T*)dsrc));
+  return adp::check_launch("adp_upsample2_bwd");
+}
+
+extern "C" int adp_ew_add_mask(int dtype, size_t n, const void* a, const void* b, const void* mask,
+                               float ms, void* out, adp_stream_t st) {
+  ADP_REQUIRE(n % 8 == 0, "adp_ew_add_mask: n must be a multiple of 8");
+  size_t g = n / 8;
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(ew_add_mask_kernel<T>, dim3(nblk(g)), dim3(TPB), 0, (hipStream_t)st, g,
+                                  (const T*)a, (const T*)b, (const T*)mask, ms, (T*)out));
+  return adp::check_launch("adp_ew_add_mask");
+}
+
+extern "C" int adp_cast(int di, int dout, size_t n, const void* src, void* dst, adp_stream_t st) {
+  hipStream_t s = (hipStream_t)st;
+  if (di == ADP_F32 && dout == ADP_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(nblk(n)), dim3(TPB), 0, s, n, (const float*)src, (bf16*)dst);
+  else if (di == ADP_BF16 && dout == ADP_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(nblk(n)), dim3(TPB), 0, s, n, (const bf16*)src, (float*)dst);
+  else if (di == ADP_F32 && dout == ADP_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(nblk(n)), dim3(TPB), 0, s, n, (const float*)src, (float*)dst);
+  else if (di == ADP_BF16 && dout == ADP_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(nblk(n)), dim3(TPB), 0, s, n, (const bf16*)src, (bf16*)dst);
+  else { adp::set_error("adp_cast: bad dtype"); return -1; }
+  return adp::check_launch("adp_cast");
+}
+
+extern "C" int adp_fill_f32(size_t n, float v, float* dst, adp_stream_t st) {
+  hipLaunchKernelGGL(fill_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, n, v, dst);
+  return adp::check_launch("adp_fill_f32");
+}
+
+extern "C" int adp_bn_finalize(int C, float count, const float* sum, const float* sq, const float* gamma,
+                               const float* beta, float eps, float momentum, float* scale, float* shift,
+                               float* mean, float* invstd, float* rmean, float* rvar, adp_stream_t st) {
+  ADP_REQUIRE(C > 0 && count != 0, "adp_bn_finalize: bad arguments");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + TPB - 1) / TPB), dim3(TPB), 0, (hipStream_t)st, C, count,
+                     sum, sq, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean, rvar);
+  return adp::check_launch("adp_bn_finalize");
+}
+
+extern "C" int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, const void* z, const float* sc,
+                                 const float* sh, const float* mean, const float* invstd, float* dgamma,
+                                 float* dbeta, adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB, "adp_bn_bwd_reduce: C must be a multiple of 8 and <= 2048");
+  int lanes = TPB / (C / 8);
+  int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 2048);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, C,
+                                  (const T*)dA, (const T*)z, sc, sh, mean, invstd, dgamma, dbeta));
+  return adp::check_launch("adp_bn_bwd_reduce");
+}
+
+extern "C" int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, const void* z, const float* sc,
+                                const float* sh, const float* mean, const float* invstd, const float* gamma,
+                                const float* dgamma, const float* dbeta, float count, void* dz,
+                                adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && count > 0, "adp_bn_bwd_apply: bad arguments");
+  size_t n = M * (C / 8);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, M, C,
+                                  (const T*)dA, (const T*)z, sc, sh, mean, invstd, gamma, dgamma, dbeta,
+                                  1.f / count, (T*)dz));
+  return adp::check_launch("adp_bn_bwd_apply");
+}
+
+extern "C" int adp_adam(size_t n, float* w, const float* g, float* m, float* v, float lr, float b1,
+                        float b2, float eps, int step, float wd, float gs, adp_stream_t st) {
+  ADP_REQUIRE(step >= 1, "adp_adam: step counts from 1");
+  double alpha = (double)lr * sqrt(1.0 - pow((double)b2, step)) / (1.0 - pow((double)b1, step));
+  hipLaunchKernelGGL(adam_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, n, w, g, m, v, lr, b1, b2,
+                     eps, (float)alpha, wd, gs);
+  return adp::check_launch("adp_adam");
+}
+
+extern "C" int adp_ema(size_t n, float* ema, const float* p, float d, adp_stream_t st) {
+  hipLaunchKernelGGL(ema_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, n, ema, p, d);
+  return adp::check_launch("adp_ema");
+}

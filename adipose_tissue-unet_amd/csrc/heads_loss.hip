@@ -1,0 +1,420 @@
+// Per-pixel heads, bilinear aux resize, BCE+Dice / OHEM loss and metric reductions.
+//   main head  Conv2D(2,1,activation='softmax') -> [...,1:2] -> squeeze
+//              Segmentation/train_adipose_unet_v3.py:729-731
+//   aux heads  Conv2D(1,1,activation='sigmoid') + tf.image.resize(bilinear)      :715-726
+//   losses     dice_loss :217-225, combined_loss_standard :228-241, label smoothing :244-279,
+//              online_hard_example_mining_loss(+smoothing) :282-363; Keras 2.13 binary_crossentropy
+//              (clip to [1e-7, 1-1e-7], log(p+1e-7), mean over the last axis)
+//   metrics    dice_coef src/utils/model.py:93-98, Keras binary_accuracy (threshold 0.5),
+//              calculate_pixel_metrics counts Segmentation/full_evaluation_enhanced.py:721-785
+#include "common.h"
+#include "../../include/adipose_hip.h"
+
+namespace {
+constexpr int TPB = 256;
+constexpr float KEPS = 1e-7f;
+
+inline int nblk(size_t n, int cap = 8192) {
+  size_t b = (n + TPB - 1) / TPB;
+  return (int)(b < (size_t)cap ? (b ? b : 1) : cap);
+}
+
+// ---------------------------------------------------------------------------------- heads
+// forward: thread per pixel, dot over Cin channels (8-channel groups), NOUT = 1 or 2
+template <typename T, int NOUT>
+__global__ void head_fwd_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* b,
+                                const float* sc, const float* sh, float* p) {
+  __shared__ float ws[NOUT * 1024];
+  for (int i = threadIdx.x; i < NOUT * Cs; i += TPB) {
+    int o = i / Cs, c = i - o * Cs;
+    ws[i] = c < Cin ? W[o * Cin + c] : 0.f;
+  }
+  __syncthreads();
+  const float b0 = b[0], b1 = NOUT == 2 ? b[1] : 0.f;
+  for (size_t m = blockIdx.x * (size_t)TPB + threadIdx.x; m < M; m += (size_t)gridDim.x * TPB) {
+    float z0 = b0, z1 = b1;
+    for (int g = 0; g < Cs; g += 8) {
+      Grp<T> gr;
+      float f[8];
+      grp_load(gr, x + m * Cs + g);
+      grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = sc ? fmaxf(fmaf(f[j], sc[g + j], sh[g + j]), 0.f) : f[j];
+        z0 = fmaf(v, ws[g + j], z0);
+        if (NOUT == 2) z1 = fmaf(v, ws[Cs + g + j], z1);
+      }
+    }
+    // softmax over 2 logits, channel 1 kept == 1/(1+exp(z0-z1)); sigmoid otherwise
+    p[m] = NOUT == 2 ? 1.f / (1.f + expf(z0 - z1)) : 1.f / (1.f + expf(-z0));
+  }
+}
+
+// backward: block = 32 pixel lanes x 8 channel groups (Cs <= 64*8); dW reduced in LDS then atomics
+template <typename T, int NOUT>
+__global__ void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* sc,
+                                const float* sh, const float* p, const float* dp, const T* addend,
+                                const T* mask, float ms, T* dx, float* dW, float* db) {
+  const int G = Cs >> 3;                 // groups per pixel
+  const int lanes = TPB / G;
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  float wd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int c = g * 8 + j;
+    float w1 = c < Cin ? W[(NOUT - 1) * Cin + c] : 0.f;
+    float w0 = (NOUT == 2 && c < Cin) ? W[c] : 0.f;
+    wd[j] = NOUT == 2 ? w1 - w0 : w1;
+  }
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float dbacc = 0.f;
+  if (pl < lanes) {
+    for (size_t m = (size_t)blockIdx.x * lanes + pl; m < M; m += (size_t)gridDim.x * lanes) {
+      const float pm = p[m];
+      const float dz = dp[m] * pm * (1.f - pm);   // d p/d(z1-z0) for softmax2, d p/dz for sigmoid
+      Grp<T> gr;
+      float f[8], o[8], a[8], mk[8];
+      grp_load(gr, x + m * Cs + g * 8);
+      grp_to_f(gr, f);
+      if (addend) { grp_load(gr, addend + m * Cs + g * 8); grp_to_f(gr, a); }
+      if (mask) { grp_load(gr, mask + m * Cs + g * 8); grp_to_f(gr, mk); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = sc ? fmaxf(fmaf(f[j], sc[g * 8 + j], sh[g * 8 + j]), 0.f) : f[j];
+        acc[j] = fmaf(dz, v, acc[j]);
+        float d = dz * wd[j] + (addend ? a[j] : 0.f);
+        if (mask) d = mk[j] > 0.f ? d * ms : 0.f;
+        o[j] = d;
+      }
+      if (dx) { grp_from_f(gr, o); grp_store(gr, dx + m * Cs + g * 8); }
+      if (g == 0) dbacc += dz;
+    }
+  }
+  __shared__ float red[TPB * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = acc[j];
+  __shared__ float redb[TPB];
+  redb[threadIdx.x] = dbacc;
+  __syncthreads();
+  for (int c = threadIdx.x; c < Cin; c += TPB) {
+    int gg = c >> 3, j = c & 7;
+    float s = 0.f;
+    for (int l = 0; l < lanes; ++l) s += red[(l * G + gg) * 8 + j];
+    if (NOUT == 2) { atomicAdd(dW + c, -s); atomicAdd(dW + Cin + c, s); }
+    else atomicAdd(dW + c, s);
+  }
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int l = 0; l < lanes; ++l) s += redb[l * G];
+    if (NOUT == 2) { atomicAdd(db, -s); atomicAdd(db + 1, s); }
+    else atomicAdd(db, s);
+  }
+}
+
+// ------------------------------------------------------------------- bilinear (half-pixel)
+// TF ResizeBilinear(half_pixel_centers=True): in = (out+0.5)*scale-0.5, lo = max(floor,0),
+// hi = min(ceil, n-1), lerp = in - floor(in); value = top + (bottom-top)*ylerp.
+ADP_DEV void bil_coord(int o, float scale, int n, int& lo, int& hi, float& t) {
+  float in = ((float)o + 0.5f) * scale - 0.5f;
+  float fl = floorf(in);
+  lo = in > 0.f ? (int)fl : 0;
+  hi = (in < (float)(n - 1)) ? (int)ceilf(in) : n - 1;
+  t = in - fl;
+}
+
+__global__ void resize_fwd_kernel(int N, int Hs, int Ws, int Ho, int Wo, const float* src, float* dst) {
+  const float sy = (float)Hs / Ho, sx = (float)Ws / Wo;
+  size_t total = (size_t)N * Ho * Wo;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int xo = (int)(i % Wo);
+    size_t t = i / Wo;
+    int yo = (int)(t % Ho), n = (int)(t / Ho);
+    int y0, y1, x0, x1;
+    float ty, tx;
+    bil_coord(yo, sy, Hs, y0, y1, ty);
+    bil_coord(xo, sx, Ws, x0, x1, tx);
+    const float* s = src + (size_t)n * Hs * Ws;
+    float tl = s[y0 * Ws + x0], tr = s[y0 * Ws + x1], bl = s[y1 * Ws + x0], br = s[y1 * Ws + x1];
+    float top = tl + (tr - tl) * tx, bot = bl + (br - bl) * tx;
+    dst[i] = top + (bot - top) * ty;
+  }
+}
+
+// adjoint as a gather: dsrc[ys][xs] = sum_{yo,xo} wy(yo,ys) wx(xo,xs) dout[yo][xo]
+ADP_DEV float bil_w(int o, float scale, int n, int s) {
+  int lo, hi;
+  float t;
+  bil_coord(o, scale, n, lo, hi, t);
+  return (lo == s ? 1.f - t : 0.f) + (hi == s ? t : 0.f);
+}
+
+__global__ void resize_bwd_kernel(int N, int Hs, int Ws, int Ho, int Wo, const float* dout, float* dsrc) {
+  const float sy = (float)Hs / Ho, sx = (float)Ws / Wo;
+  const int fy = (Ho + Hs - 1) / Hs, fx = (Wo + Ws - 1) / Ws;
+  size_t total = (size_t)N * Hs * Ws;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int xs = (int)(i % Ws);
+    size_t t = i / Ws;
+    int ys = (int)(t % Hs), n = (int)(t / Hs);
+    int ya = max(0, (ys - 1) * fy - fy), yb = min(Ho - 1, (ys + 2) * fy + fy);
+    int xa = max(0, (xs - 1) * fx - fx), xb = min(Wo - 1, (xs + 2) * fx + fx);
+    const float* d = dout + (size_t)n * Ho * Wo;
+    float acc = 0.f;
+    for (int yo = ya; yo <= yb; ++yo) {
+      float wy = bil_w(yo, sy, Hs, ys);
+      if (wy == 0.f) continue;
+      float rs = 0.f;
+      for (int xo = xa; xo <= xb; ++xo) {
+        float wx = bil_w(xo, sx, Ws, xs);
+        if (wx != 0.f) rs = fmaf(wx, d[(size_t)yo * Wo + xo], rs);
+      }
+      acc = fmaf(wy, rs, acc);
+    }
+    dsrc[i] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------- losses
+ADP_DEV float smooth_y(float y, int smooth, float ep, float en) {
+  return smooth ? y * (1.f - ep - en) + en : y;
+}
+ADP_DEV float clipp(float p) { return fminf(fmaxf(p, KEPS), 1.f - KEPS); }
+
+ADP_DEV double block_sum_d(double v, double* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += sh[i];
+  return r;   // valid in thread 0
+}
+
+// one block per image row
+__global__ void loss_rows_kernel(int N, int H, int W, const float* p, const float* y, int smooth,
+                                 float ep, float en, float* row_bce, double* stats) {
+  __shared__ double sh[16];
+  const int row = blockIdx.x;
+  const float* pr = p + (size_t)row * W;
+  const float* yr = y + (size_t)row * W;
+  float bce = 0.f, s_yp = 0.f, s_y = 0.f, s_p = 0.f, r_yp = 0.f, r_y = 0.f, r_p = 0.f, acc = 0.f;
+  for (int x = threadIdx.x; x < W; x += TPB) {
+    float pv = pr[x], yv = yr[x];
+    float ys = smooth_y(yv, smooth, ep, en);
+    float pc = clipp(pv);
+    bce -= ys * logf(pc + KEPS) + (1.f - ys) * logf(1.f - pc + KEPS);
+    s_yp += ys * pc; s_y += ys; s_p += pc;
+    r_yp += yv * pv; r_y += yv; r_p += pv;
+    acc += (yv == (pv > 0.5f ? 1.f : 0.f)) ? 1.f : 0.f;
+  }
+  double v[8] = {bce, s_yp, s_y, s_p, r_yp, r_y, r_p, acc};
+  double tot[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) tot[i] = block_sum_d(v[i], sh);
+  if (threadIdx.x == 0) {
+    row_bce[row] = (float)(tot[0] / W);
+    for (int i = 1; i < 8; ++i) atomicAdd(stats + i - 1, tot[i]);
+  }
+}
+
+// one block (1024 threads) per image: bitonic sort of (bce desc, row asc) keys, first k selected
+__global__ void loss_select_kernel(int N, int H, int W, const float* row_bce, int ohem, float keep,
+                                   float weight, float norm_rows, float* row_coef, double* out) {
+  __shared__ float kv[2048];
+  __shared__ int ki[2048];
+  __shared__ double sh[16];
+  const int b = blockIdx.x;
+  const float* rb = row_bce + (size_t)b * H;
+  float* rc = row_coef + (size_t)b * H;
+  const float coef = weight / (norm_rows * (float)W);
+  if (!ohem) {
+    double s = 0.0;
+    for (int r = threadIdx.x; r < H; r += blockDim.x) { rc[r] = coef; s += rb[r]; }
+    s = block_sum_d(s, sh);
+    if (threadIdx.x == 0) atomicAdd(out, (double)weight * s / norm_rows);
+    return;
+  }
+  int P = 1;
+  while (P < H) P <<= 1;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    kv[i] = i < H ? rb[i] : -INFINITY;
+    ki[i] = i < H ? i : 0x7fffffff;
+  }
+  __syncthreads();
+  // sort descending by value, ascending by index on ties
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        int l = i ^ j;
+        if (l > i) {
+          bool desc = (i & k) == 0;
+          float a = kv[i], c = kv[l];
+          int ia = ki[i], ic = ki[l];
+          bool a_first = (a > c) || (a == c && ia < ic);
+          if (desc != a_first) { kv[i] = c; kv[l] = a; ki[i] = ic; ki[l] = ia; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int kk = (int)((float)H * keep);
+  double s = 0.0;
+  for (int i = threadIdx.x; i < H; i += blockDim.x) {
+    bool sel = i < kk;
+    rc[ki[i]] = sel ? coef : 0.f;
+    if (sel) s += kv[i];
+  }
+  s = block_sum_d(s, sh);
+  if (threadIdx.x == 0) atomicAdd(out, (double)weight * s / norm_rows);
+}
+
+__global__ void loss_grad_kernel(int N, int H, int W, const float* p, const float* y, int smooth,
+                                 float ep, float en, const float* row_coef, const double* stats,
+                                 float weight, int accumulate, float* dp) {
+  const double I = stats[0], Sy = stats[1], Sp = stats[2];
+  const double den = Sy + Sp + 1.0;
+  const float g_i = (float)(-(weight * 2.0) / den);                  // coefficient of y_i
+  const float g_c = (float)(weight * (2.0 * I + 1.0) / (den * den));  // constant term
+  size_t total = (size_t)N * H * W;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    float pv = p[i];
+    float ys = smooth_y(y[i], smooth, ep, en);
+    float d = 0.f;
+    if (pv >= KEPS && pv <= 1.f - KEPS) {
+      float pc = pv;
+      float dbce = -ys / (pc + KEPS) + (1.f - ys) / (1.f - pc + KEPS);
+      d = row_coef[i / W] * dbce + (g_i * ys + g_c);
+    }
+    dp[i] = accumulate ? dp[i] + d : d;
+  }
+}
+
+__global__ void pixel_counts_kernel(size_t n, const float* pred, const float* truth, float thr,
+                                    unsigned long long* counts) {
+  unsigned long long c[4] = {0, 0, 0, 0};
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) {
+    bool pb = pred[i] > thr, tb = truth[i] > 0.5f;
+    c[pb ? (tb ? 0 : 1) : (tb ? 2 : 3)]++;
+  }
+  __shared__ unsigned long long sh[4][TPB / 64];
+  for (int k = 0; k < 4; ++k) {
+    unsigned long long v = c[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[k][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long v = 0;
+    for (int w = 0; w < TPB / 64; ++w) v += sh[threadIdx.x][w];
+    atomicAdd(counts + threadIdx.x, v);
+  }
+}
+}  // namespace
+
+#define DTYPE_SWITCH(dtype, T, ...)                                   \
+  do {                                                                \
+    if ((dtype) == ADP_F32) { using T = float; __VA_ARGS__; }         \
+    else if ((dtype) == ADP_BF16) { using T = bf16; __VA_ARGS__; }    \
+    else { adp::set_error("unknown dtype"); return -1; }              \
+  } while (0)
+
+extern "C" int adp_head_softmax2_fwd(int dtype, size_t M, int Cs, int Cin, const void* x, const float* W,
+                                     const float* b, const float* sc, const float* sh, float* p,
+                                     adp_stream_t st) {
+  ADP_REQUIRE(Cs % 8 == 0 && Cs <= 1024 && Cin <= Cs, "adp_head_softmax2_fwd: bad channels");
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL((head_fwd_kernel<T, 2>), dim3(nblk(M)), dim3(TPB), 0, (hipStream_t)st, M, Cs,
+                                  Cin, (const T*)x, W, b, sc, sh, p));
+  return adp::check_launch("adp_head_softmax2_fwd");
+}
+
+extern "C" int adp_head_sigmoid_fwd(int dtype, size_t M, int Cs, int Cin, const void* x, const float* W,
+                                    const float* b, const float* sc, const float* sh, float* p,
+                                    adp_stream_t st) {
+  ADP_REQUIRE(Cs % 8 == 0 && Cs <= 1024 && Cin <= Cs, "adp_head_sigmoid_fwd: bad channels");
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL((head_fwd_kernel<T, 1>), dim3(nblk(M)), dim3(TPB), 0, (hipStream_t)st, M, Cs,
+                                  Cin, (const T*)x, W, b, sc, sh, p));
+  return adp::check_launch("adp_head_sigmoid_fwd");
+}
+
+template <int NOUT>
+static int head_bwd(int dtype, size_t M, int Cs, int Cin, const void* x, const float* W, const float* sc,
+                    const float* sh, const float* p, const float* dp, const void* addend, const void* mask,
+                    float ms, void* dx, float* dW, float* db, hipStream_t s) {
+  ADP_REQUIRE(Cs % 8 == 0 && Cs / 8 <= TPB, "head backward: Cs must be a multiple of 8 and <= 2048");
+  int lanes = TPB / (Cs / 8);
+  int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 4096);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL((head_bwd_kernel<T, NOUT>), dim3(blocks), dim3(TPB), 0, s, M, Cs, Cin,
+                                  (const T*)x, W, sc, sh, p, dp, (const T*)addend, (const T*)mask, ms, (T*)dx,
+                                  dW, db));
+  return adp::check_launch("adp_head_bwd");
+}
+
+extern "C" int adp_head_softmax2_bwd(int dtype, size_t M, int Cs, int Cin, const void* x, const float* W,
+                                     const float* sc, const float* sh, const float* p, const float* dp,
+                                     const void* addend, const void* mask, float ms, void* dx, float* dW,
+                                     float* db, adp_stream_t st) {
+  return head_bwd<2>(dtype, M, Cs, Cin, x, W, sc, sh, p, dp, addend, mask, ms, dx, dW, db, (hipStream_t)st);
+}
+
+extern "C" int adp_head_sigmoid_bwd(int dtype, size_t M, int Cs, int Cin, const void* x, const float* W,
+                                    const float* sc, const float* sh, const float* p, const float* dp,
+                                    const void* addend, const void* mask, float ms, void* dx, float* dW,
+                                    float* db, adp_stream_t st) {
+  return head_bwd<1>(dtype, M, Cs, Cin, x, W, sc, sh, p, dp, addend, mask, ms, dx, dW, db, (hipStream_t)st);
+}
+
+extern "C" int adp_resize_bilinear_fwd(int N, int Hs, int Ws, int Ho, int Wo, const float* src, float* dst,
+                                       adp_stream_t st) {
+  ADP_REQUIRE(N > 0 && Hs > 0 && Ws > 0 && Ho > 0 && Wo > 0, "adp_resize_bilinear_fwd: bad dims");
+  size_t n = (size_t)N * Ho * Wo;
+  hipLaunchKernelGGL(resize_fwd_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, Hs, Ws, Ho, Wo, src, dst);
+  return adp::check_launch("adp_resize_bilinear_fwd");
+}
+
+extern "C" int adp_resize_bilinear_bwd(int N, int Hs, int Ws, int Ho, int Wo, const float* dout, float* dsrc,
+                                       adp_stream_t st) {
+  ADP_REQUIRE(N > 0 && Hs > 0 && Ws > 0 && Ho >= Hs && Wo >= Ws, "adp_resize_bilinear_bwd: upsampling only");
+  size_t n = (size_t)N * Hs * Ws;
+  hipLaunchKernelGGL(resize_bwd_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, Hs, Ws, Ho, Wo, dout, dsrc);
+  return adp::check_launch("adp_resize_bilinear_bwd");
+}
+
+extern "C" int adp_loss_rows(int N, int H, int W, const float* p, const float* y, int smooth, float ep,
+                             float en, float* row_bce, double* stats, adp_stream_t st) {
+  ADP_REQUIRE(N > 0 && H > 0 && W > 0, "adp_loss_rows: bad dims");
+  hipLaunchKernelGGL(loss_rows_kernel, dim3(N * H), dim3(TPB), 0, (hipStream_t)st, N, H, W, p, y, smooth, ep, en,
+                     row_bce, stats);
+  return adp::check_launch("adp_loss_rows");
+}
+
+extern "C" int adp_loss_select(int N, int H, int W, const float* row_bce, int ohem, float keep, float weight,
+                               float norm_rows, float* row_coef, double* out, adp_stream_t st) {
+  ADP_REQUIRE(H <= 2048, "adp_loss_select: H must be <= 2048");
+  ADP_REQUIRE(norm_rows > 0, "adp_loss_select: norm_rows must be > 0");
+  hipLaunchKernelGGL(loss_select_kernel, dim3(N), dim3(1024), 0, (hipStream_t)st, N, H, W, row_bce, ohem, keep,
+                     weight, norm_rows, row_coef, out);
+  return adp::check_launch("adp_loss_select");
+}
+
+extern "C" int adp_loss_grad(int N, int H, int W, const float* p, const float* y, int smooth, float ep,
+                             float en, const float* row_coef, const double* stats, float weight, int accumulate,
+                             float* dp, adp_stream_t st) {
+  size_t n = (size_t)N * H * W;
+  hipLaunchKernelGGL(loss_grad_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W, p, y, smooth, ep,
+                     en, row_coef, stats, weight, accumulate, dp);
+  return adp::check_launch("adp_loss_grad");
+}
+
+extern "C" int adp_pixel_counts(size_t n, const float* pred, const float* truth, float thr,
+                                unsigned long long* counts, adp_stream_t st) {
+  hipLaunchKernelGGL(pixel_counts_kernel, dim3(nblk(n, 2048)), dim3(TPB), 0, (hipStream_t)st, n, pred, truth, thr,
+                     counts);
+  return adp::check_launch("adp_pixel_counts");
+}

@@ -1,0 +1,773 @@
+"""U-Net presets as explicit, preallocated GPU schedules over the libadipose_hip kernels.
+
+Two presets share the same kernels:
+
+* ``adipose_v3`` — the reference network, AdiposeUNetV3.build_model
+  (Segmentation/train_adipose_unet_v3.py:660-758; identical copies segmentation_inference.py:88-146,
+  full_evaluation_enhanced.py:1163-1264): 1-channel input, base width 44, 3 poolings, dilated
+  bottleneck (dilations 1..32 summed), nearest-upsample+conv decoder with skip concats, Dropout(0.3),
+  2-class softmax main head (+ two sigmoid deep-supervision heads with bilinear resize).
+* ``unet_bn`` — the north-star network of BASELINE.json configs 2/3/5 (no reference code):
+  L levels, base 64, [conv3x3 -> BatchNorm -> ReLU] x 2 blocks, 2x2 max-pool, ConvTranspose 2x2/s2
+  upsampling + skip concat, 1x1 conv + sigmoid head.
+
+Nothing here runs torch compute: torch tensors are only HBM allocations; every op is a C-ABI call.
+All activations for a fixed (batch, size) are allocated once (HBM is 288 GB; no allocator churn in
+the step), so a whole step can be captured in a HIP graph.
+
+Parameter layout: one flat f32 master buffer (+ same-layout grad / Adam buffers). A dense layer owns
+``W`` packed [Npad][Kpad] (see include/adipose_hip.h) and ``b``; Keras HWIO kernels map onto it by
+``keras_to_packed`` / ``packed_to_keras`` so `.weights.h5`-style name/slot I/O is 1:1.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import ops
+from .ops import round_up
+
+
+def r8(c):
+    return round_up(c, 8)
+
+
+# --------------------------------------------------------------------------------- parameters
+class ParamStore:
+    """Flat f32 parameter buffer with named views; grads/moments share the layout."""
+
+    def __init__(self):
+        self.entries = OrderedDict()
+        self.total = 0
+        self.flat = None
+        self.grad = None
+
+    def add(self, name, shape, init="zeros"):
+        n = int(np.prod(shape))
+        self.entries[name] = (self.total, tuple(shape), init)
+        self.total += round_up(n, 64)  # 256-B aligned slices
+        return name
+
+    def allocate(self, device):
+        self.flat = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
+
+    def view(self, name, buf=None):
+        off, shape, _ = self.entries[name]
+        b = self.flat if buf is None else buf
+        return b[off:off + int(np.prod(shape))].view(shape)
+
+    def gview(self, name):
+        return self.view(name, self.grad)
+
+
+class Dense:
+    """A GEMM-lowered layer: 3x3 conv (any dilation, optional nearest-x2 input, optional concat) or
+    ConvTranspose 2x2/s2. Keras names/shapes are kept for checkpoint interop."""
+
+    def __init__(self, name, cin_parts, cout, *, k=3, dil=1, up=False, bias=True, bn=False, transpose=False,
+                 relu=True):
+        self.name = name
+        self.cin_parts = list(cin_parts)
+        self.cin_s = [r8(c) for c in cin_parts]
+        self.Cin_s = sum(self.cin_s)
+        self.cout = cout
+        self.cout_s = r8(cout)
+        self.k = 1 if transpose else k
+        self.dil = dil
+        self.up = up
+        self.bias = bias
+        self.bn = bn
+        self.relu = relu
+        self.transpose = transpose
+        if transpose:
+            self.taps = 1
+            self.Nout = 4 * self.cout_s
+        else:
+            self.taps = k * k
+            self.Nout = self.cout_s
+        self.K = self.taps * self.Cin_s
+        self.Kpad = round_up(self.K, 32)
+        self.Npad = round_up(self.Nout, 64)
+        # data-gradient launch: rows = forward input channels, K = taps * forward out channels
+        self.dtaps = 4 if transpose else self.taps
+        self.dK = self.dtaps * self.cout_s
+        self.dKpad = round_up(self.dK, 32)
+        # (+64 rows for concat inputs so the decoder-only row slice of a split data-gradient stays
+        #  a valid [Npad][Kpad] operand)
+        self.dNpad = round_up(self.Cin_s, 64) + (64 if len(self.cin_parts) > 1 else 0)
+
+    # -- parameter registration
+    def register(self, ps: ParamStore):
+        ps.add(self.name + "/W", (self.Npad, self.Kpad), init="glorot")
+        if self.bias:
+            ps.add(self.name + "/b", (self.cout_s,))
+        if self.bn:
+            ps.add(self.name + "/gamma", (self.cout_s,), init="ones")
+            ps.add(self.name + "/beta", (self.cout_s,))
+
+    def fan(self):
+        cin = sum(self.cin_parts)
+        if self.transpose:
+            return cin * 4, self.cout * 4   # torch-style fan for ConvTranspose (in*k*k, out*k*k)
+        return cin * self.taps, self.cout * self.taps
+
+    def keras_shapes(self):
+        cin = sum(self.cin_parts)
+        if self.transpose:  # torch ConvTranspose2d layout (Cin, Cout, 2, 2)
+            return (cin, self.cout, 2, 2), (self.cout,)
+        return (self.k, self.k, cin, self.cout), (self.cout,)
+
+    def _cmap(self):
+        """logical input channel -> packed input channel index"""
+        m = []
+        base = 0
+        for c, cs in zip(self.cin_parts, self.cin_s):
+            m.extend(range(base, base + c))
+            base += cs
+        return np.asarray(m)
+
+    def keras_to_packed(self, kernel):
+        kernel = np.asarray(kernel, dtype=np.float32)
+        Wp = np.zeros((self.Npad, self.Kpad), np.float32)
+        cm = self._cmap()
+        if self.transpose:
+            cin, cout = kernel.shape[:2]
+            for dy in range(2):
+                for dx in range(2):
+                    sub = dy * 2 + dx
+                    # Wp[sub*cout_s + co][ci] = kernel[ci, co, dy, dx]
+                    Wp[sub * self.cout_s: sub * self.cout_s + cout][:, cm] = kernel[:, :, dy, dx].T
+            return Wp
+        k = self.k
+        for ky in range(k):
+            for kx in range(k):
+                t = ky * k + kx
+                blk = kernel[ky, kx]  # (cin, cout)
+                Wp[: self.cout, t * self.Cin_s + cm] = blk.T
+        return Wp
+
+    def packed_to_keras(self, Wp):
+        Wp = np.asarray(Wp, dtype=np.float32)
+        cm = self._cmap()
+        kshape, _ = self.keras_shapes()
+        out = np.zeros(kshape, np.float32)
+        if self.transpose:
+            for dy in range(2):
+                for dx in range(2):
+                    sub = dy * 2 + dx
+                    out[:, :, dy, dx] = Wp[sub * self.cout_s: sub * self.cout_s + self.cout][:, cm].T
+            return out
+        k = self.k
+        for ky in range(k):
+            for kx in range(k):
+                t = ky * k + kx
+                out[ky, kx] = Wp[: self.cout, t * self.Cin_s + cm].T
+        return out
+
+
+class Head:
+    """1x1 conv head: softmax over 2 classes keeping class 1, or a 1-channel sigmoid."""
+
+    def __init__(self, name, cin, nout):
+        self.name, self.cin, self.nout = name, cin, nout
+
+    def register(self, ps):
+        ps.add(self.name + "/W", (self.nout, self.cin), init="glorot")
+        ps.add(self.name + "/b", (self.nout,))
+
+    def fan(self):
+        return self.cin, self.nout
+
+    def keras_shapes(self):
+        return (1, 1, self.cin, self.nout), (self.nout,)
+
+    def keras_to_packed(self, kernel):
+        return np.ascontiguousarray(np.asarray(kernel, np.float32)[0, 0].T)
+
+    def packed_to_keras(self, Wp):
+        return np.asarray(Wp, np.float32).T.reshape(1, 1, self.cin, self.nout)
+
+
+# ------------------------------------------------------------------------------ base engine
+class UNetEngine:
+    """Common machinery: params, per-step weight packing, Keras-name weight I/O, buffers."""
+
+    preset = None
+
+    def __init__(self, batch, size, *, dtype="bf16", device="cuda", seed=865):
+        self.B = batch
+        self.S = size
+        self.dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.dtype_name = dtype
+        self.device = torch.device(device)
+        self.seed = seed
+        self.ps = ParamStore()
+        self.layers = OrderedDict()
+        self.build_layers()
+        for l in self.layers.values():
+            l.register(self.ps)
+        self.ps.allocate(self.device)
+        self._packed = {}
+        self._bufs = {}
+        self.step_count = 0
+        self.init_weights(seed)
+
+    # -- to implement per preset
+    def build_layers(self):
+        raise NotImplementedError
+
+    # -- weights
+    def init_weights(self, seed):
+        """Keras defaults: glorot_uniform kernels, zero biases (BN: gamma 1, beta 0)."""
+        rng = np.random.default_rng(seed)
+        for l in self.layers.values():
+            fi, fo = l.fan()
+            lim = math.sqrt(6.0 / (fi + fo))
+            kshape, _ = l.keras_shapes()
+            kern = rng.uniform(-lim, lim, size=kshape).astype(np.float32)
+            self.set_layer_weights(l.name, [kern, np.zeros(l.keras_shapes()[1], np.float32)])
+            if isinstance(l, Dense) and l.bn:
+                self.ps.view(l.name + "/gamma")[: l.cout].fill_(1.0)
+
+    def set_layer_weights(self, name, arrays):
+        """Keras-style set: arrays = [kernel, bias] (bias optional for bias-free layers)."""
+        l = self.layers[name]
+        Wp = l.keras_to_packed(arrays[0])
+        self.ps.view(name + "/W").copy_(torch.from_numpy(Wp))
+        if len(arrays) > 1 and (getattr(l, "bias", True)) and (name + "/b") in self.ps.entries:
+            b = self.ps.view(name + "/b")
+            b.zero_()
+            b[: len(arrays[1])].copy_(torch.from_numpy(np.asarray(arrays[1], np.float32)))
+
+    def get_layer_weights(self, name):
+        l = self.layers[name]
+        Wp = self.ps.view(name + "/W").detach().cpu().numpy()
+        out = [l.packed_to_keras(Wp)]
+        if (name + "/b") in self.ps.entries:
+            nb = l.keras_shapes()[1][0]
+            out.append(self.ps.view(name + "/b").detach().cpu().numpy()[:nb].copy())
+        return out
+
+    def get_weights(self):
+        return OrderedDict((n, self.get_layer_weights(n)) for n in self.layers)
+
+    def set_weights(self, wd):
+        for n, arrs in wd.items():
+            if n in self.layers:
+                self.set_layer_weights(n, arrs)
+
+    def count_params(self):
+        tot = 0
+        for l in self.layers.values():
+            ks, bs = l.keras_shapes()
+            tot += int(np.prod(ks)) + (int(np.prod(bs)) if (l.name + "/b") in self.ps.entries else 0)
+            if isinstance(l, Dense) and l.bn:
+                tot += 2 * l.cout
+        return tot
+
+    # -- buffers
+    def buf(self, key, shape, dtype=None):
+        dtype = dtype or self.dt
+        t = self._bufs.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.zeros(shape, dtype=dtype, device=self.device)
+            self._bufs[key] = t
+        return t
+
+    def zero(self, t):
+        if t.dtype == torch.float32:
+            ops.fill(t, 0.0)
+        else:
+            ops.fill(t.view(torch.float32) if t.numel() % 2 == 0 else t, 0.0)
+
+    def pack_forward_weights(self):
+        """Per step: master f32 -> compute-dtype forward layout (cast) for every dense layer."""
+        for l in self.layers.values():
+            if not isinstance(l, Dense):
+                continue
+            src = self.ps.view(l.name + "/W")
+            if self.dt == torch.float32:
+                self._packed[l.name] = src
+            else:
+                dst = self.buf("wf/" + l.name, (l.Npad, l.Kpad))
+                ops.pack_weights(src, dst, 0)
+                self._packed[l.name] = dst
+
+    def pack_dgrad_weights(self, names):
+        for n in names:
+            l = self.layers[n]
+            src = self.ps.view(n + "/W")
+            dst = self.buf("wd/" + n, (l.dNpad, l.dKpad))
+            if l.transpose:
+                ops.pack_weights(src, dst, 2, taps=1, cin_s=l.Cin_s, nout=l.Nout)
+            else:
+                ops.pack_weights(src, dst, 1, taps=l.taps, cin_s=l.Cin_s, nout=l.cout_s)
+            self._packed["d/" + n] = dst
+
+    def Wf(self, name):
+        return self._packed[name]
+
+    def Wd(self, name):
+        return self._packed["d/" + name]
+
+    def bias(self, name):
+        key = name + "/b"
+        return self.ps.view(key) if key in self.ps.entries else None
+
+    # conv helpers -----------------------------------------------------------------------
+    def conv(self, l, srcA, out, *, srcB=None, bnA=None, bnB=None, dropout=0.0, seed=0, accum=None,
+             bn_stats=None):
+        if l.transpose:
+            return ops.conv_fwd(srcA, self.Wf(l.name), l.Nout, out=out, bias=self.bias(l.name), kh=1, kw=1,
+                                pad=0, bnA=bnA, out_mode=1, shuffle_c=l.cout_s)
+        return ops.conv_fwd(srcA, self.Wf(l.name), l.Nout, out=out, srcB=srcB, bnA=bnA, bnB=bnB,
+                            bias=self.bias(l.name) if l.bias else None, up=l.up, kh=l.k, kw=l.k, dil=l.dil,
+                            relu=l.relu and not l.bn, dropout_rate=dropout, dropout_seed=seed, accum=accum,
+                            bn_stats=bn_stats)
+
+    def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None):
+        dW = self.ps.gview(l.name + "/W")
+        dB = self.ps.gview(l.name + "/b") if (l.name + "/b") in self.ps.entries else None
+        if l.transpose:
+            ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, bnA=bnA, kh=1, kw=1, pad=0, shuffle_c=l.cout_s)
+        else:
+            ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, srcB=srcB, bnA=bnA, bnB=bnB, up=l.up, kh=l.k, kw=l.k,
+                           dil=l.dil)
+
+    def dgrad(self, l, dZ, out, *, Ho=None, Wo=None, addend=None, mask=None, mask_scale=1.0, split=False,
+              out2=None, mask2=None, mask2_scale=1.0, skip_first=False):
+        """Data gradient of a dense layer: a forward-shaped launch over dZ with repacked weights."""
+        Wd = self.Wd(l.name)
+        if l.transpose:
+            # input coord = 2*o + (dy,dx): 4 taps, stride 2, over the ConvT output gradient
+            return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=2, kw=2, dil=1, pad=0, stride=2,
+                                Ho=dZ.shape[1] // 2, Wo=dZ.shape[2] // 2, addend=addend, mask=mask,
+                                mask_scale=mask_scale)
+        # forward dilation d, 'same' padding: data gradient is the same gather with flipped taps
+        if split and skip_first:
+            # only the second (decoder) part of a concat input is needed: offset the weight rows
+            Wsub = Wd[l.cin_s[0]:]
+            return ops.conv_fwd(dZ, Wsub, l.cin_s[1], out=out2, kh=l.k, kw=l.k, dil=l.dil, mask=mask2,
+                                mask_scale=mask2_scale)
+        if split:
+            return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=l.k, kw=l.k, dil=l.dil, out_mode=2, out2=out2,
+                                split_c=l.cin_s[0], addend=addend, mask=mask, mask_scale=mask_scale,
+                                mask2=mask2, mask2_scale=mask2_scale)
+        return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=l.k, kw=l.k, dil=l.dil, addend=addend, mask=mask,
+                            mask_scale=mask_scale)
+
+
+# --------------------------------------------------------------------------------- adipose_v3
+class AdiposeV3Net(UNetEngine):
+    """AdiposeUNetV3 (train_adipose_unet_v3.py:660-758) generalised in the tile size S."""
+
+    preset = "adipose_v3"
+    ENCODER = ("down1_conv1", "down1_conv2", "down2_conv1", "down2_conv2", "down3_conv1", "down3_conv2")
+
+    def __init__(self, batch, size, *, dtype="bf16", device="cuda", seed=865, init_nb=44, dropout_rate=0.3,
+                 deep_supervision=True):
+        self.nb = init_nb
+        self.dropout_rate = dropout_rate
+        self.ds = deep_supervision
+        assert size % 8 == 0, "adipose_v3 needs S % 8 == 0 (3 poolings)"
+        super().__init__(batch, size, dtype=dtype, device=device, seed=seed)
+
+    def build_layers(self):
+        nb = self.nb
+        L = self.layers
+        L["down1_conv1"] = Dense("down1_conv1", [1], nb)
+        L["down1_conv2"] = Dense("down1_conv2", [nb], nb)
+        L["down2_conv1"] = Dense("down2_conv1", [nb], 2 * nb)
+        L["down2_conv2"] = Dense("down2_conv2", [2 * nb], 2 * nb)
+        L["down3_conv1"] = Dense("down3_conv1", [2 * nb], 4 * nb)
+        L["down3_conv2"] = Dense("down3_conv2", [4 * nb], 4 * nb)
+        for i, d in enumerate((1, 2, 4, 8, 16, 32)):
+            L[f"dilate{i + 1}"] = Dense(f"dilate{i + 1}", [4 * nb if i == 0 else 8 * nb], 8 * nb, dil=d)
+        L["up3_conv1"] = Dense("up3_conv1", [8 * nb], 4 * nb, up=True)
+        L["up3_conv2"] = Dense("up3_conv2", [4 * nb, 4 * nb], 4 * nb)
+        L["up3_conv3"] = Dense("up3_conv3", [4 * nb], 4 * nb)
+        L["up2_conv1"] = Dense("up2_conv1", [4 * nb], 2 * nb, up=True)
+        L["up2_conv2"] = Dense("up2_conv2", [2 * nb, 2 * nb], 2 * nb)
+        L["up2_conv3"] = Dense("up2_conv3", [2 * nb], 2 * nb)
+        L["up1_conv1"] = Dense("up1_conv1", [2 * nb], nb, up=True)
+        L["up1_conv2"] = Dense("up1_conv2", [nb, nb], nb)
+        L["up1_conv3"] = Dense("up1_conv3", [nb], nb)
+        if self.ds:
+            L["aux_out1"] = Head("aux_out1", 4 * nb, 1)
+            L["aux_out2"] = Head("aux_out2", 2 * nb, 1)
+        L["output_softmax"] = Head("output_softmax", nb, 2)
+
+    # -------------------------------------------------------------------------- forward
+    def alloc(self):
+        B, S, nb = self.B, self.S, self.nb
+        s = [S, S // 2, S // 4, S // 8]
+        c = [r8(nb), r8(2 * nb), r8(4 * nb), r8(8 * nb)]
+        a = {}
+        a["x"] = self.buf("x", (B, S, S, 8))
+        a["d1a"] = self.buf("d1a", (B, s[0], s[0], c[0]))
+        a["d1"] = self.buf("d1", (B, s[0], s[0], c[0]))
+        a["p1"] = self.buf("p1", (B, s[1], s[1], c[0]))
+        a["d2a"] = self.buf("d2a", (B, s[1], s[1], c[1]))
+        a["d2"] = self.buf("d2", (B, s[1], s[1], c[1]))
+        a["p2"] = self.buf("p2", (B, s[2], s[2], c[1]))
+        a["d3a"] = self.buf("d3a", (B, s[2], s[2], c[2]))
+        a["d3"] = self.buf("d3", (B, s[2], s[2], c[2]))
+        a["p3"] = self.buf("p3", (B, s[3], s[3], c[2]))
+        for i in range(1, 7):
+            a[f"dl{i}"] = self.buf(f"dl{i}", (B, s[3], s[3], c[3]))
+        a["dsum_f"] = self.buf("dsum_f", (B, s[3], s[3], c[3]), torch.float32)
+        a["dsum"] = a["dsum_f"] if self.dt == torch.float32 else self.buf("dsum", (B, s[3], s[3], c[3]))
+        for lvl, (sz, cc) in zip((3, 2, 1), ((s[2], c[2]), (s[1], c[1]), (s[0], c[0]))):
+            for j in ("a", "b", ""):
+                a[f"u{lvl}{j}"] = self.buf(f"u{lvl}{j}", (B, sz, sz, cc))
+        a["p_main"] = self.buf("p_main", (B, S, S), torch.float32)
+        if self.ds:
+            a["s_aux1"] = self.buf("s_aux1", (B, s[2], s[2]), torch.float32)
+            a["s_aux2"] = self.buf("s_aux2", (B, s[1], s[1]), torch.float32)
+            a["p_aux1"] = self.buf("p_aux1", (B, S, S), torch.float32)
+            a["p_aux2"] = self.buf("p_aux2", (B, S, S), torch.float32)
+        self.a = a
+        return a
+
+    def forward(self, x_prepped=None, *, train=False, seed=0):
+        """Run the network on self.a['x'] (NHWC, prepped). Returns dict of f32 probability maps."""
+        a = self.alloc() if not hasattr(self, "a") else self.a
+        if x_prepped is not None and x_prepped.data_ptr() != a["x"].data_ptr():
+            a["x"].copy_(x_prepped)
+        self.pack_forward_weights()
+        L = self.layers
+        r = self.dropout_rate if train else 0.0
+        sd = (seed * 7919 + 17) & 0xFFFFFFFF
+        self.conv(L["down1_conv1"], a["x"], a["d1a"])
+        self.conv(L["down1_conv2"], a["d1a"], a["d1"])
+        ops.maxpool2_fwd(a["d1"], a["p1"])
+        self.conv(L["down2_conv1"], a["p1"], a["d2a"])
+        self.conv(L["down2_conv2"], a["d2a"], a["d2"])
+        ops.maxpool2_fwd(a["d2"], a["p2"])
+        self.conv(L["down3_conv1"], a["p2"], a["d3a"])
+        self.conv(L["down3_conv2"], a["d3a"], a["d3"])
+        ops.maxpool2_fwd(a["d3"], a["p3"])
+        self.zero(a["dsum_f"])
+        self.conv(L["dilate1"], a["p3"], a["dl1"], dropout=r, seed=sd + 1, accum=a["dsum_f"])
+        for i in range(2, 7):
+            self.conv(L[f"dilate{i}"], a[f"dl{i - 1}"], a[f"dl{i}"], accum=a["dsum_f"])
+        if self.dt != torch.float32:
+            ops.cast(a["dsum_f"], a["dsum"])
+        self.conv(L["up3_conv1"], a["dsum"], a["u3a"])
+        self.conv(L["up3_conv2"], a["d3"], a["u3b"], srcB=a["u3a"])
+        self.conv(L["up3_conv3"], a["u3b"], a["u3"], dropout=r, seed=sd + 2)
+        self.conv(L["up2_conv1"], a["u3"], a["u2a"])
+        self.conv(L["up2_conv2"], a["d2"], a["u2b"], srcB=a["u2a"])
+        self.conv(L["up2_conv3"], a["u2b"], a["u2"], dropout=r, seed=sd + 3)
+        self.conv(L["up1_conv1"], a["u2"], a["u1a"])
+        self.conv(L["up1_conv2"], a["d1"], a["u1b"], srcB=a["u1a"])
+        self.conv(L["up1_conv3"], a["u1b"], a["u1"], dropout=r, seed=sd + 4)
+        h = L["output_softmax"]
+        ops.head_fwd(a["u1"], self.ps.view("output_softmax/W"), self.ps.view("output_softmax/b"), a["p_main"],
+                     cin=h.cin, softmax2=True)
+        out = {"main_out": a["p_main"]}
+        if self.ds:
+            for k, src, sb, pb in (("aux_out1", "u3", "s_aux1", "p_aux1"), ("aux_out2", "u2", "s_aux2", "p_aux2")):
+                hh = L[k]
+                ops.head_fwd(a[src], self.ps.view(k + "/W"), self.ps.view(k + "/b"), a[sb], cin=hh.cin,
+                             softmax2=False)
+                ops.resize_bilinear_fwd(a[sb], a[pb])
+                out[k] = a[pb]
+        self._train_fwd = train
+        return out
+
+    # ------------------------------------------------------------------------- backward
+    def trainable(self, name):
+        return not (self.frozen_encoder and name in self.ENCODER)
+
+    frozen_encoder = False
+
+    def backward(self, grads_out):
+        """grads_out: {'main_out': dL/dp (B,S,S) f32, 'aux_out1': ..., 'aux_out2': ...}.
+        Accumulates parameter gradients into self.ps.grad (caller zeroes)."""
+        a, L = self.a, self.layers
+        B, S = self.B, self.S
+        r = self.dropout_rate if self._train_fwd else 0.0
+        keep = 1.0 / (1.0 - r) if r > 0 else 1.0
+        full = not self.frozen_encoder
+        names = [n for n, l in L.items() if isinstance(l, Dense)]
+        self.pack_dgrad_weights([n for n in names if n != "down1_conv1" and (full or n not in self.ENCODER)
+                                 and (full or n != "dilate1")])
+        g = {}
+
+        def gb(key, like, dtype=None):
+            t = self.buf("g/" + key, tuple(like.shape), dtype or like.dtype)
+            return t
+
+        # heads
+        h = L["output_softmax"]
+        g["u1"] = gb("u1", a["u1"])
+        ops.head_bwd(a["u1"], self.ps.view("output_softmax/W"), a["p_main"], grads_out["main_out"],
+                     self.ps.gview("output_softmax/W"), self.ps.gview("output_softmax/b"), cin=h.cin, softmax2=True,
+                     dx=g["u1"], mask=a["u1"], mask_scale=keep)
+        aux_dx = {}
+        if self.ds:
+            for k, src, sb, pb in (("aux_out1", "u3", "s_aux1", "p_aux1"), ("aux_out2", "u2", "s_aux2", "p_aux2")):
+                hh = L[k]
+                ds = self.buf("g/" + sb, tuple(a[sb].shape), torch.float32)
+                ops.resize_bilinear_bwd(grads_out[k], ds)
+                dx = gb("aux/" + src, a[src])
+                ops.head_bwd(a[src], self.ps.view(k + "/W"), a[sb], ds, self.ps.gview(k + "/W"),
+                             self.ps.gview(k + "/b"), cin=hh.cin, softmax2=False, dx=dx)
+                aux_dx[src] = dx
+        # decoder level 1 (full resolution)
+        self._dec_level(1, g, "u1", "d1", aux_dx.get("u2"), keep, full)
+        self._dec_level(2, g, "u2", "d2", aux_dx.get("u3"), keep, full)
+        self._dec_level(3, g, "u3", "d3", None, keep, full)
+        # bottleneck: g['dsum'] = dL/d(sum) (no activation on the Add)
+        dsum = g["dsum"]
+        dz = gb("dz6", a["dl6"])
+        ops.add_mask(dsum, dz, mask=a["dl6"])
+        for i in range(6, 1, -1):
+            l = L[f"dilate{i}"]
+            self.wgrad(l, a[f"dl{i - 1}"], dz)
+            nz = gb(f"dz{i - 1}", a[f"dl{i - 1}"])
+            self.dgrad(l, dz, nz, addend=dsum, mask=a[f"dl{i - 1}"], mask_scale=keep if i == 2 else 1.0)
+            dz = nz
+        self.wgrad(L["dilate1"], a["p3"], dz)
+        if not full:
+            return
+        gp3 = gb("p3", a["p3"])
+        self.dgrad(L["dilate1"], dz, gp3)
+        # encoder: pool backward merges the concat-skip gradient and applies the ReLU mask
+        for lvl, pin in ((3, "p2"), (2, "p1"), (1, "x")):
+            dd = gb(f"d{lvl}", a[f"d{lvl}"])
+            ops.maxpool2_bwd(a[f"d{lvl}"], g[f"p{lvl}"] if lvl < 3 else gp3, dd, addend=g[f"skip{lvl}"],
+                             mask=a[f"d{lvl}"])
+            l2, l1 = L[f"down{lvl}_conv2"], L[f"down{lvl}_conv1"]
+            self.wgrad(l2, a[f"d{lvl}a"], dd)
+            dz1 = gb(f"d{lvl}a", a[f"d{lvl}a"])
+            self.dgrad(l2, dd, dz1, mask=a[f"d{lvl}a"])
+            self.wgrad(l1, a[pin], dz1)
+            if lvl > 1:
+                gp = gb(f"p{lvl - 1}", a[f"p{lvl - 1}"])
+                self.dgrad(l1, dz1, gp)
+                g[f"p{lvl - 1}"] = gp
+
+    def _dec_level(self, lvl, g, uname, dname, aux_add, keep, full):
+        """Backward through up{lvl}_conv3 / conv2 (concat) / conv1 (upsample)."""
+        a, L = self.a, self.layers
+        c3, c2, c1 = L[f"up{lvl}_conv3"], L[f"up{lvl}_conv2"], L[f"up{lvl}_conv1"]
+        if lvl == 1:
+            dz3 = g["u1"]          # head backward already applied the u1 ReLU/dropout mask
+        else:
+            dz3 = g[uname]
+        self.wgrad(c3, a[f"u{lvl}b"], dz3)
+        dz2 = self.buf(f"g/u{lvl}b", tuple(a[f"u{lvl}b"].shape))
+        self.dgrad(c3, dz3, dz2, mask=a[f"u{lvl}b"])
+        self.wgrad(c2, a[dname], dz2, srcB=a[f"u{lvl}a"])
+        dz1 = self.buf(f"g/u{lvl}a", tuple(a[f"u{lvl}a"].shape))
+        if full:
+            skip = self.buf(f"g/skip{lvl}", tuple(a[dname].shape))
+            self.dgrad(c2, dz2, skip, split=True, out2=dz1, mask2=a[f"u{lvl}a"])
+            g[f"skip{lvl}"] = skip
+        else:
+            self.dgrad(c2, dz2, None, split=True, skip_first=True, out2=dz1, mask2=a[f"u{lvl}a"])
+        # conv1 reads the nearest-upsampled source
+        src = {3: "dsum", 2: "u3", 1: "u2"}[lvl]
+        self.wgrad(c1, a[src], dz1)
+        Sup = a[f"u{lvl}a"].shape[1]
+        gup = self.buf(f"g/up{lvl}", (self.B, Sup, Sup, a[src].shape[3]))
+        self.dgrad(c1, dz1, gup)
+        dsrc = self.buf(f"g/{src}", tuple(a[src].shape))
+        if lvl == 3:
+            ops.upsample2_bwd(gup, dsrc)
+            g["dsum"] = dsrc
+        else:
+            ops.upsample2_bwd(gup, dsrc, addend=aux_add, mask=a[src], mask_scale=keep)
+            g[src] = dsrc
+
+
+# ------------------------------------------------------------------------------------ unet_bn
+class UNetBN(UNetEngine):
+    """North-star U-Net (BASELINE.json configs 2/3/5): L levels, base 64, Conv-BN-ReLU x2 blocks,
+    MaxPool 2x2, ConvTranspose 2x2/s2 + concat, 1x1 sigmoid head. BatchNorm uses batch statistics
+    in training (momentum 0.1, eps 1e-5, PyTorch semantics) and running statistics in eval."""
+
+    preset = "unet_bn"
+
+    def __init__(self, batch, size, *, levels=5, base=64, in_ch=3, dtype="bf16", device="cuda", seed=865,
+                 bn_eps=1e-5, bn_momentum=0.1):
+        self.levels = levels
+        self.base = base
+        self.in_ch = in_ch
+        self.bn_eps = bn_eps
+        self.bn_momentum = bn_momentum
+        assert size % (1 << (levels - 1)) == 0
+        super().__init__(batch, size, dtype=dtype, device=device, seed=seed)
+        self.running = {}
+        for n, l in self.layers.items():
+            if isinstance(l, Dense) and l.bn:
+                self.running[n] = (torch.zeros(l.cout_s, device=self.device),
+                                   torch.ones(l.cout_s, device=self.device))
+
+    def ch(self, i):
+        return self.base << i
+
+    def build_layers(self):
+        L = self.layers
+        Lv = self.levels
+        cin = self.in_ch
+        for i in range(Lv):
+            c = self.ch(i)
+            L[f"enc{i}_conv1"] = Dense(f"enc{i}_conv1", [cin], c, bias=False, bn=True)
+            L[f"enc{i}_conv2"] = Dense(f"enc{i}_conv2", [c], c, bias=False, bn=True)
+            cin = c
+        for i in range(Lv - 2, -1, -1):
+            c = self.ch(i)
+            L[f"dec{i}_up"] = Dense(f"dec{i}_up", [self.ch(i + 1)], c, transpose=True, relu=False)
+            L[f"dec{i}_conv1"] = Dense(f"dec{i}_conv1", [c, c], c, bias=False, bn=True)
+            L[f"dec{i}_conv2"] = Dense(f"dec{i}_conv2", [c], c, bias=False, bn=True)
+        L["head"] = Head("head", self.ch(0), 1)
+
+    def alloc(self):
+        B, S = self.B, self.S
+        a = {"x": self.buf("x", (B, S, S, 8))}
+        st = {}
+        for i in range(self.levels):
+            s, c = S >> i, self.ch(i)
+            a[f"z{i}_1"] = self.buf(f"z{i}_1", (B, s, s, c))
+            a[f"z{i}_2"] = self.buf(f"z{i}_2", (B, s, s, c))
+            if i < self.levels - 1:
+                a[f"pool{i}"] = self.buf(f"pool{i}", (B, s // 2, s // 2, c))
+                a[f"t{i}"] = self.buf(f"t{i}", (B, s, s, c))
+                a[f"y{i}_1"] = self.buf(f"y{i}_1", (B, s, s, c))
+                a[f"y{i}_2"] = self.buf(f"y{i}_2", (B, s, s, c))
+        a["p"] = self.buf("p", (B, S, S), torch.float32)
+        for n, l in self.layers.items():
+            if isinstance(l, Dense) and l.bn:
+                st[n] = self.buf("bnstat/" + n, (6, l.cout_s), torch.float32)  # sum,sq,scale,shift,mean,invstd
+        self.a, self.st = a, st
+        return a
+
+    def bnvec(self, name):
+        s = self.st[name]
+        return (s[2], s[3])
+
+    def _bn_conv(self, name, srcA, out, *, srcB=None, bnA=None, bnB=None, train=True):
+        l = self.layers[name]
+        s = self.st[name]
+        if train:
+            self.zero(s[:2])
+            self.conv(l, srcA, out, srcB=srcB, bnA=bnA, bnB=bnB, bn_stats=(s[0], s[1]))
+            count = out.shape[0] * out.shape[1] * out.shape[2]
+            rm, rv = self.running[name]
+            ops.bn_finalize(count, s[0], s[1], self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
+                            self.bn_eps, self.bn_momentum, s[2], s[3], s[4], s[5], rm, rv)
+        else:
+            self.conv(l, srcA, out, srcB=srcB, bnA=bnA, bnB=bnB)
+            rm, rv = self.running[name]
+            # eval: count < 0 -> (sum, sqsum) are read as (running mean, running var)
+            ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
+                            self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
+
+    def forward(self, x_prepped=None, *, train=False, seed=0):
+        a = self.alloc() if not hasattr(self, "a") else self.a
+        if x_prepped is not None and x_prepped.data_ptr() != a["x"].data_ptr():
+            a["x"].copy_(x_prepped)
+        self.pack_forward_weights()
+        Lv = self.levels
+        src, bn_in = a["x"], None
+        for i in range(Lv):
+            self._bn_conv(f"enc{i}_conv1", src, a[f"z{i}_1"], bnA=bn_in, train=train)
+            self._bn_conv(f"enc{i}_conv2", a[f"z{i}_1"], a[f"z{i}_2"], bnA=self.bnvec(f"enc{i}_conv1"), train=train)
+            if i < Lv - 1:
+                ops.maxpool2_fwd(a[f"z{i}_2"], a[f"pool{i}"], bn=self.bnvec(f"enc{i}_conv2"))
+                src, bn_in = a[f"pool{i}"], None
+        prev, prev_bn = a[f"z{Lv - 1}_2"], self.bnvec(f"enc{Lv - 1}_conv2")
+        for i in range(Lv - 2, -1, -1):
+            self.conv(self.layers[f"dec{i}_up"], prev, a[f"t{i}"], bnA=prev_bn)
+            self._bn_conv(f"dec{i}_conv1", a[f"z{i}_2"], a[f"y{i}_1"], srcB=a[f"t{i}"],
+                          bnA=self.bnvec(f"enc{i}_conv2"), train=train)
+            self._bn_conv(f"dec{i}_conv2", a[f"y{i}_1"], a[f"y{i}_2"], bnA=self.bnvec(f"dec{i}_conv1"), train=train)
+            prev, prev_bn = a[f"y{i}_2"], self.bnvec(f"dec{i}_conv2")
+        ops.head_fwd(prev, self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0), softmax2=False,
+                     bn=prev_bn)
+        self._train_fwd = train
+        return {"main_out": a["p"]}
+
+    def _bn_bwd(self, name, dA, z, dz):
+        """dA: gradient wrt relu(bn(z)) -> dz, and gamma/beta grads."""
+        s = self.st[name]
+        dg, db = self.ps.gview(name + "/gamma"), self.ps.gview(name + "/beta")
+        ops.bn_bwd_reduce(dA, z, s[2], s[3], s[4], s[5], dg, db)
+        count = z.shape[0] * z.shape[1] * z.shape[2]
+        ops.bn_bwd_apply(dA, z, s[2], s[3], s[4], s[5], self.ps.view(name + "/gamma"), dg, db, count, dz)
+
+    def backward(self, grads_out):
+        a, L = self.a, self.layers
+        Lv = self.levels
+        self.pack_dgrad_weights([n for n, l in L.items() if isinstance(l, Dense) and n != "enc0_conv1"])
+
+        def gb(key, like):
+            return self.buf("g/" + key, tuple(like.shape), like.dtype)
+
+        # head
+        dA = gb("y0_2", a["y0_2"])
+        ops.head_bwd(a["y0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"], self.ps.gview("head/W"),
+                     self.ps.gview("head/b"), cin=self.ch(0), softmax2=False, dx=dA, bn=self.bnvec("dec0_conv2"))
+        skip_grad = {}
+        cur_name, cur_z, cur_dA = "dec0_conv2", a["y0_2"], dA
+        # decoder from level 0 upward
+        for i in range(0, Lv - 1):
+            # dec{i}_conv2
+            dz = gb(f"dz_y{i}_2", a[f"y{i}_2"])
+            self._bn_bwd(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz)
+            l2 = L[f"dec{i}_conv2"]
+            self.wgrad(l2, a[f"y{i}_1"], dz, bnA=self.bnvec(f"dec{i}_conv1"))
+            dA1 = gb(f"dA_y{i}_1", a[f"y{i}_1"])
+            self.dgrad(l2, dz, dA1)
+            dz1 = gb(f"dz_y{i}_1", a[f"y{i}_1"])
+            self._bn_bwd(f"dec{i}_conv1", dA1, a[f"y{i}_1"], dz1)
+            l1 = L[f"dec{i}_conv1"]
+            self.wgrad(l1, a[f"z{i}_2"], dz1, srcB=a[f"t{i}"], bnA=self.bnvec(f"enc{i}_conv2"))
+            sk = gb(f"skip{i}", a[f"z{i}_2"])
+            dt = gb(f"dt{i}", a[f"t{i}"])
+            self.dgrad(l1, dz1, sk, split=True, out2=dt)
+            skip_grad[i] = sk
+            # ConvTranspose dec{i}_up: input = relu(bn(prev level output))
+            lu = L[f"dec{i}_up"]
+            if i + 1 < Lv - 1:
+                pz, pbn, pname = a[f"y{i + 1}_2"], self.bnvec(f"dec{i + 1}_conv2"), f"dec{i + 1}_conv2"
+            else:
+                pz, pbn, pname = a[f"z{Lv - 1}_2"], self.bnvec(f"enc{Lv - 1}_conv2"), f"enc{Lv - 1}_conv2"
+            self.wgrad(lu, pz, dt, bnA=pbn)
+            dAp = gb(f"dA_up{i}", pz)
+            self.dgrad(lu, dt, dAp)
+            if i + 1 < Lv - 1:
+                cur_dA = dAp
+            else:
+                bott_dA = dAp
+        # bottleneck + encoder, from the deepest level up to level 0
+        dA = bott_dA
+        for i in range(Lv - 1, -1, -1):
+            z2, z1 = a[f"z{i}_2"], a[f"z{i}_1"]
+            if i < Lv - 1:
+                # dA of enc{i}_conv2 = skip part + pool backward
+                dA2 = gb(f"dA_z{i}_2", z2)
+                ops.maxpool2_bwd(z2, dpool, dA2, bn=self.bnvec(f"enc{i}_conv2"), addend=skip_grad[i])
+            else:
+                dA2 = dA
+            dz2 = gb(f"dz_z{i}_2", z2)
+            self._bn_bwd(f"enc{i}_conv2", dA2, z2, dz2)
+            l2 = L[f"enc{i}_conv2"]
+            self.wgrad(l2, z1, dz2, bnA=self.bnvec(f"enc{i}_conv1"))
+            dA1 = gb(f"dA_z{i}_1", z1)
+            self.dgrad(l2, dz2, dA1)
+            dz1 = gb(f"dz_z{i}_1", z1)
+            self._bn_bwd(f"enc{i}_conv1", dA1, z1, dz1)
+            l1 = L[f"enc{i}_conv1"]
+            src = a["x"] if i == 0 else a[f"pool{i - 1}"]
+            self.wgrad(l1, src, dz1)
+            if i > 0:
+                dpool = gb(f"dpool{i - 1}", a[f"pool{i - 1}"])
+                self.dgrad(l1, dz1, dpool)

@@ -1,0 +1,374 @@
+"""Thin, shape-checked Python wrappers over the libadipose_hip C ABI.
+
+Tensors are torch device tensors used purely as memory (no torch compute runs on the hot path);
+every function here validates operand shapes on the host before launching, then calls exactly one
+C-ABI entry point on the current torch stream.
+
+Activation tensors are NHWC ``(N, H, W, Cs)`` with ``Cs % 8 == 0``; packed GEMM weights are
+``(Npad, Kpad)`` (see include/adipose_hip.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import BF16, F32, AdpError, ConvDesc, ConvIO, call, ptr, stream_ptr
+
+
+def round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+def dtype_code(t):
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.float32:
+        return F32
+    raise AdpError(f"unsupported dtype {t.dtype}")
+
+
+def _check(cond, msg):
+    if not cond:
+        raise AdpError(msg)
+
+
+def _act(t, name):
+    _check(t is not None and t.dim() == 4 and t.is_contiguous() and t.shape[3] % 8 == 0,
+           f"{name}: expected contiguous NHWC tensor with C%8==0, got "
+           f"{None if t is None else (tuple(t.shape), t.is_contiguous())}")
+    _check(t.is_cuda, f"{name}: must be a device tensor")
+
+
+def conv_geometry(Hs, Ws, *, up=False, stride=1, kh=3, kw=3, dil=1, pad=None, transpose_fwd=False):
+    """Output grid of a gather-conv launch (None pad -> 'same' for odd kernels)."""
+    if pad is None:
+        pad = dil * (kh // 2)
+    Hv, Wv = Hs * (2 if up else 1), Ws * (2 if up else 1)
+    Ho = (Hv + 2 * pad - dil * (kh - 1) - 1) // stride + 1
+    Wo = (Wv + 2 * pad - dil * (kw - 1) - 1) // stride + 1
+    return Ho, Wo, pad
+
+
+def _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo, nout):
+    _act(srcA, "srcA")
+    N, Hs, Ws, CA = srcA.shape
+    CB = 0
+    if srcB is not None:
+        _act(srcB, "srcB")
+        _check(tuple(srcB.shape[:3]) == (N, Hs, Ws) and srcB.dtype == srcA.dtype, "srcB shape/dtype mismatch")
+        CB = srcB.shape[3]
+    Ho_, Wo_, pad = conv_geometry(Hs, Ws, up=up, stride=stride, kh=kh, kw=kw, dil=dil, pad=pad)
+    Ho = Ho_ if Ho is None else Ho
+    Wo = Wo_ if Wo is None else Wo
+    K = kh * kw * (CA + CB)
+    Kpad = round_up(K, 32)
+    _check(W.dtype == srcA.dtype and W.is_contiguous() and W.dim() == 2, "W dtype/layout mismatch")
+    _check(W.shape[1] == Kpad and W.shape[0] >= round_up(nout, 64),
+           f"W shape {tuple(W.shape)} != (>= {round_up(nout, 64)}, {Kpad})")
+    d = ConvDesc()
+    d.N, d.Hs, d.Ws, d.CA_stride, d.CB_stride = N, Hs, Ws, CA, CB
+    d.upsample = 1 if up else 0
+    d.Ho, d.Wo, d.stride = Ho, Wo, stride
+    d.kh, d.kw, d.dil, d.pad = kh, kw, dil, pad
+    d.Nout = nout
+    d.mask_scale = 1.0
+    d.mask2_scale = 1.0
+    io = ConvIO()
+    io.srcA, io.srcB = ptr(srcA), ptr(srcB)
+    if bnA is not None:
+        _check(bnA[0].numel() >= CA and bnA[1].numel() >= CA, "bnA vectors too short")
+        io.bn_scaleA, io.bn_shiftA = ptr(bnA[0]), ptr(bnA[1])
+    if bnB is not None:
+        _check(bnB[0].numel() >= CB and bnB[1].numel() >= CB, "bnB vectors too short")
+        io.bn_scaleB, io.bn_shiftB = ptr(bnB[0]), ptr(bnB[1])
+    io.W = ptr(W)
+    if bias is not None:
+        _check(bias.dtype == torch.float32, "bias must be f32")
+        io.bias = ptr(bias)
+    return d, io, N, Ho, Wo
+
+
+def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=None, up=False, stride=1,
+             kh=3, kw=3, dil=1, pad=None, Ho=None, Wo=None, relu=False, dropout_rate=0.0, dropout_seed=0,
+             out_mode=0, shuffle_c=0, out2=None, split_c=0, addend=None, mask=None, mask_scale=1.0,
+             mask2=None, mask2_scale=1.0, accum=None, bn_stats=None):
+    """Implicit-GEMM conv forward-shaped launch (conv, conv dgrad, convT fwd/dgrad)."""
+    d, io, N, Ho, Wo = _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo, nout)
+    d.relu = 1 if relu else 0
+    d.dropout_rate = float(dropout_rate)
+    d.dropout_seed = int(dropout_seed) & 0xFFFFFFFF
+    d.out_mode = out_mode
+    if out_mode == 1:
+        _check(shuffle_c > 0 and nout % shuffle_c == 0, "pixel-shuffle needs nout % shuffle_c == 0")
+        _check(out is not None and tuple(out.shape[:3]) == (N, 2 * Ho, 2 * Wo) and out.shape[3] >= shuffle_c,
+               "convT output shape mismatch")
+        d.shuffle_c = shuffle_c
+    elif out_mode == 2:
+        _check(out2 is not None and 0 < split_c < nout, "split store needs out2 and 0<split_c<nout")
+        _act(out2, "out2")
+        _check(tuple(out2.shape[:3]) == (N, Ho, Wo) and out2.shape[3] >= nout - split_c, "out2 shape mismatch")
+        d.out2_stride, d.split_c = out2.shape[3], split_c
+        io.out2 = ptr(out2)
+        if mask2 is not None:
+            _check(tuple(mask2.shape[:3]) == (N, Ho, Wo), "mask2 shape mismatch")
+            d.mask2_stride, d.mask2_scale = mask2.shape[3], float(mask2_scale)
+            io.mask2 = ptr(mask2)
+    if out is not None:
+        _act(out, "out")
+        _check(out.dtype == srcA.dtype, "out dtype mismatch")
+        if out_mode != 1:
+            _check(tuple(out.shape[:3]) == (N, Ho, Wo), f"out shape {tuple(out.shape)} != {(N, Ho, Wo)}")
+            _check(out.shape[3] >= (split_c if out_mode == 2 else nout), "out has too few channels")
+        d.out_stride = out.shape[3]
+        io.out = ptr(out)
+    else:
+        _check(out_mode == 2, "out may only be omitted for a split store")
+    if addend is not None:
+        _check(addend.shape == out.shape and addend.dtype == out.dtype, "addend must match out")
+        io.addend = ptr(addend)
+    if mask is not None:
+        _check(tuple(mask.shape[:3]) == (N, Ho, Wo) and mask.dtype == srcA.dtype, "mask shape mismatch")
+        d.mask_stride, d.mask_scale = mask.shape[3], float(mask_scale)
+        io.mask = ptr(mask)
+    if accum is not None:
+        _check(accum.dtype == torch.float32 and tuple(accum.shape[:3]) == (N, Ho, Wo), "accum must be f32 NHWC")
+        d.accum_stride = accum.shape[3]
+        io.accum = ptr(accum)
+    if bn_stats is not None:
+        io.bn_sum, io.bn_sqsum = ptr(bn_stats[0]), ptr(bn_stats[1])
+    call("adp_conv_fwd", dtype_code(srcA), C.byref(d), C.byref(io), stream_ptr())
+    return out
+
+
+def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up=False, stride=1, kh=3, kw=3,
+               dil=1, pad=None, Ho=None, Wo=None, shuffle_c=0):
+    """dW (+)= X_tap^T dY (f32 accumulators, caller zeroes). shuffle_c>0: dY is a ConvT output."""
+    Wdummy = torch.empty(0)
+    _act(srcA, "srcA")
+    _act(dY, "dY")
+    N, Hs, Ws, CA = srcA.shape
+    CB = 0 if srcB is None else srcB.shape[3]
+    K = kh * kw * (CA + CB)
+    Kpad = round_up(K, 32)
+    _check(dW.dtype == torch.float32 and dW.is_contiguous() and dW.dim() == 2, "dW must be f32 2-D")
+    _check(dW.shape[1] == Kpad and dW.shape[0] >= nout, f"dW shape {tuple(dW.shape)} != (>={nout}, {Kpad})")
+    _check(nout % 8 == 0, "wgrad needs nout % 8 == 0")
+    d = ConvDesc()
+    io = ConvIO()
+    Ho_, Wo_, pad = conv_geometry(Hs, Ws, up=up, stride=stride, kh=kh, kw=kw, dil=dil, pad=pad)
+    Ho = Ho_ if Ho is None else Ho
+    Wo = Wo_ if Wo is None else Wo
+    d.N, d.Hs, d.Ws, d.CA_stride, d.CB_stride = N, Hs, Ws, CA, CB
+    d.upsample = 1 if up else 0
+    d.Ho, d.Wo, d.stride, d.kh, d.kw, d.dil, d.pad = Ho, Wo, stride, kh, kw, dil, pad
+    d.Nout = nout
+    if shuffle_c:
+        d.out_mode, d.shuffle_c = 1, shuffle_c
+        _check(tuple(dY.shape[:3]) == (N, 2 * Ho, 2 * Wo), "convT dY shape mismatch")
+    else:
+        _check(tuple(dY.shape[:3]) == (N, Ho, Wo) and dY.shape[3] >= nout, "dY shape mismatch")
+    io.srcA, io.srcB = ptr(srcA), ptr(srcB)
+    if bnA is not None:
+        io.bn_scaleA, io.bn_shiftA = ptr(bnA[0]), ptr(bnA[1])
+    if bnB is not None:
+        io.bn_scaleB, io.bn_shiftB = ptr(bnB[0]), ptr(bnB[1])
+    if dB is not None:
+        _check(dB.dtype == torch.float32, "dB must be f32")
+    del Wdummy
+    call("adp_conv_wgrad", dtype_code(srcA), C.byref(d), C.byref(io), ptr(dY), int(dY.shape[3]), ptr(dW),
+         ptr(dB), stream_ptr())
+
+
+def pack_weights(src, dst, mode, *, taps=1, cin_s=0, nout=0):
+    """mode 0: cast/copy [Npad][Kpad]; mode 1: conv dgrad flip+transpose; mode 2: convT transpose."""
+    _check(src.dtype == torch.float32 and src.dim() == 2 and dst.dim() == 2, "pack_weights: bad tensors")
+    if mode == 0:
+        _check(dst.shape == src.shape, "pack mode 0 needs equal shapes")
+    else:
+        _check(dst.shape[0] >= cin_s and dst.shape[1] >= taps * nout and src.shape[0] >= nout
+               and src.shape[1] >= taps * cin_s, "pack_weights: shape mismatch")
+    call("adp_pack_weights", dtype_code(dst), mode, taps, cin_s, nout, ptr(src), int(src.shape[1]), ptr(dst),
+         int(dst.shape[0]), int(dst.shape[1]), stream_ptr())
+
+
+def maxpool2_fwd(src, dst, bn=None):
+    _act(src, "src")
+    _act(dst, "dst")
+    N, H, W, Cs = src.shape
+    _check(tuple(dst.shape) == (N, H // 2, W // 2, Cs) and dst.dtype == src.dtype, "maxpool dst shape")
+    call("adp_maxpool2_fwd", dtype_code(src), N, H, W, Cs, ptr(src), ptr(bn[0]) if bn else None,
+         ptr(bn[1]) if bn else None, ptr(dst), stream_ptr())
+    return dst
+
+
+def maxpool2_bwd(src, dpool, dsrc, *, bn=None, addend=None, mask=None, mask_scale=1.0):
+    _act(src, "src")
+    N, H, W, Cs = src.shape
+    _check(tuple(dpool.shape) == (N, H // 2, W // 2, Cs), "dpool shape")
+    _check(dsrc.shape == src.shape, "dsrc shape")
+    for t in (addend, mask):
+        _check(t is None or t.shape == src.shape, "addend/mask shape")
+    call("adp_maxpool2_bwd", dtype_code(src), N, H, W, Cs, ptr(src), ptr(bn[0]) if bn else None,
+         ptr(bn[1]) if bn else None, ptr(dpool), ptr(addend), ptr(mask), float(mask_scale), ptr(dsrc), stream_ptr())
+    return dsrc
+
+
+def upsample2_bwd(dup, dsrc, *, addend=None, mask=None, mask_scale=1.0):
+    _act(dup, "dup")
+    _act(dsrc, "dsrc")
+    N, Hs, Ws, Cs = dsrc.shape
+    _check(tuple(dup.shape) == (N, 2 * Hs, 2 * Ws, Cs), "upsample grad shapes")
+    for t in (addend, mask):
+        _check(t is None or t.shape == dsrc.shape, "addend/mask shape")
+    call("adp_upsample2_bwd", dtype_code(dup), N, Hs, Ws, Cs, ptr(dup), ptr(addend), ptr(mask), float(mask_scale),
+         ptr(dsrc), stream_ptr())
+    return dsrc
+
+
+def add_mask(a, out, *, b=None, mask=None, mask_scale=1.0):
+    _check(out.shape == a.shape and a.numel() % 8 == 0, "add_mask shapes")
+    for t in (b, mask):
+        _check(t is None or t.shape == a.shape, "add_mask operand shape")
+    call("adp_ew_add_mask", dtype_code(a), a.numel(), ptr(a), ptr(b), ptr(mask), float(mask_scale), ptr(out),
+         stream_ptr())
+    return out
+
+
+def cast(src, dst):
+    _check(src.numel() == dst.numel(), "cast sizes")
+    call("adp_cast", dtype_code(src), dtype_code(dst), src.numel(), ptr(src), ptr(dst), stream_ptr())
+    return dst
+
+
+def fill(dst, value):
+    _check(dst.dtype == torch.float32, "fill is f32")
+    call("adp_fill_f32", dst.numel(), float(value), ptr(dst), stream_ptr())
+
+
+def bn_finalize(count, ssum, ssq, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean=None, rvar=None):
+    C_ = gamma.numel()
+    call("adp_bn_finalize", C_, float(count), ptr(ssum), ptr(ssq), ptr(gamma), ptr(beta), float(eps),
+         float(momentum), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), ptr(rmean), ptr(rvar), stream_ptr())
+
+
+def bn_bwd_reduce(dA, z, scale, shift, mean, invstd, dgamma, dbeta):
+    _check(dA.shape == z.shape, "bn bwd shapes")
+    Cs = z.shape[-1]
+    M = z.numel() // Cs
+    call("adp_bn_bwd_reduce", dtype_code(z), M, Cs, ptr(dA), ptr(z), ptr(scale), ptr(shift), ptr(mean),
+         ptr(invstd), ptr(dgamma), ptr(dbeta), stream_ptr())
+
+
+def bn_bwd_apply(dA, z, scale, shift, mean, invstd, gamma, dgamma, dbeta, count, dz):
+    _check(dA.shape == z.shape == dz.shape, "bn bwd shapes")
+    Cs = z.shape[-1]
+    M = z.numel() // Cs
+    call("adp_bn_bwd_apply", dtype_code(z), M, Cs, ptr(dA), ptr(z), ptr(scale), ptr(shift), ptr(mean),
+         ptr(invstd), ptr(gamma), ptr(dgamma), ptr(dbeta), float(count), ptr(dz), stream_ptr())
+
+
+def head_fwd(x, W, b, p, *, cin, softmax2, bn=None):
+    _act(x, "x")
+    Cs = x.shape[-1]
+    M = x.numel() // Cs
+    _check(p.numel() == M and p.dtype == torch.float32, "head output size")
+    _check(W.numel() == (2 if softmax2 else 1) * cin and cin <= Cs, "head weight size")
+    name = "adp_head_softmax2_fwd" if softmax2 else "adp_head_sigmoid_fwd"
+    call(name, dtype_code(x), M, Cs, cin, ptr(x), ptr(W), ptr(b), ptr(bn[0]) if bn else None,
+         ptr(bn[1]) if bn else None, ptr(p), stream_ptr())
+    return p
+
+
+def head_bwd(x, W, p, dp, dW, db, *, cin, softmax2, dx=None, bn=None, addend=None, mask=None, mask_scale=1.0):
+    _act(x, "x")
+    Cs = x.shape[-1]
+    M = x.numel() // Cs
+    _check(p.numel() == M and dp.numel() == M, "head grad sizes")
+    for t in (dx, addend, mask):
+        _check(t is None or t.shape == x.shape, "head dx/addend/mask shape")
+    name = "adp_head_softmax2_bwd" if softmax2 else "adp_head_sigmoid_bwd"
+    call(name, dtype_code(x), M, Cs, cin, ptr(x), ptr(W), ptr(bn[0]) if bn else None, ptr(bn[1]) if bn else None,
+         ptr(p), ptr(dp), ptr(addend), ptr(mask), float(mask_scale), ptr(dx), ptr(dW), ptr(db), stream_ptr())
+
+
+def resize_bilinear_fwd(src, dst):
+    N, Hs, Ws = src.shape
+    _, Ho, Wo = dst.shape
+    _check(dst.shape[0] == N and src.dtype == dst.dtype == torch.float32, "resize shapes")
+    call("adp_resize_bilinear_fwd", N, Hs, Ws, Ho, Wo, ptr(src), ptr(dst), stream_ptr())
+    return dst
+
+
+def resize_bilinear_bwd(dout, dsrc):
+    N, Ho, Wo = dout.shape
+    _, Hs, Ws = dsrc.shape
+    call("adp_resize_bilinear_bwd", N, Hs, Ws, Ho, Wo, ptr(dout), ptr(dsrc), stream_ptr())
+    return dsrc
+
+
+def loss_rows(p, y, row_bce, stats, *, smooth=False, eps_pos=0.03, eps_neg=0.07):
+    N, H, W = p.shape
+    _check(y.shape == p.shape and row_bce.numel() == N * H and stats.dtype == torch.float64, "loss_rows shapes")
+    call("adp_loss_rows", N, H, W, ptr(p), ptr(y), int(smooth), float(eps_pos), float(eps_neg), ptr(row_bce),
+         ptr(stats), stream_ptr())
+
+
+def loss_select(row_bce, row_coef, out, *, N, H, W, ohem, keep_ratio, weight, norm_rows):
+    call("adp_loss_select", N, H, W, ptr(row_bce), int(ohem), float(keep_ratio), float(weight), float(norm_rows),
+         ptr(row_coef), ptr(out), stream_ptr())
+
+
+def loss_grad(p, y, row_coef, stats, dp, *, weight, smooth=False, eps_pos=0.03, eps_neg=0.07, accumulate=False):
+    N, H, W = p.shape
+    call("adp_loss_grad", N, H, W, ptr(p), ptr(y), int(smooth), float(eps_pos), float(eps_neg), ptr(row_coef),
+         ptr(stats), float(weight), int(accumulate), ptr(dp), stream_ptr())
+
+
+def pixel_counts(pred, truth, thr, counts):
+    _check(pred.numel() == truth.numel() and counts.dtype == torch.int64 and counts.numel() >= 4, "counts")
+    call("adp_pixel_counts", pred.numel(), ptr(pred), ptr(truth), float(thr), ptr(counts), stream_ptr())
+
+
+def adam(param, grad, m, v, *, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_scale=1.0):
+    n = param.numel()
+    _check(grad.numel() == n and m.numel() == n and v.numel() == n, "adam sizes")
+    call("adp_adam", n, ptr(param), ptr(grad), ptr(m), ptr(v), float(lr), float(beta1), float(beta2), float(eps),
+         int(step), float(weight_decay), float(grad_scale), stream_ptr())
+
+
+def ema(ema_buf, param, decay):
+    call("adp_ema", param.numel(), ptr(ema_buf), ptr(param), float(decay), stream_ptr())
+
+
+def prep_input(src, dst, *, mean, std, view=0):
+    """src f32 (N,H,W) or (N,H,W,C) raw intensities -> dst NHWC normalised (pad channels zero)."""
+    if src.dim() == 3:
+        N, H, W = src.shape
+        Cin = 1
+    else:
+        N, H, W, Cin = src.shape
+    _check(src.dtype == torch.float32 and src.is_contiguous(), "prep src must be contiguous f32")
+    _check(tuple(dst.shape[:3]) == (N, H, W) and dst.shape[3] >= Cin, "prep dst shape")
+    call("adp_prep_input", dtype_code(dst), N, H, W, Cin, ptr(src), float(mean), float(std), int(view),
+         int(dst.shape[3]), ptr(dst), stream_ptr())
+    return dst
+
+
+def tta_merge(probs, views, out):
+    nv, H, W = probs.shape
+    arr = (C.c_int * 8)(*list(views) + [0] * (8 - len(views)))
+    call("adp_tta_merge", H, W, nv, arr, ptr(probs), ptr(out), stream_ptr())
+    return out
+
+
+def blend_accum(tile, weight, acc, wsum, y0, x0):
+    H, W = acc.shape
+    T = tile.shape[-1]
+    _check(y0 + T <= H and x0 + T <= W, "tile outside the canvas")
+    call("adp_blend_accum", H, W, T, int(y0), int(x0), ptr(tile), ptr(weight), ptr(acc), ptr(wsum), stream_ptr())
+
+
+def blend_finalize(acc, wsum, out, floor_=1e-8):
+    call("adp_blend_finalize", acc.numel(), ptr(acc), ptr(wsum), float(floor_), ptr(out), stream_ptr())
+    return out

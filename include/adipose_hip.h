@@ -1,0 +1,186 @@
+/*
+ * libadipose_hip — C ABI of the MI355X-native adipose U-Net hot path (gfx950 / CDNA4).
+ *
+ * The reference (MAGIC-SCAN/adipose_tissue-unet, TF 2.13 / Keras 2.13) has no FFI: its hot path is
+ * the Keras graph built by AdiposeUNetV3.build_model (Segmentation/train_adipose_unet_v3.py:660-758)
+ * plus the loss callables (:217-363), executed by TF/cuDNN. Each entry point below replaces one of
+ * those implicit TF ops; the reference line it stands in for is cited on each declaration.
+ *
+ * Conventions
+ *   - Every call returns 0 on success, <0 on error; adp_last_error() returns a thread-local message.
+ *   - Pointers are DEVICE pointers unless stated; the caller owns every buffer.
+ *   - Calls are asynchronous on the given hipStream_t (passed as void* so the header needs no HIP
+ *     include) and never allocate, free or synchronise (safe to capture in a hipGraph).
+ *   - dtype: ADP_DTYPE_F32 (parity path, exact f32 MFMA) or ADP_DTYPE_BF16 (throughput path,
+ *     f32 accumulation). Activations are NHWC with channel stride a multiple of 8.
+ *   - GEMM weights are packed [Npad][Kpad] (output-channel major, K = taps*Cin_stride contiguous,
+ *     Kpad = round_up(K,32), Npad = round_up(N,64)); tap order is row-major over (ky,kx).
+ */
+#ifndef ADIPOSE_HIP_H
+#define ADIPOSE_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADP_DTYPE_F32 0
+#define ADP_DTYPE_BF16 1
+#define ADP_ABI_VERSION 1
+
+typedef void* adp_stream_t; /* hipStream_t */
+
+/* Geometry + epilogue of one implicit-GEMM convolution launch. */
+typedef struct adp_conv_desc {
+  int N, Hs, Ws;            /* source tensor(s) batch and spatial dims */
+  int CA_stride, CB_stride; /* channel strides of source A / B (B = concat partner, 0 if none) */
+  int upsample;             /* 1: nearest x2 upsample folded into the gather (UpSampling2D) */
+  int Ho, Wo, stride;       /* output grid; input coord = o*stride + tap*dil - pad */
+  int kh, kw, dil, pad;     /* tap grid */
+  int Nout;                 /* GEMM N: output channels (padded) or 4*C for ConvTranspose */
+  int relu;                 /* ReLU in the epilogue */
+  float dropout_rate;       /* >0: inverted dropout after ReLU, stateless hash mask */
+  unsigned dropout_seed;
+  int out_stride;           /* channel stride of out */
+  int out_mode;             /* 0 plain, 1 pixel-shuffle 2x2 (ConvTranspose), 2 channel split */
+  int shuffle_c;            /* out_mode 1: channels per sub-pixel */
+  int out2_stride, split_c; /* out_mode 2: channels >= split_c go to out2 */
+  int mask_stride;          /* out = (acc [+addend]) * (mask>0) * mask_scale */
+  float mask_scale;
+  int mask2_stride;         /* same for the out2 part of a split store */
+  float mask2_scale;
+  int accum_stride;         /* accum (f32) += stored value */
+} adp_conv_desc;
+
+typedef struct adp_conv_io {
+  const void* srcA;
+  const void* srcB;
+  const float* bn_scaleA; /* optional BatchNorm-apply + ReLU on load: x' = max(x*scale+shift, 0) */
+  const float* bn_shiftA;
+  const float* bn_scaleB;
+  const float* bn_shiftB;
+  const void* W;     /* packed weights, dtype of the launch */
+  const float* bias; /* [Nout] or NULL */
+  void* out;
+  void* out2;
+  const void* addend;
+  const void* mask;
+  const void* mask2;
+  float* accum;
+  float* bn_sum;     /* per-channel sum / sum of squares of the output (atomics), or NULL */
+  float* bn_sqsum;
+} adp_conv_io;
+
+/* ---- library ---------------------------------------------------------------------------- */
+const char* adp_last_error(void);
+int adp_abi_version(void);
+
+/* ---- dense layers (replace Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter / BiasAdd /
+ *      Relu / ResizeNearestNeighbor / ConcatV2 / AddN / Dropout of
+ *      Segmentation/train_adipose_unet_v3.py:668-710, and ConvTranspose2D of the unet_bn preset) */
+int adp_conv_fwd(int dtype, const adp_conv_desc* d, const adp_conv_io* io, adp_stream_t s);
+/* dW[Npad][Kpad] (+)= sum_m dY[m][n] * X_tap(k)[m]; dB[n] (+)= sum_m dY[m][n]. f32 accumulators,
+ * caller zeroes them. The gather is described by d/io exactly as for the forward launch. */
+int adp_conv_wgrad(int dtype, const adp_conv_desc* d, const adp_conv_io* io, const void* dY,
+                   int dy_stride, float* dW, float* dB, adp_stream_t s);
+
+/* Repack f32 master weights into the launch layout: mode 0 = cast only (forward);
+ * mode 1 = 3x3 flip+transpose (data-gradient of a conv), mode 2 = ConvTranspose transpose. */
+int adp_pack_weights(int dtype_out, int mode, int taps, int Cin_s, int Nout, const float* src,
+                     int src_kpad, void* dst, int dst_rows, int dst_kpad, adp_stream_t s);
+
+/* ---- pooling / upsampling (MaxPooling2D :670,674,678; UpSampling2D grad) ------------------- */
+int adp_maxpool2_fwd(int dtype, int N, int H, int W, int C_stride, const void* src,
+                     const float* bn_scale, const float* bn_shift, void* dst, adp_stream_t s);
+int adp_maxpool2_bwd(int dtype, int N, int H, int W, int C_stride, const void* src,
+                     const float* bn_scale, const float* bn_shift, const void* dpool,
+                     const void* addend, const void* mask, float mask_scale, void* dsrc,
+                     adp_stream_t s);
+int adp_upsample2_bwd(int dtype, int N, int Hs, int Ws, int C_stride, const void* dup,
+                      const void* addend, const void* mask, float mask_scale, void* dsrc,
+                      adp_stream_t s);
+/* out = (a [+ b]) * (mask>0 ? mask_scale : 0) [mask optional]; elementwise over n elements */
+int adp_ew_add_mask(int dtype, size_t n, const void* a, const void* b, const void* mask,
+                    float mask_scale, void* out, adp_stream_t s);
+int adp_cast(int dtype_in, int dtype_out, size_t n, const void* src, void* dst, adp_stream_t s);
+int adp_fill_f32(size_t n, float value, float* dst, adp_stream_t s);
+
+/* ---- BatchNorm (unet_bn preset; training-mode batch statistics) -------------------------- */
+int adp_bn_finalize(int C, float count, const float* sum, const float* sqsum, const float* gamma,
+                    const float* beta, float eps, float momentum, float* scale, float* shift,
+                    float* mean, float* invstd, float* running_mean, float* running_var,
+                    adp_stream_t s);
+/* dBN = dA * (relu(z*scale+shift) > 0); dgamma += sum dBN*xhat; dbeta += sum dBN */
+int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, const void* z, const float* scale,
+                      const float* shift, const float* mean, const float* invstd, float* dgamma,
+                      float* dbeta, adp_stream_t s);
+int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, const void* z, const float* scale,
+                     const float* shift, const float* mean, const float* invstd,
+                     const float* gamma, const float* dgamma, const float* dbeta, float count,
+                     void* dz, adp_stream_t s);
+
+/* ---- heads (Conv2D(2,1,softmax)[...,1] :729-731; Conv2D(1,1,sigmoid) :715,722) ------------- */
+/* p = softmax(W x + b)[1] = sigmoid(z1 - z0); W f32 [2][Cin], b f32 [2] */
+int adp_head_softmax2_fwd(int dtype, size_t M, int C_stride, int Cin, const void* x, const float* W,
+                          const float* b, const float* bn_scale, const float* bn_shift, float* p,
+                          adp_stream_t s);
+int adp_head_softmax2_bwd(int dtype, size_t M, int C_stride, int Cin, const void* x, const float* W,
+                          const float* bn_scale, const float* bn_shift, const float* p,
+                          const float* dp, const void* addend, const void* mask, float mask_scale,
+                          void* dx, float* dW, float* db, adp_stream_t s);
+/* p = sigmoid(W x + b); W f32 [Cin], b f32 [1] */
+int adp_head_sigmoid_fwd(int dtype, size_t M, int C_stride, int Cin, const void* x, const float* W,
+                         const float* b, const float* bn_scale, const float* bn_shift, float* p,
+                         adp_stream_t s);
+int adp_head_sigmoid_bwd(int dtype, size_t M, int C_stride, int Cin, const void* x, const float* W,
+                         const float* bn_scale, const float* bn_shift, const float* p,
+                         const float* dp, const void* addend, const void* mask, float mask_scale,
+                         void* dx, float* dW, float* db, adp_stream_t s);
+/* tf.image.resize(..., method='bilinear') (half-pixel centres, no antialias), 1 channel, f32
+ * (:716-719, :723-726) and its adjoint. */
+int adp_resize_bilinear_fwd(int N, int Hs, int Ws, int Ho, int Wo, const float* src, float* dst,
+                            adp_stream_t s);
+int adp_resize_bilinear_bwd(int N, int Hs, int Ws, int Ho, int Wo, const float* dout, float* dsrc,
+                            adp_stream_t s);
+
+/* ---- losses & metrics (dice_loss / combined_loss_* / OHEM :217-363; dice_coef model.py:93-98) */
+/* stats[0..6] += {sum y*p', sum y, sum p', sum y*p, sum y, sum p (raw y, p), #((p>0.5)==y)} where
+ * p' = clip(p,1e-7,1-1e-7) and y is the (optionally smoothed) label; row_bce[b*H+h] = mean_w BCE. */
+int adp_loss_rows(int N, int H, int W, const float* p, const float* y, int smooth, float eps_pos,
+                  float eps_neg, float* row_bce, double* stats, adp_stream_t s);
+/* One block per image: selects rows (OHEM top-k with k = int(H*keep_ratio) or all rows), writes
+ * row_coef[b*H+h] = weight/(norm_rows*W) for selected rows else 0, and out[0] += weight*bce_part,
+ * with norm_rows the GLOBAL number of selected rows (all ranks). */
+int adp_loss_select(int N, int H, int W, const float* row_bce, int ohem, float keep_ratio,
+                    float weight, float norm_rows, float* row_coef, double* out, adp_stream_t s);
+/* dp (+)= row_coef*dBCE/dp + weight*dDice/dp (through the clip), given GLOBAL dice stats. */
+int adp_loss_grad(int N, int H, int W, const float* p, const float* y, int smooth, float eps_pos,
+                  float eps_neg, const float* row_coef, const double* stats, float weight,
+                  int accumulate, float* dp, adp_stream_t s);
+/* tp, fp, fn, tn of (pred>thr) vs (true>0.5) (full_evaluation_enhanced.py:721-785), int64 out */
+int adp_pixel_counts(size_t n, const float* pred, const float* truth, float thr,
+                     unsigned long long* counts, adp_stream_t s);
+
+/* ---- optimizer (Keras Adam / AdamW, :800-806) --------------------------------------------- */
+int adp_adam(size_t n, float* param, const float* grad, float* m, float* v, float lr, float beta1,
+             float beta2, float eps, int step, float weight_decay, float grad_scale, adp_stream_t s);
+int adp_ema(size_t n, float* ema, const float* param, float decay, adp_stream_t s);
+
+/* ---- input / inference plumbing (predict_single :153-158, TTA :181-229, SW/blend
+ *      full_evaluation_enhanced.py:115-329) ------------------------------------------------- */
+/* dst[n, y, x, c] = (src_view(view)[n, y, x, c] - mean) / (std + 1e-10); src f32 [N][H][W][Cin],
+ * dst NHWC with C_stride >= Cin (pad channels zeroed); view in 0..7 is the TTA forward transform. */
+int adp_prep_input(int dtype, int N, int H, int W, int Cin, const float* src, float mean,
+                   float std, int view, int C_stride, void* dst, adp_stream_t s);
+/* out[y,x] = mean_v inverse_view(v)(probs[v])[y,x] over nviews views listed in views[] (host) */
+int adp_tta_merge(int H, int W, int nviews, const int* views, const float* probs, float* out,
+                  adp_stream_t s);
+int adp_blend_accum(int H, int W, int T, int y0, int x0, const float* tile, const float* weight,
+                    float* acc, float* wsum, adp_stream_t s);
+int adp_blend_finalize(size_t n, const float* acc, const float* wsum, float floor_, float* out,
+                       adp_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

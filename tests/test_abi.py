@@ -1,0 +1,36 @@
+"""CPU-side checks of the C ABI: the in-tree library loads and exports every symbol the header
+declares (no compute calls: there is no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+from adipose_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "adipose_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(adp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_header_symbols():
+    lib = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), f"missing export {s}"
+    assert set(syms) == set(_lib.exported_symbols()), "ctypes signature table out of sync with the header"
+
+
+def test_abi_version_and_error_plumbing():
+    lib = _lib.lib()
+    assert lib.adp_abi_version() == 1
+    assert isinstance(lib.adp_last_error(), bytes)
+
+
+def test_conv_desc_layout_matches_header():
+    # 15 ints, float, uint, 6 ints, float, int, float, int -> 27 4-byte fields
+    assert ctypes.sizeof(_lib.ConvDesc) == 27 * 4
+    assert ctypes.sizeof(_lib.ConvIO) == 16 * 8

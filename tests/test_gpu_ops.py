@@ -1,0 +1,303 @@
+"""Kernel-level parity: every libadipose_hip op vs the CPU fp32 oracle (oracle/torch_ref.py).
+
+f32 launches run the exact-f32 MFMA path: tolerance 1e-4 relative to the output scale.
+bf16 launches are compared with the oracle evaluated on bf16-rounded operands (f32 accumulate):
+tolerance 2e-2 relative to the output scale.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from adipose_amd import ops
+from adipose_amd.nets import Dense, Head
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def nhwc_pad(x, cs, dt):
+    """logical NHWC CPU tensor -> device tensor with channel stride cs (zero pad)."""
+    N, H, W, C = x.shape
+    out = torch.zeros((N, H, W, cs), dtype=dt, device=DEV)
+    out[..., :C] = x.to(DEV, dt)
+    return out
+
+
+def relerr(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
+
+
+def rb(t, dt):
+    return t.to(dt).float() if dt == torch.bfloat16 else t
+
+
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2}
+DTS = [torch.float32, torch.bfloat16]
+
+CONV_CASES = [
+    # name, N, S, cin_parts, cout, dil, up
+    ("first", 2, 16, [1], 44, 1, False),
+    ("plain", 2, 16, [44], 88, 2, False),
+    ("dil8", 1, 32, [88], 176, 8, False),
+    ("dil32", 1, 16, [64], 64, 32, False),
+    ("up", 2, 8, [88], 44, 1, True),
+    ("concat", 2, 16, [44, 44], 44, 1, False),
+    ("wide", 1, 16, [176], 352, 4, False),
+]
+
+
+def make_case(N, S, cin_parts, cout, dil, up, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    xs = [torch.randn(N, S, S, c, generator=g) for c in cin_parts]
+    cin = sum(cin_parts)
+    kern = torch.randn(3, 3, cin, cout, generator=g) * (1.0 / np.sqrt(9 * cin))
+    bias = torch.randn(cout, generator=g) * 0.1
+    layer = Dense("t", cin_parts, cout, dil=dil, up=up)
+    return xs, kern, bias, layer
+
+
+def oracle_fwd(xs, kern, bias, dil, up, relu=True):
+    x = torch.cat(xs, -1)
+    if up:
+        x = R.upsample_nearest2(x)
+    return R.conv2d_same(x, kern, bias, dilation=dil, relu=relu)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_conv_fwd(case, dt):
+    _, N, S, parts, cout, dil, up = case
+    xs, kern, bias, l = make_case(N, S, parts, cout, dil, up)
+    Wp = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV)
+    W = Wp.to(dt).contiguous()
+    b = torch.zeros(l.cout_s, device=DEV)
+    b[:cout] = bias.to(DEV)
+    srcs = [nhwc_pad(x, cs, dt) for x, cs in zip(xs, l.cin_s)]
+    So = S * 2 if up else S
+    out = torch.zeros((N, So, So, l.cout_s), dtype=dt, device=DEV)
+    ops.conv_fwd(srcs[0], W, l.Nout, out=out, srcB=srcs[1] if len(srcs) > 1 else None, bias=b, up=up, dil=dil,
+                 relu=True)
+    torch.cuda.synchronize()
+    ref = oracle_fwd([rb(x, dt) for x in xs], rb(kern, dt), bias, dil, up)
+    assert relerr(out[..., :cout], ref) < TOL[dt]
+    if l.cout_s > cout:
+        assert out[..., cout:].abs().max().item() == 0.0  # pad channels stay zero
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_conv_grads(case, dt):
+    """wgrad (+bias grad) and dgrad vs autograd of the oracle conv (pre-activation)."""
+    _, N, S, parts, cout, dil, up = case
+    xs, kern, bias, l = make_case(N, S, parts, cout, dil, up, seed=1)
+    xs = [rb(x, dt) for x in xs]
+    kern = rb(kern, dt)
+    So = S * 2 if up else S
+    g = torch.Generator().manual_seed(5)
+    dZ = rb(torch.randn(N, So, So, cout, generator=g), dt)
+    xr = [x.clone().requires_grad_(True) for x in xs]
+    kr = kern.clone().requires_grad_(True)
+    br = bias.clone().requires_grad_(True)
+    y = oracle_fwd(xr, kr, br, dil, up, relu=False)
+    (y * dZ).sum().backward()
+    # device
+    srcs = [nhwc_pad(x, cs, dt) for x, cs in zip(xs, l.cin_s)]
+    dZd = nhwc_pad(dZ, l.cout_s, dt)
+    dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
+    dB = torch.zeros(l.cout_s, device=DEV)
+    ops.conv_wgrad(srcs[0], dZd, dW, l.Nout, dB=dB, srcB=srcs[1] if len(srcs) > 1 else None, up=up, dil=dil)
+    Wmaster = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV)
+    Wd = torch.zeros((l.dNpad, l.dKpad), dtype=dt, device=DEV)
+    ops.pack_weights(Wmaster, Wd, 1, taps=9, cin_s=l.Cin_s, nout=l.cout_s)
+    Hs = S * 2 if up else S
+    dX = torch.zeros((N, Hs, Hs, l.Cin_s), dtype=dt, device=DEV)
+    ops.conv_fwd(dZd, Wd, l.Cin_s, out=dX, dil=dil)
+    torch.cuda.synchronize()
+    dW_k = torch.from_numpy(l.packed_to_keras(dW.cpu().numpy()))
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    assert relerr(dW_k, kr.grad) < tol
+    assert relerr(dB[:cout], br.grad) < tol
+    # data gradient: for the upsample layer compare on the upsampled grid (kernel output before 2x2 sum)
+    xcat = torch.cat(xs, -1)
+    if up:
+        xu = R.upsample_nearest2(xcat).clone().requires_grad_(True)
+        (R.conv2d_same(xu, kern, bias, dilation=dil, relu=False) * dZ).sum().backward()
+        ref_dx = xu.grad
+    else:
+        ref_dx = torch.cat([x.grad for x in xr], -1)
+    got = torch.cat([dX[..., sum(l.cin_s[:i]): sum(l.cin_s[:i]) + c] for i, c in enumerate(parts)], -1)
+    assert relerr(got, ref_dx) < tol
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_conv_transpose(dt):
+    N, S, cin, cout = 2, 8, 128, 64
+    g = torch.Generator().manual_seed(3)
+    x = rb(torch.randn(N, S, S, cin, generator=g), dt)
+    k = rb(torch.randn(cin, cout, 2, 2, generator=g) * 0.1, dt)
+    b = torch.randn(cout, generator=g) * 0.1
+    l = Dense("t", [cin], cout, transpose=True, relu=False)
+    xr = x.clone().requires_grad_(True)
+    kr = k.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    y = F.conv_transpose2d(xr.permute(0, 3, 1, 2), kr, br, stride=2).permute(0, 2, 3, 1)
+    dY = rb(torch.randn(y.shape, generator=g), dt)
+    (y * dY).sum().backward()
+    Wm = torch.from_numpy(l.keras_to_packed(k.numpy())).to(DEV)
+    bd = b.to(DEV)
+    xd = nhwc_pad(x, l.Cin_s, dt)
+    out = torch.zeros((N, 2 * S, 2 * S, l.cout_s), dtype=dt, device=DEV)
+    ops.conv_fwd(xd, Wm.to(dt).contiguous(), l.Nout, out=out, bias=bd, kh=1, kw=1, pad=0, out_mode=1,
+                 shuffle_c=l.cout_s)
+    dYd = nhwc_pad(dY, l.cout_s, dt)
+    dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
+    dB = torch.zeros(l.cout_s, device=DEV)
+    ops.conv_wgrad(xd, dYd, dW, l.Nout, dB=dB, kh=1, kw=1, pad=0, shuffle_c=l.cout_s)
+    Wd = torch.zeros((l.dNpad, l.dKpad), dtype=dt, device=DEV)
+    ops.pack_weights(Wm, Wd, 2, taps=1, cin_s=l.Cin_s, nout=l.Nout)
+    dX = torch.zeros((N, S, S, l.Cin_s), dtype=dt, device=DEV)
+    ops.conv_fwd(dYd, Wd, l.Cin_s, out=dX, kh=2, kw=2, pad=0, stride=2, Ho=S, Wo=S)
+    torch.cuda.synchronize()
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    assert relerr(out, y.detach()) < tol
+    assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < tol
+    assert relerr(dB, br.grad) < tol
+    assert relerr(dX, xr.grad) < tol
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_pool_upsample(dt):
+    g = torch.Generator().manual_seed(7)
+    x = rb(torch.relu(torch.randn(2, 16, 16, 48, generator=g)), dt)
+    xd = x.to(DEV, dt).contiguous()
+    p = torch.zeros((2, 8, 8, 48), dtype=dt, device=DEV)
+    ops.maxpool2_fwd(xd, p)
+    xr = x.clone().requires_grad_(True)
+    pr = R.maxpool2(xr)
+    dp = rb(torch.randn(pr.shape, generator=g), dt)
+    (pr * dp).sum().backward()
+    add = rb(torch.randn(x.shape, generator=g), dt)
+    dx = torch.zeros_like(xd)
+    ops.maxpool2_bwd(xd, dp.to(DEV, dt).contiguous(), dx, addend=add.to(DEV, dt).contiguous(), mask=xd)
+    torch.cuda.synchronize()
+    assert relerr(p, pr.detach()) < 1e-6
+    ref = (xr.grad + add) * (x > 0).float()
+    assert relerr(dx, ref) < (1e-6 if dt == torch.float32 else 1e-2)
+    # nearest-upsample gradient = 2x2 sum
+    du = rb(torch.randn(2, 16, 16, 48, generator=g), dt)
+    ds = torch.zeros((2, 8, 8, 48), dtype=dt, device=DEV)
+    ops.upsample2_bwd(du.to(DEV, dt).contiguous(), ds)
+    torch.cuda.synchronize()
+    ref = du.reshape(2, 8, 2, 8, 2, 48).sum((2, 4))
+    assert relerr(ds, ref) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("softmax2", [True, False])
+def test_heads(dt, softmax2):
+    g = torch.Generator().manual_seed(11)
+    cin, cs = 44, 48
+    nout = 2 if softmax2 else 1
+    x = rb(torch.relu(torch.randn(2, 8, 8, cin, generator=g)), dt)
+    k = torch.randn(1, 1, cin, nout, generator=g) * 0.3
+    b = torch.randn(nout, generator=g) * 0.1
+    h = Head("h", cin, nout)
+    Wd = torch.from_numpy(h.keras_to_packed(k.numpy())).to(DEV)
+    xd = nhwc_pad(x, cs, dt)
+    p = torch.zeros((2, 8, 8), device=DEV)
+    ops.head_fwd(xd, Wd, b.to(DEV), p, cin=cin, softmax2=softmax2)
+    xr = x.clone().requires_grad_(True)
+    kr = k.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    z = R.conv1x1(xr, kr, br)
+    pr = torch.softmax(z, -1)[..., 1] if softmax2 else torch.sigmoid(z)[..., 0]
+    dp = torch.randn(pr.shape, generator=g)
+    (pr * dp).sum().backward()
+    dW = torch.zeros_like(Wd)
+    dB = torch.zeros(nout, device=DEV)
+    dx = torch.zeros_like(xd)
+    ops.head_bwd(xd, Wd, p, dp.to(DEV), dW, dB, cin=cin, softmax2=softmax2, dx=dx)
+    torch.cuda.synchronize()
+    assert relerr(p, pr.detach()) < 1e-5
+    assert relerr(torch.from_numpy(h.packed_to_keras(dW.cpu().numpy())), kr.grad) < 1e-4
+    assert relerr(dB, br.grad) < 1e-4
+    assert relerr(dx[..., :cin], xr.grad) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("scale", [2, 4])
+def test_resize_bilinear(scale):
+    g = torch.Generator().manual_seed(13)
+    s = torch.rand(2, 16, 16, generator=g)
+    sr = s.clone().requires_grad_(True)
+    o = R.resize_bilinear_half_pixel(sr[..., None], (16 * scale, 16 * scale))[..., 0]
+    do = torch.randn(o.shape, generator=g)
+    (o * do).sum().backward()
+    od = torch.zeros(o.shape, device=DEV)
+    ops.resize_bilinear_fwd(s.to(DEV), od)
+    dsd = torch.zeros(s.shape, device=DEV)
+    ops.resize_bilinear_bwd(do.to(DEV), dsd)
+    torch.cuda.synchronize()
+    assert relerr(od, o.detach()) < 1e-6
+    assert relerr(dsd, sr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("ohem,smooth", [(True, False), (False, False), (True, True), (False, True)])
+def test_loss_value_and_grad(ohem, smooth):
+    g = torch.Generator().manual_seed(17)
+    N, H, W = 2, 64, 64
+    p = torch.rand(N, H, W, generator=g)
+    p[0, 0, :4] = torch.tensor([0.0, 1.0, 1e-9, 1 - 1e-9])   # clip edges
+    y = (torch.rand(N, H, W, generator=g) > 0.6).float()
+    pr = p.clone().requires_grad_(True)
+    if ohem:
+        L = R.ohem_loss_with_smoothing(y, pr) if smooth else R.ohem_loss(y, pr)
+    else:
+        L = R.combined_loss_with_label_smoothing(y, pr) if smooth else R.combined_loss_standard(y, pr)
+    L.backward()
+    pd, yd = p.to(DEV), y.to(DEV)
+    rows = torch.zeros(N * H, device=DEV)
+    stats = torch.zeros(8, dtype=torch.float64, device=DEV)
+    coef = torch.zeros(N * H, device=DEV)
+    out = torch.zeros(1, dtype=torch.float64, device=DEV)
+    ops.loss_rows(pd, yd, rows, stats, smooth=smooth)
+    k = int(np.float32(H) * np.float32(0.7)) if ohem else H
+    ops.loss_select(rows, coef, out, N=N, H=H, W=W, ohem=ohem, keep_ratio=0.7, weight=1.0, norm_rows=N * k)
+    dp = torch.zeros_like(pd)
+    ops.loss_grad(pd, yd, coef, stats, dp, weight=1.0, smooth=smooth)
+    torch.cuda.synchronize()
+    st = stats.cpu().numpy()
+    dice = 1.0 - (2 * st[0] + 1) / (st[1] + st[2] + 1)
+    val = out.item() + dice
+    assert abs(val - L.item()) < 1e-5 * max(1.0, abs(L.item()))
+    assert relerr(dp, pr.grad) < 1e-4
+    # dice_coef / binary accuracy stats
+    assert abs((2 * st[3] + 1) / (st[4] + st[5] + 1) - R.dice_coef(y, p).item()) < 1e-6
+    assert abs(st[6] / (N * H * W) - R.binary_accuracy(y, p).item()) < 1e-6
+
+
+def test_adam_matches_keras():
+    g = torch.Generator().manual_seed(19)
+    w = torch.randn(1000, generator=g)
+    grads = [torch.randn(1000, generator=g) for _ in range(3)]
+    ref = R.KerasAdam([w.clone()], lr=1e-3, weight_decay=0.01)
+    wd, m, v = w.to(DEV), torch.zeros(1000, device=DEV), torch.zeros(1000, device=DEV)
+    for t, gr in enumerate(grads, 1):
+        ref.step([gr])
+        ops.adam(wd, gr.to(DEV), m, v, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-7, step=t, weight_decay=0.01)
+    torch.cuda.synchronize()
+    assert relerr(wd, ref.p[0]) < 1e-6
+
+
+def test_pixel_counts_and_blend():
+    g = torch.Generator().manual_seed(23)
+    pred = torch.rand(64, 64, generator=g)
+    true = (torch.rand(64, 64, generator=g) > 0.5).float()
+    c = torch.zeros(4, dtype=torch.int64, device=DEV)
+    ops.pixel_counts(pred.to(DEV), true.to(DEV), 0.5, c)
+    pb, tb = pred > 0.5, true > 0.5
+    ref = [int((pb & tb).sum()), int((pb & ~tb).sum()), int((~pb & tb).sum()), int((~pb & ~tb).sum())]
+    assert c.cpu().tolist() == ref
