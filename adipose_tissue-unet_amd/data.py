@@ -1,0 +1,218 @@
+"""Host-side data feed: synthetic histology tiles, the reference's on-disk tile format, and the
+reference's normalisations.
+
+  * TileDataset (train_adipose_unet_v3.py:510-623): pairs <stem>.jpg images with <stem>.tif masks,
+    grayscale decode (cv2.IMREAD_GRAYSCALE equivalent), optional augmentation, per-tile percentile
+    normalisation (default, :591-593) or dataset z-score (:589-590); the last batch is padded by
+    repeating its last tile (:600-602).
+  * compute_mean_std (:1125-1133) for normalization_stats.json.
+  * synthetic tiles (seed 865 from seed.csv): blurred-noise background (mean ~201,
+    std ~25) with adipocyte-like ellipses (bright lumen, dark rim); mask = ellipse interiors.
+
+cv2/tifffile are not available on this image: JPEG decoding uses PIL (ITU-R 601 luma, the same
+weights cv2 uses for IMREAD_GRAYSCALE); masks use PIL-readable TIFF.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import numpy as np
+
+SEED = 865
+
+
+def load_seed(path=None):
+    """src/utils/seed_utils.py: first integer of seed.csv (865)."""
+    if path and os.path.exists(path):
+        with open(path) as f:
+            for tok in f.read().replace(",", " ").split():
+                if tok.strip().lstrip("-").isdigit():
+                    return int(tok)
+    return SEED
+
+
+# ------------------------------------------------------------------------------ synthetic data
+def synthetic_tile(rng, size=1024, channels=3, n_cells=None):
+    """One uint8 histology-like tile (H,W,C) and its {0,1} float32 mask (H,W)."""
+    from scipy import ndimage
+
+    h = w = size
+    noise = rng.normal(0.0, 1.0, (h // 4 + 2, w // 4 + 2)).astype(np.float32)
+    bg = ndimage.gaussian_filter(noise, 2.0)
+    bg = ndimage.zoom(bg, 4, order=1)[:h, :w]
+    bg = 201.0 + 25.0 * bg / (bg.std() + 1e-6)
+    mask = np.zeros((h, w), np.float32)
+    yy, xx = np.mgrid[0:h, 0:w]
+    n_cells = n_cells or rng.integers(max(4, size // 128), max(8, size // 48))
+    img = bg.copy()
+    for _ in range(int(n_cells)):
+        cy, cx = rng.uniform(0, h), rng.uniform(0, w)
+        ry, rx = rng.uniform(0.03, 0.09) * size, rng.uniform(0.03, 0.09) * size
+        th = rng.uniform(0, np.pi)
+        c, s = np.cos(th), np.sin(th)
+        y0, y1 = int(max(0, cy - 1.2 * max(ry, rx))), int(min(h, cy + 1.2 * max(ry, rx) + 1))
+        x0, x1 = int(max(0, cx - 1.2 * max(ry, rx))), int(min(w, cx + 1.2 * max(ry, rx) + 1))
+        if y1 <= y0 or x1 <= x0:
+            continue
+        dy, dx = yy[y0:y1, x0:x1] - cy, xx[y0:y1, x0:x1] - cx
+        r = ((dy * c + dx * s) / ry) ** 2 + ((-dy * s + dx * c) / rx) ** 2
+        inside = r < 1.0
+        rim = (r >= 1.0) & (r < 1.35)
+        mask[y0:y1, x0:x1][inside] = 1.0
+        img[y0:y1, x0:x1][inside] = 235.0 + 8.0 * rng.normal(size=int(inside.sum()))
+        img[y0:y1, x0:x1][rim] = 120.0 + 15.0 * rng.normal(size=int(rim.sum()))
+    img = np.clip(img, 0, 255)
+    if channels == 1:
+        return img.astype(np.uint8), mask
+    tint = np.array([1.0, 0.86, 0.93], np.float32)[:channels]
+    rgb = np.clip(img[..., None] * tint + rng.normal(0, 3, (h, w, channels)), 0, 255)
+    return rgb.astype(np.uint8), mask
+
+
+def synthetic_batch(n, size, channels=3, seed=SEED):
+    rng = np.random.default_rng(seed)
+    xs, ys = zip(*(synthetic_tile(rng, size, channels) for _ in range(n)))
+    return np.stack(xs), np.stack(ys)
+
+
+def to_gray(rgb):
+    """cv2.COLOR_RGB2GRAY / IMREAD_GRAYSCALE weights (ITU-R BT.601)."""
+    rgb = np.asarray(rgb, np.float32)
+    return rgb[..., 0] * 0.299 + rgb[..., 1] * 0.587 + rgb[..., 2] * 0.114
+
+
+# ------------------------------------------------------------------------------ normalisation
+def normalize_image(image, method="percentile", p_low=1, p_high=99, mean=None, std=None):
+    """src/utils/data.py:398-429"""
+    if method == "percentile":
+        plow, phigh = np.percentile(image, (p_low, p_high))
+        scale = max(phigh - plow, 1e-3)
+        return np.clip((image - plow) / scale, 0, 1)
+    if method == "minmax":
+        imin, imax = image.min(), image.max()
+        return (image - imin) / max(imax - imin, 1e-3)
+    if method == "zscore":
+        return (image - image.mean()) / (image.std() + 1e-10)
+    if method == "zscore_dataset":
+        if mean is None or std is None:
+            raise ValueError("Dataset mean and std required for zscore_dataset method")
+        return (image - mean) / (std + 1e-10)
+    raise ValueError(f"Unknown normalization method: {method}")
+
+
+# ------------------------------------------------------------------------------ file format
+def read_gray(path):
+    """cv2.imread(path, IMREAD_GRAYSCALE) equivalent -> float32."""
+    from PIL import Image
+
+    with Image.open(path) as im:
+        if im.mode in ("I;16", "I;16B", "I", "F"):
+            return np.asarray(im, np.float32)
+        return np.asarray(im.convert("L"), np.float32)
+
+
+def read_mask(path):
+    from PIL import Image
+
+    with Image.open(path) as im:
+        m = np.asarray(im).astype(np.float32)
+    return m.squeeze() if m.ndim == 3 else m
+
+
+def write_mask(path, arr):
+    from PIL import Image
+
+    Image.fromarray(np.asarray(arr)).save(path)
+
+
+def compute_mean_std(image_paths, max_n=None):
+    """train_adipose_unet_v3.py:1125-1133 (float64 accumulate over all pixels)."""
+    s, s2, n = 0.0, 0.0, 0
+    for i, p in enumerate(image_paths):
+        if max_n and i >= max_n:
+            break
+        v = read_gray(p).astype(np.float64).reshape(-1)
+        s += v.sum()
+        s2 += (v * v).sum()
+        n += v.size
+    mean = s / n
+    return float(mean), float(np.sqrt(max(s2 / n - mean * mean, 0.0)) + 1e-10)
+
+
+class TileDataset:
+    """train_adipose_unet_v3.py:510-623 (generator semantics; batches are numpy float32)."""
+
+    def __init__(self, images_dir, masks_dir, batch_size, augment=True, cache_size=100, mean=None, std=None,
+                 normalization_method="zscore", percentile_low=1.0, percentile_high=99.0, augment_fn=None,
+                 augment_level="moderate", seed=None):
+        self.images_dir, self.masks_dir = Path(images_dir), Path(masks_dir)
+        self.batch_size = batch_size
+        self.augment, self.augment_fn = augment, augment_fn
+        self.cache_size = cache_size
+        self.mean, self.std = mean, std
+        self.normalization_method = normalization_method
+        self.percentile_low, self.percentile_high = percentile_low, percentile_high
+        image_files = sorted(self.images_dir.glob("*.jpg"))
+        mask_files = {p.stem: p for p in self.masks_dir.glob("*.tif")}
+        self.pairs = [(p, mask_files[p.stem]) for p in image_files if p.stem in mask_files]
+        self.cache = {}
+        self.seed = seed
+
+    def __len__(self):
+        return len(self.pairs)
+
+    def load_pair(self, img_path, mask_path):
+        key = img_path.stem
+        if key in self.cache:
+            return self.cache[key]
+        img = read_gray(img_path)
+        mask = read_mask(mask_path)
+        if len(self.cache) < self.cache_size:
+            self.cache[key] = (img.copy(), mask.copy())
+        return img, mask
+
+    def _norm(self, img):
+        if self.normalization_method == "zscore":
+            return (img - self.mean) / (self.std + 1e-10)
+        if self.normalization_method == "percentile":
+            return normalize_image(img, "percentile", self.percentile_low, self.percentile_high)
+        raise ValueError(f"Unknown normalization method: {self.normalization_method}")
+
+    def generator(self, shard=0, num_shards=1):
+        """Endless batches; with num_shards>1 each DP rank reads a disjoint slice of each epoch order."""
+        rng = np.random.RandomState(self.seed)
+        idx = np.arange(len(self.pairs))
+        while True:
+            rng.shuffle(idx)
+            mine = idx[shard::num_shards]
+            for i in range(0, len(mine), self.batch_size):
+                imgs, masks = [], []
+                for j in mine[i:i + self.batch_size]:
+                    img, mask = self.load_pair(*self.pairs[j])
+                    if self.augment and self.augment_fn is not None:
+                        img, mask = self.augment_fn(img, mask, rng)
+                    imgs.append(self._norm(img))
+                    masks.append(mask)
+                while len(imgs) < self.batch_size:
+                    imgs.append(imgs[-1])
+                    masks.append(masks[-1])
+                yield np.array(imgs, np.float32), np.array(masks, np.float32)
+
+
+def write_synthetic_build(root, n_train=8, n_val=4, size=1024, seed=SEED):
+    """Materialise a reference-format build directory (dataset/{train,val}/{images,masks}) with
+    synthetic tiles named like build_dataset.py's '{base}_r{r}_c{c}.jpg' (:1531-1532)."""
+    from PIL import Image
+
+    rng = np.random.default_rng(seed)
+    root = Path(root)
+    for split, n in (("train", n_train), ("val", n_val)):
+        (root / "dataset" / split / "images").mkdir(parents=True, exist_ok=True)
+        (root / "dataset" / split / "masks").mkdir(parents=True, exist_ok=True)
+        for i in range(n):
+            img, mask = synthetic_tile(rng, size, 3)
+            stem = f"synthetic_slide{i // 4}_r{i % 2}_c{(i // 2) % 2}"
+            Image.fromarray(img).save(root / "dataset" / split / "images" / f"{stem}.jpg", quality=100)
+            Image.fromarray(mask.astype(np.uint8)).save(root / "dataset" / split / "masks" / f"{stem}.tif")
+    return root

@@ -229,28 +229,44 @@ class UNetEngine:
             lim = math.sqrt(6.0 / (fi + fo))
             kshape, _ = l.keras_shapes()
             kern = rng.uniform(-lim, lim, size=kshape).astype(np.float32)
-            self.set_layer_weights(l.name, [kern, np.zeros(l.keras_shapes()[1], np.float32)])
-            if isinstance(l, Dense) and l.bn:
-                self.ps.view(l.name + "/gamma")[: l.cout].fill_(1.0)
+            arrs = [kern]
+            for slot in self._slots(l.name)[1:]:
+                arrs.append((np.ones if slot == "gamma" else np.zeros)(l.keras_shapes()[1], np.float32))
+            self.set_layer_weights(l.name, arrs)
+
+    def _slots(self, name):
+        """Keras-style variable slots of a layer: kernel, [bias], [gamma, beta]."""
+        slots = ["W"]
+        if (name + "/b") in self.ps.entries:
+            slots.append("b")
+        if (name + "/gamma") in self.ps.entries:
+            slots += ["gamma", "beta"]
+        return slots
 
     def set_layer_weights(self, name, arrays):
-        """Keras-style set: arrays = [kernel, bias] (bias optional for bias-free layers)."""
+        """Keras-style set: arrays = [kernel, bias] (conv/head), [kernel, gamma, beta] (conv+BN)."""
         l = self.layers[name]
+        slots = self._slots(name)
+        if len(arrays) != len(slots):
+            raise ValueError(f"{name}: expected {len(slots)} arrays ({slots}), got {len(arrays)}")
         Wp = l.keras_to_packed(arrays[0])
         self.ps.view(name + "/W").copy_(torch.from_numpy(Wp))
-        if len(arrays) > 1 and (getattr(l, "bias", True)) and (name + "/b") in self.ps.entries:
-            b = self.ps.view(name + "/b")
-            b.zero_()
-            b[: len(arrays[1])].copy_(torch.from_numpy(np.asarray(arrays[1], np.float32)))
+        for slot, arr in zip(slots[1:], arrays[1:]):
+            v = self.ps.view(f"{name}/{slot}")
+            v.zero_()
+            v[: len(arr)].copy_(torch.from_numpy(np.asarray(arr, np.float32)))
 
-    def get_layer_weights(self, name):
+    def get_layer_weights(self, name, buf=None):
         l = self.layers[name]
-        Wp = self.ps.view(name + "/W").detach().cpu().numpy()
+        Wp = self.ps.view(name + "/W", buf).detach().cpu().numpy()
         out = [l.packed_to_keras(Wp)]
-        if (name + "/b") in self.ps.entries:
-            nb = l.keras_shapes()[1][0]
-            out.append(self.ps.view(name + "/b").detach().cpu().numpy()[:nb].copy())
+        n = l.cout if isinstance(l, Dense) else l.nout
+        for slot in self._slots(name)[1:]:
+            out.append(self.ps.view(f"{name}/{slot}", buf).detach().cpu().numpy()[:n].copy())
         return out
+
+    def get_layer_grads(self, name):
+        return self.get_layer_weights(name, self.ps.grad)
 
     def get_weights(self):
         return OrderedDict((n, self.get_layer_weights(n)) for n in self.layers)
@@ -271,12 +287,31 @@ class UNetEngine:
 
     # -- buffers
     def buf(self, key, shape, dtype=None):
+        """Persistent HBM buffer, allocated once per (name, shape, dtype)."""
         dtype = dtype or self.dt
-        t = self._bufs.get(key)
-        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+        k = (key, tuple(shape), dtype)
+        t = self._bufs.get(k)
+        if t is None:
             t = torch.zeros(shape, dtype=dtype, device=self.device)
-            self._bufs[key] = t
+            self._bufs[k] = t
         return t
+
+    grad_hook = None  # called with a layer name once that layer's parameter gradients are final
+
+    def _grad_ready(self, name):
+        if self.grad_hook is not None:
+            self.grad_hook(name)
+
+    def acts(self, batch):
+        """Activation set for a batch size (allocated once, reused every step)."""
+        if not hasattr(self, "_acts"):
+            self._acts = {}
+        if batch not in self._acts:
+            self._acts[batch] = self.alloc(batch)
+        self.a = self._acts[batch]
+        if hasattr(self, "_sts"):
+            self.st = self._sts[batch]
+        return self.a
 
     def zero(self, t):
         if t.dtype == torch.float32:
@@ -337,6 +372,7 @@ class UNetEngine:
         else:
             ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, srcB=srcB, bnA=bnA, bnB=bnB, up=l.up, kh=l.k, kw=l.k,
                            dil=l.dil)
+        self._grad_ready(l.name)
 
     def dgrad(self, l, dZ, out, *, Ho=None, Wo=None, addend=None, mask=None, mask_scale=1.0, split=False,
               out2=None, mask2=None, mask2_scale=1.0, skip_first=False):
@@ -402,8 +438,8 @@ class AdiposeV3Net(UNetEngine):
         L["output_softmax"] = Head("output_softmax", nb, 2)
 
     # -------------------------------------------------------------------------- forward
-    def alloc(self):
-        B, S, nb = self.B, self.S, self.nb
+    def alloc(self, B):
+        S, nb = self.S, self.nb
         s = [S, S // 2, S // 4, S // 8]
         c = [r8(nb), r8(2 * nb), r8(4 * nb), r8(8 * nb)]
         a = {}
@@ -430,15 +466,14 @@ class AdiposeV3Net(UNetEngine):
             a["s_aux2"] = self.buf("s_aux2", (B, s[1], s[1]), torch.float32)
             a["p_aux1"] = self.buf("p_aux1", (B, S, S), torch.float32)
             a["p_aux2"] = self.buf("p_aux2", (B, S, S), torch.float32)
-        self.a = a
         return a
 
-    def forward(self, x_prepped=None, *, train=False, seed=0):
-        """Run the network on self.a['x'] (NHWC, prepped). Returns dict of f32 probability maps."""
-        a = self.alloc() if not hasattr(self, "a") else self.a
-        if x_prepped is not None and x_prepped.data_ptr() != a["x"].data_ptr():
-            a["x"].copy_(x_prepped)
-        self.pack_forward_weights()
+    def forward(self, batch=None, *, train=False, seed=0, pack=True):
+        """Run the network on acts(batch)['x'] (NHWC, prepped by ops.prep_input).
+        Returns dict of f32 probability maps (views of persistent buffers)."""
+        a = self.acts(batch or self.B)
+        if pack:
+            self.pack_forward_weights()
         L = self.layers
         r = self.dropout_rate if train else 0.0
         sd = (seed * 7919 + 17) & 0xFFFFFFFF
@@ -490,7 +525,6 @@ class AdiposeV3Net(UNetEngine):
         """grads_out: {'main_out': dL/dp (B,S,S) f32, 'aux_out1': ..., 'aux_out2': ...}.
         Accumulates parameter gradients into self.ps.grad (caller zeroes)."""
         a, L = self.a, self.layers
-        B, S = self.B, self.S
         r = self.dropout_rate if self._train_fwd else 0.0
         keep = 1.0 / (1.0 - r) if r > 0 else 1.0
         full = not self.frozen_encoder
@@ -509,6 +543,7 @@ class AdiposeV3Net(UNetEngine):
         ops.head_bwd(a["u1"], self.ps.view("output_softmax/W"), a["p_main"], grads_out["main_out"],
                      self.ps.gview("output_softmax/W"), self.ps.gview("output_softmax/b"), cin=h.cin, softmax2=True,
                      dx=g["u1"], mask=a["u1"], mask_scale=keep)
+        self._grad_ready("output_softmax")
         aux_dx = {}
         if self.ds:
             for k, src, sb, pb in (("aux_out1", "u3", "s_aux1", "p_aux1"), ("aux_out2", "u2", "s_aux2", "p_aux2")):
@@ -518,6 +553,7 @@ class AdiposeV3Net(UNetEngine):
                 dx = gb("aux/" + src, a[src])
                 ops.head_bwd(a[src], self.ps.view(k + "/W"), a[sb], ds, self.ps.gview(k + "/W"),
                              self.ps.gview(k + "/b"), cin=hh.cin, softmax2=False, dx=dx)
+                self._grad_ready(k)
                 aux_dx[src] = dx
         # decoder level 1 (full resolution)
         self._dec_level(1, g, "u1", "d1", aux_dx.get("u2"), keep, full)
@@ -576,7 +612,7 @@ class AdiposeV3Net(UNetEngine):
         src = {3: "dsum", 2: "u3", 1: "u2"}[lvl]
         self.wgrad(c1, a[src], dz1)
         Sup = a[f"u{lvl}a"].shape[1]
-        gup = self.buf(f"g/up{lvl}", (self.B, Sup, Sup, a[src].shape[3]))
+        gup = self.buf(f"g/up{lvl}", (a["x"].shape[0], Sup, Sup, a[src].shape[3]))
         self.dgrad(c1, dz1, gup)
         dsrc = self.buf(f"g/{src}", tuple(a[src].shape))
         if lvl == 3:
@@ -629,8 +665,8 @@ class UNetBN(UNetEngine):
             L[f"dec{i}_conv2"] = Dense(f"dec{i}_conv2", [c], c, bias=False, bn=True)
         L["head"] = Head("head", self.ch(0), 1)
 
-    def alloc(self):
-        B, S = self.B, self.S
+    def alloc(self, B):
+        S = self.S
         a = {"x": self.buf("x", (B, S, S, 8))}
         st = {}
         for i in range(self.levels):
@@ -646,7 +682,7 @@ class UNetBN(UNetEngine):
         for n, l in self.layers.items():
             if isinstance(l, Dense) and l.bn:
                 st[n] = self.buf("bnstat/" + n, (6, l.cout_s), torch.float32)  # sum,sq,scale,shift,mean,invstd
-        self.a, self.st = a, st
+        self.st = st  # batch-independent shapes: shared by every activation set
         return a
 
     def bnvec(self, name):
@@ -670,11 +706,10 @@ class UNetBN(UNetEngine):
             ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                             self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
 
-    def forward(self, x_prepped=None, *, train=False, seed=0):
-        a = self.alloc() if not hasattr(self, "a") else self.a
-        if x_prepped is not None and x_prepped.data_ptr() != a["x"].data_ptr():
-            a["x"].copy_(x_prepped)
-        self.pack_forward_weights()
+    def forward(self, batch=None, *, train=False, seed=0, pack=True):
+        a = self.acts(batch or self.B)
+        if pack:
+            self.pack_forward_weights()
         Lv = self.levels
         src, bn_in = a["x"], None
         for i in range(Lv):
@@ -715,6 +750,7 @@ class UNetBN(UNetEngine):
         dA = gb("y0_2", a["y0_2"])
         ops.head_bwd(a["y0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"], self.ps.gview("head/W"),
                      self.ps.gview("head/b"), cin=self.ch(0), softmax2=False, dx=dA, bn=self.bnvec("dec0_conv2"))
+        self._grad_ready("head")
         skip_grad = {}
         cur_name, cur_z, cur_dA = "dec0_conv2", a["y0_2"], dA
         # decoder from level 0 upward

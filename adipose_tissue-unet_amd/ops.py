@@ -20,6 +20,48 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
+class LaunchTimer:
+    """Optional per-launch HIP-event timing of the GEMM kernels (bench.py roofline leg).
+    Events are recorded on the launch stream (torch's current stream), so they bracket exactly the
+    kernel they surround."""
+
+    def __init__(self):
+        self.recs = []
+
+    def wrap(self, kernel, flops, fn):
+        s = torch.cuda.current_stream()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        fn()
+        e1.record(s)
+        self.recs.append((kernel, flops, e0, e1))
+
+    def summary(self):
+        """kernel -> (launches, total flops, total ms) (synchronises)."""
+        torch.cuda.synchronize()
+        out = {}
+        for k, f, e0, e1 in self.recs:
+            n, fl, ms = out.get(k, (0, 0.0, 0.0))
+            out[k] = (n + 1, fl + f, ms + e0.elapsed_time(e1))
+        return out
+
+
+_timer = None
+
+
+def set_launch_timer(t):
+    global _timer
+    _timer = t
+
+
+def _timed(kernel, flops, fn):
+    if _timer is None:
+        fn()
+    else:
+        _timer.wrap(kernel, flops, fn)
+
+
 def dtype_code(t):
     if t.dtype == torch.bfloat16:
         return BF16
@@ -137,7 +179,10 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
         io.accum = ptr(accum)
     if bn_stats is not None:
         io.bn_sum, io.bn_sqsum = ptr(bn_stats[0]), ptr(bn_stats[1])
-    call("adp_conv_fwd", dtype_code(srcA), C.byref(d), C.byref(io), stream_ptr())
+    dc = dtype_code(srcA)
+    flops = 2.0 * N * Ho * Wo * nout * kh * kw * (d.CA_stride + d.CB_stride)
+    _timed(("igemm_fwd", dc), flops,
+           lambda: call("adp_conv_fwd", dc, C.byref(d), C.byref(io), stream_ptr()))
     return out
 
 
@@ -176,8 +221,11 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     if dB is not None:
         _check(dB.dtype == torch.float32, "dB must be f32")
     del Wdummy
-    call("adp_conv_wgrad", dtype_code(srcA), C.byref(d), C.byref(io), ptr(dY), int(dY.shape[3]), ptr(dW),
-         ptr(dB), stream_ptr())
+    dc = dtype_code(srcA)
+    flops = 2.0 * N * Ho * Wo * nout * K
+    _timed(("igemm_wgrad", dc), flops,
+           lambda: call("adp_conv_wgrad", dc, C.byref(d), C.byref(io), ptr(dY), int(dY.shape[3]), ptr(dW),
+                        ptr(dB), stream_ptr()))
 
 
 def pack_weights(src, dst, mode, *, taps=1, cin_s=0, nout=0):

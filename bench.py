@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""bench.py — 1024^2 tiles/sec (train) of the MI355X-native U-Net step.
+
+Workload (BASELINE.json configs[2], the configuration the metric "1024^2 tiles/sec (train)" is quoted
+on; it fits one GPU): `unet_bn` 5-level U-Net, base 64 channels, 1024x1024x3 synthetic histology
+tiles, bf16 compute (f32 accumulate, f32 master weights), batch 4 per GPU, pure data parallel (weak
+scaling). One step = prep -> forward -> BCE+Dice loss/grad -> backward -> RCCL gradient all-reduce
+(N>1, bucketed, overlapped with backward) -> Adam, on inputs already resident in HBM.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+Rank 0 prints ONE JSON line (plus `roofline` and `cpu_baseline` objects).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MI355X_PEAK = {"bf16": 2500.0, "f32": 157.3}   # TFLOP/s dense (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--preset", default="unet_bn", choices=["unet_bn", "adipose_v3"])
+    p.add_argument("--batch", type=int, default=4, help="tiles per GPU")
+    p.add_argument("--size", type=int, default=1024)
+    p.add_argument("--levels", type=int, default=5)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-size", type=int, default=1024, help="tile size of the CPU baseline sample")
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle (torch CPU fp32 restatement, oracle/torch_ref.py) on a bounded sample: ONE training step
+    (forward + loss + backward + Adam) on 1 tile of the same workload, on the host cores."""
+    import numpy as np
+    import torch
+
+    from oracle import torch_ref as R
+
+    threads = torch.get_num_threads()
+    S = args.cpu_size
+    g = torch.Generator().manual_seed(865)
+    if args.preset == "unet_bn":
+        w = R.unet_bn_keras_weights(levels=args.levels, base=64, in_ch=3, seed=865)
+        W = {k: [torch.tensor(v, requires_grad=True) for v in vs] for k, vs in w.items()}
+        x = torch.randn(1, S, S, 3, generator=g)
+        fwd = lambda: R.unet_bn_forward(x, W, levels=args.levels)  # noqa: E731
+        lossf = R.combined_loss_standard
+    else:
+        w = R.adipose_v3_keras_weights(seed=865)
+        W = {k: [torch.tensor(v, requires_grad=True) for v in vs] for k, vs in w.items()}
+        x = torch.randn(1, S, S, generator=g)
+        fwd = lambda: R.adipose_v3_forward(x, W)  # noqa: E731
+        lossf = None
+    y = (torch.rand(1, S, S, generator=g) > 0.7).float()
+    params = [p for vs in W.values() for p in vs]
+    opt = R.KerasAdam(params, lr=1e-4)
+    t0 = time.perf_counter()
+    out = fwd()
+    loss = lossf(y, out) if lossf else R.ds_total_loss(y, out)
+    loss.backward()
+    opt.step([p.grad for p in params])
+    dt = time.perf_counter() - t0
+    tiles = (S / 1024.0) ** 2
+    return {"value": round(tiles / dt, 6), "unit": "1024^2 tiles/s", "cores": threads, "kind": "port",
+            "sample": f"1 train step (fwd+BCE/Dice+bwd+Adam) on 1 {S}x{S} tile, torch CPU fp32, "
+                      f"{threads} threads ({os.cpu_count()} host CPUs visible), {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import _adipose_pkg  # noqa: F401
+    from adipose_amd import ops
+    from adipose_amd.data import synthetic_batch
+    from adipose_amd.nets import AdiposeV3Net, UNetBN
+    from adipose_amd.trainer import LossConfig, Trainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    B, S = args.batch, args.size
+    if args.preset == "unet_bn":
+        net = UNetBN(B, S, levels=args.levels, base=64, in_ch=3, dtype=args.dtype, device=dev, seed=865)
+        cfg = LossConfig(use_hard_mining=False)
+        C = 3
+    else:
+        net = AdiposeV3Net(B, S, dtype=args.dtype, device=dev, seed=865)
+        cfg = LossConfig()
+        C = None
+    tr = Trainer(net, cfg, lr=1e-4, distributed=world > 1)
+
+    # synthetic histology tiles, resident in HBM before timing (per-rank shard of the data)
+    xs, ys = synthetic_batch(B, S, channels=3, seed=865 + rank)
+    xs = xs.astype(np.float32)
+    if C is None:
+        from adipose_amd.data import to_gray
+        xs = to_gray(xs)
+    mean, std = float(xs.mean()), float(xs.std())
+    x = torch.from_numpy((xs - mean) / (std + 1e-10)).to(dev).contiguous()
+    y = torch.from_numpy(ys).to(dev).contiguous()
+
+    for _ in range(args.warmup):
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+
+    timer = ops.LaunchTimer()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.set_launch_timer(timer)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ops.set_launch_timer(None)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    met = tr.read_metrics()
+    # Dice@val: forward (eval) on a separate seeded synthetic val stream of this workload
+    xv, yv = synthetic_batch(B, S, channels=3, seed=865 + 10_000 + rank)
+    xv = xv.astype(np.float32)
+    if C is None:
+        from adipose_amd.data import to_gray
+        xv = to_gray(xv)
+    tr.eval_step(torch.from_numpy((xv - mean) / (std + 1e-10)).to(dev).contiguous(),
+                 torch.from_numpy(yv).to(dev).contiguous())
+    val = tr.read_metrics()
+
+    summ = timer.summary()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    tiles = B * world * args.steps * (S / 1024.0) ** 2
+    value = tiles / elapsed
+    # roofline of the dominant kernel (largest total time among the GEMM kernels)
+    dom = max(summ.items(), key=lambda kv: kv[1][2])
+    (kname, dcode), (n, flops, ms) = dom
+    dname = "bf16" if dcode == 1 else "f32"
+    sym = {"igemm_fwd": "igemm_fwd_kernel", "igemm_wgrad": "igemm_wgrad_kernel"}[kname]
+    achieved = flops / (ms * 1e-3) / 1e12
+    per_kernel = {f"{k[0]}<{'bf16' if k[1] == 1 else 'f32'}>": {
+        "launches": v[0], "avg_ms": round(v[2] / v[0], 4), "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
+        "share_of_step": round(v[2] / (elapsed * 1e3 / world ** 0), 4)} for k, v in summ.items()}
+    roof = {"bound": "mfma", "kernel": f"{sym}<{dname}>", "achieved": round(achieved, 2),
+            "peak": MI355X_PEAK[dname], "unit": "TFLOP/s", "frac": round(achieved / MI355X_PEAK[dname], 4),
+            "traffic": None, "avg_launch_ms": round(ms / n, 4), "launches": n,
+            "flops_per_launch": round(flops / n / 1e9, 3), "per_kernel": per_kernel}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args)
+        except Exception as e:  # report, never fake
+            cpu = {"value": None, "error": repr(e)}
+    wl = ("unet_bn L5 base64 1024x1024x3 bf16 B=4/GPU DP (BASELINE configs[2])" if args.preset == "unet_bn"
+          else "adipose_v3 (reference topology) train step")
+    line = {
+        "metric": "1024^2 tiles/sec (train)", "value": round(value, 4), "unit": "tiles/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (seeded histology-like tiles, resident in HBM)",
+        "config": {"workload": wl, "preset": args.preset, "levels": args.levels if args.preset == "unet_bn" else 4,
+                   "tile": S, "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+        "train_loss": round(met["loss"], 5), "dice_val": round(val["main_out_dice_coef"], 5),
+        "roofline": roof, "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

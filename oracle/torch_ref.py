@@ -96,7 +96,7 @@ def adipose_v3_forward(x, weights, deep_supervision=True, dropout_masks=None):
     """AdiposeUNetV3.build_model (train_adipose_unet_v3.py:660-758), generalised in S.
     x: (B, S, S) normalised float32. Dropout is identity unless masks are given (inference / parity).
     Returns dict main_out / aux_out1 / aux_out2 of (B, S, S)."""
-    t = lambda a: torch.as_tensor(np.asarray(a))  # noqa: E731
+    t = lambda a: a if torch.is_tensor(a) else torch.as_tensor(np.asarray(a))  # noqa: E731
     W = {k: [t(v[0]), t(v[1])] for k, v in weights.items()}
     S = x.shape[1]
     h = x.reshape(x.shape[0], S, S, 1)
@@ -170,7 +170,7 @@ def bn_relu_train(z, gamma, beta, eps=1e-5):
 
 def unet_bn_forward(x, weights, levels=5):
     """x: (B,S,S,C_in) NHWC; training-mode BatchNorm (batch statistics). Returns (B,S,S) sigmoid."""
-    t = lambda a: torch.as_tensor(np.asarray(a))  # noqa: E731
+    t = lambda a: a if torch.is_tensor(a) else torch.as_tensor(np.asarray(a))  # noqa: E731
     W = {k: [t(v) for v in vs] for k, vs in weights.items()}
 
     def blk(name, inp):

@@ -1,0 +1,180 @@
+"""Whole-network parity of the HIP engine against the CPU fp32 oracle (oracle/torch_ref.py).
+
+adipose_v3 (reference topology, train_adipose_unet_v3.py:660-758) and unet_bn (north-star preset)
+on identical weights and seeded inputs:
+  * f32: forward probabilities within 1e-4 abs; per-layer parameter gradients of the reference loss
+    (OHEM main + 0.4/0.3 aux BCE+Dice, dropout off) within 1e-3 relative; Dice/IoU of the thresholded
+    predictions within 1e-4 (BASELINE.json north_star acceptance).
+  * bf16: reported-only precision — forward within 2e-2 abs, gradients cosine >= 0.99.
+"""
+import numpy as np
+import pytest
+import torch
+
+from adipose_amd import ops
+from adipose_amd.nets import AdiposeV3Net, UNetBN
+from adipose_amd.trainer import LossConfig, Trainer
+from oracle import numpy_ref as NR
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def synth_batch(B, S, C=None, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((B, S, S) if C is None else (B, S, S, C), generator=g)
+    yy, xx = torch.meshgrid(torch.arange(S), torch.arange(S), indexing="ij")
+    y = torch.zeros(B, S, S)
+    for b in range(B):
+        cy, cx = torch.randint(0, S, (2,), generator=g)
+        y[b] = (((yy - cy) ** 2 + (xx - cx) ** 2) < (S / 3) ** 2).float()
+    return x, y
+
+
+def cos(a, b):
+    a, b = a.flatten().double(), b.flatten().double()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def adipose_weights():
+    return R.adipose_v3_keras_weights(seed=865)
+
+
+def build_adipose(dtype, weights, B=2, S=64):
+    net = AdiposeV3Net(B, S, dtype=dtype, device=DEV)
+    net.set_weights(weights)
+    return net
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_adipose_forward(dtype, adipose_weights):
+    B, S = 2, 64
+    x, _ = synth_batch(B, S)
+    net = build_adipose(dtype, adipose_weights, B, S)
+    a = net.acts(B)
+    ops.prep_input(x.to(DEV), a["x"], mean=0.0, std=1.0)
+    outs = net.forward(B, train=False)
+    ref = R.adipose_v3_forward(x, adipose_weights)
+    tol = 1e-4 if dtype == "f32" else 2e-2
+    for k in ("main_out", "aux_out1", "aux_out2"):
+        err = (outs[k].cpu() - ref[k]).abs().max().item()
+        assert err < tol, (k, err)
+    if dtype == "f32":
+        # thresholded Dice/IoU parity (calculate_pixel_metrics, full_evaluation_enhanced.py:721-785)
+        for b in range(B):
+            truth = (ref["main_out"][b] > 0.5).numpy().astype(np.float32)
+            m_gpu = NR.calculate_pixel_metrics(outs["main_out"][b].cpu().numpy(), truth)
+            m_ref = NR.calculate_pixel_metrics(ref["main_out"][b].numpy(), truth)
+            assert abs(m_gpu["dice_score"] - m_ref["dice_score"]) < 1e-4
+            assert abs(m_gpu["jaccard_index"] - m_ref["jaccard_index"]) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("hard_mining", [True, False])
+def test_adipose_grads(dtype, hard_mining, adipose_weights):
+    B, S = 2, 64
+    x, y = synth_batch(B, S, seed=4)
+    net = build_adipose(dtype, adipose_weights, B, S)
+    tr = Trainer(net, LossConfig(use_hard_mining=hard_mining))
+    a = net.acts(B)
+    ops.prep_input(x.to(DEV), a["x"], mean=0.0, std=1.0)
+    outs = net.forward(B, train=False)
+    grads = tr.loss_and_grads(outs, y.to(DEV))
+    ops.fill(net.ps.grad, 0.0)
+    net.backward(grads)
+    torch.cuda.synchronize()
+    # oracle
+    W = {k: [torch.tensor(v[0], requires_grad=True), torch.tensor(v[1], requires_grad=True)]
+         for k, v in adipose_weights.items()}
+    ref_out = R.adipose_v3_forward(x, {k: v for k, v in W.items()})
+    loss = R.ds_total_loss(y, ref_out, use_hard_mining=hard_mining)
+    loss.backward()
+    met = tr.read_metrics()
+    assert abs(met["loss"] - loss.item()) < (1e-4 if dtype == "f32" else 2e-2) * max(1, abs(loss.item()))
+    for name, (k, b) in W.items():
+        gk, gb = net.get_layer_grads(name)
+        if dtype == "f32":
+            rk = (torch.as_tensor(gk) - k.grad).abs().max().item() / max(k.grad.abs().max().item(), 1e-12)
+            rb = (torch.as_tensor(gb) - b.grad).abs().max().item() / max(b.grad.abs().max().item(), 1e-12)
+            assert rk < 1e-3 and rb < 1e-3, (name, rk, rb)
+        else:
+            assert cos(torch.as_tensor(gk), k.grad) > 0.99, name
+
+
+def test_adipose_frozen_encoder_grads(adipose_weights):
+    """Phase 1: encoder frozen -> encoder grads exactly zero, decoder grads unchanged."""
+    B, S = 2, 64
+    x, y = synth_batch(B, S, seed=6)
+    net = build_adipose("f32", adipose_weights, B, S)
+    tr = Trainer(net, LossConfig())
+    a = net.acts(B)
+    ops.prep_input(x.to(DEV), a["x"], mean=0.0, std=1.0)
+    outs = net.forward(B, train=False)
+    grads = tr.loss_and_grads(outs, y.to(DEV))
+    ops.fill(net.ps.grad, 0.0)
+    net.backward(grads)
+    full = {n: net.get_layer_grads(n) for n in ("up1_conv2", "dilate1", "down1_conv1")}
+    tr.set_frozen(AdiposeV3Net.ENCODER)
+    outs = net.forward(B, train=False)
+    grads = tr.loss_and_grads(outs, y.to(DEV))
+    ops.fill(net.ps.grad, 0.0)
+    net.backward(grads)
+    assert np.abs(net.get_layer_grads("down1_conv1")[0]).max() == 0.0
+    for n in ("up1_conv2", "dilate1"):
+        np.testing.assert_allclose(net.get_layer_grads(n)[0], full[n][0], rtol=1e-5, atol=1e-9)
+
+
+def test_adipose_train_step_adam(adipose_weights):
+    """Two full train steps (f32, dropout off) vs oracle autograd + Keras Adam."""
+    B, S = 2, 32
+    x, y = synth_batch(B, S, seed=8)
+    net = build_adipose("f32", adipose_weights, B, S)
+    net.dropout_rate = 0.0
+    tr = Trainer(net, LossConfig(), lr=1e-3)
+    W = {k: [torch.tensor(v[0], requires_grad=True), torch.tensor(v[1], requires_grad=True)]
+         for k, v in adipose_weights.items()}
+    params = [p for v in W.values() for p in v]
+    opt = R.KerasAdam(params, lr=1e-3)
+    for _ in range(2):
+        tr.train_step(x.to(DEV), y.to(DEV))
+        for p in params:
+            p.grad = None
+        R.ds_total_loss(y, R.adipose_v3_forward(x, W)).backward()
+        opt.step([p.grad for p in params])
+    torch.cuda.synchronize()
+    for name, (k, b) in W.items():
+        gk, gb = net.get_layer_weights(name)
+        assert (torch.as_tensor(gk) - k.detach()).abs().max().item() < 1e-4, name
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_unet_bn_forward_and_grads(dtype):
+    B, S, L = 2, 32, 3
+    w = R.unet_bn_keras_weights(levels=L, base=16, in_ch=3, seed=5)
+    x, y = synth_batch(B, S, C=3, seed=9)
+    net = UNetBN(B, S, levels=L, base=16, in_ch=3, dtype=dtype, device=DEV)
+    net.set_weights(w)
+    tr = Trainer(net, LossConfig(use_hard_mining=False))
+    a = net.acts(B)
+    ops.prep_input(x.to(DEV), a["x"], mean=0.0, std=1.0)
+    outs = net.forward(B, train=True)
+    grads = tr.loss_and_grads(outs, y.to(DEV))
+    ops.fill(net.ps.grad, 0.0)
+    net.backward(grads)
+    torch.cuda.synchronize()
+    W = {k: [torch.tensor(v, requires_grad=True) for v in vs] for k, vs in w.items()}
+    p = R.unet_bn_forward(x, W, levels=L)
+    loss = R.combined_loss_standard(y, p)
+    loss.backward()
+    tol = 1e-4 if dtype == "f32" else 3e-2
+    assert (outs["main_out"].cpu() - p.detach()).abs().max().item() < tol
+    for name, ts in W.items():
+        got = net.get_layer_grads(name)
+        for gi, t in zip(got, ts):
+            if dtype == "f32":
+                r = (torch.as_tensor(gi) - t.grad).abs().max().item() / max(t.grad.abs().max().item(), 1e-12)
+                assert r < 2e-3, (name, r)
+            else:
+                assert cos(torch.as_tensor(gi), t.grad) > 0.95, name  # bf16 dz storage through BN bwd
