@@ -53,6 +53,7 @@ _S = C.c_size_t
 # name -> argtypes (restype is always c_int)
 _SIGS = {
     "adp_abi_version": [],
+    "adp_set_option": [C.c_char_p, _I],
     "adp_conv_fwd": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P],
     "adp_conv_wgrad": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P, _I, _P, _P, _P],
     "adp_pack_weights": [_I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _P],
@@ -63,7 +64,8 @@ _SIGS = {
     "adp_cast": [_I, _I, _S, _P, _P, _P],
     "adp_fill_f32": [_S, _F, _P, _P],
     "adp_bn_finalize": [_I, _F, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P],
-    "adp_bn_bwd_reduce": [_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "adp_bn_apply": [_I, _S, _I, _P, _P, _P, _P, _P],
+    "adp_bn_bwd_reduce":[_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "adp_bn_bwd_apply": [_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P],
     "adp_head_softmax2_fwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "adp_head_softmax2_bwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P],
@@ -77,7 +79,7 @@ _SIGS = {
     "adp_pixel_counts": [_S, _P, _P, _F, _P, _P],
     "adp_adam": [_S, _P, _P, _P, _P, _F, _F, _F, _F, _I, _F, _F, _P],
     "adp_ema": [_S, _P, _P, _F, _P],
-    "adp_prep_input": [_I, _I, _I, _I, _I, _P, _F, _F, _I, _I, _P, _P],
+    "adp_prep_input": [_I, _I, _I, _I, _I, _P, C.c_longlong, C.c_longlong, _F, _F, _I, _I, _P, _P],
     "adp_tta_merge": [_I, _I, _I, C.POINTER(C.c_int), _P, _P, _P],
     "adp_blend_accum": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "adp_blend_finalize": [_S, _P, _P, _F, _P, _P],

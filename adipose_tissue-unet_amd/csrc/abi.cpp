@@ -1,5 +1,7 @@
 // Library-level C ABI: error plumbing and version. Kernels live in the *.hip translation units.
 #include <hip/hip_runtime.h>
+#include <map>
+#include <mutex>
 #include <string>
 #include "../../include/adipose_hip.h"
 
@@ -14,7 +16,24 @@ int check_launch(const char* what) {
   }
   return 0;
 }
+static std::mutex g_opt_mu;
+static std::map<std::string, int>& opts() {
+  static std::map<std::string, int> m;
+  return m;
+}
+int option(const char* name, int dflt) {
+  std::lock_guard<std::mutex> lk(g_opt_mu);
+  auto it = opts().find(name);
+  return it == opts().end() ? dflt : it->second;
+}
 }  // namespace adp
+
+extern "C" int adp_set_option(const char* name, int value) {
+  if (!name) return -1;
+  std::lock_guard<std::mutex> lk(adp::g_opt_mu);
+  adp::opts()[name] = value;
+  return 0;
+}
 
 extern "C" const char* adp_last_error(void) { return adp::g_err.c_str(); }
 extern "C" int adp_abi_version(void) { return ADP_ABI_VERSION; }

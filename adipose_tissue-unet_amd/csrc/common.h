@@ -87,6 +87,7 @@ ADP_DEV float wave_sum(float v) {
 namespace adp {
 void set_error(const std::string& msg);
 int check_launch(const char* what);
+int option(const char* name, int dflt);  // runtime switches set through adp_set_option
 }  // namespace adp
 #define ADP_REQUIRE(cond, msg)          \
   do {                                  \

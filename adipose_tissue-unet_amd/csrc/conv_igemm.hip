@@ -17,6 +17,7 @@
 // Tiling: 256 threads = 4 waves (2x2), block tile 128(M pixels) x 64(N channels) x 32(K), register-
 // staged double-buffered LDS, v_mfma_f32_16x16x32_bf16 (bf16) or v_mfma_f32_16x16x4_f32 (f32, exact).
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
@@ -130,6 +131,79 @@ ADP_DEV int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
+// Shared epilogue of the forward-shaped kernels: acc[mi][ni] holds the 16x16 MFMA tile whose
+// rows are mbase + mi*16 + 4*(lane>>4) + r and columns nbase + ni*16 + (lane&15).
+template <typename T, int MI, int NI>
+ADP_DEV void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[MI][NI], int mbase, int nbase, int lane) {
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+  const int HWo = a.Ho * a.Wo;
+  float bsum[NI], bsq[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) { bsum[ni] = 0.f; bsq[ni] = 0.f; }
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int n = nbase + ni * 16 + col;
+    const bool nvalid = n < a.Nout;
+    const float bias = (nvalid && a.bias) ? a.bias[a.out_mode == 1 ? n % a.Cps : n] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mbase + mi * 16 + rq + r;
+        if (!nvalid || m >= a.M) continue;
+        float v = acc[mi][ni][r] + bias;
+        if (a.relu) v = fmaxf(v, 0.f);
+        if (a.drop_rate > 0.f) {
+          float u = adp_uniform(a.drop_seed, (uint64_t)m * (uint64_t)a.Nout + n);
+          v = (u >= a.drop_rate) ? v * (1.f / (1.f - a.drop_rate)) : 0.f;
+        }
+        if (a.out_mode == 1) {
+          // ConvTranspose 2x2/s2: n = sub*Cps + c, sub = 2*dy + dx
+          int sub = n / a.Cps, c = n - sub * a.Cps;
+          int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+          size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
+          reinterpret_cast<T*>(a.out)[pix * a.out_stride + c] = from_f<T>(v);
+          if (a.bn_sum) { bsum[ni] += v; bsq[ni] += v * v; }
+          continue;
+        }
+        if (a.out_mode == 2 && n >= a.split_c) {
+          const int c = n - a.split_c;
+          if (a.mask2) {
+            float mv = to_f(reinterpret_cast<const T*>(a.mask2)[(size_t)m * a.mask2_stride + c]);
+            v = mv > 0.f ? v * a.mask2_scale : 0.f;
+          }
+          reinterpret_cast<T*>(a.out2)[(size_t)m * a.out2_stride + c] = from_f<T>(v);
+          continue;
+        }
+        if (!a.out) continue;
+        if (a.addend) v += to_f(reinterpret_cast<const T*>(a.addend)[(size_t)m * a.addend_stride + n]);
+        if (a.mask) {
+          float mv = to_f(reinterpret_cast<const T*>(a.mask)[(size_t)m * a.mask_stride + n]);
+          v = mv > 0.f ? v * a.mask_scale : 0.f;
+        }
+        const T vs = from_f<T>(v);
+        reinterpret_cast<T*>(a.out)[(size_t)m * a.out_stride + n] = vs;
+        if (a.accum) a.accum[(size_t)m * a.accum_stride + n] += to_f(vs);
+        if (a.bn_sum) { bsum[ni] += v; bsq[ni] += v * v; }
+      }
+    }
+  }
+  if (a.bn_sum) {
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      float s = bsum[ni], q = bsq[ni];
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      const int n = nbase + ni * 16 + col;
+      if (lane < 16 && n < a.Nout) {
+        int c = a.out_mode == 1 ? n % a.Cps : n;
+        atomicAdd(a.bn_sum + c, s);
+        atomicAdd(a.bn_sq + c, q);
+      }
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void igemm_fwd_kernel(FwdArgs a) {
   constexpr int LDK = LdsTr<T>::LDK;
@@ -200,71 +274,369 @@ __global__ __launch_bounds__(NT) void igemm_fwd_kernel(FwdArgs a) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  const int col = lane & 15, rq = (lane >> 4) * 4;
-  float bsum[2] = {0.f, 0.f}, bsq[2] = {0.f, 0.f};
+  fwd_epilogue<T, 4, 2>(a, acc, m0 + wr * 64, n0 + wc * 32, lane);
+}
+
+// LDS-staged epilogue of the bf16 throughput kernel: every wave dumps its f32 accumulators into a
+// [BM][BN+4] LDS tile, then each thread finishes whole 8-channel groups (16-B loads of addend/mask,
+// 16-B stores), keeping per-thread BN partial sums for a fixed channel group.
+template <int BM, int BN>
+ADP_DEV void fwd_epilogue_lds(const FwdArgs& a, f32x4 (&acc)[4][4], float* tile, int m0, int n0, int wr,
+                              int wc, int tid) {
+  constexpr int LT = BN + 4;
+  constexpr int GPR = BN / 8;                 // groups per tile row
+  constexpr int NG = BM * GPR / NT;           // groups per thread
+  const int lane = tid & 63, col = lane & 15, rq = (lane >> 4) * 4;
+  __syncthreads();  // main loop LDS reads done before the tile overwrites the staging buffers
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int n = n0 + wc * 32 + ni * 16 + col;
-    const bool nvalid = n < a.Nout;
-    const float bias = (nvalid && a.bias) ? a.bias[a.out_mode == 1 ? n % a.Cps : n] : 0.f;
+  for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
+    for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 64 + mi * 16 + rq + r;
-        if (!nvalid || m >= a.M) continue;
-        float v = acc[mi][ni][r] + bias;
-        if (a.relu) v = fmaxf(v, 0.f);
-        if (a.drop_rate > 0.f) {
-          float u = adp_uniform(a.drop_seed, (uint64_t)m * (uint64_t)a.Nout + n);
-          v = (u >= a.drop_rate) ? v * (1.f / (1.f - a.drop_rate)) : 0.f;
-        }
-        if (a.out_mode == 1) {
-          // ConvTranspose 2x2/s2: n = sub*Cps + c, sub = 2*dy + dx
-          int sub = n / a.Cps, c = n - sub * a.Cps;
-          int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
-          size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
-          reinterpret_cast<T*>(a.out)[pix * a.out_stride + c] = from_f<T>(v);
-          if (a.bn_sum) { bsum[ni] += v; bsq[ni] += v * v; }
-          continue;
-        }
-        if (a.out_mode == 2 && n >= a.split_c) {
-          const int c = n - a.split_c;
-          if (a.mask2) {
-            float mv = to_f(reinterpret_cast<const T*>(a.mask2)[(size_t)m * a.mask2_stride + c]);
-            v = mv > 0.f ? v * a.mask2_scale : 0.f;
-          }
-          reinterpret_cast<T*>(a.out2)[(size_t)m * a.out2_stride + c] = from_f<T>(v);
-          continue;
-        }
-        if (!a.out) continue;
-        if (a.addend) v += to_f(reinterpret_cast<const T*>(a.addend)[(size_t)m * a.addend_stride + n]);
-        if (a.mask) {
-          float mv = to_f(reinterpret_cast<const T*>(a.mask)[(size_t)m * a.mask_stride + n]);
-          v = mv > 0.f ? v * a.mask_scale : 0.f;
-        }
-        const T vs = from_f<T>(v);
-        reinterpret_cast<T*>(a.out)[(size_t)m * a.out_stride + n] = vs;
-        if (a.accum) a.accum[(size_t)m * a.accum_stride + n] += to_f(vs);
-        if (a.bn_sum) { bsum[ni] += v; bsq[ni] += v * v; }
+      for (int r = 0; r < 4; ++r)
+        tile[(wr * 64 + mi * 16 + rq + r) * LT + wc * 64 + ni * 16 + col] = acc[mi][ni][r];
+  __syncthreads();
+  const int cg = tid % GPR;
+  const int n = n0 + cg * 8;
+  const bool nvalid = n < a.Nout;
+  const int HWo = a.Ho * a.Wo;
+  float bias[8], bs[8], bq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bs[j] = 0.f; bq[j] = 0.f;
+    bias[j] = (nvalid && a.bias) ? a.bias[a.out_mode == 1 ? (n + j) % a.Cps : n + j] : 0.f;
+  }
+  for (int g = 0; g < NG; ++g) {
+    const int row = (tid + g * NT) / GPR;
+    const int m = m0 + row;
+    if (!nvalid || m >= a.M) continue;
+    float v[8];
+    const float4* tp = reinterpret_cast<const float4*>(tile + row * LT + cg * 8);
+    float4 t0 = tp[0], t1 = tp[1];
+    v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w; v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] += bias[j];
+      if (a.relu) v[j] = fmaxf(v[j], 0.f);
+    }
+    if (a.drop_rate > 0.f) {
+      const float ks = 1.f / (1.f - a.drop_rate);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float u = adp_uniform(a.drop_seed, (uint64_t)m * (uint64_t)a.Nout + n + j);
+        v[j] = (u >= a.drop_rate) ? v[j] * ks : 0.f;
       }
+    }
+    Grp<bf16> gr;
+    if (a.out_mode == 1) {
+      int sub = n / a.Cps, c = n - sub * a.Cps;
+      int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+      size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
+      grp_from_f(gr, v);
+      grp_store(gr, reinterpret_cast<bf16*>(a.out) + pix * a.out_stride + c);
+    } else if (a.out_mode == 2 && n >= a.split_c) {
+      const int c = n - a.split_c;
+      if (a.mask2) {
+        float mk[8];
+        grp_load(gr, reinterpret_cast<const bf16*>(a.mask2) + (size_t)m * a.mask2_stride + c);
+        grp_to_f(gr, mk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.f ? v[j] * a.mask2_scale : 0.f;
+      }
+      grp_from_f(gr, v);
+      grp_store(gr, reinterpret_cast<bf16*>(a.out2) + (size_t)m * a.out2_stride + c);
+      continue;
+    } else {
+      if (!a.out) continue;
+      float f[8];
+      if (a.addend) {
+        grp_load(gr, reinterpret_cast<const bf16*>(a.addend) + (size_t)m * a.addend_stride + n);
+        grp_to_f(gr, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += f[j];
+      }
+      if (a.mask) {
+        grp_load(gr, reinterpret_cast<const bf16*>(a.mask) + (size_t)m * a.mask_stride + n);
+        grp_to_f(gr, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f[j] > 0.f ? v[j] * a.mask_scale : 0.f;
+      }
+      grp_from_f(gr, v);
+      grp_store(gr, reinterpret_cast<bf16*>(a.out) + (size_t)m * a.out_stride + n);
+      if (a.accum) {
+        float* ap = a.accum + (size_t)m * a.accum_stride + n;
+        float r[8];
+        grp_to_f(gr, r);   // accumulate the value as stored (bf16-rounded), like the generic path
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ap[j] += r[j];
+      }
+    }
+    if (a.bn_sum) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { bs[j] += v[j]; bq[j] += v[j] * v[j]; }
     }
   }
   if (a.bn_sum) {
+    // threads with equal cg hold partials of the same 8 channels: reduce through LDS, then atomics
+    __syncthreads();
+    float* red = tile;
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      float s = bsum[ni], q = bsq[ni];
-      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-      const int n = n0 + wc * 32 + ni * 16 + col;
-      if (lane < 16 && n < a.Nout) {
-        int c = a.out_mode == 1 ? n % a.Cps : n;
+    for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = bs[j]; red[tid * 16 + 8 + j] = bq[j]; }
+    __syncthreads();
+    if (tid < BN) {
+      const int gg = tid >> 3, j = tid & 7;
+      float s = 0.f, q = 0.f;
+      for (int t = gg; t < NT; t += GPR) { s += red[t * 16 + j]; q += red[t * 16 + 8 + j]; }
+      const int nn = n0 + tid;
+      if (nn < a.Nout) {
+        const int c = a.out_mode == 1 ? nn % a.Cps : nn;
         atomicAdd(a.bn_sum + c, s);
         atomicAdd(a.bn_sq + c, q);
       }
     }
   }
+}
+
+// --------------------------------------------------------------- bf16 throughput forward kernel
+// 4 waves, each owning a 64x64 output tile (16 accumulators of 16x16), block tile BM x BN with
+// BM*BN = 4*64*64, BK = 64 per LDS stage (two MFMA k-substeps per barrier, 32 MFMAs per wave per
+// barrier), register-staged double buffer, 2 blocks per CU. Same gather/epilogue semantics as
+// igemm_fwd_kernel.
+template <int BM, int BN>
+__global__ __launch_bounds__(NT, 2) void igemm_fwd_bf16_kernel(FwdArgs a) {
+  constexpr int WN = BN / 64;
+  constexpr int LDK = 64 + 8;            // 144-B rows
+  constexpr int AG = BM / 32, BG = BN / 32;  // 16-B groups per thread per stage
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * LDK];
+  // stage b: A tile at smem + b*(BM+BN)*LDK, B tile right after it
+#define ADP_AS(b) (smem + (b) * (BM + BN) * LDK)
+#define ADP_BS(b) (smem + (b) * (BM + BN) * LDK + BM * LDK)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int lin = xcd_remap(blockIdx.x, a.nblocks);
+  const int tn = lin % a.ntile_n, tm = lin / a.ntile_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kg = tid & 7, prow = tid >> 3;   // group column (8 per 64-wide k row), base row
+
+  int an[AG], ay[AG], ax[AG];
+  bool av[AG];
+  const int HWo = a.Ho * a.Wo;
+#pragma unroll
+  for (int i = 0; i < AG; ++i) {
+    int m = m0 + prow + 32 * i;
+    av[i] = m < a.M;
+    int mm = av[i] ? m : 0;
+    an[i] = mm / HWo;
+    int rem = mm - an[i] * HWo;
+    int yo = rem / a.Wo;
+    ay[i] = yo * a.stride;
+    ax[i] = (rem - yo * a.Wo) * a.stride;
+  }
+  const int Cin_s = a.CAs + a.CBs;
+  int k = kg * 8;
+  int tap = k / Cin_s, ci = k - tap * Cin_s;
+  const bf16* Wp = reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + prow) * a.Kpad + kg * 8;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Grp<bf16> ga[AG], gb[BG];
+  const int nk = (a.Kpad + 63) / 64;
+  auto load_stage = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < AG; ++i) load_a_group<bf16>(a, ga[i], av[i], an[i], ay[i], ax[i], tap, ci, k);
+    const bool kin = kt * 64 + kg * 8 < a.Kpad;
+#pragma unroll
+    for (int j = 0; j < BG; ++j) {
+      if (kin) grp_load(gb[j], Wp + (size_t)(32 * j) * a.Kpad + (size_t)kt * 64);
+      else grp_zero(gb[j]);
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AG; ++i) grp_store(ga[i], ADP_AS(buf) + (prow + 32 * i) * LDK + kg * 8);
+#pragma unroll
+    for (int j = 0; j < BG; ++j) grp_store(gb[j], ADP_BS(buf) + (prow + 32 * j) * LDK + kg * 8);
+  };
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  const int r = lane & 15, kq = (lane >> 4) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      k += 64; ci += 64;
+      while (ci >= Cin_s) { ci -= Cin_s; ++tap; }
+      load_stage(kt + 1);
+    }
+    const bf16* A = ADP_AS(cur) + (wr * 64 + r) * LDK + kq;
+    const bf16* Bq = ADP_BS(cur) + (wc * 64 + r) * LDK + kq;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 b[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) b[ni] = *reinterpret_cast<const bf16x8*>(Bq + ni * 16 * LDK + s * 32);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        bf16x8 av8 = *reinterpret_cast<const bf16x8*>(A + mi * 16 * LDK + s * 32);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av8, b[ni], acc[mi][ni], 0, 0, 0);
+      }
+    }
+    if (more) store_stage(cur ^ 1);
+    __syncthreads();
+  }
+  fwd_epilogue_lds<BM, BN>(a, acc, reinterpret_cast<float*>(smem), m0, n0, wr, wc, tid);
+#undef ADP_AS
+#undef ADP_BS
+}
+
+// ------------------------------------------------------ bf16 forward kernel, LDS-DMA staged ("glds")
+// Same GEMM decomposition as igemm_fwd_bf16_kernel (4 waves x 64x64, BK = 64) but both operands are
+// moved HBM/L2 -> LDS by global_load_lds_dwordx4 (no VGPR staging, so a whole stage is in flight per
+// wave while the previous stage computes). The implicit-GEMM gather is the per-lane SOURCE address;
+// padding taps read a zero page. The LDS image is linear (128-B rows, 8 x 16-B chunks); chunk c of
+// tile row r is stored at position c ^ ((r >> 1) & 7), a swizzle that makes the ds_read_b128 fragment
+// reads of the 16x16x32 MFMA bank-conflict free. No BN-on-load (the BN preset materialises its
+// activations for this path).
+__device__ __attribute__((aligned(256))) uint4 adp_zero_page[64];
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+ADP_DEV int swz(int r) { return (r >> 1) & 7; }
+
+template <int BM, int BN>
+__global__ __launch_bounds__(NT, 2) void igemm_fwd_glds_kernel(FwdArgs a) {
+  constexpr int WN = BN / 64;
+  constexpr int ROWB = 128;                         // bytes per LDS row (64 bf16)
+  constexpr int STAGE = (BM + BN) * ROWB;           // bytes per stage
+  constexpr int AI = BM / 32, BI = BN / 32;         // glds instructions per wave per stage
+  constexpr int EPI = BM * (BN + 4) * 4;            // epilogue tile bytes
+  constexpr int SMEM = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int lin = xcd_remap(blockIdx.x, a.nblocks);
+  const int tn = lin % a.ntile_n, tm = lin / a.ntile_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lrow = lane >> 3, pos = lane & 7;
+  const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
+  const int Cin_s = a.CAs + a.CBs;
+  const int Wrows = (a.Nout + 63) / 64 * 64;
+
+  // A: this wave loads tile rows [wave*BM/4, (wave+1)*BM/4), 8 rows per instruction
+  int a_n[AI], a_y[AI], a_x[AI], a_tap[AI], a_ci[AI], a_ty[AI], a_tx[AI], a_k[AI];
+  bool a_v[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = wave * (BM / 4) + 8 * i + lrow;
+    const int m = m0 + r;
+    a_v[i] = m < a.M;
+    const int mm = a_v[i] ? m : 0;
+    a_n[i] = mm / HWo;
+    const int rem = mm - a_n[i] * HWo, yo = rem / a.Wo;
+    a_y[i] = yo * a.stride - a.pad;
+    a_x[i] = (rem - yo * a.Wo) * a.stride - a.pad;
+    const int c = pos ^ swz(r);
+    a_k[i] = 8 * c;
+    a_tap[i] = a_k[i] / Cin_s;
+    a_ci[i] = a_k[i] - a_tap[i] * Cin_s;
+    a_ty[i] = a_tap[i] / a.kw;
+    a_tx[i] = a_tap[i] - a_ty[i] * a.kw;
+  }
+  // B: tile rows [wave*BN/4, ...)
+  const bf16* b_src[BI];
+  int b_c[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int r = wave * (BN / 4) + 8 * i + lrow;
+    b_c[i] = pos ^ swz(r);
+    b_src[i] = (n0 + r < Wrows) ? reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + r) * a.Kpad + 8 * b_c[i] : nullptr;
+  }
+  const bf16* srcA = reinterpret_cast<const bf16*>(a.srcA);
+  const bf16* srcB = reinterpret_cast<const bf16*>(a.srcB);
+
+  auto issue = [&](int kt, int buf) {
+    unsigned char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const void* p = adp_zero_page;
+      if (a_v[i] && a_k[i] < a.K) {
+        int yi = a_y[i] + a_ty[i] * a.dil, xi = a_x[i] + a_tx[i] * a.dil;
+        if (yi >= 0 && xi >= 0 && yi < Hv && xi < Wv) {
+          if (a.up == 2) { yi >>= 1; xi >>= 1; }
+          const size_t pix = ((size_t)a_n[i] * a.Hs + yi) * a.Ws + xi;
+          p = a_ci[i] < a.CAs ? (const void*)(srcA + pix * a.CAs + a_ci[i])
+                              : (const void*)(srcB + pix * a.CBs + (a_ci[i] - a.CAs));
+        }
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(sb + (wave * (BM / 4) + 8 * i) * ROWB), 16, 0, 0);
+      // advance this slot's K position by one stage (64)
+      a_k[i] += 64;
+      a_ci[i] += 64;
+      while (a_ci[i] >= Cin_s) {
+        a_ci[i] -= Cin_s;
+        if (++a_tx[i] == a.kw) { a_tx[i] = 0; ++a_ty[i]; }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const void* p = adp_zero_page;
+      if (b_src[i] && kt * 64 + 8 * b_c[i] < a.Kpad) p = b_src[i] + (size_t)kt * 64;
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(sb + BM * ROWB + (wave * (BN / 4) + 8 * i) * ROWB), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.Kpad + 63) / 64;
+  const int r16 = lane & 15, h = lane >> 4;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AI + BI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const unsigned char* sA = smem + cur * STAGE;
+    const unsigned char* sB = sA + BM * ROWB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 4 * s + h;
+      bf16x8 b[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int row = wc * 64 + ni * 16 + r16;
+        b[ni] = *reinterpret_cast<const bf16x8*>(sB + row * ROWB + ((c ^ swz(row)) << 4));
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = wr * 64 + mi * 16 + r16;
+        const bf16x8 av8 = *reinterpret_cast<const bf16x8*>(sA + row * ROWB + ((c ^ swz(row)) << 4));
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av8, b[ni], acc[mi][ni], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  fwd_epilogue_lds<BM, BN>(a, acc, reinterpret_cast<float*>(smem), m0, n0, wr, wc, tid);
 }
 
 // ------------------------------------------------------------------------------------ wgrad
@@ -422,6 +794,381 @@ __global__ __launch_bounds__(NT) void igemm_wgrad_kernel(WgradArgs a) {
     atomicAdd(a.dB + (a.dy_mode == 1 ? (n0 + tid) % a.Cps : n0 + tid), dbacc);
 }
 
+// ------------------------------------------------------------------- bf16 throughput wgrad kernel
+// dW[n][k] += sum_m dY[m][n] X(k)[m]. Block tile TN (n) x TK (k); 4 waves, each a 64x64 output tile;
+// 64 pixels per LDS stage (2 MFMA k-substeps, 32 MFMAs per wave per barrier).
+// Both operands are staged in their natural [pixel][channel] layout (coalesced 16-B loads, one
+// ds_write_b128 per group) and fed to v_mfma_f32_16x16x32_bf16 with ds_read_b64_tr_b16, which
+// transposes on the read (MFMA k = pixel). The pixel (reduction) order inside a 32-pixel substep is
+// permuted, rho(8g+e) = 16(g>>1) + 8(e>>2) + 4(g&1) + (e&3), so that the 8 rows one 32-lane half reads
+// are 8 consecutive LDS rows; with row strides of 32*odd bytes that read is bank-conflict free.
+typedef short v4s16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s16 lds_v4s16;
+
+ADP_DEV bf16x8 tr_frag(const bf16* lds_base, int row0, int rowstride_el, int col0, int lane) {
+  // lane (g = lane>>4, i = lane&15 = 4q+p) -> 8 consecutive k (pixels) of column col0 + i
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int rlo = 16 * (g >> 1) + 4 * (g & 1) + q;   // e = q      (rho(8g+q))
+  const bf16* a0 = lds_base + (row0 + rlo) * rowstride_el + col0 + 4 * p;
+  const bf16* a1 = a0 + 8 * rowstride_el;             // e = 4 + q  (rho(8g+4+q))
+  v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a0));
+  v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a1));
+  bf16x8 r;
+  const bf16* l = reinterpret_cast<const bf16*>(&lo);
+  const bf16* h = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
+  return r;
+}
+
+template <int TN, int TK>
+__global__ __launch_bounds__(NT, 2) void igemm_wgrad_bf16_kernel(WgradArgs a) {
+  constexpr int MS = 64;                        // pixels per stage
+  constexpr int LX = TK + 16, LD = TN + 16;     // row strides (elements): 2*T + 32 bytes
+  constexpr int WK = TK / 64;                   // waves along k
+  constexpr int GXR = TK / 8, GDR = TN / 8;     // 16-B groups per staged row
+  constexpr int GX = MS * GXR / NT, GD = MS * GDR / NT;  // groups per thread
+  constexpr int RX = NT / GXR, RD = NT / GDR;   // row step between a thread's groups
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * MS * (LX + LD)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WK, wk = wave % WK;
+  const int tk = blockIdx.x % a.ntile_k, tn = blockIdx.x / a.ntile_k;
+  const int k0 = tk * TK, n0 = tn * TN;
+  const int mbeg = blockIdx.y * a.mchunk;
+  const int mend = min(a.M, mbeg + a.mchunk);
+  if (mbeg >= mend) return;
+
+  // X staging: fixed k-group per thread -> fixed tap / channel / source
+  const int kgx = tid % GXR, rowx = tid / GXR;
+  const int Cin_s = a.CAs + a.CBs;
+  const int k = k0 + kgx * 8;
+  const bool kvalid = k < a.K;
+  const int tap = kvalid ? k / Cin_s : 0;
+  const int ci = k - tap * Cin_s;
+  const int ty = tap / a.kw, tx = tap - ty * a.kw;
+  const bool useB = ci >= a.CAs;
+  const int cl = useB ? ci - a.CAs : ci;
+  const bf16* src = reinterpret_cast<const bf16*>(useB ? a.srcB : a.srcA);
+  const int cs = useB ? a.CBs : a.CAs;
+  const float* sc = useB ? a.scB : a.scA;
+  const float* sh = useB ? a.shB : a.shA;
+  // dY staging
+  const int cgd = tid % GDR, rowd = tid / GDR;
+  const int nn = n0 + cgd * 8;
+  const bool nvalid = nn < a.Nout;
+  const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
+  const bf16* dy = reinterpret_cast<const bf16*>(a.dY);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool do_bias = a.dB && tk == 0 && nvalid;
+
+  Grp<bf16> gx[GX], gd[GD];
+  auto load_stage = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < GX; ++i) {
+      grp_zero(gx[i]);
+      const int m = mb + rowx + RX * i;
+      if (m < mend && kvalid) {
+        int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+        int yi = yo * a.stride + ty * a.dil - a.pad, xi = xo * a.stride + tx * a.dil - a.pad;
+        if (yi >= 0 && xi >= 0 && yi < Hv && xi < Wv) {
+          if (a.up == 2) { yi >>= 1; xi >>= 1; }
+          grp_load(gx[i], src + (((size_t)nimg * a.Hs + yi) * a.Ws + xi) * cs + cl);
+          if (sc) {
+            float f[8];
+            grp_to_f(gx[i], f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[cl + j], sh[cl + j]), 0.f);
+            grp_from_f(gx[i], f);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GD; ++i) {
+      grp_zero(gd[i]);
+      const int m = mb + rowd + RD * i;
+      if (m < mend && nvalid) {
+        if (a.dy_mode == 0) {
+          grp_load(gd[i], dy + (size_t)m * a.dy_stride + nn);
+        } else {
+          int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+          int sub = nn / a.Cps, c = nn - sub * a.Cps;
+          size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
+          grp_load(gd[i], dy + pix * a.dy_stride + c);
+        }
+        if (do_bias) {
+          float f[8];
+          grp_to_f(gd[i], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bacc[j] += f[j];
+        }
+      }
+    }
+  };
+  auto store_stage = [&](int buf) {
+    bf16* Xs = smem + buf * MS * (LX + LD);
+    bf16* Ds = Xs + MS * LX;
+#pragma unroll
+    for (int i = 0; i < GX; ++i) grp_store(gx[i], Xs + (rowx + RX * i) * LX + kgx * 8);
+#pragma unroll
+    for (int i = 0; i < GD; ++i) grp_store(gd[i], Ds + (rowd + RD * i) * LD + cgd * 8);
+  };
+
+  load_stage(mbeg);
+  store_stage(0);
+  __syncthreads();
+  int buf = 0;
+  for (int mb = mbeg; mb < mend; mb += MS) {
+    const bool more = mb + MS < mend;
+    if (more) load_stage(mb + MS);
+    const bf16* Xs = smem + buf * MS * (LX + LD);
+    const bf16* Ds = Xs + MS * LX;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bx[4];
+#pragma unroll
+      for (int ki = 0; ki < 4; ++ki) bx[ki] = tr_frag(Xs, 32 * s, LX, wk * 64 + ki * 16, lane);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        bf16x8 ad = tr_frag(Ds, 32 * s, LD, wn * 64 + ni * 16, lane);
+#pragma unroll
+        for (int ki = 0; ki < 4; ++ki)
+          acc[ni][ki] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, bx[ki], acc[ni][ki], 0, 0, 0);
+      }
+    }
+    if (more) store_stage(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+    for (int ki = 0; ki < 4; ++ki)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + ni * 16 + rq + r;
+        const int kk = k0 + wk * 64 + ki * 16 + col;
+        if (n < a.Nout && kk < a.K) atomicAdd(a.dW + (size_t)n * a.Kpad + kk, acc[ni][ki][r]);
+      }
+  if (a.dB && tk == 0) {
+    // reduce the per-thread 8-channel partial sums of threads sharing a channel group
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bacc[j];
+    __syncthreads();
+    if (tid < TN) {
+      const int g = tid >> 3, j = tid & 7;
+      float s = 0.f;
+      for (int t = g; t < NT; t += GDR) s += red[t * 8 + j];
+      const int n = n0 + tid;
+      if (n < a.Nout) atomicAdd(a.dB + (a.dy_mode == 1 ? n % a.Cps : n), s);
+    }
+  }
+}
+
+// ---------------------------------------------------------- bf16 wgrad kernel, LDS-DMA staged
+// Operands X[pixel][k] and dY[pixel][n] are moved by global_load_lds into linear rows of RB bytes
+// (RB = 2*TK or 2*TN); 16-B chunk c of row r sits at chunk position c ^ g(r), g(r) = 2*(r & 7) for
+// RB >= 256 and 2*((r >> 1) & 3) for RB = 128, which spreads the 8 rows read by one 32-lane half of a
+// ds_read_b64_tr_b16 over 8 distinct 32-B bank slots. Pixel order inside a 32-pixel substep is the
+// rho permutation of igemm_wgrad_bf16_kernel. The bias gradient is a separate channel-sum launch.
+template <int RB>
+ADP_DEV int gsw(int r) { return RB >= 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }
+
+template <int RB>
+ADP_DEV bf16x8 tr_frag_sw(const unsigned char* base, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = row0 + 16 * (g >> 1) + 4 * (g & 1) + q;
+  const int r1 = r0 + 8;
+  const int col = col0 + 4 * p;
+  const int chunk = col >> 3, inb = (col & 7) * 2;
+  const unsigned char* a0 = base + r0 * RB + ((chunk ^ gsw<RB>(r0)) << 4) + inb;
+  const unsigned char* a1 = base + r1 * RB + ((chunk ^ gsw<RB>(r1)) << 4) + inb;
+  v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a0));
+  v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a1));
+  bf16x8 r;
+  const bf16* l = reinterpret_cast<const bf16*>(&lo);
+  const bf16* h = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
+  return r;
+}
+
+template <int TN, int TK>
+__global__ __launch_bounds__(NT, 2) void igemm_wgrad_glds_kernel(WgradArgs a) {
+  constexpr int MS = 64;
+  constexpr int RX = 2 * TK, RD = 2 * TN;              // row bytes
+  constexpr int SX = MS * RX, SD = MS * RD, STAGE = SX + SD;
+  constexpr int XI = SX / 1024 / 4, DI = SD / 1024 / 4; // glds per wave per stage
+  constexpr int XRPI = 1024 / RX, DRPI = 1024 / RD;     // rows per instruction
+  constexpr int WK = TK / 64;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WK, wk = wave % WK;
+  const int tk = blockIdx.x % a.ntile_k, tn = blockIdx.x / a.ntile_k;
+  const int k0 = tk * TK, n0 = tn * TN;
+  const int mbeg = blockIdx.y * a.mchunk;
+  const int mend = min(a.M, mbeg + a.mchunk);
+  if (mbeg >= mend) return;
+  const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
+  const int Cin_s = a.CAs + a.CBs;
+
+  // X slots: instruction i of this wave covers rows wave*(MS/4) + XRPI*i + lane / (RX/16)
+  int xr[XI], xdy[XI], xdx[XI], xcl[XI];
+  const bf16* xsrc[XI];
+  int xcs[XI];
+  bool xk[XI];
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int r = wave * (MS / 4) + XRPI * i + lane / (RX / 16);
+    const int pos = lane % (RX / 16);
+    const int c = pos ^ gsw<RX>(r);
+    const int k = k0 + 8 * c;
+    xr[i] = r;
+    xk[i] = k < a.K;
+    const int tap = xk[i] ? k / Cin_s : 0;
+    const int ci = k - tap * Cin_s;
+    const int ty = tap / a.kw, tx = tap - ty * a.kw;
+    xdy[i] = ty * a.dil - a.pad;
+    xdx[i] = tx * a.dil - a.pad;
+    const bool useB = ci >= a.CAs;
+    xcl[i] = useB ? ci - a.CAs : ci;
+    xsrc[i] = reinterpret_cast<const bf16*>(useB ? a.srcB : a.srcA);
+    xcs[i] = useB ? a.CBs : a.CAs;
+  }
+  int dr[DI], dn[DI];
+#pragma unroll
+  for (int i = 0; i < DI; ++i) {
+    const int r = wave * (MS / 4) + DRPI * i + lane / (RD / 16);
+    const int pos = lane % (RD / 16);
+    dr[i] = r;
+    dn[i] = n0 + 8 * (pos ^ gsw<RD>(r));
+  }
+  const bf16* dy = reinterpret_cast<const bf16*>(a.dY);
+
+  auto issue = [&](int mb, int buf) {
+    unsigned char* sb = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const void* p = adp_zero_page;
+      const int m = mb + xr[i];
+      if (m < mend && xk[i]) {
+        const int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+        int yi = yo * a.stride + xdy[i], xi = xo * a.stride + xdx[i];
+        if (yi >= 0 && xi >= 0 && yi < Hv && xi < Wv) {
+          if (a.up == 2) { yi >>= 1; xi >>= 1; }
+          p = xsrc[i] + (((size_t)nimg * a.Hs + yi) * a.Ws + xi) * xcs[i] + xcl[i];
+        }
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(sb + (wave * (MS / 4) + XRPI * i) * RX), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const void* p = adp_zero_page;
+      const int m = mb + dr[i];
+      if (m < mend && dn[i] < a.Nout) {
+        if (a.dy_mode == 0) {
+          p = dy + (size_t)m * a.dy_stride + dn[i];
+        } else {
+          const int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+          const int sub = dn[i] / a.Cps, c = dn[i] - sub * a.Cps;
+          const size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
+          p = dy + pix * a.dy_stride + c;
+        }
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(sb + SX + (wave * (MS / 4) + DRPI * i) * RD), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(mbeg, 0);
+  int buf = 0;
+  for (int mb = mbeg; mb < mend; mb += MS) {
+    if (mb + MS < mend) {
+      issue(mb + MS, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(XI + DI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const unsigned char* Xs = smem + buf * STAGE;
+    const unsigned char* Ds = Xs + SX;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 bx[4];
+#pragma unroll
+      for (int ki = 0; ki < 4; ++ki) bx[ki] = tr_frag_sw<RX>(Xs, 32 * s, wk * 64 + ki * 16, lane);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const bf16x8 ad = tr_frag_sw<RD>(Ds, 32 * s, wn * 64 + ni * 16, lane);
+#pragma unroll
+        for (int ki = 0; ki < 4; ++ki)
+          acc[ni][ki] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, bx[ki], acc[ni][ki], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    buf ^= 1;
+  }
+
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+    for (int ki = 0; ki < 4; ++ki)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + ni * 16 + rq + r;
+        const int kk = k0 + wk * 64 + ki * 16 + col;
+        if (n < a.Nout && kk < a.K) atomicAdd(a.dW + (size_t)n * a.Kpad + kk, acc[ni][ki][r]);
+      }
+}
+
+// per-channel sum over pixels (bias gradient); plain [M][C] or pixel-shuffled ConvT gradient
+// (channel n of the GEMM = sub*Cps + c -> bias c)
+template <typename T>
+__global__ void channel_sum_kernel(size_t M, int C, int stride, const T* x, float* out, int fold) {
+  const int G = C >> 3;
+  const int lanes = NT / G;
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (pl < lanes) {
+    for (size_t m = (size_t)blockIdx.x * lanes + pl; m < M; m += (size_t)gridDim.x * lanes) {
+      Grp<T> gr;
+      float f[8];
+      grp_load(gr, x + m * stride + g * 8);
+      grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+  }
+  __shared__ float red[NT * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = s[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    float t = 0.f;
+    for (int l = 0; l < lanes; ++l) t += red[(l * G + (c >> 3)) * 8 + (c & 7)];
+    atomicAdd(out + (fold ? c % fold : c), t);
+  }
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -452,6 +1199,34 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   ADP_REQUIRE(a.M > 0 && a.Nout > 0, "adp_conv_fwd: empty problem");
   ADP_REQUIRE(d->out_mode != 1 || (d->shuffle_c > 0 && d->Nout % d->shuffle_c == 0), "adp_conv_fwd: bad shuffle_c");
   ADP_REQUIRE(d->out_mode != 2 || (io->out2 && d->split_c > 0), "adp_conv_fwd: split store needs out2/split_c");
+  const int fast = adp::option("conv_fast", 2);
+  if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB) {
+    const int w64 = (a.Nout + 63) / 64 * 64 - a.Nout, w128 = (a.Nout + 127) / 128 * 128 - a.Nout;
+    if (a.Nout > 64 && w128 <= w64) {
+      a.ntile_n = (a.Nout + 127) / 128;
+      a.nblocks = ((a.M + 127) / 128) * a.ntile_n;
+      hipLaunchKernelGGL((igemm_fwd_glds_kernel<128, 128>), dim3(a.nblocks), dim3(NT), 0, s, a);
+    } else {
+      a.ntile_n = (a.Nout + 63) / 64;
+      a.nblocks = ((a.M + 255) / 256) * a.ntile_n;
+      hipLaunchKernelGGL((igemm_fwd_glds_kernel<256, 64>), dim3(a.nblocks), dim3(NT), 0, s, a);
+    }
+    return adp::check_launch("adp_conv_fwd");
+  }
+  if (std::is_same<T, bf16>::value && fast >= 1) {
+    // tile choice: least padded-N waste, ties -> 128x128 (more A reuse per block)
+    const int w64 = (a.Nout + 63) / 64 * 64 - a.Nout, w128 = (a.Nout + 127) / 128 * 128 - a.Nout;
+    if (a.Nout > 64 && w128 <= w64) {
+      a.ntile_n = (a.Nout + 127) / 128;
+      a.nblocks = ((a.M + 127) / 128) * a.ntile_n;
+      hipLaunchKernelGGL((igemm_fwd_bf16_kernel<128, 128>), dim3(a.nblocks), dim3(NT), 0, s, a);
+    } else {
+      a.ntile_n = (a.Nout + 63) / 64;
+      a.nblocks = ((a.M + 255) / 256) * a.ntile_n;
+      hipLaunchKernelGGL((igemm_fwd_bf16_kernel<256, 64>), dim3(a.nblocks), dim3(NT), 0, s, a);
+    }
+    return adp::check_launch("adp_conv_fwd");
+  }
   a.ntile_n = (a.Nout + BN - 1) / BN;
   const int ntm = (a.M + BM - 1) / BM;
   a.nblocks = ntm * a.ntile_n;
@@ -475,6 +1250,54 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
   ADP_REQUIRE(a.CAs % 8 == 0 && a.CBs % 8 == 0 && a.Nout % 8 == 0,
               "adp_conv_wgrad: channel strides and Nout must be multiples of 8");
   ADP_REQUIRE(d->out_mode != 2, "adp_conv_wgrad: split-store descriptors are dgrad-only");
+  if (std::is_same<T, bf16>::value && adp::option("conv_fast", 2) == 2 && !a.scA && !a.scB) {
+    const int TN = (a.Nout <= 64 && adp::option("wgrad_glds_tn64", 1)) ? 64 : 128, TK = TN == 64 ? 256 : 128;
+    a.ntile_k = (a.K + TK - 1) / TK;
+    a.ntile_n = (a.Nout + TN - 1) / TN;
+    const int tiles = a.ntile_k * a.ntile_n;
+    int splits = (2048 + tiles - 1) / tiles;
+    const int maxsplit = (a.M + 511) / 512;
+    splits = std::max(1, std::min(splits, maxsplit));
+    a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
+    splits = (a.M + a.mchunk - 1) / a.mchunk;
+    if (TN == 64)
+      hipLaunchKernelGGL((igemm_wgrad_glds_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((igemm_wgrad_glds_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a);
+    if (a.dB) {
+      const int G = a.Nout / 8, lanes = NT / G;
+      const int blocks = (int)std::min<long long>((a.M + lanes - 1) / lanes, 1024);
+      if (a.dy_mode == 0) {
+        hipLaunchKernelGGL(channel_sum_kernel<bf16>, dim3(blocks), dim3(NT), 0, s, (size_t)a.M, a.Nout,
+                           a.dy_stride, reinterpret_cast<const bf16*>(a.dY), a.dB, 0);
+      } else {
+        // ConvT: bias c collects all 4 sub-pixels -> sum the 2x-resolution gradient per channel
+        const int Gc = a.Cps / 8, lc = NT / Gc;
+        const size_t Mo = (size_t)a.M * 4;
+        const int bl = (int)std::min<size_t>((Mo + lc - 1) / lc, 1024);
+        hipLaunchKernelGGL(channel_sum_kernel<bf16>, dim3(bl), dim3(NT), 0, s, Mo, a.Cps, a.dy_stride,
+                           reinterpret_cast<const bf16*>(a.dY), a.dB, 0);
+      }
+    }
+    return adp::check_launch("adp_conv_wgrad");
+  }
+  if (std::is_same<T, bf16>::value && adp::option("conv_fast", 2) >= 1) {
+    // 64x256 only when explicitly asked ("wgrad_tn64"): measured slower than 128x128 at N=64
+    const int TN = (a.Nout <= 64 && adp::option("wgrad_tn64", 0)) ? 64 : 128, TK = TN == 64 ? 256 : 128;
+    a.ntile_k = (a.K + TK - 1) / TK;
+    a.ntile_n = (a.Nout + TN - 1) / TN;
+    const int tiles = a.ntile_k * a.ntile_n;
+    int splits = (1536 + tiles - 1) / tiles;
+    const int maxsplit = (a.M + 511) / 512;
+    splits = std::max(1, std::min(splits, maxsplit));
+    a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
+    splits = (a.M + a.mchunk - 1) / a.mchunk;
+    if (TN == 64)
+      hipLaunchKernelGGL((igemm_wgrad_bf16_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((igemm_wgrad_bf16_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a);
+    return adp::check_launch("adp_conv_wgrad");
+  }
   a.ntile_k = (a.K + 63) / 64;
   a.ntile_n = (a.Nout + 63) / 64;
   const int tiles = a.ntile_k * a.ntile_n;

@@ -285,6 +285,24 @@ __global__ void bn_bwd_apply_kernel(size_t M, int C, const T* dA, const T* z, co
   }
 }
 
+// a = relu(z*scale + shift): materialised post-BN activation (lets every consumer use LDS-DMA loads)
+template <typename T>
+__global__ void bn_apply_kernel(size_t M, int C, const T* z, const float* sc, const float* sh, T* out) {
+  const int G = C >> 3;
+  size_t total = M * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    const int g = (int)(i % G);
+    Grp<T> gr;
+    float f[8];
+    grp_load(gr, z + i * 8);
+    grp_to_f(gr, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[g * 8 + j], sh[g * 8 + j]), 0.f);
+    grp_from_f(gr, f);
+    grp_store(gr, out + i * 8);
+  }
+}
+
 // ------------------------------------------------------------------------------ optimizer
 // Keras 2.13 Adam.update_step: alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1);
 // v += (g^2-v)(1-b2); w -= m*alpha/(sqrt(v)+eps). AdamW first applies w -= w*wd*lr.
@@ -422,6 +440,16 @@ extern "C" int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, cons
                                   (const T*)dA, (const T*)z, sc, sh, mean, invstd, gamma, dgamma, dbeta,
                                   1.f / count, (T*)dz));
   return adp::check_launch("adp_bn_bwd_apply");
+}
+
+extern "C" int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* sc, const float* sh, void* out,
+                            adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && sc && sh, "adp_bn_apply: bad arguments");
+  size_t n = M * (C / 8);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, M, C,
+                                  (const T*)z, sc, sh, (T*)out));
+  return adp::check_launch("adp_bn_apply");
 }
 
 extern "C" int adp_adam(size_t n, float* w, const float* g, float* m, float* v, float lr, float b1,

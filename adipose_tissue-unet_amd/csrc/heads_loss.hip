@@ -200,7 +200,7 @@ __global__ void loss_rows_kernel(int N, int H, int W, const float* p, const floa
   const int row = blockIdx.x;
   const float* pr = p + (size_t)row * W;
   const float* yr = y + (size_t)row * W;
-  float bce = 0.f, s_yp = 0.f, s_y = 0.f, s_p = 0.f, r_yp = 0.f, r_y = 0.f, r_p = 0.f, acc = 0.f;
+  float bce = 0.f, s_yp = 0.f, s_y = 0.f, s_p = 0.f, r_yp = 0.f, r_y = 0.f, r_p = 0.f, acc = 0.f, r_yi = 0.f;
   for (int x = threadIdx.x; x < W; x += TPB) {
     float pv = pr[x], yv = yr[x];
     float ys = smooth_y(yv, smooth, ep, en);
@@ -208,15 +208,17 @@ __global__ void loss_rows_kernel(int N, int H, int W, const float* p, const floa
     bce -= ys * logf(pc + KEPS) + (1.f - ys) * logf(1.f - pc + KEPS);
     s_yp += ys * pc; s_y += ys; s_p += pc;
     r_yp += yv * pv; r_y += yv; r_p += pv;
-    acc += (yv == (pv > 0.5f ? 1.f : 0.f)) ? 1.f : 0.f;
+    const float pb = pv > 0.5f ? 1.f : 0.f;   // == round(clip(p,0,1)) (round half to even)
+    acc += (yv == pb) ? 1.f : 0.f;
+    r_yi += yv * pb;
   }
-  double v[8] = {bce, s_yp, s_y, s_p, r_yp, r_y, r_p, acc};
-  double tot[8];
+  double v[9] = {bce, s_yp, s_y, s_p, r_yp, r_y, r_p, acc, r_yi};
+  double tot[9];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) tot[i] = block_sum_d(v[i], sh);
+  for (int i = 0; i < 9; ++i) tot[i] = block_sum_d(v[i], sh);
   if (threadIdx.x == 0) {
     row_bce[row] = (float)(tot[0] / W);
-    for (int i = 1; i < 8; ++i) atomicAdd(stats + i - 1, tot[i]);
+    for (int i = 1; i < 9; ++i) atomicAdd(stats + i - 1, tot[i]);
   }
 }
 

@@ -44,9 +44,10 @@ ADP_DEV void view_dst(int v, int i, int j, int S, int& a, int& b) {
 }
 
 template <typename T>
-__global__ void prep_kernel(int N, int H, int W, int Cin, const float* src, float mean, float stdv,
-                            int view, int Cs, T* dst) {
-  const float inv = 1.f / (stdv + 1e-10f);
+__global__ void prep_kernel(int N, int H, int W, int Cin, const float* src, long long row_stride,
+                            long long img_stride, float mean, float stdv, int view, int Cs, T* dst) {
+  // reference: (image - mean) / (std + 1e-10) in float32 (segmentation_inference.py:155)
+  const float den = stdv + 1e-10f;
   size_t total = (size_t)N * H * W;
   for (size_t p = blockIdx.x * (size_t)TPB + threadIdx.x; p < total; p += (size_t)gridDim.x * TPB) {
     int b = (int)(p % W);
@@ -54,9 +55,9 @@ __global__ void prep_kernel(int N, int H, int W, int Cin, const float* src, floa
     int a = (int)(t % H), n = (int)(t / H);
     int i, j;
     view_src(view, a, b, H, i, j);
-    const float* s = src + (((size_t)n * H + i) * W + j) * Cin;
+    const float* s = src + (size_t)n * img_stride + ((size_t)i * row_stride + j) * Cin;
     T* d = dst + p * Cs;
-    for (int c = 0; c < Cs; ++c) d[c] = from_f<T>(c < Cin ? (s[c] - mean) * inv : 0.f);
+    for (int c = 0; c < Cs; ++c) d[c] = from_f<T>(c < Cin ? __fdiv_rn(__fsub_rn(s[c], mean), den) : 0.f);
   }
 }
 
@@ -85,29 +86,38 @@ __global__ void blend_accum_kernel(int H, int W, int T, int y0, int x0, const fl
     if (y >= H || x >= W) continue;
     float w = wmap ? wmap[p] : 1.f;
     size_t o = (size_t)y * W + x;
-    acc[o] += tile[p] * w;
-    wsum[o] += w;
+    // separate roundings (hipcc contracts a*b+c into v_fmac by default): bit-identical to numpy's
+    // accumulator += tile * weight
+    {
+#pragma clang fp contract(off)
+      acc[o] = acc[o] + tile[p] * w;
+    }
+    wsum[o] = __fadd_rn(wsum[o], w);
   }
 }
 
 __global__ void blend_final_kernel(size_t n, const float* acc, const float* wsum, float fl, float* out) {
   for (size_t p = blockIdx.x * (size_t)TPB + threadIdx.x; p < n; p += (size_t)gridDim.x * TPB)
-    out[p] = acc[p] / fmaxf(wsum[p], fl);
+    out[p] = __fdiv_rn(acc[p], fmaxf(wsum[p], fl));  // IEEE division, as numpy
 }
 }  // namespace
 
-extern "C" int adp_prep_input(int dtype, int N, int H, int W, int Cin, const float* src, float mean, float stdv,
-                              int view, int Cs, void* dst, adp_stream_t st) {
+extern "C" int adp_prep_input(int dtype, int N, int H, int W, int Cin, const float* src, long long src_row_stride,
+                              long long src_img_stride, float mean, float stdv, int view, int Cs, void* dst,
+                              adp_stream_t st) {
   ADP_REQUIRE(view >= 0 && view < 8, "adp_prep_input: view must be 0..7");
   ADP_REQUIRE(view == 0 || view == 4 || view == 5 || H == W, "adp_prep_input: rotated views need square tiles");
   ADP_REQUIRE(Cs >= Cin && Cs % 8 == 0, "adp_prep_input: bad channel stride");
+  if (src_row_stride <= 0) src_row_stride = W;
+  if (src_img_stride <= 0) src_img_stride = (long long)H * src_row_stride * Cin;
+  ADP_REQUIRE(src_row_stride >= W, "adp_prep_input: row stride smaller than the tile width");
   size_t n = (size_t)N * H * W;
   if (dtype == ADP_F32)
-    hipLaunchKernelGGL(prep_kernel<float>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W, Cin, src, mean,
-                       stdv, view, Cs, (float*)dst);
+    hipLaunchKernelGGL(prep_kernel<float>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W, Cin, src,
+                       src_row_stride, src_img_stride, mean, stdv, view, Cs, (float*)dst);
   else if (dtype == ADP_BF16)
-    hipLaunchKernelGGL(prep_kernel<bf16>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W, Cin, src, mean,
-                       stdv, view, Cs, (bf16*)dst);
+    hipLaunchKernelGGL(prep_kernel<bf16>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W, Cin, src,
+                       src_row_stride, src_img_stride, mean, stdv, view, Cs, (bf16*)dst);
   else { adp::set_error("adp_prep_input: bad dtype"); return -1; }
   return adp::check_launch("adp_prep_input");
 }

@@ -671,13 +671,12 @@ class UNetBN(UNetEngine):
         st = {}
         for i in range(self.levels):
             s, c = S >> i, self.ch(i)
-            a[f"z{i}_1"] = self.buf(f"z{i}_1", (B, s, s, c))
-            a[f"z{i}_2"] = self.buf(f"z{i}_2", (B, s, s, c))
+            for key in ([f"z{i}_1", f"z{i}_2"] + ([f"y{i}_1", f"y{i}_2"] if i < self.levels - 1 else [])):
+                a[key] = self.buf(key, (B, s, s, c))          # conv output (pre-BN), kept for BN backward
+                a["a" + key] = self.buf("a" + key, (B, s, s, c))  # relu(bn(z)), read by every consumer
             if i < self.levels - 1:
                 a[f"pool{i}"] = self.buf(f"pool{i}", (B, s // 2, s // 2, c))
                 a[f"t{i}"] = self.buf(f"t{i}", (B, s, s, c))
-                a[f"y{i}_1"] = self.buf(f"y{i}_1", (B, s, s, c))
-                a[f"y{i}_2"] = self.buf(f"y{i}_2", (B, s, s, c))
         a["p"] = self.buf("p", (B, S, S), torch.float32)
         for n, l in self.layers.items():
             if isinstance(l, Dense) and l.bn:
@@ -689,44 +688,44 @@ class UNetBN(UNetEngine):
         s = self.st[name]
         return (s[2], s[3])
 
-    def _bn_conv(self, name, srcA, out, *, srcB=None, bnA=None, bnB=None, train=True):
+    def _bn_conv(self, name, srcA, out, act, *, srcB=None, train=True):
+        """conv -> BN statistics (epilogue) -> scale/shift -> act = relu(bn(out)) materialised."""
         l = self.layers[name]
         s = self.st[name]
         if train:
             self.zero(s[:2])
-            self.conv(l, srcA, out, srcB=srcB, bnA=bnA, bnB=bnB, bn_stats=(s[0], s[1]))
+            self.conv(l, srcA, out, srcB=srcB, bn_stats=(s[0], s[1]))
             count = out.shape[0] * out.shape[1] * out.shape[2]
             rm, rv = self.running[name]
             ops.bn_finalize(count, s[0], s[1], self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                             self.bn_eps, self.bn_momentum, s[2], s[3], s[4], s[5], rm, rv)
         else:
-            self.conv(l, srcA, out, srcB=srcB, bnA=bnA, bnB=bnB)
+            self.conv(l, srcA, out, srcB=srcB)
             rm, rv = self.running[name]
             # eval: count < 0 -> (sum, sqsum) are read as (running mean, running var)
             ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                             self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
+        ops.bn_apply(out, s[2], s[3], act)
 
     def forward(self, batch=None, *, train=False, seed=0, pack=True):
         a = self.acts(batch or self.B)
         if pack:
             self.pack_forward_weights()
         Lv = self.levels
-        src, bn_in = a["x"], None
+        src = a["x"]
         for i in range(Lv):
-            self._bn_conv(f"enc{i}_conv1", src, a[f"z{i}_1"], bnA=bn_in, train=train)
-            self._bn_conv(f"enc{i}_conv2", a[f"z{i}_1"], a[f"z{i}_2"], bnA=self.bnvec(f"enc{i}_conv1"), train=train)
+            self._bn_conv(f"enc{i}_conv1", src, a[f"z{i}_1"], a[f"az{i}_1"], train=train)
+            self._bn_conv(f"enc{i}_conv2", a[f"az{i}_1"], a[f"z{i}_2"], a[f"az{i}_2"], train=train)
             if i < Lv - 1:
-                ops.maxpool2_fwd(a[f"z{i}_2"], a[f"pool{i}"], bn=self.bnvec(f"enc{i}_conv2"))
-                src, bn_in = a[f"pool{i}"], None
-        prev, prev_bn = a[f"z{Lv - 1}_2"], self.bnvec(f"enc{Lv - 1}_conv2")
+                ops.maxpool2_fwd(a[f"az{i}_2"], a[f"pool{i}"])
+                src = a[f"pool{i}"]
+        prev = a[f"az{Lv - 1}_2"]
         for i in range(Lv - 2, -1, -1):
-            self.conv(self.layers[f"dec{i}_up"], prev, a[f"t{i}"], bnA=prev_bn)
-            self._bn_conv(f"dec{i}_conv1", a[f"z{i}_2"], a[f"y{i}_1"], srcB=a[f"t{i}"],
-                          bnA=self.bnvec(f"enc{i}_conv2"), train=train)
-            self._bn_conv(f"dec{i}_conv2", a[f"y{i}_1"], a[f"y{i}_2"], bnA=self.bnvec(f"dec{i}_conv1"), train=train)
-            prev, prev_bn = a[f"y{i}_2"], self.bnvec(f"dec{i}_conv2")
-        ops.head_fwd(prev, self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0), softmax2=False,
-                     bn=prev_bn)
+            self.conv(self.layers[f"dec{i}_up"], prev, a[f"t{i}"])
+            self._bn_conv(f"dec{i}_conv1", a[f"az{i}_2"], a[f"y{i}_1"], a[f"ay{i}_1"], srcB=a[f"t{i}"], train=train)
+            self._bn_conv(f"dec{i}_conv2", a[f"ay{i}_1"], a[f"y{i}_2"], a[f"ay{i}_2"], train=train)
+            prev = a[f"ay{i}_2"]
+        ops.head_fwd(prev, self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0), softmax2=False)
         self._train_fwd = train
         return {"main_out": a["p"]}
 
@@ -746,57 +745,54 @@ class UNetBN(UNetEngine):
         def gb(key, like):
             return self.buf("g/" + key, tuple(like.shape), like.dtype)
 
-        # head
+        # head: dA = dL/d(relu(bn(y0_2)))
         dA = gb("y0_2", a["y0_2"])
-        ops.head_bwd(a["y0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"], self.ps.gview("head/W"),
-                     self.ps.gview("head/b"), cin=self.ch(0), softmax2=False, dx=dA, bn=self.bnvec("dec0_conv2"))
+        ops.head_bwd(a["ay0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"], self.ps.gview("head/W"),
+                     self.ps.gview("head/b"), cin=self.ch(0), softmax2=False, dx=dA)
         self._grad_ready("head")
         skip_grad = {}
-        cur_name, cur_z, cur_dA = "dec0_conv2", a["y0_2"], dA
-        # decoder from level 0 upward
+        cur_dA = dA
+        bott_dA = None
+        # decoder, from level 0 down to the bottleneck
         for i in range(0, Lv - 1):
-            # dec{i}_conv2
             dz = gb(f"dz_y{i}_2", a[f"y{i}_2"])
             self._bn_bwd(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz)
             l2 = L[f"dec{i}_conv2"]
-            self.wgrad(l2, a[f"y{i}_1"], dz, bnA=self.bnvec(f"dec{i}_conv1"))
+            self.wgrad(l2, a[f"ay{i}_1"], dz)
             dA1 = gb(f"dA_y{i}_1", a[f"y{i}_1"])
             self.dgrad(l2, dz, dA1)
             dz1 = gb(f"dz_y{i}_1", a[f"y{i}_1"])
             self._bn_bwd(f"dec{i}_conv1", dA1, a[f"y{i}_1"], dz1)
             l1 = L[f"dec{i}_conv1"]
-            self.wgrad(l1, a[f"z{i}_2"], dz1, srcB=a[f"t{i}"], bnA=self.bnvec(f"enc{i}_conv2"))
+            self.wgrad(l1, a[f"az{i}_2"], dz1, srcB=a[f"t{i}"])
             sk = gb(f"skip{i}", a[f"z{i}_2"])
             dt = gb(f"dt{i}", a[f"t{i}"])
             self.dgrad(l1, dz1, sk, split=True, out2=dt)
             skip_grad[i] = sk
-            # ConvTranspose dec{i}_up: input = relu(bn(prev level output))
+            # ConvTranspose dec{i}_up reads the previous level's activation
             lu = L[f"dec{i}_up"]
-            if i + 1 < Lv - 1:
-                pz, pbn, pname = a[f"y{i + 1}_2"], self.bnvec(f"dec{i + 1}_conv2"), f"dec{i + 1}_conv2"
-            else:
-                pz, pbn, pname = a[f"z{Lv - 1}_2"], self.bnvec(f"enc{Lv - 1}_conv2"), f"enc{Lv - 1}_conv2"
-            self.wgrad(lu, pz, dt, bnA=pbn)
-            dAp = gb(f"dA_up{i}", pz)
+            pact = a[f"ay{i + 1}_2"] if i + 1 < Lv - 1 else a[f"az{Lv - 1}_2"]
+            self.wgrad(lu, pact, dt)
+            dAp = gb(f"dA_up{i}", pact)
             self.dgrad(lu, dt, dAp)
             if i + 1 < Lv - 1:
                 cur_dA = dAp
             else:
                 bott_dA = dAp
         # bottleneck + encoder, from the deepest level up to level 0
-        dA = bott_dA
+        dpool = None
         for i in range(Lv - 1, -1, -1):
             z2, z1 = a[f"z{i}_2"], a[f"z{i}_1"]
             if i < Lv - 1:
-                # dA of enc{i}_conv2 = skip part + pool backward
+                # dA of enc{i}_conv2 = concat-skip part + pool backward (argmax on the activation)
                 dA2 = gb(f"dA_z{i}_2", z2)
-                ops.maxpool2_bwd(z2, dpool, dA2, bn=self.bnvec(f"enc{i}_conv2"), addend=skip_grad[i])
+                ops.maxpool2_bwd(a[f"az{i}_2"], dpool, dA2, addend=skip_grad[i])
             else:
-                dA2 = dA
+                dA2 = bott_dA
             dz2 = gb(f"dz_z{i}_2", z2)
             self._bn_bwd(f"enc{i}_conv2", dA2, z2, dz2)
             l2 = L[f"enc{i}_conv2"]
-            self.wgrad(l2, z1, dz2, bnA=self.bnvec(f"enc{i}_conv1"))
+            self.wgrad(l2, a[f"az{i}_1"], dz2)
             dA1 = gb(f"dA_z{i}_1", z1)
             self.dgrad(l2, dz2, dA1)
             dz1 = gb(f"dz_z{i}_1", z1)

@@ -300,6 +300,13 @@ def bn_finalize(count, ssum, ssq, gamma, beta, eps, momentum, scale, shift, mean
          float(momentum), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), ptr(rmean), ptr(rvar), stream_ptr())
 
 
+def bn_apply(z, scale, shift, out):
+    _check(out.shape == z.shape and out.dtype == z.dtype, "bn_apply shapes")
+    Cs = z.shape[-1]
+    call("adp_bn_apply", dtype_code(z), z.numel() // Cs, Cs, ptr(z), ptr(scale), ptr(shift), ptr(out), stream_ptr())
+    return out
+
+
 def bn_bwd_reduce(dA, z, scale, shift, mean, invstd, dgamma, dbeta):
     _check(dA.shape == z.shape, "bn bwd shapes")
     Cs = z.shape[-1]
@@ -390,16 +397,22 @@ def ema(ema_buf, param, decay):
 
 
 def prep_input(src, dst, *, mean, std, view=0):
-    """src f32 (N,H,W) or (N,H,W,C) raw intensities -> dst NHWC normalised (pad channels zero)."""
+    """src f32 (N,H,W) or (N,H,W,C) raw intensities -> dst NHWC normalised (pad channels zero).
+    ``src`` may be a strided window of a larger image (e.g. img[y:y+T, x:x+T]): rows are read in
+    place with the parent's row stride."""
     if src.dim() == 3:
         N, H, W = src.shape
         Cin = 1
+        rs, ims = src.stride(1), src.stride(0)
+        _check(src.stride(2) == 1, "prep src rows must be contiguous")
     else:
         N, H, W, Cin = src.shape
-    _check(src.dtype == torch.float32 and src.is_contiguous(), "prep src must be contiguous f32")
+        _check(src.stride(3) == 1 and src.stride(2) == Cin, "prep src pixels must be contiguous")
+        rs, ims = src.stride(1) // Cin, src.stride(0)
+    _check(src.dtype == torch.float32 and src.is_cuda, "prep src must be a device f32 tensor")
     _check(tuple(dst.shape[:3]) == (N, H, W) and dst.shape[3] >= Cin, "prep dst shape")
-    call("adp_prep_input", dtype_code(dst), N, H, W, Cin, ptr(src), float(mean), float(std), int(view),
-         int(dst.shape[3]), ptr(dst), stream_ptr())
+    call("adp_prep_input", dtype_code(dst), N, H, W, Cin, ptr(src), int(rs), int(ims), float(mean), float(std),
+         int(view), int(dst.shape[3]), ptr(dst), stream_ptr())
     return dst
 
 

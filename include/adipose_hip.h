@@ -74,6 +74,9 @@ typedef struct adp_conv_io {
 /* ---- library ---------------------------------------------------------------------------- */
 const char* adp_last_error(void);
 int adp_abi_version(void);
+/* Runtime switches (A/B of kernel variants in one process): "conv_fast" (default 1) selects the
+ * bf16 64x64-per-wave forward and the transposed-read wgrad kernels; 0 = generic kernels. */
+int adp_set_option(const char* name, int value);
 
 /* ---- dense layers (replace Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter / BiasAdd /
  *      Relu / ResizeNearestNeighbor / ConcatV2 / AddN / Dropout of
@@ -110,6 +113,9 @@ int adp_bn_finalize(int C, float count, const float* sum, const float* sqsum, co
                     const float* beta, float eps, float momentum, float* scale, float* shift,
                     float* mean, float* invstd, float* running_mean, float* running_var,
                     adp_stream_t s);
+/* a = relu(z*scale + shift), the post-BatchNorm activation, materialised once per layer */
+int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* scale, const float* shift,
+                 void* out, adp_stream_t s);
 /* dBN = dA * (relu(z*scale+shift) > 0); dgamma += sum dBN*xhat; dbeta += sum dBN */
 int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, const void* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, float* dgamma,
@@ -144,7 +150,8 @@ int adp_resize_bilinear_bwd(int N, int Hs, int Ws, int Ho, int Wo, const float* 
                             adp_stream_t s);
 
 /* ---- losses & metrics (dice_loss / combined_loss_* / OHEM :217-363; dice_coef model.py:93-98) */
-/* stats[0..6] += {sum y*p', sum y, sum p', sum y*p, sum y, sum p (raw y, p), #((p>0.5)==y)} where
+/* stats[0..7] += {sum y*p', sum y, sum p', sum y*p, sum y, sum p (raw y, p), #((p>0.5)==y),
+ *                 sum y*(p>0.5)} where
  * p' = clip(p,1e-7,1-1e-7) and y is the (optionally smoothed) label; row_bce[b*H+h] = mean_w BCE. */
 int adp_loss_rows(int N, int H, int W, const float* p, const float* y, int smooth, float eps_pos,
                   float eps_neg, float* row_bce, double* stats, adp_stream_t s);
@@ -168,10 +175,13 @@ int adp_ema(size_t n, float* ema, const float* param, float decay, adp_stream_t 
 
 /* ---- input / inference plumbing (predict_single :153-158, TTA :181-229, SW/blend
  *      full_evaluation_enhanced.py:115-329) ------------------------------------------------- */
-/* dst[n, y, x, c] = (src_view(view)[n, y, x, c] - mean) / (std + 1e-10); src f32 [N][H][W][Cin],
- * dst NHWC with C_stride >= Cin (pad channels zeroed); view in 0..7 is the TTA forward transform. */
-int adp_prep_input(int dtype, int N, int H, int W, int Cin, const float* src, float mean,
-                   float std, int view, int C_stride, void* dst, adp_stream_t s);
+/* dst[n, y, x, c] = (src_view(view)[n, y, x, c] - mean) / (std + 1e-10); src f32 rows of Cin
+ * interleaved channels with a row stride of src_row_stride pixels and an image stride of
+ * src_img_stride floats (<= 0: dense), so a sliding-window tile is read in place from the full
+ * image; dst NHWC with C_stride >= Cin (pad channels zeroed); view 0..7 = TTA forward transform. */
+int adp_prep_input(int dtype, int N, int H, int W, int Cin, const float* src,
+                   long long src_row_stride, long long src_img_stride, float mean, float std,
+                   int view, int C_stride, void* dst, adp_stream_t s);
 /* out[y,x] = mean_v inverse_view(v)(probs[v])[y,x] over nviews views listed in views[] (host) */
 int adp_tta_merge(int H, int W, int nviews, const int* views, const float* probs, float* out,
                   adp_stream_t s);

@@ -170,11 +170,16 @@ def test_unet_bn_forward_and_grads(dtype):
     loss.backward()
     tol = 1e-4 if dtype == "f32" else 3e-2
     assert (outs["main_out"].cpu() - p.detach()).abs().max().item() < tol
+    bad = []
     for name, ts in W.items():
         got = net.get_layer_grads(name)
-        for gi, t in zip(got, ts):
+        for si, (gi, t) in enumerate(zip(got, ts)):
             if dtype == "f32":
                 r = (torch.as_tensor(gi) - t.grad).abs().max().item() / max(t.grad.abs().max().item(), 1e-12)
-                assert r < 2e-3, (name, r)
+                if r >= 2e-3:
+                    bad.append((name, si, r))
             else:
-                assert cos(torch.as_tensor(gi), t.grad) > 0.95, name  # bf16 dz storage through BN bwd
+                c = cos(torch.as_tensor(gi), t.grad)
+                if c <= 0.95:  # bf16 dz storage through BN bwd
+                    bad.append((name, si, c))
+    assert not bad, bad

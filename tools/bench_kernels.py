@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Per-layer conv kernel microbenchmark (A/B of kernel variants in ONE process, interleaved rounds).
+
+For the unet_bn L5 / 1024^2 / B=4 layer shapes: forward, data-gradient and weight-gradient launches,
+timed with HIP events; reports TFLOP/s per variant ("conv_fast" option 0 = generic, 1 = fast path).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--variants", default="0,1,2")
+    p.add_argument("--batch", type=int, default=4)
+    args = p.parse_args()
+    import torch
+
+    import _adipose_pkg  # noqa: F401
+    from adipose_amd import _lib, ops
+
+    dev = torch.device("cuda", 0)
+    B = args.batch
+    # (name, S, Cin, Cout): 3x3 convs of unet_bn L5 (one per (level, shape) class)
+    shapes = [("L0 64->64", 1024, 64, 64), ("L0 128->64", 1024, 128, 64), ("L1 128->128", 512, 128, 128),
+              ("L2 256->256", 256, 256, 256), ("L3 512->512", 128, 512, 512), ("L4 1024->1024", 64, 1024, 1024),
+              ("L3 1024->512", 128, 1024, 512)]
+    variants = [int(v) for v in args.variants.split(",")]
+    res = {}
+    for name, S, cin, cout in shapes:
+        K = 9 * cin
+        Kpad = (K + 31) // 32 * 32
+        x = torch.randn(B, S, S, cin, device=dev).to(torch.bfloat16)
+        W = (torch.randn(((cout + 63) // 64 * 64), Kpad, device=dev) * 0.02).to(torch.bfloat16)
+        y = torch.empty(B, S, S, cout, device=dev, dtype=torch.bfloat16)
+        dW = torch.zeros(((cout + 63) // 64 * 64), Kpad, device=dev)
+        flops = 2.0 * B * S * S * cout * K
+        for kind in ("fwd", "wgrad"):
+            for v in variants:
+                res.setdefault((name, kind, v), [])
+        for r in range(args.rounds):
+            for v in variants:
+                _lib.lib().adp_set_option(b"conv_fast", v)
+                for kind in ("fwd", "wgrad"):
+                    fn = (lambda: ops.conv_fwd(x, W, cout, out=y)) if kind == "fwd" else \
+                        (lambda: ops.conv_wgrad(x, y, dW, cout))
+                    fn()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(args.reps):
+                        fn()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ms = e0.elapsed_time(e1) / args.reps
+                    res[(name, kind, v)].append(ms)
+        for kind in ("fwd", "wgrad"):
+            line = {"layer": name, "kind": kind}
+            for v in variants:
+                ms = min(res[(name, kind, v)])
+                line[f"v{v}_ms"] = round(ms, 4)
+                line[f"v{v}_tflops"] = round(flops / ms / 1e9, 1)
+            print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
