@@ -1,0 +1,170 @@
+// Shared pieces of the implicit-GEMM convolution kernels (conv_igemm.hip, conv_fwd_tap64.hip):
+// the forward-shaped launch arguments, the XCD-aware block remap and the LDS-staged epilogue.
+#pragma once
+#include "common.h"
+
+struct FwdArgs {
+  const void* srcA; const void* srcB;
+  const float* scA; const float* shA;   // BN-apply(+ReLU) on load of source A (nullable)
+  const float* scB; const float* shB;
+  int CAs, CBs;          // channel strides of the sources (%8 == 0); CBs == 0 -> single source
+  int Nimg, Hs, Ws;      // source spatial dims
+  int up;                // 1 or 2: nearest upsample folded into the gather
+  int Ho, Wo, stride;    // output spatial, input stride
+  int kh, kw, dil, pad;  // tap grid; input coord = o*stride + tap*dil - pad (virtual grid)
+  const void* W; int Kpad; int K;
+  const float* bias;
+  int Nout;              // logical GEMM N
+  int relu;
+  uint32_t drop_seed; float drop_rate;   // drop_rate > 0 -> inverted dropout after ReLU
+  void* out; int out_stride; int out_mode; int Cps;   // out_mode 0 plain, 1 pixel-shuffle, 2 split
+  void* out2; int out2_stride; int split_c;
+  const void* addend; int addend_stride;
+  const void* mask; int mask_stride; float mask_scale;
+  const void* mask2; int mask2_stride; float mask2_scale;
+  float* accum; int accum_stride;
+  float* bn_sum; float* bn_sq;
+  int M;
+  int ntile_n;           // gridDim decomposition helper
+  int nblocks;
+};
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// XCD-aware bijective remap of the linear block id: each XCD (blocks b, b+8, ...) receives a
+// contiguous run of tiles, N-tile fastest, so the A (activation) panel of one M-tile is shared
+// through one XCD's L2 by all its N-tiles.
+ADP_DEV int xcd_remap(int bid, int nwg) {
+  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// XOR swizzle of the 16-B chunks of a 128-B LDS row (rows of 64 bf16): chunk c of row r is stored at
+// position c ^ swz(r); makes the 16x16x32 MFMA fragment reads (16 rows x one 16-B chunk per 16-lane
+// group) bank-conflict free.
+ADP_DEV int swz(int r) { return (r >> 1) & 7; }
+
+// ---------------------------------------------------------------- LDS-staged bf16 epilogue
+// `tile` holds `rows` x BN f32 accumulators (row stride BN + 4) for output pixels m0.. and GEMM
+// columns n0..; NTH threads each own one 8-column group (cg = tid % (BN/8)) and walk the rows.
+// Applies bias, ReLU, dropout, the pixel-shuffle / split / addend / mask / accumulate store modes
+// and collects BatchNorm partial sums of the stored values into bs/bq.
+template <int NTH, int BN>
+ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int n0, int tid,
+                      float (&bs)[8], float (&bq)[8]) {
+  constexpr int LT = BN + 4;
+  constexpr int GPR = BN / 8;
+  static_assert(NTH % GPR == 0, "epilogue: threads must tile the row groups");
+  constexpr int RSTEP = NTH / GPR;
+  const int cg = tid % GPR;
+  const int n = n0 + cg * 8;
+  if (n >= a.Nout) return;
+  const int HWo = a.Ho * a.Wo;
+  float bias[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bias[j] = a.bias ? a.bias[a.out_mode == 1 ? (n + j) % a.Cps : n + j] : 0.f;
+  for (int row = tid / GPR; row < rows; row += RSTEP) {
+    const int m = m0 + row;
+    if (m >= a.M) break;
+    float v[8];
+    const float4* tp = reinterpret_cast<const float4*>(tile + row * LT + cg * 8);
+    float4 t0 = tp[0], t1 = tp[1];
+    v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w; v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] += bias[j];
+      if (a.relu) v[j] = fmaxf(v[j], 0.f);
+    }
+    if (a.drop_rate > 0.f) {
+      const float ks = 1.f / (1.f - a.drop_rate);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float u = adp_uniform(a.drop_seed, (uint64_t)m * (uint64_t)a.Nout + n + j);
+        v[j] = (u >= a.drop_rate) ? v[j] * ks : 0.f;
+      }
+    }
+    Grp<bf16> gr;
+    if (a.out_mode == 1) {
+      int sub = n / a.Cps, c = n - sub * a.Cps;
+      int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+      size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
+      grp_from_f(gr, v);
+      grp_store(gr, reinterpret_cast<bf16*>(a.out) + pix * a.out_stride + c);
+    } else if (a.out_mode == 2 && n >= a.split_c) {
+      const int c = n - a.split_c;
+      if (a.mask2) {
+        float mk[8];
+        grp_load(gr, reinterpret_cast<const bf16*>(a.mask2) + (size_t)m * a.mask2_stride + c);
+        grp_to_f(gr, mk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.f ? v[j] * a.mask2_scale : 0.f;
+      }
+      grp_from_f(gr, v);
+      grp_store(gr, reinterpret_cast<bf16*>(a.out2) + (size_t)m * a.out2_stride + c);
+      continue;
+    } else {
+      if (!a.out) continue;
+      float f[8];
+      if (a.addend) {
+        grp_load(gr, reinterpret_cast<const bf16*>(a.addend) + (size_t)m * a.addend_stride + n);
+        grp_to_f(gr, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += f[j];
+      }
+      if (a.mask) {
+        grp_load(gr, reinterpret_cast<const bf16*>(a.mask) + (size_t)m * a.mask_stride + n);
+        grp_to_f(gr, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f[j] > 0.f ? v[j] * a.mask_scale : 0.f;
+      }
+      grp_from_f(gr, v);
+      grp_store(gr, reinterpret_cast<bf16*>(a.out) + (size_t)m * a.out_stride + n);
+      if (a.accum) {
+        float* ap = a.accum + (size_t)m * a.accum_stride + n;
+        float r[8];
+        grp_to_f(gr, r);   // accumulate the value as stored (bf16-rounded), like the generic path
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ap[j] += r[j];
+      }
+    }
+    if (a.bn_sum) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { bs[j] += v[j]; bq[j] += v[j] * v[j]; }
+    }
+  }
+}
+
+// Threads with equal column group hold partial BN sums of the same 8 channels: reduce them through
+// LDS (`red` needs NTH*16 floats; caller guarantees no pending reads of it), then one atomic per
+// channel and block.
+template <int NTH, int BN>
+ADP_DEV void epi_bn_flush(const FwdArgs& a, float* red, int n0, int tid, const float (&bs)[8],
+                          const float (&bq)[8]) {
+  constexpr int GPR = BN / 8;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = bs[j]; red[tid * 16 + 8 + j] = bq[j]; }
+  __syncthreads();
+  if (tid < BN) {
+    const int gg = tid >> 3, j = tid & 7;
+    float s = 0.f, q = 0.f;
+    for (int t = gg; t < NTH; t += GPR) { s += red[t * 16 + j]; q += red[t * 16 + 8 + j]; }
+    const int nn = n0 + tid;
+    if (nn < a.Nout) {
+      const int c = a.out_mode == 1 ? nn % a.Cps : nn;
+      atomicAdd(a.bn_sum + c, s);
+      atomicAdd(a.bn_sq + c, q);
+    }
+  }
+}
+
+}  // namespace
+
+namespace adp {
+// conv_fwd_tap64.hip: 8-phase LDS-DMA forward kernel for layers whose channel stride is a multiple
+// of 64 (every 64-deep K step lies inside one tap). Returns 1 if it launched, 0 if not eligible.
+int launch_fwd_tap64(FwdArgs& a, hipStream_t s);
+}

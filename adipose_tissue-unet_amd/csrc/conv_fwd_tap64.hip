@@ -1,0 +1,288 @@
+// 8-phase LDS-DMA implicit-GEMM forward kernel ("tap64") for every layer whose channel stride is a
+// multiple of 64 — all 3x3 convs of the unet_bn preset after the input layer, their data-gradients,
+// the ConvTranspose 2x2/s2 forward (1x1 + pixel-shuffle store) and data-gradient (stride-2 4-tap
+// gather). Semantics are those of igemm_fwd_kernel (conv_igemm.hip); only the schedule differs.
+//
+// Because Cin_s % 64 == 0, each 64-deep K step lies inside one tap and one source, so the per-lane
+// gather address of a K step is (row base pixel + tap offset) * stride + channel: a bounds test and
+// two adds, no per-lane division.
+//
+// Schedule (cf. the 256x256 8-phase GEMM template of the CDNA4 programming guide): a block of
+// WM x WN waves computes BM x BN = (WM*TM) x (WN*64); each wave a TM x 64 tile held as
+// (TM/16) x 4 accumulators of v_mfma_f32_16x16x32_bf16. Every K step (64) is staged in four
+// quarter-tiles — A0/A1 (the upper/lower TM/2 rows of every wave row group) and B0/B1 (the left/right
+// 32 columns of every wave column group) — moved HBM/L2 -> LDS by global_load_lds_dwordx4 into a
+// lane-linear image whose 16-B chunks are XOR-swizzled on the SOURCE address. Per K step t four
+// phases compute the quadrants (A0,B0) (A0,B1) (A1,B1) (A1,B0); a quarter is refilled with K step t+2
+// as soon as its last reader phase has passed a barrier, so two K steps of loads are in flight and
+// the only wait is one counted `s_waitcnt vmcnt` per K step (never 0 inside the loop).
+#include "conv_common.h"
+
+namespace {
+
+__device__ __attribute__((aligned(256))) uint4 tap64_zero_page[64];
+
+constexpr int cmax(int x, int y) { return x > y ? x : y; }
+
+// compiler fence + hardware barrier + compiler fence: keeps LDS reads and LDS-DMA issues on their
+// side of the barrier (the s_barrier builtin alone does not order memory operations)
+#define T64_BAR()                          \
+  do {                                     \
+    asm volatile("" ::: "memory");         \
+    __builtin_amdgcn_s_barrier();          \
+    asm volatile("" ::: "memory");         \
+  } while (0)
+
+template <int WM, int WN, int TM>
+__global__ __launch_bounds__(WM * WN * 64, 1) void igemm_fwd_tap64_kernel(FwdArgs a) {
+  constexpr int NTH = WM * WN * 64;
+  constexpr int BM = WM * TM, BN = WN * 64;
+  constexpr int ROWB = 128;                        // one K step of one row: 64 bf16
+  constexpr int QA = BM / 2, QB = BN / 2;          // rows per quarter-tile
+  constexpr int GA = QA * 8 / NTH, GB = QB * 8 / NTH;  // glds per thread per quarter
+  static_assert(GA >= 1 && GB >= 1 && GA * NTH == QA * 8 && GB * NTH == QB * 8, "quarters must split evenly");
+  constexpr int HM = TM / 2;                       // rows of a wave's A quarter
+  constexpr int MIQ = TM / 32;                     // 16-row fragments per wave per A quarter
+  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int OA1 = QA * ROWB, OB0 = BM * ROWB, OB1 = (BM + QB) * ROWB;
+  constexpr int EPI = TM * (BN + 4) * 4;
+  constexpr int SMEM = cmax(cmax(2 * STAGE, EPI), NTH * 16 * 4);
+  constexpr int NIN = 2 * (GA + GB);               // glds a thread issues per K step
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int lin = xcd_remap(blockIdx.x, a.nblocks);
+  const int tn = lin % a.ntile_n, tm = lin / a.ntile_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int pos = lane & 7;
+  const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
+  const int Cin_s = a.CAs + a.CBs;
+  const int Wrows = (a.Nout + 63) / 64 * 64;
+  const int nk = a.K / 64;
+
+  // ---- per-thread staging rows: quarter h, instruction i -> quarter row q = i*(NTH/8) + tid/8
+  int ry[2][GA], rx[2][GA], rn[2][GA], rc[2][GA];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int q = i * (NTH / 8) + (tid >> 3);
+      const int m = m0 + (q / HM) * TM + h * HM + (q % HM);
+      const bool v = m < a.M;
+      const int mm = v ? m : 0;
+      const int n = mm / HWo, rem = mm - n * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+      ry[h][i] = yo * a.stride - a.pad;
+      rx[h][i] = xo * a.stride - a.pad;
+      rn[h][i] = v ? n * a.Hs : -1;
+      rc[h][i] = 8 * (pos ^ swz(q));
+    }
+  const bf16* bp[2][GB];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int q = i * (NTH / 8) + (tid >> 3);
+      const int col = (q / 32) * 64 + h * 32 + (q % 32);
+      bp[h][i] = (n0 + col < Wrows)
+                     ? reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + col) * a.Kpad + 8 * (pos ^ swz(q))
+                     : nullptr;
+    }
+  const bf16* srcA = reinterpret_cast<const bf16*>(a.srcA);
+  const bf16* srcB = reinterpret_cast<const bf16*>(a.srcB);
+
+  // K step -> (tap offsets, source, channel); uniform across the block
+  struct Kt { int oy, ox, cs; const bf16* base; int kt; };
+  auto kinfo = [&](int kt) {
+    Kt r;
+    const int k = kt * 64, tap = k / Cin_s, ci = k - tap * Cin_s;
+    const int ty = tap / a.kw, tx = tap - ty * a.kw;
+    r.oy = ty * a.dil; r.ox = tx * a.dil; r.kt = kt;
+    if (ci < a.CAs) { r.base = srcA + ci; r.cs = a.CAs; }
+    else { r.base = srcB + (ci - a.CAs); r.cs = a.CBs; }
+    return r;
+  };
+  auto issueA = [&](int h, const Kt& k, int buf) {
+    unsigned char* dst = smem + buf * STAGE + h * OA1 + wave * 8 * ROWB;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const void* p = tap64_zero_page;
+      int yi = ry[h][i] + k.oy, xi = rx[h][i] + k.ox;
+      if (rn[h][i] >= 0 && (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv) {
+        if (a.up == 2) { yi >>= 1; xi >>= 1; }
+        p = k.base + (size_t)((rn[h][i] + yi) * a.Ws + xi) * k.cs + rc[h][i];
+      }
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
+    }
+  };
+  auto issueB = [&](int h, const Kt& k, int buf) {
+    unsigned char* dst = smem + buf * STAGE + (h ? OB1 : OB0) + wave * 8 * ROWB;
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const void* p = bp[h][i] ? (const void*)(bp[h][i] + (size_t)k.kt * 64) : (const void*)tap64_zero_page;
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
+    }
+  };
+
+  const int r16 = lane & 15, h4 = lane >> 4;
+  auto readA = [&](int buf, int h, bf16x8 (&fa)[MIQ][2]) {
+    const unsigned char* base = smem + buf * STAGE + h * OA1;
+#pragma unroll
+    for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int q = wr * HM + mi * 16 + r16, c = 4 * s + h4;
+        fa[mi][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
+      }
+  };
+  auto readB = [&](int buf, int h, bf16x8 (&fb)[2][2]) {
+    const unsigned char* base = smem + buf * STAGE + (h ? OB1 : OB0);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int q = wc * 32 + ni * 16 + r16, c = 4 * s + h4;
+        fb[ni][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
+      }
+  };
+
+  f32x4 acc[2 * MIQ][4];
+#pragma unroll
+  for (int i = 0; i < 2 * MIQ; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[ha * MIQ + mi][hb * 2 + ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][s], fb[ni][s], acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- prologue: K steps 0 and 1 in flight, wait for step 0
+  {
+    const Kt k0 = kinfo(0);
+    issueA(0, k0, 0); issueB(0, k0, 0); issueB(1, k0, 0); issueA(1, k0, 0);
+    if (nk > 1) {
+      const Kt k1 = kinfo(1);
+      issueA(0, k1, 1); issueB(0, k1, 1); issueB(1, k1, 1); issueA(1, k1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    T64_BAR();
+  }
+
+  bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool pre = t + 2 < nk;
+    const Kt k2 = kinfo(pre ? t + 2 : t);
+    // P0: (A0,B0)
+    readA(buf, 0, fa);
+    readB(buf, 0, fb0);
+    T64_BAR();
+    mma(fa, fb0, 0, 0);
+    T64_BAR();
+    // P1: (A0,B1); A0 and B0 of this buffer are dead -> refill with step t+2
+    if (pre) { issueA(0, k2, buf); issueB(0, k2, buf); }
+    readB(buf, 1, fb1);
+    T64_BAR();
+    mma(fa, fb1, 0, 1);
+    T64_BAR();
+    // P2: (A1,B1); B1 dead
+    if (pre) issueB(1, k2, buf);
+    readA(buf, 1, fa);
+    T64_BAR();
+    mma(fa, fb1, 1, 1);
+    T64_BAR();
+    // P3: (A1,B0) from registers; A1 dead. Retire step t+1 (everything older than this K step's
+    // issues) before the barrier that precedes its first read.
+    if (pre) issueA(1, k2, buf);
+    mma(fa, fb0, 1, 0);
+    if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    T64_BAR();
+  }
+
+  // ---- epilogue: one wave row group (TM rows x BN) at a time through LDS
+  float* tile = reinterpret_cast<float*>(smem);
+  constexpr int LT = BN + 4;
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+  float bs[8], bq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bs[j] = 0.f; bq[j] = 0.f; }
+  for (int p = 0; p < WM; ++p) {
+    if (wr == p) {
+#pragma unroll
+      for (int mt = 0; mt < 2 * MIQ; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            tile[((mt / MIQ) * HM + (mt % MIQ) * 16 + rq + r) * LT + wc * 64 + nt * 16 + col] = acc[mt][nt][r];
+    }
+    __syncthreads();
+    epi_rows<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
+    __syncthreads();
+  }
+  if (a.bn_sum) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
+}
+
+#undef T64_BAR
+
+template <int WM, int WN, int TM>
+void launch_cfg(FwdArgs& a, hipStream_t s) {
+  constexpr int BM = WM * TM, BN = WN * 64;
+  a.ntile_n = (a.Nout + BN - 1) / BN;
+  a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
+  hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM>), dim3(a.nblocks), dim3(WM * WN * 64), 0, s, a);
+}
+
+// configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 256x128 (8 waves, 64x64),
+// 2 = 512x64 (4 waves, 128x64)
+constexpr int CFG_BM[3] = {256, 256, 512};
+constexpr int CFG_BN[3] = {256, 128, 64};
+// relative per-block throughput, measured on the unet_bn layer shapes (tools/bench_kernels.py): the
+// 512x64 tile loses to the 4-wave 256x64 LDS-DMA kernel of conv_igemm.hip at N = 64 (A-gather bound),
+// so auto mode never picks it and leaves N <= 64 layers to that kernel.
+constexpr double CFG_EFF[3] = {1.0, 0.85, 0.0};
+
+}  // namespace
+
+namespace adp {
+int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
+  const int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
+  if (mode == 0) return 0;
+  const int Cin_s = a.CAs + a.CBs;
+  if (a.scA || a.scB || a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 ||
+      a.Kpad != a.K)
+    return 0;
+  int cfg = mode - 2;
+  if (mode == 1) {
+    // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency
+    // A configuration whose N tile is less than 3/4 used is not considered: the 256x64 kernel of
+    // conv_igemm.hip is faster on such narrow layers.
+    double best = 0.0;
+    for (int c = 0; c < 3; ++c) {
+      const long long tn = (a.Nout + CFG_BN[c] - 1) / CFG_BN[c], tmm = (a.M + CFG_BM[c] - 1) / CFG_BM[c];
+      const long long blocks = tn * tmm, waves = (blocks + 255) / 256;
+      const double colu = (double)a.Nout / (tn * CFG_BN[c]);
+      if (colu < 0.75) continue;
+      const double sc = colu * (double)blocks / (waves * 256) * CFG_EFF[c];
+      if (sc > best) { best = sc; cfg = c; }
+    }
+    if (best <= 0.0) return 0;
+  }
+  if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
+  else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);
+  else if (cfg == 2) launch_cfg<4, 1, 128>(a, s);
+  else return 0;
+  return 1;
+}
+}  // namespace adp

@@ -16,7 +16,7 @@
 //
 // Tiling: 256 threads = 4 waves (2x2), block tile 128(M pixels) x 64(N channels) x 32(K), register-
 // staged double-buffered LDS, v_mfma_f32_16x16x32_bf16 (bf16) or v_mfma_f32_16x16x4_f32 (f32, exact).
-#include "common.h"
+#include "conv_common.h"
 #include <type_traits>
 
 namespace {
@@ -27,31 +27,6 @@ template <typename T> struct LdsTr;
 template <> struct LdsTr<bf16> { static constexpr int LDK = BK + 8; };   // 80 B rows
 template <> struct LdsTr<float> { static constexpr int LDK = BK + 4; };  // 144 B rows
 
-struct FwdArgs {
-  const void* srcA; const void* srcB;
-  const float* scA; const float* shA;   // BN-apply(+ReLU) on load of source A (nullable)
-  const float* scB; const float* shB;
-  int CAs, CBs;          // channel strides of the sources (%8 == 0); CBs == 0 -> single source
-  int Nimg, Hs, Ws;      // source spatial dims
-  int up;                // 1 or 2: nearest upsample folded into the gather
-  int Ho, Wo, stride;    // output spatial, input stride
-  int kh, kw, dil, pad;  // tap grid; input coord = o*stride + tap*dil - pad (virtual grid)
-  const void* W; int Kpad; int K;
-  const float* bias;
-  int Nout;              // logical GEMM N
-  int relu;
-  uint32_t drop_seed; float drop_rate;   // drop_rate > 0 -> inverted dropout after ReLU
-  void* out; int out_stride; int out_mode; int Cps;   // out_mode 0 plain, 1 pixel-shuffle, 2 split
-  void* out2; int out2_stride; int split_c;
-  const void* addend; int addend_stride;
-  const void* mask; int mask_stride; float mask_scale;
-  const void* mask2; int mask2_stride; float mask2_scale;
-  float* accum; int accum_stride;
-  float* bn_sum; float* bn_sq;
-  int M;
-  int ntile_n;           // gridDim decomposition helper
-  int nblocks;
-};
 
 template <typename T>
 ADP_DEV void load_a_group(const FwdArgs& a, Grp<T>& g, bool rowvalid, int n, int ybase, int xbase,
@@ -122,14 +97,6 @@ ADP_DEV void mma_tile<float>(const float* As, const float* Bs, int wr, int wc, i
   }
 }
 
-// XCD-aware bijective remap of the linear block id: each XCD (blocks b, b+8, ...) receives a
-// contiguous run of tiles, N-tile fastest, so the A (activation) panel of one M-tile is shared
-// through one XCD's L2 by all its N-tiles.
-ADP_DEV int xcd_remap(int bid, int nwg) {
-  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (bid >> 3);
-}
 
 // Shared epilogue of the forward-shaped kernels: acc[mi][ni] holds the 16x16 MFMA tile whose
 // rows are mbase + mi*16 + 4*(lane>>4) + r and columns nbase + ni*16 + (lane&15).
@@ -284,8 +251,6 @@ template <int BM, int BN>
 ADP_DEV void fwd_epilogue_lds(const FwdArgs& a, f32x4 (&acc)[4][4], float* tile, int m0, int n0, int wr,
                               int wc, int tid) {
   constexpr int LT = BN + 4;
-  constexpr int GPR = BN / 8;                 // groups per tile row
-  constexpr int NG = BM * GPR / NT;           // groups per thread
   const int lane = tid & 63, col = lane & 15, rq = (lane >> 4) * 4;
   __syncthreads();  // main loop LDS reads done before the tile overwrites the staging buffers
 #pragma unroll
@@ -296,105 +261,11 @@ ADP_DEV void fwd_epilogue_lds(const FwdArgs& a, f32x4 (&acc)[4][4], float* tile,
       for (int r = 0; r < 4; ++r)
         tile[(wr * 64 + mi * 16 + rq + r) * LT + wc * 64 + ni * 16 + col] = acc[mi][ni][r];
   __syncthreads();
-  const int cg = tid % GPR;
-  const int n = n0 + cg * 8;
-  const bool nvalid = n < a.Nout;
-  const int HWo = a.Ho * a.Wo;
-  float bias[8], bs[8], bq[8];
+  float bs[8], bq[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bs[j] = 0.f; bq[j] = 0.f;
-    bias[j] = (nvalid && a.bias) ? a.bias[a.out_mode == 1 ? (n + j) % a.Cps : n + j] : 0.f;
-  }
-  for (int g = 0; g < NG; ++g) {
-    const int row = (tid + g * NT) / GPR;
-    const int m = m0 + row;
-    if (!nvalid || m >= a.M) continue;
-    float v[8];
-    const float4* tp = reinterpret_cast<const float4*>(tile + row * LT + cg * 8);
-    float4 t0 = tp[0], t1 = tp[1];
-    v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w; v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      v[j] += bias[j];
-      if (a.relu) v[j] = fmaxf(v[j], 0.f);
-    }
-    if (a.drop_rate > 0.f) {
-      const float ks = 1.f / (1.f - a.drop_rate);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float u = adp_uniform(a.drop_seed, (uint64_t)m * (uint64_t)a.Nout + n + j);
-        v[j] = (u >= a.drop_rate) ? v[j] * ks : 0.f;
-      }
-    }
-    Grp<bf16> gr;
-    if (a.out_mode == 1) {
-      int sub = n / a.Cps, c = n - sub * a.Cps;
-      int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
-      size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
-      grp_from_f(gr, v);
-      grp_store(gr, reinterpret_cast<bf16*>(a.out) + pix * a.out_stride + c);
-    } else if (a.out_mode == 2 && n >= a.split_c) {
-      const int c = n - a.split_c;
-      if (a.mask2) {
-        float mk[8];
-        grp_load(gr, reinterpret_cast<const bf16*>(a.mask2) + (size_t)m * a.mask2_stride + c);
-        grp_to_f(gr, mk);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.f ? v[j] * a.mask2_scale : 0.f;
-      }
-      grp_from_f(gr, v);
-      grp_store(gr, reinterpret_cast<bf16*>(a.out2) + (size_t)m * a.out2_stride + c);
-      continue;
-    } else {
-      if (!a.out) continue;
-      float f[8];
-      if (a.addend) {
-        grp_load(gr, reinterpret_cast<const bf16*>(a.addend) + (size_t)m * a.addend_stride + n);
-        grp_to_f(gr, f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += f[j];
-      }
-      if (a.mask) {
-        grp_load(gr, reinterpret_cast<const bf16*>(a.mask) + (size_t)m * a.mask_stride + n);
-        grp_to_f(gr, f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = f[j] > 0.f ? v[j] * a.mask_scale : 0.f;
-      }
-      grp_from_f(gr, v);
-      grp_store(gr, reinterpret_cast<bf16*>(a.out) + (size_t)m * a.out_stride + n);
-      if (a.accum) {
-        float* ap = a.accum + (size_t)m * a.accum_stride + n;
-        float r[8];
-        grp_to_f(gr, r);   // accumulate the value as stored (bf16-rounded), like the generic path
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ap[j] += r[j];
-      }
-    }
-    if (a.bn_sum) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { bs[j] += v[j]; bq[j] += v[j] * v[j]; }
-    }
-  }
-  if (a.bn_sum) {
-    // threads with equal cg hold partials of the same 8 channels: reduce through LDS, then atomics
-    __syncthreads();
-    float* red = tile;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = bs[j]; red[tid * 16 + 8 + j] = bq[j]; }
-    __syncthreads();
-    if (tid < BN) {
-      const int gg = tid >> 3, j = tid & 7;
-      float s = 0.f, q = 0.f;
-      for (int t = gg; t < NT; t += GPR) { s += red[t * 16 + j]; q += red[t * 16 + 8 + j]; }
-      const int nn = n0 + tid;
-      if (nn < a.Nout) {
-        const int c = a.out_mode == 1 ? nn % a.Cps : nn;
-        atomicAdd(a.bn_sum + c, s);
-        atomicAdd(a.bn_sq + c, q);
-      }
-    }
-  }
+  for (int j = 0; j < 8; ++j) { bs[j] = 0.f; bq[j] = 0.f; }
+  epi_rows<NT, BN>(a, tile, BM, m0, n0, tid, bs, bq);
+  if (a.bn_sum) epi_bn_flush<NT, BN>(a, tile, n0, tid, bs, bq);
 }
 
 // --------------------------------------------------------------- bf16 throughput forward kernel
@@ -507,10 +378,6 @@ __global__ __launch_bounds__(NT, 2) void igemm_fwd_bf16_kernel(FwdArgs a) {
 // reads of the 16x16x32 MFMA bank-conflict free. No BN-on-load (the BN preset materialises its
 // activations for this path).
 __device__ __attribute__((aligned(256))) uint4 adp_zero_page[64];
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-ADP_DEV int swz(int r) { return (r >> 1) & 7; }
 
 template <int BM, int BN>
 __global__ __launch_bounds__(NT, 2) void igemm_fwd_glds_kernel(FwdArgs a) {
@@ -1201,6 +1068,7 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   ADP_REQUIRE(d->out_mode != 2 || (io->out2 && d->split_c > 0), "adp_conv_fwd: split store needs out2/split_c");
   const int fast = adp::option("conv_fast", 2);
   if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB) {
+    if (adp::launch_fwd_tap64(a, s)) return adp::check_launch("adp_conv_fwd");
     const int w64 = (a.Nout + 63) / 64 * 64 - a.Nout, w128 = (a.Nout + 127) / 128 * 128 - a.Nout;
     if (a.Nout > 64 && w128 <= w64) {
       a.ntile_n = (a.Nout + 127) / 128;

@@ -149,12 +149,13 @@ def test_adipose_train_step_adam(adipose_weights):
         assert (torch.as_tensor(gk) - k.detach()).abs().max().item() < 1e-4, name
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_unet_bn_forward_and_grads(dtype):
+@pytest.mark.parametrize("dtype,base", [("f32", 16), ("bf16", 16), ("bf16", 64)])
+def test_unet_bn_forward_and_grads(dtype, base):
+    """base 64 puts every layer but the input conv on the tap64 kernel (fwd, dgrad, ConvT, concat)."""
     B, S, L = 2, 32, 3
-    w = R.unet_bn_keras_weights(levels=L, base=16, in_ch=3, seed=5)
+    w = R.unet_bn_keras_weights(levels=L, base=base, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
-    net = UNetBN(B, S, levels=L, base=16, in_ch=3, dtype=dtype, device=DEV)
+    net = UNetBN(B, S, levels=L, base=base, in_ch=3, dtype=dtype, device=DEV)
     net.set_weights(w)
     tr = Trainer(net, LossConfig(use_hard_mining=False))
     a = net.acts(B)

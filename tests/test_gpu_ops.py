@@ -47,6 +47,10 @@ CONV_CASES = [
     ("up", 2, 8, [88], 44, 1, True),
     ("concat", 2, 16, [44, 44], 44, 1, False),
     ("wide", 1, 16, [176], 352, 4, False),
+    # channel strides % 64 == 0 -> bf16 launches take the 8-phase tap64 kernel (ragged M, partial N tile)
+    ("c64", 2, 24, [64], 64, 1, False),
+    ("c128_320", 1, 20, [128], 320, 2, False),
+    ("concat64", 2, 16, [64, 64], 128, 1, False),
 ]
 
 
@@ -131,6 +135,31 @@ def test_conv_grads(case, dt):
         ref_dx = torch.cat([x.grad for x in xr], -1)
     got = torch.cat([dX[..., sum(l.cin_s[:i]): sum(l.cin_s[:i]) + c] for i, c in enumerate(parts)], -1)
     assert relerr(got, ref_dx) < tol
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "256x128", "512x64"])
+def test_tap64_configs(cfg):
+    """Each forced tile configuration of the tap64 kernel: output and fused BatchNorm statistics vs the
+    oracle on a ragged pixel count (M = 529) and a partial N tile (Nout = 192)."""
+    N, S, cin, cout = 1, 23, 128, 192
+    xs, kern, bias, l = make_case(N, S, [cin], cout, 1, False, seed=7)
+    dt = torch.bfloat16
+    W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).to(dt).contiguous()
+    b = bias.to(DEV)
+    x = nhwc_pad(xs[0], l.Cin_s, dt)
+    out = torch.zeros((N, S, S, l.cout_s), dtype=dt, device=DEV)
+    st = torch.zeros(2, l.cout_s, device=DEV)
+    ops.set_option("fwd_tap64", cfg)
+    try:
+        ops.conv_fwd(x, W, l.Nout, out=out, bias=b, relu=True, bn_stats=(st[0], st[1]))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("fwd_tap64", 1)
+    ref = oracle_fwd([rb(xs[0], dt)], rb(kern, dt), bias, 1, False)
+    assert relerr(out[..., :cout], ref) < 2e-2
+    rs = ref.reshape(-1, cout)
+    assert relerr(st[0, :cout], rs.sum(0)) < 2e-2
+    assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
 @pytest.mark.parametrize("dt", DTS)

@@ -2,7 +2,9 @@
 """Per-layer conv kernel microbenchmark (A/B of kernel variants in ONE process, interleaved rounds).
 
 For the unet_bn L5 / 1024^2 / B=4 layer shapes: forward, data-gradient and weight-gradient launches,
-timed with HIP events; reports TFLOP/s per variant ("conv_fast" option 0 = generic, 1 = fast path).
+timed with HIP events; reports TFLOP/s per variant. A variant is a comma-separated list of native
+options (ops.set_option), variants are separated by ';', e.g.
+  --variants "conv_fast=2,fwd_tap64=0;fwd_tap64=1;fwd_tap64=2"
 """
 import argparse
 import json
@@ -17,21 +19,26 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--reps", type=int, default=5)
-    p.add_argument("--variants", default="0,1,2")
+    p.add_argument("--variants", default="conv_fast=2,fwd_tap64=0;conv_fast=2,fwd_tap64=1")
+    p.add_argument("--kinds", default="fwd,wgrad")
     p.add_argument("--batch", type=int, default=4)
     args = p.parse_args()
     import torch
 
     import _adipose_pkg  # noqa: F401
-    from adipose_amd import _lib, ops
+    from adipose_amd import ops
 
     dev = torch.device("cuda", 0)
     B = args.batch
     # (name, S, Cin, Cout): 3x3 convs of unet_bn L5 (one per (level, shape) class)
     shapes = [("L0 64->64", 1024, 64, 64), ("L0 128->64", 1024, 128, 64), ("L1 128->128", 512, 128, 128),
               ("L2 256->256", 256, 256, 256), ("L3 512->512", 128, 512, 512), ("L4 1024->1024", 64, 1024, 1024),
-              ("L3 1024->512", 128, 1024, 512)]
-    variants = [int(v) for v in args.variants.split(",")]
+              ("L3 1024->512", 128, 1024, 512), ("L4 1024->512", 64, 1024, 512), ("L1 256->128", 512, 256, 128)]
+    variants = list(range(len(args.variants.split(";"))))
+    settings = [[(kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",") if kv]
+                for v in args.variants.split(";")]
+    kinds = args.kinds.split(",")
+    print(json.dumps({"variants": {f"v{i}": args.variants.split(";")[i] for i in variants}}), flush=True)
     res = {}
     for name, S, cin, cout in shapes:
         K = 9 * cin
@@ -41,13 +48,14 @@ def main():
         y = torch.empty(B, S, S, cout, device=dev, dtype=torch.bfloat16)
         dW = torch.zeros(((cout + 63) // 64 * 64), Kpad, device=dev)
         flops = 2.0 * B * S * S * cout * K
-        for kind in ("fwd", "wgrad"):
+        for kind in kinds:
             for v in variants:
                 res.setdefault((name, kind, v), [])
         for r in range(args.rounds):
             for v in variants:
-                _lib.lib().adp_set_option(b"conv_fast", v)
-                for kind in ("fwd", "wgrad"):
+                for k_, v_ in settings[v]:
+                    ops.set_option(k_, v_)
+                for kind in kinds:
                     fn = (lambda: ops.conv_fwd(x, W, cout, out=y)) if kind == "fwd" else \
                         (lambda: ops.conv_wgrad(x, y, dW, cout))
                     fn()
@@ -59,7 +67,7 @@ def main():
                     torch.cuda.synchronize()
                     ms = e0.elapsed_time(e1) / args.reps
                     res[(name, kind, v)].append(ms)
-        for kind in ("fwd", "wgrad"):
+        for kind in kinds:
             line = {"layer": name, "kind": kind}
             for v in variants:
                 ms = min(res[(name, kind, v)])
