@@ -33,8 +33,12 @@ constexpr int cmax(int x, int y) { return x > y ? x : y; }
     asm volatile("" ::: "memory");         \
   } while (0)
 
+// blocks per CU the LDS footprint allows (2 when two double-buffered stages fit in 80 KB)
 template <int WM, int WN, int TM>
-__global__ __launch_bounds__(WM * WN * 64, 1) void igemm_fwd_tap64_kernel(FwdArgs a) {
+constexpr int tap64_occ() { return 2 * (WM * TM + WN * 64) * 128 <= 81920 ? 2 : 1; }
+
+template <int WM, int WN, int TM>
+__global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
   constexpr int ROWB = 128;                        // one K step of one row: 64 bf16
@@ -245,13 +249,13 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 256x128 (8 waves, 64x64),
-// 2 = 512x64 (4 waves, 128x64)
-constexpr int CFG_BM[3] = {256, 256, 512};
-constexpr int CFG_BN[3] = {256, 128, 64};
-// relative per-block throughput, measured on the unet_bn layer shapes (tools/bench_kernels.py): the
-// 512x64 tile loses to the 4-wave 256x64 LDS-DMA kernel of conv_igemm.hip at N = 64 (A-gather bound),
-// so auto mode never picks it and leaves N <= 64 layers to that kernel.
-constexpr double CFG_EFF[3] = {1.0, 0.85, 0.0};
+// 2 = 512x64 (4 waves, 128x64), 3 = 256x64 (4 waves, 64x64, two blocks per CU)
+constexpr int CFG_BM[4] = {256, 256, 512, 256};
+constexpr int CFG_BN[4] = {256, 128, 64, 64};
+// relative per-block throughput, measured on the unet_bn layer shapes (tools/bench_kernels.py):
+// 256x256 > 256x128 > 256x64 (two blocks per CU; the only one used at N = 64, +21-26 % over the
+// 4-wave kernel of conv_igemm.hip) ; 512x64 (one wave per SIMD) is never picked.
+constexpr double CFG_EFF[4] = {1.0, 0.85, 0.0, 0.6};
 
 }  // namespace
 
@@ -266,10 +270,9 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   int cfg = mode - 2;
   if (mode == 1) {
     // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency
-    // A configuration whose N tile is less than 3/4 used is not considered: the 256x64 kernel of
-    // conv_igemm.hip is faster on such narrow layers.
+    // a configuration whose N tile is less than 3/4 used is not considered
     double best = 0.0;
-    for (int c = 0; c < 3; ++c) {
+    for (int c = 0; c < 4; ++c) {
       const long long tn = (a.Nout + CFG_BN[c] - 1) / CFG_BN[c], tmm = (a.M + CFG_BM[c] - 1) / CFG_BM[c];
       const long long blocks = tn * tmm, waves = (blocks + 255) / 256;
       const double colu = (double)a.Nout / (tn * CFG_BN[c]);
@@ -282,6 +285,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);
   else if (cfg == 2) launch_cfg<4, 1, 128>(a, s);
+  else if (cfg == 3) launch_cfg<4, 1, 64>(a, s);
   else return 0;
   return 1;
 }

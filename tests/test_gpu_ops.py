@@ -137,7 +137,7 @@ def test_conv_grads(case, dt):
     assert relerr(got, ref_dx) < tol
 
 
-@pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "256x128", "512x64"])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5], ids=["256x256", "256x128", "512x64", "256x64"])
 def test_tap64_configs(cfg):
     """Each forced tile configuration of the tap64 kernel: output and fused BatchNorm statistics vs the
     oracle on a ragged pixel count (M = 529) and a partial N tile (Nout = 192)."""
