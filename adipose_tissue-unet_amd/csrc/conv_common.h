@@ -29,9 +29,25 @@ struct FwdArgs {
   int nblocks;
 };
 
+// weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
+struct WgradArgs {
+  const void* srcA; const void* srcB;
+  const float* scA; const float* shA; const float* scB; const float* shB;
+  int CAs, CBs, Nimg, Hs, Ws, up, Ho, Wo, stride, kh, kw, dil, pad;
+  int K, Kpad;
+  const void* dY; int dy_stride; int dy_mode; int Cps;   // dy_mode 0 plain [M][N], 1 pixel-shuffle gather
+  int Nout;
+  float* dW;            // [Npad][Kpad] f32, accumulated with atomics
+  float* dB;            // [Nout] f32 or null
+  int M, mchunk, ntile_k, ntile_n;
+};
+
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef short v4s16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s16 lds_v4s16;
+
 
 // XCD-aware bijective remap of the linear block id: each XCD (blocks b, b+8, ...) receives a
 // contiguous run of tiles, N-tile fastest, so the A (activation) panel of one M-tile is shared
@@ -46,6 +62,35 @@ ADP_DEV int xcd_remap(int bid, int nwg) {
 // position c ^ swz(r); makes the 16x16x32 MFMA fragment reads (16 rows x one 16-B chunk per 16-lane
 // group) bank-conflict free.
 ADP_DEV int swz(int r) { return (r >> 1) & 7; }
+
+// ------------------------------------------------ transposed fragment reads (weight gradient)
+// Operands X[pixel][k] and dY[pixel][n] sit in LDS as linear rows of RB bytes (pixel = row); 16-B
+// chunk c of row r is stored at chunk position c ^ gsw(r), gsw(r) = 2*(r & 7) for RB >= 256 and
+// 2*((r >> 1) & 3) for RB = 128, which spreads the 8 rows read by one 32-lane half of a
+// ds_read_b64_tr_b16 over 8 distinct 32-B bank slots. Inside a 32-pixel MFMA k step the pixel order
+// is permuted, rho(8g+e) = 16(g>>1) + 8(e>>2) + 4(g&1) + (e&3), so that the 8 rows one half-wave
+// reads are 8 consecutive LDS rows (both operands use the same permutation).
+template <int RB>
+ADP_DEV int gsw(int r) { return RB >= 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }
+
+template <int RB>
+ADP_DEV bf16x8 tr_frag_sw(const unsigned char* base, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = row0 + 16 * (g >> 1) + 4 * (g & 1) + q;
+  const int r1 = r0 + 8;
+  const int col = col0 + 4 * p;
+  const int chunk = col >> 3, inb = (col & 7) * 2;
+  const unsigned char* a0 = base + r0 * RB + ((chunk ^ gsw<RB>(r0)) << 4) + inb;
+  const unsigned char* a1 = base + r1 * RB + ((chunk ^ gsw<RB>(r1)) << 4) + inb;
+  v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a0));
+  v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a1));
+  bf16x8 r;
+  const bf16* l = reinterpret_cast<const bf16*>(&lo);
+  const bf16* h = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
+  return r;
+}
 
 // ---------------------------------------------------------------- LDS-staged bf16 epilogue
 // `tile` holds `rows` x BN f32 accumulators (row stride BN + 4) for output pixels m0.. and GEMM
@@ -167,4 +212,6 @@ namespace adp {
 // conv_fwd_tap64.hip: 8-phase LDS-DMA forward kernel for layers whose channel stride is a multiple
 // of 64 (every 64-deep K step lies inside one tap). Returns 1 if it launched, 0 if not eligible.
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s);
+// conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
+int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
 }

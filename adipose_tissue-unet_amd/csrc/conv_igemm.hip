@@ -507,17 +507,6 @@ __global__ __launch_bounds__(NT, 2) void igemm_fwd_glds_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------ wgrad
-struct WgradArgs {
-  const void* srcA; const void* srcB;
-  const float* scA; const float* shA; const float* scB; const float* shB;
-  int CAs, CBs, Nimg, Hs, Ws, up, Ho, Wo, stride, kh, kw, dil, pad;
-  int K, Kpad;
-  const void* dY; int dy_stride; int dy_mode; int Cps;   // dy_mode 0 plain [M][N], 1 pixel-shuffle gather
-  int Nout;
-  float* dW;            // [Npad][Kpad] f32, accumulated with atomics
-  float* dB;            // [Nout] f32 or null
-  int M, mchunk, ntile_k, ntile_n;
-};
 
 template <typename T> struct WTr;
 template <> struct WTr<bf16> { static constexpr int LDM = 32 + 8; };
@@ -669,8 +658,6 @@ __global__ __launch_bounds__(NT) void igemm_wgrad_kernel(WgradArgs a) {
 // transposes on the read (MFMA k = pixel). The pixel (reduction) order inside a 32-pixel substep is
 // permuted, rho(8g+e) = 16(g>>1) + 8(e>>2) + 4(g&1) + (e&3), so that the 8 rows one 32-lane half reads
 // are 8 consecutive LDS rows; with row strides of 32*odd bytes that read is bank-conflict free.
-typedef short v4s16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4s16 lds_v4s16;
 
 ADP_DEV bf16x8 tr_frag(const bf16* lds_base, int row0, int rowstride_el, int col0, int lane) {
   // lane (g = lane>>4, i = lane&15 = 4q+p) -> 8 consecutive k (pixels) of column col0 + i
@@ -849,28 +836,6 @@ __global__ __launch_bounds__(NT, 2) void igemm_wgrad_bf16_kernel(WgradArgs a) {
 // RB >= 256 and 2*((r >> 1) & 3) for RB = 128, which spreads the 8 rows read by one 32-lane half of a
 // ds_read_b64_tr_b16 over 8 distinct 32-B bank slots. Pixel order inside a 32-pixel substep is the
 // rho permutation of igemm_wgrad_bf16_kernel. The bias gradient is a separate channel-sum launch.
-template <int RB>
-ADP_DEV int gsw(int r) { return RB >= 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }
-
-template <int RB>
-ADP_DEV bf16x8 tr_frag_sw(const unsigned char* base, int row0, int col0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int r0 = row0 + 16 * (g >> 1) + 4 * (g & 1) + q;
-  const int r1 = r0 + 8;
-  const int col = col0 + 4 * p;
-  const int chunk = col >> 3, inb = (col & 7) * 2;
-  const unsigned char* a0 = base + r0 * RB + ((chunk ^ gsw<RB>(r0)) << 4) + inb;
-  const unsigned char* a1 = base + r1 * RB + ((chunk ^ gsw<RB>(r1)) << 4) + inb;
-  v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a0));
-  v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(a1));
-  bf16x8 r;
-  const bf16* l = reinterpret_cast<const bf16*>(&lo);
-  const bf16* h = reinterpret_cast<const bf16*>(&hi);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
-  return r;
-}
-
 template <int TN, int TK>
 __global__ __launch_bounds__(NT, 2) void igemm_wgrad_glds_kernel(WgradArgs a) {
   constexpr int MS = 64;
@@ -1119,19 +1084,21 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
               "adp_conv_wgrad: channel strides and Nout must be multiples of 8");
   ADP_REQUIRE(d->out_mode != 2, "adp_conv_wgrad: split-store descriptors are dgrad-only");
   if (std::is_same<T, bf16>::value && adp::option("conv_fast", 2) == 2 && !a.scA && !a.scB) {
-    const int TN = (a.Nout <= 64 && adp::option("wgrad_glds_tn64", 1)) ? 64 : 128, TK = TN == 64 ? 256 : 128;
-    a.ntile_k = (a.K + TK - 1) / TK;
-    a.ntile_n = (a.Nout + TN - 1) / TN;
-    const int tiles = a.ntile_k * a.ntile_n;
-    int splits = (2048 + tiles - 1) / tiles;
-    const int maxsplit = (a.M + 511) / 512;
-    splits = std::max(1, std::min(splits, maxsplit));
-    a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
-    splits = (a.M + a.mchunk - 1) / a.mchunk;
-    if (TN == 64)
-      hipLaunchKernelGGL((igemm_wgrad_glds_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a);
-    else
-      hipLaunchKernelGGL((igemm_wgrad_glds_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a);
+    if (!adp::launch_wgrad_tap64(a, s)) {
+      const int TN = (a.Nout <= 64 && adp::option("wgrad_glds_tn64", 1)) ? 64 : 128, TK = TN == 64 ? 256 : 128;
+      a.ntile_k = (a.K + TK - 1) / TK;
+      a.ntile_n = (a.Nout + TN - 1) / TN;
+      const int tiles = a.ntile_k * a.ntile_n;
+      int splits = (2048 + tiles - 1) / tiles;
+      const int maxsplit = (a.M + 511) / 512;
+      splits = std::max(1, std::min(splits, maxsplit));
+      a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
+      splits = (a.M + a.mchunk - 1) / a.mchunk;
+      if (TN == 64)
+        hipLaunchKernelGGL((igemm_wgrad_glds_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a);
+      else
+        hipLaunchKernelGGL((igemm_wgrad_glds_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a);
+    }
     if (a.dB) {
       const int G = a.Nout / 8, lanes = NT / G;
       const int blocks = (int)std::min<long long>((a.M + lanes - 1) / lanes, 1024);

@@ -1,0 +1,319 @@
+// Phase-pipelined LDS-DMA weight-gradient kernel ("wgrad tap64") for layers whose channel stride is
+// a multiple of 64 (every unet_bn conv after the input layer, their ConvTranspose layers):
+//   dW[n][k] += sum_m dY[m][n] * X(k)[m]      (k = tap * Cin_s + ci, m = output pixel)
+// Semantics are those of igemm_wgrad_kernel (conv_igemm.hip); the bias gradient is the separate
+// channel-sum launch.
+//
+// Block = WN x WK waves, dW tile TN x TK = (WN*TNW) x (WK*64); each wave a TNW x 64 tile of
+// v_mfma_f32_16x16x32_bf16 accumulators whose A operand (dY^T) and B operand (X^T) are read from the
+// natural [pixel][channel] LDS images with ds_read_b64_tr_b16 (MFMA k = pixel). A stage is 64 pixels,
+// staged as four quarter images — dY and X for pixels 0-31 (q0) and 32-63 (q1) — moved by
+// global_load_lds_dwordx4. Phases: q0 (split into the two n halves of the wave when TNW = 128), then
+// q1; a quarter is refilled with stage t+2 (q0) or t+1 (q1) as soon as its reader phases have passed a
+// barrier, and each phase pair ends in one counted `s_waitcnt vmcnt` (never 0 in the loop).
+//
+// Per-lane gather: a thread's 16-B chunk column is fixed for the whole kernel (the row swizzle only
+// depends on row bits a thread's rows share), so its tap, source and channel are constants and its
+// pixel rows advance by 64 per stage with incremental (image, y, x) coordinates — no divisions in
+// the loop.
+#include "conv_common.h"
+
+namespace {
+
+__device__ __attribute__((aligned(256))) uint4 wg64_zero_page[64];
+
+
+#define W64_BAR()                          \
+  do {                                     \
+    asm volatile("" ::: "memory");         \
+    __builtin_amdgcn_s_barrier();          \
+    asm volatile("" ::: "memory");         \
+  } while (0)
+
+struct PixSlot { int m, n, y, x; };
+
+ADP_DEV void slot_init(PixSlot& s, int m, int HWo, int Wo) {
+  s.m = m;
+  s.n = m / HWo;
+  const int rem = m - s.n * HWo;
+  s.y = rem / Wo;
+  s.x = rem - s.y * Wo;
+}
+// next stage (pixel + 64) as a branch-free mixed-radix add of (an, ay, ax) = 64 in (image, y, x) digits
+struct Adv { int an, ay, ax; };
+ADP_DEV void slot_adv(PixSlot& s, const Adv& d, int Ho, int Wo) {
+  s.m += 64;
+  s.x += d.ax;
+  const int cx = s.x >= Wo;
+  s.x -= cx ? Wo : 0;
+  s.y += d.ay + cx;
+  const int cy = s.y >= Ho;
+  s.y -= cy ? Ho : 0;
+  s.n += d.an + cy;
+}
+
+// ds_read_b64_tr_b16 as inline asm: the builtin form makes hipcc wait vmcnt(0) (every LDS-DMA in
+// flight) before each read, because it cannot tell the read from the pending DMA writes. The caller
+// orders these reads with explicit lgkmcnt waits.
+ADP_DEV v4s16 ds_tr16(uint32_t lds_addr) {
+  v4s16 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
+  return r;
+}
+ADP_DEV uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+template <int RB>
+ADP_DEV bf16x8 tr_frag_asm(uint32_t base, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r0 = 16 * (g >> 1) + 4 * (g & 1) + q, r1 = r0 + 8;
+  const int col = col0 + 4 * p, chunk = col >> 3, inb = (col & 7) * 2;
+  const v4s16 lo = ds_tr16(base + r0 * RB + ((chunk ^ gsw<RB>(r0)) << 4) + inb);
+  const v4s16 hi = ds_tr16(base + r1 * RB + ((chunk ^ gsw<RB>(r1)) << 4) + inb);
+  bf16x8 r;
+  const bf16* l = reinterpret_cast<const bf16*>(&lo);
+  const bf16* h = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
+  return r;
+}
+
+template <int WN, int WK, int TNW>
+constexpr int wg64_occ() { return 2 * 2 * 32 * (2 * WN * TNW + 2 * WK * 64) <= 81920 ? 2 : 1; }
+
+template <int WN, int WK, int TNW>
+__global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm_wgrad_tap64_kernel(WgradArgs a) {
+  constexpr int NTH = WN * WK * 64;
+  constexpr int TN = WN * TNW, TK = WK * 64;
+  constexpr int RD = 2 * TN, RX = 2 * TK;              // LDS row bytes (one pixel)
+  constexpr int QD = 32 * RD, QX = 32 * RX;            // quarter image bytes
+  constexpr int STAGE = 2 * (QD + QX);
+  constexpr int CPRD = RD / 16, CPRX = RX / 16;        // 16-B chunks per row
+  constexpr int RPID = NTH / CPRD, RPIX = NTH / CPRX;  // rows per glds instruction (whole block)
+  constexpr int GD = 32 / RPID, GX = 32 / RPIX;        // glds per thread per quarter
+  static_assert(GD >= 1 && GX >= 1 && GD * RPID == 32 && GX * RPIX == 32, "quarters must split evenly");
+  static_assert(RPID % 8 == 0 && RPIX % 8 == 0, "a thread's rows must share the swizzle bits");
+  constexpr int NH = GD + GX;                          // glds per thread per pixel half
+  constexpr bool SPLIT = TNW == 128;                   // two phases (n halves) per pixel half
+  constexpr int NB = TNW / 16;                         // 16-row n blocks per wave
+  constexpr int NBP = SPLIT ? NB / 2 : NB;             // n blocks per phase
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WK, wk = wave % WK;
+  // 1-D grid, XCD remap with the tile index fastest: all dW tiles of one pixel split run back to
+  // back on one XCD and share its L2 for dY (every tile of the split) and X (neighbouring taps)
+  const int tiles = a.ntile_k * a.ntile_n;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / tiles, tile = lin - split * tiles;
+  const int tk = tile % a.ntile_k, tn = tile / a.ntile_k;
+  const int k0 = tk * TK, n0 = tn * TN;
+  const int mbeg = split * a.mchunk;
+  const int mend = min(a.M, mbeg + a.mchunk);
+  if (mbeg >= mend) return;
+  const int ns = (mend - mbeg + 63) / 64;
+  const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
+  const int Cin_s = a.CAs + a.CBs;
+
+  // ---- fixed chunk columns
+  const int kx = k0 + 8 * ((tid % CPRX) ^ gsw<RX>(tid / CPRX));
+  const bool kvalid = kx < a.K;
+  int oy = 0, ox = 0, xcs = a.CAs;
+  const bf16* xbase = reinterpret_cast<const bf16*>(a.srcA);
+  if (kvalid) {
+    const int tap = kx / Cin_s, ci = kx - tap * Cin_s;
+    const int ty = tap / a.kw, tx = tap - ty * a.kw;
+    oy = ty * a.dil - a.pad;
+    ox = tx * a.dil - a.pad;
+    if (ci < a.CAs) xbase += ci;
+    else { xbase = reinterpret_cast<const bf16*>(a.srcB) + (ci - a.CAs); xcs = a.CBs; }
+  }
+  const int nd = n0 + 8 * ((tid % CPRD) ^ gsw<RD>(tid / CPRD));
+  const bool nvalid = nd < a.Nout;
+  int dsub = 0, dc = nd;
+  if (a.dy_mode == 1) { dsub = nd / a.Cps; dc = nd - dsub * a.Cps; }
+  const bf16* dy = reinterpret_cast<const bf16*>(a.dY);
+
+  // ---- pixel slots (quarter q, instruction i)
+  PixSlot sx[2][GX], sd[2][GD];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+#pragma unroll
+    for (int i = 0; i < GX; ++i) slot_init(sx[q][i], mbeg + 32 * q + i * RPIX + tid / CPRX, HWo, a.Wo);
+#pragma unroll
+    for (int i = 0; i < GD; ++i) slot_init(sd[q][i], mbeg + 32 * q + i * RPID + tid / CPRD, HWo, a.Wo);
+  }
+
+  Adv adv;
+  adv.an = 64 / HWo;
+  adv.ay = (64 - adv.an * HWo) / a.Wo;
+  adv.ax = 64 - adv.an * HWo - adv.ay * a.Wo;
+
+  // issue quarter q of the stage the slots currently point at into buffer buf, then advance them
+  auto issue = [&](int q, int buf) {
+    unsigned char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < GD; ++i) {
+      PixSlot& s = sd[q][i];
+      size_t off;
+      if (a.dy_mode == 0) {
+        off = (size_t)s.m * a.dy_stride + nd;
+      } else {
+        off = (((size_t)s.n * (2 * a.Ho) + 2 * s.y + (dsub >> 1)) * (2 * a.Wo) + 2 * s.x + (dsub & 1)) * a.dy_stride + dc;
+      }
+      const bool ok = s.m < mend && nvalid;
+      const void* p = ok ? (const void*)(dy + off) : (const void*)wg64_zero_page;
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + q * QD + (i * RPID + wave * (64 / CPRD)) * RD), 16, 0, 0);
+      slot_adv(s, adv, a.Ho, a.Wo);
+    }
+#pragma unroll
+    for (int i = 0; i < GX; ++i) {
+      PixSlot& s = sx[q][i];
+      int yi = s.y * a.stride + oy, xi = s.x * a.stride + ox;
+      const bool ok = s.m < mend && kvalid && (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
+      if (a.up == 2) { yi >>= 1; xi >>= 1; }
+      const void* p = ok ? (const void*)(xbase + (size_t)((s.n * a.Hs + yi) * a.Ws + xi) * xcs)
+                         : (const void*)wg64_zero_page;
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + 2 * QD + q * QX + (i * RPIX + wave * (64 / CPRX)) * RX),
+                                       16, 0, 0);
+      slot_adv(s, adv, a.Ho, a.Wo);
+    }
+  };
+
+  f32x4 acc[NB][4];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fd[NBP], fx[4];
+  const uint32_t sbase = lds_off(smem);
+  auto readD = [&](int buf, int q, int h) {
+    const uint32_t base = sbase + buf * STAGE + q * QD;
+#pragma unroll
+    for (int nb = 0; nb < NBP; ++nb) fd[nb] = tr_frag_asm<RD>(base, wn * TNW + (h * NBP + nb) * 16, lane);
+  };
+  auto readX = [&](int buf, int q) {
+    const uint32_t base = sbase + buf * STAGE + 2 * QD + q * QX;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) fx[kb] = tr_frag_asm<RX>(base, wk * 64 + kb * 16, lane);
+  };
+  auto mma = [&](int h) {
+    // the fragments come from inline-asm LDS reads: wait for them explicitly and keep the MFMAs
+    // from being scheduled above the wait
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int nb = 0; nb < NBP; ++nb)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+        acc[h * NBP + nb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[nb], fx[kb], acc[h * NBP + nb][kb], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- prologue: stage 0 (q0, q1) and stage 1 q0 in flight; wait for stage 0 q0
+  issue(0, 0);
+  issue(1, 0);
+  if (ns > 1) {
+    issue(0, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NH) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NH) : "memory");
+  }
+  W64_BAR();
+
+  for (int t = 0; t < ns; ++t) {
+    const int buf = t & 1;
+    const bool n1 = t + 1 < ns, n2 = t + 2 < ns;
+    // ---- pixel half 0 (q0); q1 of the other buffer is free -> stage t+1 q1
+    if (n1) issue(1, buf ^ 1);
+    readD(buf, 0, 0);
+    readX(buf, 0);
+    W64_BAR();
+    mma(0);
+    if (SPLIT) {
+      W64_BAR();
+      readD(buf, 0, 1);
+      W64_BAR();
+      mma(1);
+    }
+    // retire stage t q1 (issued after it: stage t+1 q0 and q1, iff they exist)
+    if (n1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NH) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    W64_BAR();
+    // ---- pixel half 1 (q1); q0 of this buffer is free -> stage t+2 q0
+    if (n2) issue(0, buf);
+    readD(buf, 1, 0);
+    readX(buf, 1);
+    W64_BAR();
+    mma(0);
+    if (SPLIT) {
+      W64_BAR();
+      readD(buf, 1, 1);
+      W64_BAR();
+      mma(1);
+    }
+    // retire stage t+1 q0 (issued after it: stage t+1 q1, stage t+2 q0 iff it exists)
+    if (n2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NH) : "memory");
+    else if (n1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NH) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    W64_BAR();
+  }
+
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * TNW + nb * 16 + rq + r;
+        const int kk = k0 + wk * 64 + kb * 16 + col;
+        if (n < a.Nout && kk < a.K) atomicAdd(a.dW + (size_t)n * a.Kpad + kk, acc[nb][kb][r]);
+      }
+}
+
+#undef W64_BAR
+
+// Pixel splits: enough blocks to fill the chip (target_blocks), but every split keeps at least
+// min_chunk pixels so that the f32 atomic epilogue (blocks x TN x TK x 4 bytes at ~1.3 TB/s) stays
+// small against the GEMM.
+template <int WN, int WK, int TNW>
+void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) {
+  constexpr int TN = WN * TNW, TK = WK * 64;
+  a.ntile_k = (a.K + TK - 1) / TK;
+  a.ntile_n = (a.Nout + TN - 1) / TN;
+  const int tiles = a.ntile_k * a.ntile_n;
+  int splits = (target_blocks + tiles - 1) / tiles;
+  const int maxsplit = (a.M + min_chunk - 1) / min_chunk;
+  splits = std::max(1, std::min(splits, maxsplit));
+  a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
+  splits = (a.M + a.mchunk - 1) / a.mchunk;
+  hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW>), dim3(tiles * splits), dim3(WN * WK * 64), 0, s, a);
+}
+
+}  // namespace
+
+namespace adp {
+// configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 128x256 (8 waves, 64x64),
+// 2 = 64x256 (4 waves, 64x64, two blocks per CU)
+int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
+  const int mode = option("wgrad_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
+  if (mode == 0) return 0;
+  const int Cin_s = a.CAs + a.CBs;
+  if (a.scA || a.scB || a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 ||
+      a.Kpad != a.K)
+    return 0;
+  int cfg = mode - 2;
+  if (mode == 1) cfg = a.Nout >= 192 ? 0 : a.Nout > 64 ? 1 : 2;
+  // block targets measured on the unet_bn layer shapes (tools/bench_kernels.py)
+  const int target = option("wgrad_blocks", cfg == 0 ? 1024 : cfg == 1 ? 2048 : 4096);
+  const int min_chunk = option("wgrad_min_chunk", cfg == 0 ? 2048 : 1024);
+  if (cfg == 0) launch_wcfg<2, 4, 128>(a, s, target, min_chunk);
+  else if (cfg == 1) launch_wcfg<2, 4, 64>(a, s, target, min_chunk);
+  else if (cfg == 2) launch_wcfg<1, 4, 64>(a, s, target, min_chunk);
+  else return 0;
+  return 1;
+}
+}  // namespace adp

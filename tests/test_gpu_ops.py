@@ -162,6 +162,29 @@ def test_tap64_configs(cfg):
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "128x256", "64x256"])
+@pytest.mark.parametrize("cout", [64, 192])
+def test_wgrad_tap64_configs(cfg, cout):
+    """Each forced tile configuration of the tap64 weight-gradient kernel vs autograd of the oracle
+    conv on a ragged pixel count (M = 2*23*23 = 1058, several 64-pixel stages per split)."""
+    N, S, cin = 2, 23, 128
+    xs, kern, bias, l = make_case(N, S, [cin], cout, 1, False, seed=11)
+    dt = torch.bfloat16
+    x = rb(xs[0], dt)
+    g = torch.Generator().manual_seed(12)
+    dZ = rb(torch.randn(N, S, S, cout, generator=g), dt)
+    kr = rb(kern, dt).clone().requires_grad_(True)
+    (R.conv2d_same(x, kr, None, relu=False) * dZ).sum().backward()
+    dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
+    ops.set_option("wgrad_tap64", cfg)
+    try:
+        ops.conv_wgrad(nhwc_pad(x, l.Cin_s, dt), nhwc_pad(dZ, l.cout_s, dt), dW, l.Nout)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("wgrad_tap64", 1)
+    assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
+
+
 @pytest.mark.parametrize("dt", DTS)
 def test_conv_transpose(dt):
     N, S, cin, cout = 2, 8, 128, 64
