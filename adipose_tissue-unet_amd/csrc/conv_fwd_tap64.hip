@@ -37,7 +37,9 @@ constexpr int cmax(int x, int y) { return x > y ? x : y; }
 template <int WM, int WN, int TM>
 constexpr int tap64_occ() { return 2 * (WM * TM + WN * 64) * 128 <= 81920 ? 2 : 1; }
 
-template <int WM, int WN, int TM>
+// TWO_BAR: barrier between a phase's LDS reads and its MFMAs as well as after them (the guide's
+// template); otherwise one barrier per phase, which lets one wave's reads overlap another's MFMAs.
+template <int WM, int WN, int TM, bool TWO_BAR>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
@@ -190,19 +192,19 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     // P0: (A0,B0)
     readA(buf, 0, fa);
     readB(buf, 0, fb0);
-    T64_BAR();
+    if (TWO_BAR) T64_BAR();
     mma(fa, fb0, 0, 0);
     T64_BAR();
     // P1: (A0,B1); A0 and B0 of this buffer are dead -> refill with step t+2
     if (pre) { issueA(0, k2, buf); issueB(0, k2, buf); }
     readB(buf, 1, fb1);
-    T64_BAR();
+    if (TWO_BAR) T64_BAR();
     mma(fa, fb1, 0, 1);
     T64_BAR();
     // P2: (A1,B1); B1 dead
     if (pre) issueB(1, k2, buf);
     readA(buf, 1, fa);
-    T64_BAR();
+    if (TWO_BAR) T64_BAR();
     mma(fa, fb1, 1, 1);
     T64_BAR();
     // P3: (A1,B0) from registers; A1 dead. Retire step t+1 (everything older than this K step's
@@ -242,10 +244,14 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
 
 template <int WM, int WN, int TM>
 void launch_cfg(FwdArgs& a, hipStream_t s) {
+  const bool two = adp::option("tap64_bar", 1) == 2;
   constexpr int BM = WM * TM, BN = WN * 64;
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
-  hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM>), dim3(a.nblocks), dim3(WM * WN * 64), 0, s, a);
+  if (two)
+    hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true>), dim3(a.nblocks), dim3(WM * WN * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false>), dim3(a.nblocks), dim3(WM * WN * 64), 0, s, a);
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 256x128 (8 waves, 64x64),

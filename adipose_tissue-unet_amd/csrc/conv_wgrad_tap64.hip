@@ -81,7 +81,10 @@ ADP_DEV bf16x8 tr_frag_asm(uint32_t base, int col0, int lane) {
 template <int WN, int WK, int TNW>
 constexpr int wg64_occ() { return 2 * 2 * 32 * (2 * WN * TNW + 2 * WK * 64) <= 81920 ? 2 : 1; }
 
-template <int WN, int WK, int TNW>
+// RA (row-aligned): Wo % 64 == 0, no upsample and 64-aligned splits, so every 64-pixel stage lies in
+// one image row: the stage origin (image, y, x0) is block-uniform (scalar registers) and each
+// slot's gather address is that origin plus a per-slot 64-bit constant.
+template <int WN, int WK, int TNW, bool TWO_BAR, bool RA>
 __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm_wgrad_tap64_kernel(WgradArgs a) {
   constexpr int NTH = WN * WK * 64;
   constexpr int TN = WN * TNW, TK = WK * 64;
@@ -99,7 +102,8 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
   constexpr int NBP = SPLIT ? NB / 2 : NB;             // n blocks per phase
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS-DMA bases in SGPRs
   const int wn = wave / WK, wk = wave % WK;
   // 1-D grid, XCD remap with the tile index fastest: all dW tiles of one pixel split run back to
   // back on one XCD and share its L2 for dY (every tile of the split) and X (neighbouring taps)
@@ -134,49 +138,109 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
   if (a.dy_mode == 1) { dsub = nd / a.Cps; dc = nd - dsub * a.Cps; }
   const bf16* dy = reinterpret_cast<const bf16*>(a.dY);
 
-  // ---- pixel slots (quarter q, instruction i)
-  PixSlot sx[2][GX], sd[2][GD];
+  // ---- general path: per-slot incremental (image, y, x) coordinates
+  PixSlot sx[2][RA ? 1 : GX], sd[2][RA ? 1 : GD];
+  Adv adv{0, 0, 0};
+  // ---- row-aligned path: per-slot byte addresses relative to the stage origin
+  const char* xb[2][GX];
+  const char* db[2][GD];
+  int xcol[2][GX], drow[2][GD];
+  struct StageOrg { int m, n, y, x0; } org[2];
+  const int ys_ok_lo = -oy;   // (y*stride + oy) in [0, Hv)  <=>  y*stride in [-oy, Hv - oy)
+  if constexpr (RA) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < 2; ++q) {
 #pragma unroll
-    for (int i = 0; i < GX; ++i) slot_init(sx[q][i], mbeg + 32 * q + i * RPIX + tid / CPRX, HWo, a.Wo);
+      for (int i = 0; i < GX; ++i) {
+        const int r = 32 * q + i * RPIX + tid / CPRX;
+        xcol[q][i] = r * a.stride + ox;
+        xb[q][i] = reinterpret_cast<const char*>(xbase) + 2LL * ((long long)oy * a.Ws + xcol[q][i]) * xcs;
+      }
 #pragma unroll
-    for (int i = 0; i < GD; ++i) slot_init(sd[q][i], mbeg + 32 * q + i * RPID + tid / CPRD, HWo, a.Wo);
+      for (int i = 0; i < GD; ++i) {
+        const int r = 32 * q + i * RPID + tid / CPRD;
+        drow[q][i] = r;
+        const long long e = a.dy_mode == 0 ? (long long)r * a.dy_stride + nd
+                                           : ((long long)(dsub >> 1) * 2 * a.Wo + 2 * r + (dsub & 1)) * a.dy_stride + dc;
+        db[q][i] = reinterpret_cast<const char*>(dy) + 2 * e;
+      }
+      org[q].m = mbeg;
+      org[q].n = mbeg / HWo;
+      const int rem = mbeg - org[q].n * HWo;
+      org[q].y = rem / a.Wo;
+      org[q].x0 = rem - org[q].y * a.Wo;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int i = 0; i < GX; ++i) slot_init(sx[q][i], mbeg + 32 * q + i * RPIX + tid / CPRX, HWo, a.Wo);
+#pragma unroll
+      for (int i = 0; i < GD; ++i) slot_init(sd[q][i], mbeg + 32 * q + i * RPID + tid / CPRD, HWo, a.Wo);
+    }
+    adv.an = 64 / HWo;
+    adv.ay = (64 - adv.an * HWo) / a.Wo;
+    adv.ax = 64 - adv.an * HWo - adv.ay * a.Wo;
   }
 
-  Adv adv;
-  adv.an = 64 / HWo;
-  adv.ay = (64 - adv.an * HWo) / a.Wo;
-  adv.ax = 64 - adv.an * HWo - adv.ay * a.Wo;
-
-  // issue quarter q of the stage the slots currently point at into buffer buf, then advance them
+  // issue quarter q of the next stage into buffer buf, then advance to the following stage
   auto issue = [&](int q, int buf) {
     unsigned char* base = smem + buf * STAGE;
+    if constexpr (RA) {
+      StageOrg& o = org[q];
+      const int left = mend - o.m;                                   // valid rows of this stage
+      const long long xo = 2LL * (((long long)o.n * a.Hs + o.y * a.stride) * a.Ws + (long long)o.x0 * a.stride);
+      const long long dof = a.dy_mode == 0 ? 2LL * o.m * a.dy_stride
+                                           : 2LL * (((long long)o.n * 2 * a.Ho + 2 * o.y) * 2 * a.Wo + 2 * o.x0) * a.dy_stride;
+      const bool yok = kvalid && o.y * a.stride >= ys_ok_lo && o.y * a.stride + oy < Hv;
+      const int x0s = o.x0 * a.stride;
 #pragma unroll
-    for (int i = 0; i < GD; ++i) {
-      PixSlot& s = sd[q][i];
-      size_t off;
-      if (a.dy_mode == 0) {
-        off = (size_t)s.m * a.dy_stride + nd;
-      } else {
-        off = (((size_t)s.n * (2 * a.Ho) + 2 * s.y + (dsub >> 1)) * (2 * a.Wo) + 2 * s.x + (dsub & 1)) * a.dy_stride + dc;
+      for (int i = 0; i < GD; ++i) {
+        const bool ok = nvalid && drow[q][i] < left;
+        const void* p = ok ? (const void*)(db[q][i] + dof) : (const void*)wg64_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + q * QD + (i * RPID + wave * (64 / CPRD)) * RD), 16, 0, 0);
       }
-      const bool ok = s.m < mend && nvalid;
-      const void* p = ok ? (const void*)(dy + off) : (const void*)wg64_zero_page;
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + q * QD + (i * RPID + wave * (64 / CPRD)) * RD), 16, 0, 0);
-      slot_adv(s, adv, a.Ho, a.Wo);
-    }
 #pragma unroll
-    for (int i = 0; i < GX; ++i) {
-      PixSlot& s = sx[q][i];
-      int yi = s.y * a.stride + oy, xi = s.x * a.stride + ox;
-      const bool ok = s.m < mend && kvalid && (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
-      if (a.up == 2) { yi >>= 1; xi >>= 1; }
-      const void* p = ok ? (const void*)(xbase + (size_t)((s.n * a.Hs + yi) * a.Ws + xi) * xcs)
-                         : (const void*)wg64_zero_page;
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + 2 * QD + q * QX + (i * RPIX + wave * (64 / CPRX)) * RX),
-                                       16, 0, 0);
-      slot_adv(s, adv, a.Ho, a.Wo);
+      for (int i = 0; i < GX; ++i) {
+        const int xr = 32 * q + i * RPIX + tid / CPRX;
+        const bool ok = yok && xr < left && (unsigned)(x0s + xcol[q][i]) < (unsigned)Wv;
+        const void* p = ok ? (const void*)(xb[q][i] + xo * xcs) : (const void*)wg64_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + 2 * QD + q * QX + (i * RPIX + wave * (64 / CPRX)) * RX),
+                                         16, 0, 0);
+      }
+      o.m += 64;
+      o.x0 += 64;
+      if (o.x0 >= a.Wo) {
+        o.x0 = 0;
+        if (++o.y == a.Ho) { o.y = 0; ++o.n; }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < GD; ++i) {
+        PixSlot& s = sd[q][i];
+        size_t off;
+        if (a.dy_mode == 0) {
+          off = (size_t)s.m * a.dy_stride + nd;
+        } else {
+          off = (((size_t)s.n * (2 * a.Ho) + 2 * s.y + (dsub >> 1)) * (2 * a.Wo) + 2 * s.x + (dsub & 1)) * a.dy_stride + dc;
+        }
+        const bool ok = s.m < mend && nvalid;
+        const void* p = ok ? (const void*)(dy + off) : (const void*)wg64_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + q * QD + (i * RPID + wave * (64 / CPRD)) * RD), 16, 0, 0);
+        slot_adv(s, adv, a.Ho, a.Wo);
+      }
+#pragma unroll
+      for (int i = 0; i < GX; ++i) {
+        PixSlot& s = sx[q][i];
+        int yi = s.y * a.stride + oy, xi = s.x * a.stride + ox;
+        const bool ok = s.m < mend && kvalid && (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
+        if (a.up == 2) { yi >>= 1; xi >>= 1; }
+        const void* p = ok ? (const void*)(xbase + (size_t)((s.n * a.Hs + yi) * a.Ws + xi) * xcs)
+                           : (const void*)wg64_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(base + 2 * QD + q * QX + (i * RPIX + wave * (64 / CPRX)) * RX),
+                                         16, 0, 0);
+        slot_adv(s, adv, a.Ho, a.Wo);
+      }
     }
   };
 
@@ -230,12 +294,12 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
     if (n1) issue(1, buf ^ 1);
     readD(buf, 0, 0);
     readX(buf, 0);
-    W64_BAR();
+    if (TWO_BAR) W64_BAR();
     mma(0);
     if (SPLIT) {
       W64_BAR();
       readD(buf, 0, 1);
-      W64_BAR();
+      if (TWO_BAR) W64_BAR();
       mma(1);
     }
     // retire stage t q1 (issued after it: stage t+1 q0 and q1, iff they exist)
@@ -246,12 +310,12 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
     if (n2) issue(0, buf);
     readD(buf, 1, 0);
     readX(buf, 1);
-    W64_BAR();
+    if (TWO_BAR) W64_BAR();
     mma(0);
     if (SPLIT) {
       W64_BAR();
       readD(buf, 1, 1);
-      W64_BAR();
+      if (TWO_BAR) W64_BAR();
       mma(1);
     }
     // retire stage t+1 q0 (issued after it: stage t+1 q1, stage t+2 q0 iff it exists)
@@ -290,7 +354,13 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   splits = std::max(1, std::min(splits, maxsplit));
   a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
   splits = (a.M + a.mchunk - 1) / a.mchunk;
-  hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW>), dim3(tiles * splits), dim3(WN * WK * 64), 0, s, a);
+  const bool ra = a.Wo % 64 == 0 && a.up == 1 && adp::option("wgrad_ra", 1);
+  const bool two = adp::option("tap64_bar", 1) == 2;
+  const dim3 grid(tiles * splits), block(WN * WK * 64);
+  if (ra && !two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, true>), grid, block, 0, s, a);
+  else if (ra) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, true>), grid, block, 0, s, a);
+  else if (!two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, false>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, false>), grid, block, 0, s, a);
 }
 
 }  // namespace

@@ -149,10 +149,11 @@ def test_adipose_train_step_adam(adipose_weights):
         assert (torch.as_tensor(gk) - k.detach()).abs().max().item() < 1e-4, name
 
 
-@pytest.mark.parametrize("dtype,base", [("f32", 16), ("bf16", 16), ("bf16", 64)])
-def test_unet_bn_forward_and_grads(dtype, base):
-    """base 64 puts every layer but the input conv on the tap64 kernel (fwd, dgrad, ConvT, concat)."""
-    B, S, L = 2, 32, 3
+@pytest.mark.parametrize("dtype,base,S", [("f32", 16, 32), ("bf16", 16, 32), ("bf16", 64, 32), ("bf16", 64, 128)])
+def test_unet_bn_forward_and_grads(dtype, base, S):
+    """base 64 puts every layer but the input conv on the tap64 kernels (fwd, dgrad, wgrad, ConvT,
+    concat); S = 128 makes the two upper levels row-aligned (Wo % 64 == 0) for the wgrad gather."""
+    B, L = 2, 3
     w = R.unet_bn_keras_weights(levels=L, base=base, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
     net = UNetBN(B, S, levels=L, base=base, in_ch=3, dtype=dtype, device=DEV)
@@ -167,6 +168,7 @@ def test_unet_bn_forward_and_grads(dtype, base):
     torch.cuda.synchronize()
     W = {k: [torch.tensor(v, requires_grad=True) for v in vs] for k, vs in w.items()}
     p = R.unet_bn_forward(x, W, levels=L)
+    p.retain_grad()
     loss = R.combined_loss_standard(y, p)
     loss.backward()
     tol = 1e-4 if dtype == "f32" else 3e-2
@@ -183,4 +185,8 @@ def test_unet_bn_forward_and_grads(dtype, base):
                 c = cos(torch.as_tensor(gi), t.grad)
                 if c <= 0.95:  # bf16 dz storage through BN bwd
                     bad.append((name, si, c))
+    if bad:  # localise: is the loss gradient dL/dp already off, or only the backward pass?
+        dp_err = (grads["main_out"].cpu() - p.grad).abs().max().item() / p.grad.abs().max().item()
+        met = tr.read_metrics()
+        bad.insert(0, ("dL/dp", dp_err, "loss", met["loss"], loss.item()))
     assert not bad, bad

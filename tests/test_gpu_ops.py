@@ -164,10 +164,12 @@ def test_tap64_configs(cfg):
 
 @pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "128x256", "64x256"])
 @pytest.mark.parametrize("cout", [64, 192])
-def test_wgrad_tap64_configs(cfg, cout):
+@pytest.mark.parametrize("S", [23, 64], ids=["ragged", "rowaligned"])
+def test_wgrad_tap64_configs(cfg, cout, S):
     """Each forced tile configuration of the tap64 weight-gradient kernel vs autograd of the oracle
-    conv on a ragged pixel count (M = 2*23*23 = 1058, several 64-pixel stages per split)."""
-    N, S, cin = 2, 23, 128
+    conv: a ragged pixel count (S = 23: M = 1058, general gather path) and row-aligned images
+    (S = 64: Wo % 64 == 0, the scalar stage-origin gather path)."""
+    N, cin = 2, 128
     xs, kern, bias, l = make_case(N, S, [cin], cout, 1, False, seed=11)
     dt = torch.bfloat16
     x = rb(xs[0], dt)
@@ -186,8 +188,9 @@ def test_wgrad_tap64_configs(cfg, cout):
 
 
 @pytest.mark.parametrize("dt", DTS)
-def test_conv_transpose(dt):
-    N, S, cin, cout = 2, 8, 128, 64
+@pytest.mark.parametrize("S", [8, 64])
+def test_conv_transpose(dt, S):
+    N, cin, cout = 2, 128, 64
     g = torch.Generator().manual_seed(3)
     x = rb(torch.randn(N, S, S, cin, generator=g), dt)
     k = rb(torch.randn(cin, cout, 2, 2, generator=g) * 0.1, dt)

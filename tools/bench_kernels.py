@@ -21,6 +21,7 @@ def main():
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--variants", default="conv_fast=2,fwd_tap64=0;conv_fast=2,fwd_tap64=1")
     p.add_argument("--kinds", default="fwd,wgrad")
+    p.add_argument("--layers", default="", help="comma-separated substrings selecting layer shapes")
     p.add_argument("--batch", type=int, default=4)
     args = p.parse_args()
     import torch
@@ -34,6 +35,9 @@ def main():
     shapes = [("L0 64->64", 1024, 64, 64), ("L0 128->64", 1024, 128, 64), ("L1 128->128", 512, 128, 128),
               ("L2 256->256", 256, 256, 256), ("L3 512->512", 128, 512, 512), ("L4 1024->1024", 64, 1024, 1024),
               ("L3 1024->512", 128, 1024, 512), ("L4 1024->512", 64, 1024, 512), ("L1 256->128", 512, 256, 128)]
+    if args.layers:
+        keys = args.layers.split(",")
+        shapes = [sh for sh in shapes if any(k in sh[0] for k in keys)]
     variants = list(range(len(args.variants.split(";"))))
     settings = [[(kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",") if kv]
                 for v in args.variants.split(";")]
