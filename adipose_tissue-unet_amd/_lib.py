@@ -36,13 +36,14 @@ class ConvDesc(C.Structure):
         ("out2_stride", C.c_int), ("split_c", C.c_int),
         ("mask_stride", C.c_int), ("mask_scale", C.c_float),
         ("mask2_stride", C.c_int), ("mask2_scale", C.c_float),
-        ("accum_stride", C.c_int)]
+        ("accum_stride", C.c_int), ("bnr_stride", C.c_int)]
 
 
 class ConvIO(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in (
         "srcA", "srcB", "bn_scaleA", "bn_shiftA", "bn_scaleB", "bn_shiftB", "W", "bias",
-        "out", "out2", "addend", "mask", "mask2", "accum", "bn_sum", "bn_sqsum")]
+        "out", "out2", "addend", "mask", "mask2", "accum", "bn_sum", "bn_sqsum",
+        "bnr_z", "bnr_scale", "bnr_shift", "bnr_mean", "bnr_invstd", "bnr_dgamma", "bnr_dbeta")]
 
 
 _P = C.c_void_p

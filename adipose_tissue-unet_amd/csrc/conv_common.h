@@ -24,6 +24,10 @@ struct FwdArgs {
   const void* mask2; int mask2_stride; float mask2_scale;
   float* accum; int accum_stride;
   float* bn_sum; float* bn_sq;
+  // fused BatchNorm-backward reduction of the stored output (see adp_conv_io.bnr_*)
+  const void* bnr_z; int bnr_zs;
+  const float* bnr_sc; const float* bnr_sh; const float* bnr_mean; const float* bnr_invstd;
+  float* bnr_dgamma; float* bnr_dbeta;
   int M;
   int ntile_n;           // gridDim decomposition helper
   int nblocks;
@@ -96,7 +100,8 @@ ADP_DEV bf16x8 tr_frag_sw(const unsigned char* base, int row0, int col0, int lan
 // `tile` holds `rows` x BN f32 accumulators (row stride BN + 4) for output pixels m0.. and GEMM
 // columns n0..; NTH threads each own one 8-column group (cg = tid % (BN/8)) and walk the rows.
 // Applies bias, ReLU, dropout, the pixel-shuffle / split / addend / mask / accumulate store modes
-// and collects BatchNorm partial sums of the stored values into bs/bq.
+// and collects per-channel partial sums into bs/bq: BatchNorm statistics (sum, sum of squares) of the
+// stored values, or with bnr_z the BatchNorm-backward sums (db, db*xhat) of the stored gradient.
 template <int NTH, int BN>
 ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int n0, int tid,
                       float (&bs)[8], float (&bq)[8]) {
@@ -182,6 +187,64 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
   }
 }
 
+// Epilogue of a data-gradient launch with the fused BatchNorm-backward reduction (bnr_*): plain store
+// of the gradient dA (+addend, *mask), then the sums db = dA*(z*scale+shift > 0) and db*xhat over the
+// stored (bf16-rounded) dA, exactly what adp_bn_bwd_reduce would read. Kept separate from epi_rows so
+// that the per-channel parameters cost registers only in the kernels that use them (they are read
+// per row from L1 rather than held across the row loop).
+template <int NTH, int BN>
+ADP_DEV void epi_rows_bnr(const FwdArgs& a, const float* tile, int rows, int m0, int n0, int tid,
+                          float (&bs)[8], float (&bq)[8]) {
+  constexpr int LT = BN + 4;
+  constexpr int GPR = BN / 8;
+  constexpr int RSTEP = NTH / GPR;
+  const int cg = tid % GPR;
+  const int n = n0 + cg * 8;
+  if (n >= a.Nout) return;
+  for (int row = tid / GPR; row < rows; row += RSTEP) {
+    const int m = m0 + row;
+    if (m >= a.M) break;
+    float v[8], f[8];
+    const float4* tp = reinterpret_cast<const float4*>(tile + row * LT + cg * 8);
+    float4 t0 = tp[0], t1 = tp[1];
+    v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w; v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
+    Grp<bf16> gr;
+    if (a.addend) {
+      grp_load(gr, reinterpret_cast<const bf16*>(a.addend) + (size_t)m * a.addend_stride + n);
+      grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += f[j];
+    }
+    if (a.mask) {
+      grp_load(gr, reinterpret_cast<const bf16*>(a.mask) + (size_t)m * a.mask_stride + n);
+      grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = f[j] > 0.f ? v[j] * a.mask_scale : 0.f;
+    }
+    grp_from_f(gr, v);
+    grp_store(gr, reinterpret_cast<bf16*>(a.out) + (size_t)m * a.out_stride + n);
+    grp_to_f(gr, v);   // the stored (rounded) gradient
+    grp_load(gr, reinterpret_cast<const bf16*>(a.bnr_z) + (size_t)m * a.bnr_zs + n);
+    grp_to_f(gr, f);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 sc = *reinterpret_cast<const float4*>(a.bnr_sc + n + 4 * h);
+      const float4 sh = *reinterpret_cast<const float4*>(a.bnr_sh + n + 4 * h);
+      const float4 mu = *reinterpret_cast<const float4*>(a.bnr_mean + n + 4 * h);
+      const float4 is = *reinterpret_cast<const float4*>(a.bnr_invstd + n + 4 * h);
+      const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+      const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int jj = 4 * h + j;
+        const float db = fmaf(f[jj], scv[j], shv[j]) > 0.f ? v[jj] : 0.f;
+        bs[jj] += db;
+        bq[jj] += db * (f[jj] - muv[j]) * isv[j];
+      }
+    }
+  }
+}
+
 // Threads with equal column group hold partial BN sums of the same 8 channels: reduce them through
 // LDS (`red` needs NTH*16 floats; caller guarantees no pending reads of it), then one atomic per
 // channel and block.
@@ -200,8 +263,8 @@ ADP_DEV void epi_bn_flush(const FwdArgs& a, float* red, int n0, int tid, const f
     const int nn = n0 + tid;
     if (nn < a.Nout) {
       const int c = a.out_mode == 1 ? nn % a.Cps : nn;
-      atomicAdd(a.bn_sum + c, s);
-      atomicAdd(a.bn_sq + c, q);
+      atomicAdd((a.bnr_z ? a.bnr_dbeta : a.bn_sum) + c, s);
+      atomicAdd((a.bnr_z ? a.bnr_dgamma : a.bn_sq) + c, q);
     }
   }
 }

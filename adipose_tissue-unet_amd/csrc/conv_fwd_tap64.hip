@@ -39,7 +39,8 @@ constexpr int tap64_occ() { return 2 * (WM * TM + WN * 64) * 128 <= 81920 ? 2 : 
 
 // TWO_BAR: barrier between a phase's LDS reads and its MFMAs as well as after them (the guide's
 // template); otherwise one barrier per phase, which lets one wave's reads overlap another's MFMAs.
-template <int WM, int WN, int TM, bool TWO_BAR>
+// BNR: data-gradient launch with the fused BatchNorm-backward reduction epilogue (epi_rows_bnr).
+template <int WM, int WN, int TM, bool TWO_BAR, bool BNR>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
@@ -234,10 +235,11 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
             tile[((mt / MIQ) * HM + (mt % MIQ) * 16 + rq + r) * LT + wc * 64 + nt * 16 + col] = acc[mt][nt][r];
     }
     __syncthreads();
-    epi_rows<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
+    if constexpr (BNR) epi_rows_bnr<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
+    else epi_rows<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
     __syncthreads();
   }
-  if (a.bn_sum) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
+  if (a.bn_sum || a.bnr_z) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
 }
 
 #undef T64_BAR
@@ -248,10 +250,14 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM, BN = WN * 64;
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
-  if (two)
-    hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true>), dim3(a.nblocks), dim3(WM * WN * 64), 0, s, a);
-  else
-    hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false>), dim3(a.nblocks), dim3(WM * WN * 64), 0, s, a);
+  const dim3 g(a.nblocks), b(WM * WN * 64);
+  if (a.bnr_z) {
+    if (two) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, true>), g, b, 0, s, a);
+  } else {
+    if (two) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, false>), g, b, 0, s, a);
+  }
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 256x128 (8 waves, 64x64),
@@ -269,6 +275,8 @@ namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   const int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
+  // the fused BN-backward epilogue handles plain stores only (what the data-gradient launches use)
+  if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const int Cin_s = a.CAs + a.CBs;
   if (a.scA || a.scB || a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 ||
       a.Kpad != a.K)

@@ -1008,6 +1008,9 @@ __global__ void channel_sum_kernel(size_t M, int C, int stride, const T* x, floa
 
 namespace {
 template <typename T>
+int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast);
+
+template <typename T>
 int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   FwdArgs a{};
   a.srcA = io->srcA; a.srcB = io->srcB;
@@ -1026,14 +1029,34 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   a.mask2 = io->mask2; a.mask2_stride = d->mask2_stride; a.mask2_scale = d->mask2_scale;
   a.accum = io->accum; a.accum_stride = d->accum_stride;
   a.bn_sum = io->bn_sum; a.bn_sq = io->bn_sqsum;
+  a.bnr_z = io->bnr_z; a.bnr_zs = d->bnr_stride;
+  a.bnr_sc = io->bnr_scale; a.bnr_sh = io->bnr_shift; a.bnr_mean = io->bnr_mean; a.bnr_invstd = io->bnr_invstd;
+  a.bnr_dgamma = io->bnr_dgamma; a.bnr_dbeta = io->bnr_dbeta;
   a.M = d->N * d->Ho * d->Wo;
   ADP_REQUIRE(a.CAs % 8 == 0 && a.CBs % 8 == 0, "adp_conv_fwd: channel strides must be multiples of 8");
   ADP_REQUIRE(a.M > 0 && a.Nout > 0, "adp_conv_fwd: empty problem");
   ADP_REQUIRE(d->out_mode != 1 || (d->shuffle_c > 0 && d->Nout % d->shuffle_c == 0), "adp_conv_fwd: bad shuffle_c");
   ADP_REQUIRE(d->out_mode != 2 || (io->out2 && d->split_c > 0), "adp_conv_fwd: split store needs out2/split_c");
+  ADP_REQUIRE(!a.bnr_z || (d->out_mode == 0 && !a.bn_sum && a.bnr_sc && a.bnr_sh && a.bnr_mean && a.bnr_invstd &&
+                           a.bnr_dgamma && a.bnr_dbeta && a.bnr_zs == a.out_stride && a.bnr_zs % 8 == 0 &&
+                           a.Nout % 8 == 0),
+              "adp_conv_fwd: fused BN-backward reduction needs out_mode 0, all bnr_* pointers, z stride == out stride");
   const int fast = adp::option("conv_fast", 2);
+  if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB && adp::launch_fwd_tap64(a, s))
+    return adp::check_launch("adp_conv_fwd");
+  // every other kernel: plain launch, then the standalone BN-backward reduction on the stored output
+  const FwdArgs bnr = a;
+  a.bnr_z = nullptr;
+  const int rc = launch_fwd_plain<T>(a, s, fast);
+  if (rc != 0 || !bnr.bnr_z) return rc;
+  return adp_bn_bwd_reduce(std::is_same<T, bf16>::value ? ADP_BF16 : ADP_F32, (size_t)bnr.M, bnr.out_stride, bnr.out,
+                           bnr.bnr_z, bnr.bnr_sc, bnr.bnr_sh, bnr.bnr_mean, bnr.bnr_invstd, bnr.bnr_dgamma,
+                           bnr.bnr_dbeta, (adp_stream_t)s);
+}
+
+template <typename T>
+int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
   if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB) {
-    if (adp::launch_fwd_tap64(a, s)) return adp::check_launch("adp_conv_fwd");
     const int w64 = (a.Nout + 63) / 64 * 64 - a.Nout, w128 = (a.Nout + 127) / 128 * 128 - a.Nout;
     if (a.Nout > 64 && w128 <= w64) {
       a.ntile_n = (a.Nout + 127) / 128;

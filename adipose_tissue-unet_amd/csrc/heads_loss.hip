@@ -8,6 +8,7 @@
 //   metrics    dice_coef src/utils/model.py:93-98, Keras binary_accuracy (threshold 0.5),
 //              calculate_pixel_metrics counts Segmentation/full_evaluation_enhanced.py:721-785
 #include "common.h"
+#include <algorithm>
 #include "../../include/adipose_hip.h"
 
 namespace {
@@ -47,6 +48,61 @@ __global__ void head_fwd_kernel(size_t M, int Cs, int Cin, const T* x, const flo
     }
     // softmax over 2 logits, channel 1 kept == 1/(1+exp(z0-z1)); sigmoid otherwise
     p[m] = NOUT == 2 ? 1.f / (1.f + expf(z0 - z1)) : 1.f / (1.f + expf(-z0));
+  }
+}
+
+// forward, coalesced form for G = Cs/8 a power of two <= 64: the G lanes of one pixel each own one
+// 8-channel group (adjacent 16-B loads), partial dot products are summed with lane shuffles.
+template <typename T, int NOUT, int G>
+__global__ void head_fwd_grp_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* b,
+                                    const float* sc, const float* sh, float* p) {
+  const int g = threadIdx.x % G;
+  float w0[8], w1[8], s_[8], h_[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = g * 8 + j;
+    w0[j] = c < Cin ? W[c] : 0.f;
+    w1[j] = (NOUT == 2 && c < Cin) ? W[Cin + c] : 0.f;
+    s_[j] = sc ? sc[c] : 1.f;
+    h_[j] = sc ? sh[c] : 0.f;
+  }
+  const float b0 = b[0], b1 = NOUT == 2 ? b[1] : 0.f;
+  const size_t lanes = TPB / G;
+  for (size_t m = blockIdx.x * lanes + threadIdx.x / G; m < M; m += (size_t)gridDim.x * lanes) {
+    Grp<T> gr;
+    float f[8];
+    grp_load(gr, x + m * Cs + g * 8);
+    grp_to_f(gr, f);
+    float z0 = 0.f, z1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = sc ? fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f) : f[j];
+      z0 = fmaf(v, w0[j], z0);
+      if (NOUT == 2) z1 = fmaf(v, w1[j], z1);
+    }
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) {
+      z0 += __shfl_xor(z0, o, 64);
+      if (NOUT == 2) z1 += __shfl_xor(z1, o, 64);
+    }
+    if (g == 0) {
+      z0 += b0; z1 += b1;
+      p[m] = NOUT == 2 ? 1.f / (1.f + expf(z0 - z1)) : 1.f / (1.f + expf(-z0));
+    }
+  }
+}
+
+template <typename T, int NOUT>
+void launch_head_fwd(size_t M, int Cs, int Cin, const T* x, const float* W, const float* b, const float* sc,
+                     const float* sh, float* p, hipStream_t s) {
+  const int G = Cs / 8;
+  const int blk = (int)std::min<size_t>((M * G + TPB - 1) / TPB, 8192);
+  switch (G) {
+#define ADP_HG(GG) case GG: hipLaunchKernelGGL((head_fwd_grp_kernel<T, NOUT, GG>), dim3(blk), dim3(TPB), 0, s, M, Cs, Cin, x, W, b, sc, sh, p); return;
+    ADP_HG(1) ADP_HG(2) ADP_HG(4) ADP_HG(8) ADP_HG(16) ADP_HG(32) ADP_HG(64)
+#undef ADP_HG
+    default:
+      hipLaunchKernelGGL((head_fwd_kernel<T, NOUT>), dim3(nblk(M)), dim3(TPB), 0, s, M, Cs, Cin, x, W, b, sc, sh, p);
   }
 }
 
@@ -194,31 +250,51 @@ ADP_DEV double block_sum_d(double v, double* sh) {
 }
 
 // one block per image row
+ADP_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// one wave per image row (row BCE by lane shuffles); the 8 global statistics are accumulated per
+// lane across the wave's rows and reduced once per block (one f64 atomic per statistic and block)
 __global__ void loss_rows_kernel(int N, int H, int W, const float* p, const float* y, int smooth,
                                  float ep, float en, float* row_bce, double* stats) {
-  __shared__ double sh[16];
-  const int row = blockIdx.x;
-  const float* pr = p + (size_t)row * W;
-  const float* yr = y + (size_t)row * W;
-  float bce = 0.f, s_yp = 0.f, s_y = 0.f, s_p = 0.f, r_yp = 0.f, r_y = 0.f, r_p = 0.f, acc = 0.f, r_yi = 0.f;
-  for (int x = threadIdx.x; x < W; x += TPB) {
-    float pv = pr[x], yv = yr[x];
-    float ys = smooth_y(yv, smooth, ep, en);
-    float pc = clipp(pv);
-    bce -= ys * logf(pc + KEPS) + (1.f - ys) * logf(1.f - pc + KEPS);
-    s_yp += ys * pc; s_y += ys; s_p += pc;
-    r_yp += yv * pv; r_y += yv; r_p += pv;
-    const float pb = pv > 0.5f ? 1.f : 0.f;   // == round(clip(p,0,1)) (round half to even)
-    acc += (yv == pb) ? 1.f : 0.f;
-    r_yi += yv * pb;
+  constexpr int WPB = TPB / 64;
+  __shared__ double sh[8][WPB];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int row = blockIdx.x * WPB + wave; row < N * H; row += gridDim.x * WPB) {
+    const float* pr = p + (size_t)row * W;
+    const float* yr = y + (size_t)row * W;
+    float bce = 0.f, s_yp = 0.f, s_y = 0.f, s_p = 0.f, r_yp = 0.f, r_y = 0.f, r_p = 0.f, acc = 0.f, r_yi = 0.f;
+    for (int x = lane; x < W; x += 64) {
+      float pv = pr[x], yv = yr[x];
+      float ys = smooth_y(yv, smooth, ep, en);
+      float pc = clipp(pv);
+      bce -= ys * logf(pc + KEPS) + (1.f - ys) * logf(1.f - pc + KEPS);
+      s_yp += ys * pc; s_y += ys; s_p += pc;
+      r_yp += yv * pv; r_y += yv; r_p += pv;
+      const float pb = pv > 0.5f ? 1.f : 0.f;   // == round(clip(p,0,1)) (round half to even)
+      acc += (yv == pb) ? 1.f : 0.f;
+      r_yi += yv * pb;
+    }
+    const double rb = wave_sum_d((double)bce);
+    if (lane == 0) row_bce[row] = (float)(rb / W);
+    st[0] += s_yp; st[1] += s_y; st[2] += s_p; st[3] += r_yp;
+    st[4] += r_y; st[5] += r_p; st[6] += acc; st[7] += r_yi;
   }
-  double v[9] = {bce, s_yp, s_y, s_p, r_yp, r_y, r_p, acc, r_yi};
-  double tot[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) tot[i] = block_sum_d(v[i], sh);
-  if (threadIdx.x == 0) {
-    row_bce[row] = (float)(tot[0] / W);
-    for (int i = 1; i < 9; ++i) atomicAdd(stats + i - 1, tot[i]);
+  for (int i = 0; i < 8; ++i) {
+    const double v = wave_sum_d(st[i]);
+    if (lane == 0) sh[i][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < WPB; ++w) t += sh[threadIdx.x][w];
+    atomicAdd(stats + threadIdx.x, t);
   }
 }
 
@@ -329,8 +405,7 @@ extern "C" int adp_head_softmax2_fwd(int dtype, size_t M, int Cs, int Cin, const
                                      adp_stream_t st) {
   ADP_REQUIRE(Cs % 8 == 0 && Cs <= 1024 && Cin <= Cs, "adp_head_softmax2_fwd: bad channels");
   DTYPE_SWITCH(dtype, T,
-               hipLaunchKernelGGL((head_fwd_kernel<T, 2>), dim3(nblk(M)), dim3(TPB), 0, (hipStream_t)st, M, Cs,
-                                  Cin, (const T*)x, W, b, sc, sh, p));
+               launch_head_fwd<T, 2>(M, Cs, Cin, (const T*)x, W, b, sc, sh, p, (hipStream_t)st));
   return adp::check_launch("adp_head_softmax2_fwd");
 }
 
@@ -339,8 +414,7 @@ extern "C" int adp_head_sigmoid_fwd(int dtype, size_t M, int Cs, int Cin, const 
                                     adp_stream_t st) {
   ADP_REQUIRE(Cs % 8 == 0 && Cs <= 1024 && Cin <= Cs, "adp_head_sigmoid_fwd: bad channels");
   DTYPE_SWITCH(dtype, T,
-               hipLaunchKernelGGL((head_fwd_kernel<T, 1>), dim3(nblk(M)), dim3(TPB), 0, (hipStream_t)st, M, Cs,
-                                  Cin, (const T*)x, W, b, sc, sh, p));
+               launch_head_fwd<T, 1>(M, Cs, Cin, (const T*)x, W, b, sc, sh, p, (hipStream_t)st));
   return adp::check_launch("adp_head_sigmoid_fwd");
 }
 
@@ -391,7 +465,8 @@ extern "C" int adp_resize_bilinear_bwd(int N, int Hs, int Ws, int Ho, int Wo, co
 extern "C" int adp_loss_rows(int N, int H, int W, const float* p, const float* y, int smooth, float ep,
                              float en, float* row_bce, double* stats, adp_stream_t st) {
   ADP_REQUIRE(N > 0 && H > 0 && W > 0, "adp_loss_rows: bad dims");
-  hipLaunchKernelGGL(loss_rows_kernel, dim3(N * H), dim3(TPB), 0, (hipStream_t)st, N, H, W, p, y, smooth, ep, en,
+  const int lrb = std::min((N * H + TPB / 64 - 1) / (TPB / 64), 512);
+  hipLaunchKernelGGL(loss_rows_kernel, dim3(lrb), dim3(TPB), 0, (hipStream_t)st, N, H, W, p, y, smooth, ep, en,
                      row_bce, stats);
   return adp::check_launch("adp_loss_rows");
 }

@@ -375,14 +375,15 @@ class UNetEngine:
         self._grad_ready(l.name)
 
     def dgrad(self, l, dZ, out, *, Ho=None, Wo=None, addend=None, mask=None, mask_scale=1.0, split=False,
-              out2=None, mask2=None, mask2_scale=1.0, skip_first=False):
-        """Data gradient of a dense layer: a forward-shaped launch over dZ with repacked weights."""
+              out2=None, mask2=None, mask2_scale=1.0, skip_first=False, bn_reduce=None):
+        """Data gradient of a dense layer: a forward-shaped launch over dZ with repacked weights.
+        bn_reduce: fuse the BatchNorm-backward reduction of the layer `out` is the gradient of."""
         Wd = self.Wd(l.name)
         if l.transpose:
             # input coord = 2*o + (dy,dx): 4 taps, stride 2, over the ConvT output gradient
             return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=2, kw=2, dil=1, pad=0, stride=2,
                                 Ho=dZ.shape[1] // 2, Wo=dZ.shape[2] // 2, addend=addend, mask=mask,
-                                mask_scale=mask_scale)
+                                mask_scale=mask_scale, bn_reduce=bn_reduce)
         # forward dilation d, 'same' padding: data gradient is the same gather with flipped taps
         if split and skip_first:
             # only the second (decoder) part of a concat input is needed: offset the weight rows
@@ -394,7 +395,7 @@ class UNetEngine:
                                 split_c=l.cin_s[0], addend=addend, mask=mask, mask_scale=mask_scale,
                                 mask2=mask2, mask2_scale=mask2_scale)
         return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=l.k, kw=l.k, dil=l.dil, addend=addend, mask=mask,
-                            mask_scale=mask_scale)
+                            mask_scale=mask_scale, bn_reduce=bn_reduce)
 
 
 # --------------------------------------------------------------------------------- adipose_v3
@@ -729,11 +730,18 @@ class UNetBN(UNetEngine):
         self._train_fwd = train
         return {"main_out": a["p"]}
 
-    def _bn_bwd(self, name, dA, z, dz):
-        """dA: gradient wrt relu(bn(z)) -> dz, and gamma/beta grads."""
+    def _bn_red(self, name, z):
+        """bn_reduce argument for a dgrad launch whose output is the gradient of relu(bn_name(z))."""
+        s = self.st[name]
+        return (z, s[2], s[3], s[4], s[5], self.ps.gview(name + "/gamma"), self.ps.gview(name + "/beta"))
+
+    def _bn_bwd(self, name, dA, z, dz, reduced=False):
+        """dA: gradient wrt relu(bn(z)) -> dz, and gamma/beta grads (already summed by the producer of
+        dA when reduced=True)."""
         s = self.st[name]
         dg, db = self.ps.gview(name + "/gamma"), self.ps.gview(name + "/beta")
-        ops.bn_bwd_reduce(dA, z, s[2], s[3], s[4], s[5], dg, db)
+        if not reduced:
+            ops.bn_bwd_reduce(dA, z, s[2], s[3], s[4], s[5], dg, db)
         count = z.shape[0] * z.shape[1] * z.shape[2]
         ops.bn_bwd_apply(dA, z, s[2], s[3], s[4], s[5], self.ps.view(name + "/gamma"), dg, db, count, dz)
 
@@ -756,13 +764,14 @@ class UNetBN(UNetEngine):
         # decoder, from level 0 down to the bottleneck
         for i in range(0, Lv - 1):
             dz = gb(f"dz_y{i}_2", a[f"y{i}_2"])
-            self._bn_bwd(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz)
+            # level 0's dA comes from the head; deeper levels' from the ConvT dgrad (reduction fused)
+            self._bn_bwd(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz, reduced=i > 0)
             l2 = L[f"dec{i}_conv2"]
             self.wgrad(l2, a[f"ay{i}_1"], dz)
             dA1 = gb(f"dA_y{i}_1", a[f"y{i}_1"])
-            self.dgrad(l2, dz, dA1)
+            self.dgrad(l2, dz, dA1, bn_reduce=self._bn_red(f"dec{i}_conv1", a[f"y{i}_1"]))
             dz1 = gb(f"dz_y{i}_1", a[f"y{i}_1"])
-            self._bn_bwd(f"dec{i}_conv1", dA1, a[f"y{i}_1"], dz1)
+            self._bn_bwd(f"dec{i}_conv1", dA1, a[f"y{i}_1"], dz1, reduced=True)
             l1 = L[f"dec{i}_conv1"]
             self.wgrad(l1, a[f"az{i}_2"], dz1, srcB=a[f"t{i}"])
             sk = gb(f"skip{i}", a[f"z{i}_2"])
@@ -774,7 +783,11 @@ class UNetBN(UNetEngine):
             pact = a[f"ay{i + 1}_2"] if i + 1 < Lv - 1 else a[f"az{Lv - 1}_2"]
             self.wgrad(lu, pact, dt)
             dAp = gb(f"dA_up{i}", pact)
-            self.dgrad(lu, dt, dAp)
+            if i + 1 < Lv - 1:
+                red = self._bn_red(f"dec{i + 1}_conv2", a[f"y{i + 1}_2"])
+            else:
+                red = self._bn_red(f"enc{Lv - 1}_conv2", a[f"z{Lv - 1}_2"])
+            self.dgrad(lu, dt, dAp, bn_reduce=red)
             if i + 1 < Lv - 1:
                 cur_dA = dAp
             else:
@@ -790,13 +803,13 @@ class UNetBN(UNetEngine):
             else:
                 dA2 = bott_dA
             dz2 = gb(f"dz_z{i}_2", z2)
-            self._bn_bwd(f"enc{i}_conv2", dA2, z2, dz2)
+            self._bn_bwd(f"enc{i}_conv2", dA2, z2, dz2, reduced=i == Lv - 1)
             l2 = L[f"enc{i}_conv2"]
             self.wgrad(l2, a[f"az{i}_1"], dz2)
             dA1 = gb(f"dA_z{i}_1", z1)
-            self.dgrad(l2, dz2, dA1)
+            self.dgrad(l2, dz2, dA1, bn_reduce=self._bn_red(f"enc{i}_conv1", z1))
             dz1 = gb(f"dz_z{i}_1", z1)
-            self._bn_bwd(f"enc{i}_conv1", dA1, z1, dz1)
+            self._bn_bwd(f"enc{i}_conv1", dA1, z1, dz1, reduced=True)
             l1 = L[f"enc{i}_conv1"]
             src = a["x"] if i == 0 else a[f"pool{i - 1}"]
             self.wgrad(l1, src, dz1)

@@ -141,8 +141,11 @@ def _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo
 def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=None, up=False, stride=1,
              kh=3, kw=3, dil=1, pad=None, Ho=None, Wo=None, relu=False, dropout_rate=0.0, dropout_seed=0,
              out_mode=0, shuffle_c=0, out2=None, split_c=0, addend=None, mask=None, mask_scale=1.0,
-             mask2=None, mask2_scale=1.0, accum=None, bn_stats=None):
-    """Implicit-GEMM conv forward-shaped launch (conv, conv dgrad, convT fwd/dgrad)."""
+             mask2=None, mask2_scale=1.0, accum=None, bn_stats=None, bn_reduce=None):
+    """Implicit-GEMM conv forward-shaped launch (conv, conv dgrad, convT fwd/dgrad).
+
+    bn_reduce=(z, scale, shift, mean, invstd, dgamma, dbeta): fuse the BatchNorm-backward reduction
+    (bn_bwd_reduce) of the layer whose activation relu(z*scale+shift) `out` is the gradient of."""
     d, io, N, Ho, Wo = _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo, nout)
     d.relu = 1 if relu else 0
     d.dropout_rate = float(dropout_rate)
@@ -186,6 +189,13 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
         io.accum = ptr(accum)
     if bn_stats is not None:
         io.bn_sum, io.bn_sqsum = ptr(bn_stats[0]), ptr(bn_stats[1])
+    if bn_reduce is not None:
+        z, sc, sh, mu, ist, dg, dbt = bn_reduce
+        _check(out_mode == 0 and out is not None and z.shape == out.shape and z.dtype == out.dtype,
+               "bn_reduce needs a plain store with z shaped like out")
+        d.bnr_stride = z.shape[3]
+        io.bnr_z, io.bnr_scale, io.bnr_shift, io.bnr_mean = ptr(z), ptr(sc), ptr(sh), ptr(mu)
+        io.bnr_invstd, io.bnr_dgamma, io.bnr_dbeta = ptr(ist), ptr(dg), ptr(dbt)
     dc = dtype_code(srcA)
     flops = 2.0 * N * Ho * Wo * nout * kh * kw * (d.CA_stride + d.CB_stride)
     _timed(("igemm_fwd", dc), flops,

@@ -26,7 +26,7 @@ extern "C" {
 
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
-#define ADP_ABI_VERSION 1
+#define ADP_ABI_VERSION 2
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -50,6 +50,7 @@ typedef struct adp_conv_desc {
   int mask2_stride;         /* same for the out2 part of a split store */
   float mask2_scale;
   int accum_stride;         /* accum (f32) += stored value */
+  int bnr_stride;           /* channel stride of io->bnr_z */
 } adp_conv_desc;
 
 typedef struct adp_conv_io {
@@ -69,6 +70,16 @@ typedef struct adp_conv_io {
   float* accum;
   float* bn_sum;     /* per-channel sum / sum of squares of the output (atomics), or NULL */
   float* bn_sqsum;
+  /* optional fused BatchNorm-backward reduction over the stored output dA (out_mode 0; the
+     adp_bn_bwd_reduce of the layer whose activation relu(z*scale+shift) this output is the
+     gradient of): dbeta[c] += sum db, dgamma[c] += sum db*(z-mean)*invstd, db = dA*(z*scale+shift>0) */
+  const void* bnr_z;
+  const float* bnr_scale;
+  const float* bnr_shift;
+  const float* bnr_mean;
+  const float* bnr_invstd;
+  float* bnr_dgamma;
+  float* bnr_dbeta;
 } adp_conv_io;
 
 /* ---- library ---------------------------------------------------------------------------- */

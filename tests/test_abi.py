@@ -26,11 +26,12 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_error_plumbing():
     lib = _lib.lib()
-    assert lib.adp_abi_version() == 1
+    assert lib.adp_abi_version() == 2
     assert isinstance(lib.adp_last_error(), bytes)
 
 
 def test_conv_desc_layout_matches_header():
-    # 15 ints, float, uint, 6 ints, float, int, float, int -> 27 4-byte fields
-    assert ctypes.sizeof(_lib.ConvDesc) == 27 * 4
-    assert ctypes.sizeof(_lib.ConvIO) == 16 * 8
+    # 15 ints, float, uint, 6 ints, float, int, float, int, int -> 28 4-byte fields
+    assert ctypes.sizeof(_lib.ConvDesc) == 28 * 4
+    # 16 operand pointers + 7 fused BatchNorm-backward reduction pointers
+    assert ctypes.sizeof(_lib.ConvIO) == 23 * 8
