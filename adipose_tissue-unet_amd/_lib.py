@@ -90,7 +90,7 @@ _lib = None
 
 
 def exported_symbols():
-    return ["adp_last_error"] + list(_SIGS)
+    return ["adp_last_error", "adp_last_kernel"] + list(_SIGS)
 
 
 def lib():
@@ -104,6 +104,8 @@ def lib():
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
         L.adp_last_error.restype = C.c_char_p
         L.adp_last_error.argtypes = []
+        L.adp_last_kernel.restype = C.c_char_p
+        L.adp_last_kernel.argtypes = []
         for name, args in _SIGS.items():
             fn = getattr(L, name)
             fn.restype = C.c_int

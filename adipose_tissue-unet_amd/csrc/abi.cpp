@@ -1,4 +1,6 @@
 // Library-level C ABI: error plumbing and version. Kernels live in the *.hip translation units.
+#include <cstdarg>
+#include <cstdio>
 #include <hip/hip_runtime.h>
 #include <map>
 #include <mutex>
@@ -7,6 +9,13 @@
 
 namespace adp {
 static thread_local std::string g_err;
+static thread_local char g_kernel[160] = "";
+void set_kernel(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_kernel, sizeof(g_kernel), fmt, ap);
+  va_end(ap);
+}
 void set_error(const std::string& msg) { g_err = msg; }
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -36,4 +45,5 @@ extern "C" int adp_set_option(const char* name, int value) {
 }
 
 extern "C" const char* adp_last_error(void) { return adp::g_err.c_str(); }
+extern "C" const char* adp_last_kernel(void) { return adp::g_kernel; }
 extern "C" int adp_abi_version(void) { return ADP_ABI_VERSION; }

@@ -88,6 +88,8 @@ namespace adp {
 void set_error(const std::string& msg);
 int check_launch(const char* what);
 int option(const char* name, int dflt);  // runtime switches set through adp_set_option
+// name of the kernel the last conv launch of this thread used (adp_last_kernel), printf-style
+void set_kernel(const char* fmt, ...);
 }  // namespace adp
 #define ADP_REQUIRE(cond, msg)          \
   do {                                  \

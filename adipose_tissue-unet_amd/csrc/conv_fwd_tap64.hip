@@ -251,6 +251,8 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
   const dim3 g(a.nblocks), b(WM * WN * 64);
+  adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s>", WM, WN, TM, two ? "true" : "false",
+                  a.bnr_z ? "true" : "false");
   if (a.bnr_z) {
     if (two) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, true>), g, b, 0, s, a);

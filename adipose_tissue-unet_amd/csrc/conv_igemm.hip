@@ -1061,10 +1061,12 @@ int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
     if (a.Nout > 64 && w128 <= w64) {
       a.ntile_n = (a.Nout + 127) / 128;
       a.nblocks = ((a.M + 127) / 128) * a.ntile_n;
+      adp::set_kernel("igemm_fwd_glds_kernel<128, 128>");
       hipLaunchKernelGGL((igemm_fwd_glds_kernel<128, 128>), dim3(a.nblocks), dim3(NT), 0, s, a);
     } else {
       a.ntile_n = (a.Nout + 63) / 64;
       a.nblocks = ((a.M + 255) / 256) * a.ntile_n;
+      adp::set_kernel("igemm_fwd_glds_kernel<256, 64>");
       hipLaunchKernelGGL((igemm_fwd_glds_kernel<256, 64>), dim3(a.nblocks), dim3(NT), 0, s, a);
     }
     return adp::check_launch("adp_conv_fwd");
@@ -1075,10 +1077,12 @@ int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
     if (a.Nout > 64 && w128 <= w64) {
       a.ntile_n = (a.Nout + 127) / 128;
       a.nblocks = ((a.M + 127) / 128) * a.ntile_n;
+      adp::set_kernel("igemm_fwd_bf16_kernel<128, 128>");
       hipLaunchKernelGGL((igemm_fwd_bf16_kernel<128, 128>), dim3(a.nblocks), dim3(NT), 0, s, a);
     } else {
       a.ntile_n = (a.Nout + 63) / 64;
       a.nblocks = ((a.M + 255) / 256) * a.ntile_n;
+      adp::set_kernel("igemm_fwd_bf16_kernel<256, 64>");
       hipLaunchKernelGGL((igemm_fwd_bf16_kernel<256, 64>), dim3(a.nblocks), dim3(NT), 0, s, a);
     }
     return adp::check_launch("adp_conv_fwd");
@@ -1086,6 +1090,7 @@ int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
   a.ntile_n = (a.Nout + BN - 1) / BN;
   const int ntm = (a.M + BM - 1) / BM;
   a.nblocks = ntm * a.ntile_n;
+  adp::set_kernel(std::is_same<T, bf16>::value ? "igemm_fwd_kernel<bf16>" : "igemm_fwd_kernel<float>");
   hipLaunchKernelGGL(igemm_fwd_kernel<T>, dim3(a.nblocks), dim3(NT), 0, s, a);
   return adp::check_launch("adp_conv_fwd");
 }
@@ -1118,9 +1123,11 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
       a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
       splits = (a.M + a.mchunk - 1) / a.mchunk;
       if (TN == 64)
-        hipLaunchKernelGGL((igemm_wgrad_glds_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a);
+        { adp::set_kernel("igemm_wgrad_glds_kernel<64, 256>");
+          hipLaunchKernelGGL((igemm_wgrad_glds_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a); }
       else
-        hipLaunchKernelGGL((igemm_wgrad_glds_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a);
+        { adp::set_kernel("igemm_wgrad_glds_kernel<128, 128>");
+          hipLaunchKernelGGL((igemm_wgrad_glds_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a); }
     }
     if (a.dB) {
       const int G = a.Nout / 8, lanes = NT / G;
@@ -1151,9 +1158,11 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
     a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
     splits = (a.M + a.mchunk - 1) / a.mchunk;
     if (TN == 64)
-      hipLaunchKernelGGL((igemm_wgrad_bf16_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a);
+      { adp::set_kernel("igemm_wgrad_bf16_kernel<64, 256>");
+        hipLaunchKernelGGL((igemm_wgrad_bf16_kernel<64, 256>), dim3(tiles, splits), dim3(NT), 0, s, a); }
     else
-      hipLaunchKernelGGL((igemm_wgrad_bf16_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a);
+      { adp::set_kernel("igemm_wgrad_bf16_kernel<128, 128>");
+        hipLaunchKernelGGL((igemm_wgrad_bf16_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a); }
     return adp::check_launch("adp_conv_wgrad");
   }
   a.ntile_k = (a.K + 63) / 64;
@@ -1165,6 +1174,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
   if (splits < 1) splits = 1;
   a.mchunk = ((a.M + splits - 1) / splits + 31) / 32 * 32;
   splits = (a.M + a.mchunk - 1) / a.mchunk;
+  adp::set_kernel(std::is_same<T, bf16>::value ? "igemm_wgrad_kernel<bf16>" : "igemm_wgrad_kernel<float>");
   hipLaunchKernelGGL(igemm_wgrad_kernel<T>, dim3(tiles, splits), dim3(NT), 0, s, a);
   return adp::check_launch("adp_conv_wgrad");
 }

@@ -357,6 +357,8 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   const bool ra = a.Wo % 64 == 0 && a.up == 1 && adp::option("wgrad_ra", 1);
   const bool two = adp::option("tap64_bar", 1) == 2;
   const dim3 grid(tiles * splits), block(WN * WK * 64);
+  adp::set_kernel("igemm_wgrad_tap64_kernel<%d, %d, %d, %s, %s>", WN, WK, TNW, two ? "true" : "false",
+                  ra ? "true" : "false");
   if (ra && !two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, true>), grid, block, 0, s, a);
   else if (ra) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, true>), grid, block, 0, s, a);
   else if (!two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, false>), grid, block, 0, s, a);

@@ -13,7 +13,7 @@ import ctypes as C
 
 import torch
 
-from ._lib import BF16, F32, AdpError, ConvDesc, ConvIO, call, ptr, stream_ptr
+from ._lib import BF16, F32, AdpError, ConvDesc, ConvIO, call, lib, ptr, stream_ptr
 
 
 def round_up(x, m):
@@ -23,22 +23,23 @@ def round_up(x, m):
 class LaunchTimer:
     """Optional per-launch HIP-event timing of the GEMM kernels (bench.py roofline leg).
     Events are recorded on the launch stream (torch's current stream), so they bracket exactly the
-    kernel they surround."""
+    kernel they surround; each launch is keyed by the kernel instantiation the library reports for
+    it (adp_last_kernel, the name rocprofv3 prints) and the launch dtype."""
 
     def __init__(self):
         self.recs = []
 
-    def wrap(self, kernel, flops, fn):
+    def wrap(self, dcode, flops, fn):
         s = torch.cuda.current_stream()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(s)
         fn()
         e1.record(s)
-        self.recs.append((kernel, flops, e0, e1))
+        self.recs.append(((lib().adp_last_kernel().decode(), dcode), flops, e0, e1))
 
     def summary(self):
-        """kernel -> (launches, total flops, total ms) (synchronises)."""
+        """(kernel name, dtype code) -> (launches, total flops, total ms) (synchronises)."""
         torch.cuda.synchronize()
         out = {}
         for k, f, e0, e1 in self.recs:
@@ -55,11 +56,11 @@ def set_launch_timer(t):
     _timer = t
 
 
-def _timed(kernel, flops, fn):
+def _timed(dcode, flops, fn):
     if _timer is None:
         fn()
     else:
-        _timer.wrap(kernel, flops, fn)
+        _timer.wrap(dcode, flops, fn)
 
 
 def set_option(name, value):
@@ -198,7 +199,7 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
         io.bnr_invstd, io.bnr_dgamma, io.bnr_dbeta = ptr(ist), ptr(dg), ptr(dbt)
     dc = dtype_code(srcA)
     flops = 2.0 * N * Ho * Wo * nout * kh * kw * (d.CA_stride + d.CB_stride)
-    _timed(("igemm_fwd", dc), flops,
+    _timed(dc, flops,
            lambda: call("adp_conv_fwd", dc, C.byref(d), C.byref(io), stream_ptr()))
     return out
 
@@ -240,7 +241,7 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     del Wdummy
     dc = dtype_code(srcA)
     flops = 2.0 * N * Ho * Wo * nout * K
-    _timed(("igemm_wgrad", dc), flops,
+    _timed(dc, flops,
            lambda: call("adp_conv_wgrad", dc, C.byref(d), C.byref(io), ptr(dY), int(dY.shape[3]), ptr(dW),
                         ptr(dB), stream_ptr()))
 

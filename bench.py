@@ -76,6 +76,24 @@ def cpu_baseline(args):
                       f"{threads} threads ({os.cpu_count()} host CPUs visible), {dt:.2f} s"}
 
 
+def committed_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<round>_traffic.json, written by tools/profile_round.sh from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this same bench command); (None, None) if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+    except (OSError, ValueError):
+        return None, None
+    e = d.get(kernel)
+    if not e or e.get("traffic_bytes") is None:
+        return None, os.path.basename(files[-1])
+    return int(e["traffic_bytes"]), os.path.basename(files[-1])
+
+
 def main():
     args = parse()
     import numpy as np
@@ -158,19 +176,25 @@ def main():
         return
     tiles = B * world * args.steps * (S / 1024.0) ** 2
     value = tiles / elapsed
-    # roofline of the dominant kernel (largest total time among the GEMM kernels)
+    # roofline of the dominant kernel: the GEMM kernel instantiation with the largest total time
+    # (names as rocprofv3 prints them; profiles/ holds the matching --kernel-trace --stats summary)
     dom = max(summ.items(), key=lambda kv: kv[1][2])
     (kname, dcode), (n, flops, ms) = dom
     dname = "bf16" if dcode == 1 else "f32"
-    sym = {"igemm_fwd": "igemm_fwd_kernel", "igemm_wgrad": "igemm_wgrad_kernel"}[kname]
     achieved = flops / (ms * 1e-3) / 1e12
-    per_kernel = {f"{k[0]}<{'bf16' if k[1] == 1 else 'f32'}>": {
-        "launches": v[0], "avg_ms": round(v[2] / v[0], 4), "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
-        "share_of_step": round(v[2] / (elapsed * 1e3 / world ** 0), 4)} for k, v in summ.items()}
-    roof = {"bound": "mfma", "kernel": f"{sym}<{dname}>", "achieved": round(achieved, 2),
+    step_ms = elapsed * 1e3
+    per_kernel = {k[0]: {"launches": v[0], "avg_ms": round(v[2] / v[0], 4),
+                         "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2), "share_of_step": round(v[2] / step_ms, 4)}
+                  for k, v in sorted(summ.items(), key=lambda kv: -kv[1][2])}
+    traffic, tsrc = committed_traffic(kname)
+    roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2),
             "peak": MI355X_PEAK[dname], "unit": "TFLOP/s", "frac": round(achieved / MI355X_PEAK[dname], 4),
-            "traffic": None, "avg_launch_ms": round(ms / n, 4), "launches": n,
-            "flops_per_launch": round(flops / n / 1e9, 3), "per_kernel": per_kernel}
+            "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc,
+            "avg_launch_ms": round(ms / n, 4), "launches": n,
+            "flops_per_launch": round(flops / n / 1e9, 3),
+            "gemm_share_of_step": round(sum(v[2] for v in summ.values()) / step_ms, 4),
+            "gemm_tflops_all": round(sum(v[1] for v in summ.values()) / (sum(v[2] for v in summ.values()) * 1e-3) / 1e12, 2),
+            "per_kernel": per_kernel}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         try:

@@ -84,6 +84,9 @@ typedef struct adp_conv_io {
 
 /* ---- library ---------------------------------------------------------------------------- */
 const char* adp_last_error(void);
+/* Name of the kernel instantiation the calling thread's last adp_conv_fwd / adp_conv_wgrad launched
+   (as rocprofv3 prints it), for per-kernel timing and roofline accounting. */
+const char* adp_last_kernel(void);
 int adp_abi_version(void);
 /* Runtime switches (A/B of kernel variants in one process): "conv_fast" (default 1) selects the
  * bf16 64x64-per-wave forward and the transposed-read wgrad kernels; 0 = generic kernels. */

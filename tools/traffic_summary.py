@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch, per kernel instantiation, from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+usage: python tools/traffic_summary.py FETCH_counter_collection.csv WRITE_counter_collection.csv OUT.json
+
+Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced streaming read (16 B/lane loads and LDS-DMA alike), so read bytes = 2 x FETCH_SIZE KiB;
+WRITE_SIZE is exact for 16-B streaming stores and float atomics. Both are KiB per dispatch summed over
+the chip. The JSON maps kernel name -> {launches, read_bytes, write_bytes, traffic_bytes} (means per
+launch; traffic = read + write).
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+
+def short(name):
+    m = re.search(r"(\w+_kernel)(<[^>(]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:80]
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+    return acc
+
+
+def main():
+    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, [])
+        w = write.get(k, [])
+        rd = 2.0 * sum(f) / len(f) if f else None
+        wr = sum(w) / len(w) if w else None
+        out[k] = {"launches": max(len(f), len(w)), "read_bytes": rd, "write_bytes": wr,
+                  "traffic_bytes": (rd or 0.0) + (wr or 0.0) if rd is not None and wr is not None else None}
+    json.dump(out, open(sys.argv[3], "w"), indent=1, sort_keys=True)
+    print(f"{len(out)} kernels -> {sys.argv[3]}")
+
+
+if __name__ == "__main__":
+    main()
