@@ -48,6 +48,15 @@ class LossConfig:
         return specs
 
 
+def dp_row_normaliser(world, batch_local, rows_kept):
+    """Denominator of every per-row BCE coefficient under data parallelism: the GLOBAL number of kept
+    rows (world x local batch x rows kept per image), so the per-rank row terms sum to the reference's
+    single-device mean over the whole batch (Keras SUM_OVER_BATCH_SIZE of the per-row BCE; the OHEM
+    top-k mean of train_adipose_unet_v3.py:282-318). The Dice term is made batch-global by
+    all-reducing its three sums before the gradient (Trainer.loss_and_grads)."""
+    return float(world * batch_local * rows_kept)
+
+
 class GradBuckets:
     """Bucketed, backward-overlapped SUM all-reduce over the flat gradient buffer."""
 
@@ -96,8 +105,10 @@ class GradBuckets:
                                           async_op=True))
 
     def finish(self):
+        # every gradient is final here: reduce any bucket a ready-hook did not launch (a layer that never
+        # reported, or frozen-only buckets, whose zero gradients are harmless to sum)
         for i, done in enumerate(self.launched):
-            if not done and not self.pending[i]:
+            if not done:
                 self._launch(i)
         for w in self.works:
             w.wait()  # current stream waits on the RCCL stream
@@ -178,7 +189,7 @@ class Trainer:
             k = int(np.float32(H) * np.float32(cfg.hard_example_ratio)) if ohem else H
             coef = self._dpbuf("coef/" + name, (B * H,))
             ops.loss_select(rows[name], coef, self.lossbuf[i:i + 1], N=B, H=H, W=W, ohem=ohem,
-                            keep_ratio=cfg.hard_example_ratio, weight=w, norm_rows=float(self.world * B * k))
+                            keep_ratio=cfg.hard_example_ratio, weight=w, norm_rows=dp_row_normaliser(self.world, B, k))
             if compute_grad:
                 dp = self._dpbuf("dp/" + name, (B, H, W))
                 ops.loss_grad(outputs[name], y, coef, self.stats[i], dp, weight=w, smooth=cfg.use_label_smoothing,
