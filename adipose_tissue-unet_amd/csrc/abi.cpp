@@ -1,4 +1,5 @@
 // Library-level C ABI: error plumbing and version. Kernels live in the *.hip translation units.
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <hip/hip_runtime.h>
@@ -40,7 +41,8 @@ int option(const char* name, int dflt) {
 extern "C" int adp_set_option(const char* name, int value) {
   if (!name) return -1;
   std::lock_guard<std::mutex> lk(adp::g_opt_mu);
-  adp::opts()[name] = value;
+  if (value == INT_MIN) adp::opts().erase(name);   // back to the built-in default
+  else adp::opts()[name] = value;
   return 0;
 }
 

@@ -29,6 +29,8 @@ struct FwdArgs {
   const float* bnr_sc; const float* bnr_sh; const float* bnr_mean; const float* bnr_invstd;
   float* bnr_dgamma; float* bnr_dbeta;
   int M;
+  int korder;            // tap64: 0 = K steps tap-major (k order), 1 = 64-channel-chunk-major (all taps
+                         // of a chunk back to back: the shifted re-reads of one input window are adjacent)
   int ntile_n;           // gridDim decomposition helper
   int nblocks;
 };
@@ -44,6 +46,7 @@ struct WgradArgs {
   float* dW;            // [Npad][Kpad] f32, accumulated with atomics
   float* dB;            // [Nout] f32 or null
   int M, mchunk, ntile_k, ntile_n;
+  int debug_flags;      // timing-only ablations (tools/bench_kernels.py): bit0 skips the dW atomics
 };
 
 namespace {
@@ -275,6 +278,8 @@ namespace adp {
 // conv_fwd_tap64.hip: 8-phase LDS-DMA forward kernel for layers whose channel stride is a multiple
 // of 64 (every 64-deep K step lies inside one tap). Returns 1 if it launched, 0 if not eligible.
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s);
+// conv_fwd_halo.hip: halo-reuse 3x3 kernel for narrow (<= 128 output channels) stride-1 layers.
+int launch_fwd_halo(FwdArgs& a, hipStream_t s);
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
 }

@@ -1,0 +1,261 @@
+// Halo-reuse 3x3 convolution ("halo") for the narrow, full-resolution layers: 3x3, stride 1, dilation
+// 1, 'same' padding, Cin_s % 64 == 0 and at most 128 output channels (unet_bn levels 0-1 forward and
+// data-gradient launches). Semantics are those of igemm_fwd_kernel (conv_igemm.hip).
+//
+// Why: with 64-128 output columns the implicit GEMM re-gathers every input pixel once per tap (9x) and
+// the LDS-DMA gather rate, not the MFMA rate, bounds the tap64 kernel. Here a block owns an 8 x 32
+// output patch; per 64-channel input chunk it moves the 10 x 34 input halo into LDS once and all nine
+// taps read shifted 16-pixel windows of it (340 instead of 2304 pixel rows per chunk, 6.8x less A
+// traffic). The weights stream per tap through a 3-deep LDS ring.
+//
+// Block: 4 (M) x WN (N) x KS waves, each 64 output pixels (two patch rows of 32) x 64 channels = 4 x 4
+// v_mfma_f32_16x16x32_bf16 accumulators; with KS = 2 (the 64-channel layers) the two wave groups take
+// the two 32-deep halves of every step and their accumulators are summed through LDS at the end, so
+// that two waves share each SIMD. LDS: 2 halo buffers (double-buffered over chunks) + 3 weight
+// slots, all filled by global_load_lds_dwordx4 with the XOR chunk swizzle on the source address.
+// K loop: step s = chunk * ceil(9/TPS) + j covers taps j*TPS ..; at step s the block issues the weights
+// of step s+2 (and, at a chunk's first step, the next chunk's halo) and retires step s+1 with one
+// counted vmcnt before the step's barrier. The 64-channel layers take two taps per step.
+#include "conv_common.h"
+
+namespace {
+
+__device__ __attribute__((aligned(256))) uint4 halo_zero_page[64];
+
+constexpr int PH = 8, PW = 32;                  // output patch
+constexpr int HH = PH + 2, HW = PW + 2;         // input halo
+constexpr int HROWS = HH * HW;                  // 340 halo pixels
+constexpr int ROWB = 128;                       // 64 bf16 channels per LDS row
+
+#define HALO_BAR()                         \
+  do {                                     \
+    asm volatile("" ::: "memory");         \
+    __builtin_amdgcn_s_barrier();          \
+    asm volatile("" ::: "memory");         \
+  } while (0)
+
+// TPS taps per K step (a weight slot holds TPS taps; steps per chunk = ceil(9 / TPS)). NHB halo
+// buffers: 2 double-buffers the halo over input chunks; 1 (single-chunk layers, Cin_s == 64) halves the
+// LDS footprint so that two blocks share a CU and one block's halo load overlaps the other's MFMAs.
+template <int WN, int KS, int TPS, int NHB>
+constexpr int halo_lds() {
+  constexpr int NTH = 4 * WN * KS * 64;
+  constexpr int GH = (HROWS * 8 + NTH - 1) / NTH;
+  return NHB * (GH * NTH / 8) * ROWB + 3 * TPS * WN * 64 * ROWB;
+}
+
+template <int WN, int KS, int TPS, int NHB, bool BNR>
+__global__ __launch_bounds__(4 * WN * KS * 64, (halo_lds<WN, KS, TPS, NHB>() <= 81920 ? 2 : 1))
+void igemm_fwd_halo_kernel(FwdArgs a) {
+  constexpr int NTH = 4 * WN * KS * 64;
+  constexpr int BN = WN * 64;
+  constexpr int SPC = (9 + TPS - 1) / TPS;
+  constexpr int GH = (HROWS * 8 + NTH - 1) / NTH;          // halo glds per thread per chunk
+  constexpr int HROWS_PAD = GH * NTH / 8;                  // rows the last instruction may touch
+  constexpr int HBUF = HROWS_PAD * ROWB;
+  constexpr int GB1 = BN * 8 / NTH;                        // weight glds per thread per tap
+  static_assert(GB1 * NTH == BN * 8, "weight slot must split evenly");
+  constexpr int GB = GB1 * TPS;                            // ... per step
+  constexpr int WTAP = BN * ROWB;
+  constexpr int WSLOT = TPS * WTAP;
+  constexpr int OFF_W = NHB * HBUF;
+  constexpr int LT = BN + 4;
+  constexpr int EPI = PH * PW * LT * 4;
+  constexpr int SMEM = (OFF_W + 3 * WSLOT > EPI) ? OFF_W + 3 * WSLOT : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % 4, wn = (wave / 4) % WN, kh = wave / (4 * WN);
+  // block -> (n-tile, image, patch row, patch col), n-tile fastest, XCD-grouped
+  const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
+  const int lin = xcd_remap(blockIdx.x, a.nblocks);
+  const int tn = lin % a.ntile_n;
+  int rest = lin / a.ntile_n;
+  const int px = rest % tx_n; rest /= tx_n;
+  const int py = rest % ty_n;
+  const int img = rest / ty_n;
+  const int y0 = py * PH, x0 = px * PW, n0 = tn * BN;
+  const int Cin_s = a.CAs + a.CBs;
+  const int nchunk = Cin_s / 64, nsteps = nchunk * SPC;
+  const int Wrows = (a.Nout + 63) / 64 * 64;
+  const bf16* srcA = reinterpret_cast<const bf16*>(a.srcA);
+  const bf16* srcB = reinterpret_cast<const bf16*>(a.srcB);
+
+  // ---- halo slots of this thread: pixel offset (image-relative) or -1 (padding / beyond the halo)
+  int hoff[GH], hcol[GH];
+#pragma unroll
+  for (int i = 0; i < GH; ++i) {
+    const int idx = i * NTH + tid;
+    const int hr = idx >> 3, pos = idx & 7;
+    hcol[i] = 8 * (pos ^ swz(hr));
+    const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
+    hoff[i] = (hr < HROWS && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws) ? (img * a.Hs + gy) * a.Ws + gx : -1;
+  }
+  // ---- weight slots: row q of the slot = output channel n0 + q
+  const bf16* wp[GB1];
+#pragma unroll
+  for (int i = 0; i < GB1; ++i) {
+    const int idx = i * NTH + tid;
+    const int q = idx >> 3, pos = idx & 7;
+    wp[i] = (n0 + q < Wrows) ? reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + q) * a.Kpad + 8 * (pos ^ swz(q))
+                             : nullptr;
+  }
+
+  auto issue_halo = [&](int c, int buf) {
+    const int ci = c * 64;
+    const bf16* base = ci < a.CAs ? srcA + ci : srcB + (ci - a.CAs);
+    const int cs = ci < a.CAs ? a.CAs : a.CBs;
+    unsigned char* dst = smem + buf * HBUF + wave * 8 * ROWB;
+#pragma unroll
+    for (int i = 0; i < GH; ++i) {
+      const void* p = hoff[i] >= 0 ? (const void*)(base + (size_t)hoff[i] * cs + hcol[i]) : (const void*)halo_zero_page;
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
+    }
+  };
+  auto issue_w = [&](int s) {
+    const int c = s / SPC, j = s - SPC * c;
+#pragma unroll
+    for (int u = 0; u < TPS; ++u) {
+      const int t = j * TPS + u;                 // t == 9 only in a chunk's short last step: a zero load
+      const int k = t * Cin_s + c * 64;          // keeps the per-step glds count uniform
+      unsigned char* dst = smem + OFF_W + (s % 3) * WSLOT + u * WTAP + wave * 8 * ROWB;
+#pragma unroll
+      for (int i = 0; i < GB1; ++i) {
+        const void* p = (wp[i] && t < 9) ? (const void*)(wp[i] + k) : (const void*)halo_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, h4 = lane >> 4;
+  // ---- prologue: halo(0), weights(0), weights(1); retire halo(0) + weights(0)
+  issue_halo(0, 0);
+  issue_w(0);
+  if (nsteps > 1) {
+    issue_w(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  HALO_BAR();
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int c = s / SPC, j = s - SPC * c;
+    const bool nh = NHB == 2 && j == 0 && c + 1 < nchunk;   // prefetch the next chunk's halo
+    if (nh) issue_halo(c + 1, (c + 1) & 1);
+    const bool nw = s + 2 < nsteps;
+    if (nw) issue_w(s + 2);
+    const unsigned char* H = smem + (NHB == 2 ? (c & 1) : 0) * HBUF;
+#pragma unroll
+    for (int u = 0; u < TPS; ++u) {
+    const int t = j * TPS + u;
+    if (t >= 9) break;
+    // ---- 64 pixels x 64 channels x 64 deep of tap t for this wave
+    const int dy = t / 3, dx = t - 3 * dy;
+    const unsigned char* Wt = smem + OFF_W + (s % 3) * WSLOT + u * WTAP;
+#pragma unroll
+    for (int kq = 0; kq < 2 / KS; ++kq) {
+      const int ck = 4 * (KS == 2 ? kh : kq) + h4;
+      bf16x8 fb[4], fa[4];
+#pragma unroll
+      for (int nf = 0; nf < 4; ++nf) {
+        const int q = wn * 64 + nf * 16 + r16;
+        fb[nf] = *reinterpret_cast<const bf16x8*>(Wt + q * ROWB + ((ck ^ swz(q)) << 4));
+      }
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) {
+        const int prow = 2 * wm + (mf >> 1), pcol = (mf & 1) * 16 + r16;
+        const int hr = (prow + dy) * HW + pcol + dx;
+        fa[mf] = *reinterpret_cast<const bf16x8*>(H + hr * ROWB + ((ck ^ swz(hr)) << 4));
+      }
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf)
+          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mf], fb[nf], acc[mf][nf], 0, 0, 0);
+    }
+    }
+    // retire step s+1 (weights of s+1 and, at a chunk boundary, the halo of chunk c+1, both issued
+    // before this step's issues) before the barrier that precedes its reads
+    if (nw) {
+      if (nh) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GH) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    HALO_BAR();
+  }
+
+  // ---- epilogue: accumulators -> LDS tile [patch pixel][channel] -> one patch row at a time
+  float* tile = reinterpret_cast<float*>(smem);
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int part = 0; part < KS; ++part) {   // KS = 2: k-half 0 stores, k-half 1 adds
+    if (kh == part) {
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int p = (2 * wm + (mf >> 1)) * PW + (mf & 1) * 16 + rq + r;
+            float* e = tile + p * LT + wn * 64 + nf * 16 + col;
+            *e = part == 0 ? acc[mf][nf][r] : *e + acc[mf][nf][r];
+          }
+    }
+    __syncthreads();
+  }
+  float bs[8], bq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bs[j] = 0.f; bq[j] = 0.f; }
+  for (int pr = 0; pr < PH; ++pr) {
+    const int m0 = (img * a.Ho + y0 + pr) * a.Wo + x0;
+    if constexpr (BNR) epi_rows_bnr<NTH, BN>(a, tile + pr * PW * LT, PW, m0, n0, tid, bs, bq);
+    else epi_rows<NTH, BN>(a, tile + pr * PW * LT, PW, m0, n0, tid, bs, bq);
+  }
+  if (a.bn_sum || a.bnr_z) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
+}
+
+#undef HALO_BAR
+
+template <int WN, int KS, int TPS, int NHB>
+void launch_halo(FwdArgs& a, hipStream_t s) {
+  constexpr int BN = WN * 64;
+  a.ntile_n = (a.Nout + BN - 1) / BN;
+  a.nblocks = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * a.ntile_n;
+  adp::set_kernel("igemm_fwd_halo_kernel<%d, %d, %d, %d, %s>", WN, KS, TPS, NHB, a.bnr_z ? "true" : "false");
+  const dim3 g(a.nblocks), b(4 * WN * KS * 64);
+  if (a.bnr_z) hipLaunchKernelGGL((igemm_fwd_halo_kernel<WN, KS, TPS, NHB, true>), g, b, 0, s, a);
+  else hipLaunchKernelGGL((igemm_fwd_halo_kernel<WN, KS, TPS, NHB, false>), g, b, 0, s, a);
+}
+
+}  // namespace
+
+namespace adp {
+int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
+  const int mode = option("fwd_halo", 1);   // 0 off, 1 auto, 2 = no single-buffer form (A/B)
+  if (mode == 0) return 0;
+  const int Cin_s = a.CAs + a.CBs;
+  if (a.scA || a.scB || a.kh != 3 || a.kw != 3 || a.dil != 1 || a.pad != 1 || a.stride != 1 || a.up != 1 ||
+      a.Ho != a.Hs || a.Wo != a.Ws || a.Ho % PH != 0 || a.Wo % PW != 0 || a.CAs % 64 != 0 || a.CBs % 64 != 0 ||
+      a.K != 9 * Cin_s || a.Kpad != a.K || a.Nout > 128)
+    return 0;
+  if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
+  const bool one_chunk = Cin_s == 64;
+  if (a.Nout <= 64) {
+    if (one_chunk && mode != 2) launch_halo<1, 2, 1, 1>(a, s);   // two blocks per CU
+    else launch_halo<1, 2, 2, 2>(a, s);
+  } else {
+    if (one_chunk && mode != 2) launch_halo<2, 1, 1, 1>(a, s);
+    else launch_halo<2, 1, 1, 2>(a, s);
+  }
+  return 1;
+}
+}  // namespace adp

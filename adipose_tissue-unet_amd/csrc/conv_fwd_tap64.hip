@@ -37,10 +37,11 @@ constexpr int cmax(int x, int y) { return x > y ? x : y; }
 template <int WM, int WN, int TM>
 constexpr int tap64_occ() { return 2 * (WM * TM + WN * 64) * 128 <= 81920 ? 2 : 1; }
 
-// TWO_BAR: barrier between a phase's LDS reads and its MFMAs as well as after them (the guide's
-// template); otherwise one barrier per phase, which lets one wave's reads overlap another's MFMAs.
+// One barrier per phase (a barrier between the reads and the MFMAs as well, as in the guide's template,
+// measured 2-5 % slower here). BAL: one quarter-tile refill per phase (B0 of step t+1 at P0, A0/B1/A1 of
+// step t+2 at P1/P2/P3: three quarters in flight across the wait) instead of A0+B0 together at P1.
 // BNR: data-gradient launch with the fused BatchNorm-backward reduction epilogue (epi_rows_bnr).
-template <int WM, int WN, int TM, bool TWO_BAR, bool BNR>
+template <int WM, int WN, int TM, bool BAL, bool BNR>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
@@ -100,11 +101,17 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
 
   // K step -> (tap offsets, source, channel); uniform across the block
   struct Kt { int oy, ox, cs; const bf16* base; int kt; };
+  const int ntaps = a.kh * a.kw;
   auto kinfo = [&](int kt) {
     Kt r;
-    const int k = kt * 64, tap = k / Cin_s, ci = k - tap * Cin_s;
+    int k = kt * 64;
+    if (a.korder) {   // chunk-major: step kt = chunk * ntaps + tap
+      const int chunk = kt / ntaps, t = kt - chunk * ntaps;
+      k = t * Cin_s + chunk * 64;
+    }
+    const int tap = k / Cin_s, ci = k - tap * Cin_s;
     const int ty = tap / a.kw, tx = tap - ty * a.kw;
-    r.oy = ty * a.dil; r.ox = tx * a.dil; r.kt = kt;
+    r.oy = ty * a.dil; r.ox = tx * a.dil; r.kt = k / 64;
     if (ci < a.CAs) { r.base = srcA + ci; r.cs = a.CAs; }
     else { r.base = srcB + (ci - a.CAs); r.cs = a.CBs; }
     return r;
@@ -171,14 +178,17 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // ---- prologue: K steps 0 and 1 in flight, wait for step 0
+  // ---- prologue: K step 0 and (all but B0 of) step 1 in flight, wait for step 0
   {
     const Kt k0 = kinfo(0);
     issueA(0, k0, 0); issueB(0, k0, 0); issueB(1, k0, 0); issueA(1, k0, 0);
     if (nk > 1) {
       const Kt k1 = kinfo(1);
-      issueA(0, k1, 1); issueB(0, k1, 1); issueB(1, k1, 1); issueA(1, k1, 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
+      issueA(0, k1, 1);
+      if (!BAL) issueB(0, k1, 1);
+      issueB(1, k1, 1); issueA(1, k1, 1);
+      if (BAL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GA + GB) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -188,32 +198,37 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
-    const bool pre = t + 2 < nk;
+    const bool n1 = t + 1 < nk, pre = t + 2 < nk;
     const Kt k2 = kinfo(pre ? t + 2 : t);
-    // P0: (A0,B0)
+    // P0: (A0,B0); BAL: B0 of the other buffer (read at P0 of step t-1) is dead -> step t+1
+    if (BAL && n1) issueB(0, kinfo(t + 1), buf ^ 1);
     readA(buf, 0, fa);
     readB(buf, 0, fb0);
-    if (TWO_BAR) T64_BAR();
     mma(fa, fb0, 0, 0);
     T64_BAR();
-    // P1: (A0,B1); A0 and B0 of this buffer are dead -> refill with step t+2
-    if (pre) { issueA(0, k2, buf); issueB(0, k2, buf); }
+    // P1: (A0,B1); A0 (and B0) of this buffer are dead -> refill with step t+2
+    if (pre) {
+      issueA(0, k2, buf);
+      if (!BAL) issueB(0, k2, buf);
+    }
     readB(buf, 1, fb1);
-    if (TWO_BAR) T64_BAR();
     mma(fa, fb1, 0, 1);
     T64_BAR();
     // P2: (A1,B1); B1 dead
     if (pre) issueB(1, k2, buf);
     readA(buf, 1, fa);
-    if (TWO_BAR) T64_BAR();
     mma(fa, fb1, 1, 1);
     T64_BAR();
-    // P3: (A1,B0) from registers; A1 dead. Retire step t+1 (everything older than this K step's
-    // issues) before the barrier that precedes its first read.
+    // P3: (A1,B0) from registers; A1 dead. Retire step t+1 (everything issued before this step's
+    // step-t+2 refills) before the barrier that precedes its first read.
     if (pre) issueA(1, k2, buf);
     mma(fa, fb0, 1, 0);
-    if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pre) {
+      if (BAL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GA + GB) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     T64_BAR();
   }
 
@@ -246,18 +261,18 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
 
 template <int WM, int WN, int TM>
 void launch_cfg(FwdArgs& a, hipStream_t s) {
-  const bool two = adp::option("tap64_bar", 1) == 2;
+  const bool bal = adp::option("tap64_bal", 0) != 0;
   constexpr int BM = WM * TM, BN = WN * 64;
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
   const dim3 g(a.nblocks), b(WM * WN * 64);
-  adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s>", WM, WN, TM, two ? "true" : "false",
+  adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s>", WM, WN, TM, bal ? "true" : "false",
                   a.bnr_z ? "true" : "false");
   if (a.bnr_z) {
-    if (two) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, true>), g, b, 0, s, a);
+    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, true>), g, b, 0, s, a);
   } else {
-    if (two) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false>), g, b, 0, s, a);
+    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false>), g, b, 0, s, a);
     else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, false>), g, b, 0, s, a);
   }
 }
@@ -283,6 +298,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   if (a.scA || a.scB || a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 ||
       a.Kpad != a.K)
     return 0;
+  a.korder = option("tap64_korder", 0);
   int cfg = mode - 2;
   if (mode == 1) {
     // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency

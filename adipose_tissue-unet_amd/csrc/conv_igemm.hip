@@ -1042,7 +1042,8 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
                            a.Nout % 8 == 0),
               "adp_conv_fwd: fused BN-backward reduction needs out_mode 0, all bnr_* pointers, z stride == out stride");
   const int fast = adp::option("conv_fast", 2);
-  if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB && adp::launch_fwd_tap64(a, s))
+  if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB &&
+      (adp::launch_fwd_halo(a, s) || adp::launch_fwd_tap64(a, s)))
     return adp::check_launch("adp_conv_fwd");
   // every other kernel: plain launch, then the standalone BN-backward reduction on the stored output
   const FwdArgs bnr = a;

@@ -17,6 +17,7 @@
 // pixel rows advance by 64 per stage with incremental (image, y, x) coordinates — no divisions in
 // the loop.
 #include "conv_common.h"
+#include <type_traits>
 
 namespace {
 
@@ -63,6 +64,12 @@ ADP_DEV v4s16 ds_tr16(uint32_t lds_addr) {
 ADP_DEV uint32_t lds_off(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
+template <int N>
+ADP_DEV void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int RB>
 ADP_DEV bf16x8 tr_frag_asm(uint32_t base, int col0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
@@ -262,17 +269,24 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) fx[kb] = tr_frag_asm<RX>(base, wk * 64 + kb * 16, lane);
   };
-  auto mma = [&](int h) {
-    // the fragments come from inline-asm LDS reads: wait for them explicitly and keep the MFMAs
-    // from being scheduled above the wait
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int nb = 0; nb < NBP; ++nb)
+  // MFMAs of one phase. The fragments come from inline-asm LDS reads issued X first, then dY block by
+  // block (2 reads each): wait only for what the next dY block needs (lgkmcnt counts the dY reads
+  // still outstanding) and pin the MFMAs below each wait with a scheduling barrier.
+  auto mma_nb = [&](auto nbc, int h) {
+    constexpr int nb = decltype(nbc)::value;
+    if constexpr (nb < NBP) {
+      lgkm_wait<2 * (NBP - 1 - nb)>();
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
         acc[h * NBP + nb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[nb], fx[kb], acc[h * NBP + nb][kb], 0, 0, 0);
+    }
+  };
+  auto mma = [&](int h) {
+    __builtin_amdgcn_s_setprio(1);
+    mma_nb(std::integral_constant<int, 0>{}, h);
+    mma_nb(std::integral_constant<int, 1>{}, h);
+    mma_nb(std::integral_constant<int, 2>{}, h);
+    mma_nb(std::integral_constant<int, 3>{}, h);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -292,12 +306,12 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
     const bool n1 = t + 1 < ns, n2 = t + 2 < ns;
     // ---- pixel half 0 (q0); q1 of the other buffer is free -> stage t+1 q1
     if (n1) issue(1, buf ^ 1);
-    readD(buf, 0, 0);
     readX(buf, 0);
+    readD(buf, 0, 0);
     if (TWO_BAR) W64_BAR();
     mma(0);
     if (SPLIT) {
-      W64_BAR();
+      if (TWO_BAR) W64_BAR();
       readD(buf, 0, 1);
       if (TWO_BAR) W64_BAR();
       mma(1);
@@ -308,12 +322,12 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
     W64_BAR();
     // ---- pixel half 1 (q1); q0 of this buffer is free -> stage t+2 q0
     if (n2) issue(0, buf);
-    readD(buf, 1, 0);
     readX(buf, 1);
+    readD(buf, 1, 0);
     if (TWO_BAR) W64_BAR();
     mma(0);
     if (SPLIT) {
-      W64_BAR();
+      if (TWO_BAR) W64_BAR();
       readD(buf, 1, 1);
       if (TWO_BAR) W64_BAR();
       mma(1);
@@ -326,6 +340,13 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
   }
 
   const int col = lane & 15, rq = (lane >> 4) * 4;
+  if (a.debug_flags & 1) {   // timing-only ablation: keep the accumulators live, skip the atomics
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) asm volatile("" ::"v"(acc[nb][kb]));
+    return;
+  }
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
@@ -355,6 +376,7 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   a.mchunk = ((a.M + splits - 1) / splits + 63) / 64 * 64;
   splits = (a.M + a.mchunk - 1) / a.mchunk;
   const bool ra = a.Wo % 64 == 0 && a.up == 1 && adp::option("wgrad_ra", 1);
+  a.debug_flags = adp::option("wgrad_debug", 0);
   const bool two = adp::option("tap64_bar", 1) == 2;
   const dim3 grid(tiles * splits), block(WN * WK * 64);
   adp::set_kernel("igemm_wgrad_tap64_kernel<%d, %d, %d, %s, %s>", WN, WK, TNW, two ? "true" : "false",

@@ -64,10 +64,9 @@ def _timed(dcode, flops, fn):
 
 
 def set_option(name, value):
-    """Set a kernel-selection option of the native library (adp_set_option); returns nothing.
-    Options: conv_fast (0 generic, 1 register-staged, 2 LDS-DMA), fwd_tap64 (0 off, 1 auto, 2/3/4 force
-    the 256x256 / 256x128 / 512x64 tile), wgrad_glds_tn64."""
-    call("adp_set_option", name.encode(), int(value))
+    """Set a kernel-selection option of the native library (adp_set_option; see include/adipose_hip.h).
+    value=None restores the built-in default."""
+    call("adp_set_option", name.encode(), -(2 ** 31) if value is None else int(value))
 
 
 def dtype_code(t):

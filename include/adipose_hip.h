@@ -88,8 +88,11 @@ const char* adp_last_error(void);
    (as rocprofv3 prints it), for per-kernel timing and roofline accounting. */
 const char* adp_last_kernel(void);
 int adp_abi_version(void);
-/* Runtime switches (A/B of kernel variants in one process): "conv_fast" (default 1) selects the
- * bf16 64x64-per-wave forward and the transposed-read wgrad kernels; 0 = generic kernels. */
+/* Runtime switches, process-global (A/B of kernel variants in one process). value == INT_MIN restores
+ * the built-in default. Kernel selection: "conv_fast" (2 = LDS-DMA kernels, default; 1 = register-staged;
+ * 0 = generic), "fwd_tap64" / "wgrad_tap64" (0 off, 1 auto, 2+c force tile configuration c),
+ * "tap64_bal", "tap64_korder", "wgrad_ra", "wgrad_blocks", "wgrad_min_chunk", "wgrad_glds_tn64";
+ * "wgrad_debug" is a timing-only ablation (bit 0 skips the dW atomics: results invalid). */
 int adp_set_option(const char* name, int value);
 
 /* ---- dense layers (replace Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter / BiasAdd /

@@ -51,6 +51,11 @@ CONV_CASES = [
     ("c64", 2, 24, [64], 64, 1, False),
     ("c128_320", 1, 20, [128], 320, 2, False),
     ("concat64", 2, 16, [64, 64], 128, 1, False),
+    # 3x3 stride-1 layers with <= 128 output channels and 8x32-divisible images -> halo kernel (bf16)
+    ("halo64", 2, 32, [64], 64, 1, False),
+    ("halo_cat", 1, 32, [64, 64], 128, 1, False),
+    ("halo_n96", 1, 64, [128], 96, 1, False),
+    ("halo_c64_n128", 1, 32, [64], 128, 1, False),
 ]
 
 
@@ -160,6 +165,41 @@ def test_tap64_configs(cfg):
     rs = ref.reshape(-1, cout)
     assert relerr(st[0, :cout], rs.sum(0)) < 2e-2
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
+
+
+def test_halo_fused_epilogues():
+    """Halo kernel (conv_fwd_halo.hip): fused BatchNorm statistics of a forward launch vs the oracle,
+    and the fused BatchNorm-backward reduction of a data-gradient launch vs adp_bn_bwd_reduce run on
+    the same stored gradient."""
+    dt = torch.bfloat16
+    N, S, cin, cout = 2, 32, 64, 64
+    xs, kern, bias, l = make_case(N, S, [cin], cout, 1, False, seed=21)
+    W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).to(dt).contiguous()
+    x = nhwc_pad(xs[0], l.Cin_s, dt)
+    out = torch.zeros((N, S, S, l.cout_s), dtype=dt, device=DEV)
+    st = torch.zeros(2, l.cout_s, device=DEV)
+    ops.conv_fwd(x, W, l.Nout, out=out, bias=bias.to(DEV), relu=True, bn_stats=(st[0], st[1]))
+    from adipose_amd import _lib
+    assert "halo" in _lib.lib().adp_last_kernel().decode()
+    ref = oracle_fwd([rb(xs[0], dt)], rb(kern, dt), bias, 1, False).reshape(-1, cout)
+    assert relerr(st[0, :cout], ref.sum(0)) < 2e-2 and relerr(st[1, :cout], (ref * ref).sum(0)) < 2e-2
+    # data gradient with the fused reduction; z/scale/shift/mean/invstd of a synthetic BN layer
+    g = torch.Generator().manual_seed(22)
+    dZ = nhwc_pad(torch.randn(N, S, S, cout, generator=g), l.cout_s, dt)
+    Wd = torch.zeros((l.dNpad, l.dKpad), dtype=dt, device=DEV)
+    ops.pack_weights(torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV), Wd, 1, taps=9, cin_s=l.Cin_s,
+                     nout=l.cout_s)
+    z = nhwc_pad(torch.randn(N, S, S, cin, generator=g), l.Cin_s, dt)
+    sc, sh = (torch.rand(l.Cin_s, generator=g) + 0.5).to(DEV), (torch.randn(l.Cin_s, generator=g) * 0.2).to(DEV)
+    mu, ist = (torch.randn(l.Cin_s, generator=g) * 0.1).to(DEV), (torch.rand(l.Cin_s, generator=g) + 0.5).to(DEV)
+    dA = torch.zeros((N, S, S, l.Cin_s), dtype=dt, device=DEV)
+    dg, db = torch.zeros(l.Cin_s, device=DEV), torch.zeros(l.Cin_s, device=DEV)
+    ops.conv_fwd(dZ, Wd, l.Cin_s, out=dA, bn_reduce=(z, sc, sh, mu, ist, dg, db))
+    assert "halo" in _lib.lib().adp_last_kernel().decode()
+    dg2, db2 = torch.zeros_like(dg), torch.zeros_like(db)
+    ops.bn_bwd_reduce(dA, z, sc, sh, mu, ist, dg2, db2)
+    torch.cuda.synchronize()
+    assert relerr(db, db2) < 1e-4 and relerr(dg, dg2) < 1e-4
 
 
 @pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "128x256", "64x256"])

@@ -57,6 +57,8 @@ def main():
                 res.setdefault((name, kind, v), [])
         for r in range(args.rounds):
             for v in variants:
+                for k_ in {kk for st in settings for kk, _ in st}:
+                    ops.set_option(k_, None)      # every variant starts from the defaults
                 for k_, v_ in settings[v]:
                     ops.set_option(k_, v_)
                 for kind in kinds:
