@@ -69,13 +69,15 @@ class Dense:
     ConvTranspose 2x2/s2. Keras names/shapes are kept for checkpoint interop."""
 
     def __init__(self, name, cin_parts, cout, *, k=3, dil=1, up=False, bias=True, bn=False, transpose=False,
-                 relu=True):
+                 relu=True, cpad=8, in_pad=None):
+        """cpad: channel-stride granule of the output (and, unless in_pad says otherwise, the input)
+        tensors; 64 puts every 64-deep K step inside one tap (the tap64 / halo kernels)."""
         self.name = name
         self.cin_parts = list(cin_parts)
-        self.cin_s = [r8(c) for c in cin_parts]
+        self.cin_s = [round_up(c, in_pad or cpad) for c in cin_parts]
         self.Cin_s = sum(self.cin_s)
         self.cout = cout
-        self.cout_s = r8(cout)
+        self.cout_s = round_up(cout, cpad)
         self.k = 1 if transpose else k
         self.dil = dil
         self.up = up
@@ -406,33 +408,38 @@ class AdiposeV3Net(UNetEngine):
     ENCODER = ("down1_conv1", "down1_conv2", "down2_conv1", "down2_conv2", "down3_conv1", "down3_conv2")
 
     def __init__(self, batch, size, *, dtype="bf16", device="cuda", seed=865, init_nb=44, dropout_rate=0.3,
-                 deep_supervision=True):
+                 deep_supervision=True, cpad=None):
         self.nb = init_nb
         self.dropout_rate = dropout_rate
         self.ds = deep_supervision
+        # channel-stride granule: 44/88/176/352 are stored 64/128/192/384 wide in bf16 so that every layer
+        # but the 1-channel input runs on the tap64 / halo MFMA kernels (the pad channels are exact zeros:
+        # zero weights and biases in, ReLU(0) = 0 out, zero gradients back); f32 keeps the 8-granule layout
+        self.cpad = cpad or (64 if dtype == "bf16" else 8)
         assert size % 8 == 0, "adipose_v3 needs S % 8 == 0 (3 poolings)"
         super().__init__(batch, size, dtype=dtype, device=device, seed=seed)
 
     def build_layers(self):
         nb = self.nb
         L = self.layers
-        L["down1_conv1"] = Dense("down1_conv1", [1], nb)
-        L["down1_conv2"] = Dense("down1_conv2", [nb], nb)
-        L["down2_conv1"] = Dense("down2_conv1", [nb], 2 * nb)
-        L["down2_conv2"] = Dense("down2_conv2", [2 * nb], 2 * nb)
-        L["down3_conv1"] = Dense("down3_conv1", [2 * nb], 4 * nb)
-        L["down3_conv2"] = Dense("down3_conv2", [4 * nb], 4 * nb)
+        cp = dict(cpad=self.cpad)
+        L["down1_conv1"] = Dense("down1_conv1", [1], nb, in_pad=8, **cp)
+        L["down1_conv2"] = Dense("down1_conv2", [nb], nb, **cp)
+        L["down2_conv1"] = Dense("down2_conv1", [nb], 2 * nb, **cp)
+        L["down2_conv2"] = Dense("down2_conv2", [2 * nb], 2 * nb, **cp)
+        L["down3_conv1"] = Dense("down3_conv1", [2 * nb], 4 * nb, **cp)
+        L["down3_conv2"] = Dense("down3_conv2", [4 * nb], 4 * nb, **cp)
         for i, d in enumerate((1, 2, 4, 8, 16, 32)):
-            L[f"dilate{i + 1}"] = Dense(f"dilate{i + 1}", [4 * nb if i == 0 else 8 * nb], 8 * nb, dil=d)
-        L["up3_conv1"] = Dense("up3_conv1", [8 * nb], 4 * nb, up=True)
-        L["up3_conv2"] = Dense("up3_conv2", [4 * nb, 4 * nb], 4 * nb)
-        L["up3_conv3"] = Dense("up3_conv3", [4 * nb], 4 * nb)
-        L["up2_conv1"] = Dense("up2_conv1", [4 * nb], 2 * nb, up=True)
-        L["up2_conv2"] = Dense("up2_conv2", [2 * nb, 2 * nb], 2 * nb)
-        L["up2_conv3"] = Dense("up2_conv3", [2 * nb], 2 * nb)
-        L["up1_conv1"] = Dense("up1_conv1", [2 * nb], nb, up=True)
-        L["up1_conv2"] = Dense("up1_conv2", [nb, nb], nb)
-        L["up1_conv3"] = Dense("up1_conv3", [nb], nb)
+            L[f"dilate{i + 1}"] = Dense(f"dilate{i + 1}", [4 * nb if i == 0 else 8 * nb], 8 * nb, dil=d, **cp)
+        L["up3_conv1"] = Dense("up3_conv1", [8 * nb], 4 * nb, up=True, **cp)
+        L["up3_conv2"] = Dense("up3_conv2", [4 * nb, 4 * nb], 4 * nb, **cp)
+        L["up3_conv3"] = Dense("up3_conv3", [4 * nb], 4 * nb, **cp)
+        L["up2_conv1"] = Dense("up2_conv1", [4 * nb], 2 * nb, up=True, **cp)
+        L["up2_conv2"] = Dense("up2_conv2", [2 * nb, 2 * nb], 2 * nb, **cp)
+        L["up2_conv3"] = Dense("up2_conv3", [2 * nb], 2 * nb, **cp)
+        L["up1_conv1"] = Dense("up1_conv1", [2 * nb], nb, up=True, **cp)
+        L["up1_conv2"] = Dense("up1_conv2", [nb, nb], nb, **cp)
+        L["up1_conv3"] = Dense("up1_conv3", [nb], nb, **cp)
         if self.ds:
             L["aux_out1"] = Head("aux_out1", 4 * nb, 1)
             L["aux_out2"] = Head("aux_out2", 2 * nb, 1)
@@ -442,7 +449,7 @@ class AdiposeV3Net(UNetEngine):
     def alloc(self, B):
         S, nb = self.S, self.nb
         s = [S, S // 2, S // 4, S // 8]
-        c = [r8(nb), r8(2 * nb), r8(4 * nb), r8(8 * nb)]
+        c = [round_up(k * nb, self.cpad) for k in (1, 2, 4, 8)]
         a = {}
         a["x"] = self.buf("x", (B, S, S, 8))
         a["d1a"] = self.buf("d1a", (B, s[0], s[0], c[0]))

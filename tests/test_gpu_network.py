@@ -42,17 +42,20 @@ def adipose_weights():
     return R.adipose_v3_keras_weights(seed=865)
 
 
-def build_adipose(dtype, weights, B=2, S=64):
-    net = AdiposeV3Net(B, S, dtype=dtype, device=DEV)
+def build_adipose(dtype, weights, B=2, S=64, cpad=None):
+    net = AdiposeV3Net(B, S, dtype=dtype, device=DEV, cpad=cpad)
     net.set_weights(weights)
     return net
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_adipose_forward(dtype, adipose_weights):
-    B, S = 2, 64
+# bf16 default: channels stored 64-granular (44 -> 64, 88 -> 128, ...: tap64 / halo kernels);
+# cpad=8 keeps the 48/88/176/352 strides of the generic LDS-DMA kernels
+@pytest.mark.parametrize("dtype,cpad,S", [("f32", None, 64), ("bf16", None, 64), ("bf16", None, 128),
+                                          ("bf16", 8, 64)])
+def test_adipose_forward(dtype, cpad, S, adipose_weights):
+    B = 2
     x, _ = synth_batch(B, S)
-    net = build_adipose(dtype, adipose_weights, B, S)
+    net = build_adipose(dtype, adipose_weights, B, S, cpad)
     a = net.acts(B)
     ops.prep_input(x.to(DEV), a["x"], mean=0.0, std=1.0)
     outs = net.forward(B, train=False)
@@ -71,12 +74,13 @@ def test_adipose_forward(dtype, adipose_weights):
             assert abs(m_gpu["jaccard_index"] - m_ref["jaccard_index"]) < 1e-4
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("hard_mining", [True, False])
-def test_adipose_grads(dtype, hard_mining, adipose_weights):
-    B, S = 2, 64
+@pytest.mark.parametrize("dtype,cpad,S,hard_mining", [("f32", None, 64, True), ("f32", None, 64, False),
+                                                      ("bf16", None, 64, True), ("bf16", None, 64, False),
+                                                      ("bf16", None, 128, True), ("bf16", 8, 64, True)])
+def test_adipose_grads(dtype, cpad, S, hard_mining, adipose_weights):
+    B = 2
     x, y = synth_batch(B, S, seed=4)
-    net = build_adipose(dtype, adipose_weights, B, S)
+    net = build_adipose(dtype, adipose_weights, B, S, cpad)
     tr = Trainer(net, LossConfig(use_hard_mining=hard_mining))
     a = net.acts(B)
     ops.prep_input(x.to(DEV), a["x"], mean=0.0, std=1.0)

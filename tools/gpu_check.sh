@@ -15,6 +15,15 @@ for s in $STEPS; do
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 ;;
     prof) bash tools/profile_round.sh "$TAG" > gpurun_out/prof.log 2>&1 ;;
+    nettests) timeout -k 10 600 python -u -m pytest tests/test_gpu_network.py -x -v --timeout 120 \
+             --timeout-method thread > gpurun_out/gpu_nettests.log 2>&1 ;;
+    v3bench) timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --no-cpu-baseline \
+               > gpurun_out/v3_bench_cpad64.log 2>&1 &&
+             timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --cpad 8 --no-cpu-baseline \
+               > gpurun_out/v3_bench_cpad8.log 2>&1 ;;
+    infer) timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 > gpurun_out/infer_tiles.log 2>&1 &&
+           timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8 > gpurun_out/infer_tiles_cpad8.log 2>&1 &&
+           timeout -k 10 400 python bench_infer.py --mode wsi > gpurun_out/infer_wsi.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   rc=$?
