@@ -412,34 +412,41 @@ class AdiposeV3Net(UNetEngine):
         self.nb = init_nb
         self.dropout_rate = dropout_rate
         self.ds = deep_supervision
-        # channel-stride granule: 44/88/176/352 are stored 64/128/192/384 wide in bf16 so that every layer
-        # but the 1-channel input runs on the tap64 / halo MFMA kernels (the pad channels are exact zeros:
-        # zero weights and biases in, ReLU(0) = 0 out, zero gradients back); f32 keeps the 8-granule layout
-        self.cpad = cpad or (64 if dtype == "bf16" else 8)
+        # channel-stride granule per resolution level (int = all levels): a 64 granule stores 44/88/176/352
+        # as 64/128/192/384 so those levels run on the tap64 / halo MFMA kernels (the pad channels are exact
+        # zeros: zero weights and biases in, ReLU(0) = 0 out, zero gradients back); 8 keeps 48/88/176/352 on
+        # the generic LDS-DMA kernels. f32 (parity) uses 8 everywhere.
+        if cpad is None:
+            cpad = 64 if dtype == "bf16" else 8
+        self.cpad = tuple(cpad) if isinstance(cpad, (tuple, list)) else (int(cpad),) * 4
         assert size % 8 == 0, "adipose_v3 needs S % 8 == 0 (3 poolings)"
         super().__init__(batch, size, dtype=dtype, device=device, seed=seed)
 
     def build_layers(self):
         nb = self.nb
         L = self.layers
-        cp = dict(cpad=self.cpad)
-        L["down1_conv1"] = Dense("down1_conv1", [1], nb, in_pad=8, **cp)
-        L["down1_conv2"] = Dense("down1_conv2", [nb], nb, **cp)
-        L["down2_conv1"] = Dense("down2_conv1", [nb], 2 * nb, **cp)
-        L["down2_conv2"] = Dense("down2_conv2", [2 * nb], 2 * nb, **cp)
-        L["down3_conv1"] = Dense("down3_conv1", [2 * nb], 4 * nb, **cp)
-        L["down3_conv2"] = Dense("down3_conv2", [4 * nb], 4 * nb, **cp)
+
+        def D(name, lin, cin_parts, lout, cout, **kw):
+            in_pad = 8 if lin is None else self.cpad[lin]
+            L[name] = Dense(name, cin_parts, cout, cpad=self.cpad[lout], in_pad=in_pad, **kw)
+
+        D("down1_conv1", None, [1], 0, nb)
+        D("down1_conv2", 0, [nb], 0, nb)
+        D("down2_conv1", 0, [nb], 1, 2 * nb)
+        D("down2_conv2", 1, [2 * nb], 1, 2 * nb)
+        D("down3_conv1", 1, [2 * nb], 2, 4 * nb)
+        D("down3_conv2", 2, [4 * nb], 2, 4 * nb)
         for i, d in enumerate((1, 2, 4, 8, 16, 32)):
-            L[f"dilate{i + 1}"] = Dense(f"dilate{i + 1}", [4 * nb if i == 0 else 8 * nb], 8 * nb, dil=d, **cp)
-        L["up3_conv1"] = Dense("up3_conv1", [8 * nb], 4 * nb, up=True, **cp)
-        L["up3_conv2"] = Dense("up3_conv2", [4 * nb, 4 * nb], 4 * nb, **cp)
-        L["up3_conv3"] = Dense("up3_conv3", [4 * nb], 4 * nb, **cp)
-        L["up2_conv1"] = Dense("up2_conv1", [4 * nb], 2 * nb, up=True, **cp)
-        L["up2_conv2"] = Dense("up2_conv2", [2 * nb, 2 * nb], 2 * nb, **cp)
-        L["up2_conv3"] = Dense("up2_conv3", [2 * nb], 2 * nb, **cp)
-        L["up1_conv1"] = Dense("up1_conv1", [2 * nb], nb, up=True, **cp)
-        L["up1_conv2"] = Dense("up1_conv2", [nb, nb], nb, **cp)
-        L["up1_conv3"] = Dense("up1_conv3", [nb], nb, **cp)
+            D(f"dilate{i + 1}", 2 if i == 0 else 3, [4 * nb if i == 0 else 8 * nb], 3, 8 * nb, dil=d)
+        D("up3_conv1", 3, [8 * nb], 2, 4 * nb, up=True)
+        D("up3_conv2", 2, [4 * nb, 4 * nb], 2, 4 * nb)
+        D("up3_conv3", 2, [4 * nb], 2, 4 * nb)
+        D("up2_conv1", 2, [4 * nb], 1, 2 * nb, up=True)
+        D("up2_conv2", 1, [2 * nb, 2 * nb], 1, 2 * nb)
+        D("up2_conv3", 1, [2 * nb], 1, 2 * nb)
+        D("up1_conv1", 1, [2 * nb], 0, nb, up=True)
+        D("up1_conv2", 0, [nb, nb], 0, nb)
+        D("up1_conv3", 0, [nb], 0, nb)
         if self.ds:
             L["aux_out1"] = Head("aux_out1", 4 * nb, 1)
             L["aux_out2"] = Head("aux_out2", 2 * nb, 1)
@@ -449,7 +456,7 @@ class AdiposeV3Net(UNetEngine):
     def alloc(self, B):
         S, nb = self.S, self.nb
         s = [S, S // 2, S // 4, S // 8]
-        c = [round_up(k * nb, self.cpad) for k in (1, 2, 4, 8)]
+        c = [round_up(k * nb, self.cpad[i]) for i, k in enumerate((1, 2, 4, 8))]
         a = {}
         a["x"] = self.buf("x", (B, S, S, 8))
         a["d1a"] = self.buf("d1a", (B, s[0], s[0], c[0]))

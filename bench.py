@@ -33,7 +33,7 @@ def parse():
     p.add_argument("--size", type=int, default=1024)
     p.add_argument("--levels", type=int, default=5)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    p.add_argument("--cpad", type=int, default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
+    p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-size", type=int, default=1024, help="tile size of the CPU baseline sample")
     return p.parse_args()

@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--overlap", type=float, default=0.75)
     p.add_argument("--tta", default="full", choices=["none", "minimal", "basic", "full"])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    p.add_argument("--cpad", type=int, default=None, help="channel-stride granule (default 64 for bf16)")
+    p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="channel-stride granule per level, e.g. 8,8,64,64 (bf16 default: predictor.INFER_CPAD)")
     p.add_argument("--batch", type=int, default=8, help="tile x view forwards per batched launch")
     p.add_argument("--steps", type=int, default=1, help="WSIs (mode wsi) / batches (mode tiles) timed")
     p.add_argument("--warmup", type=int, default=1)
@@ -54,7 +54,7 @@ def main():
     from adipose_amd import ops
     from adipose_amd.data import synthetic_tile, to_gray
     from adipose_amd.nets import AdiposeV3Net
-    from adipose_amd.predictor import HipUnetPredictor, SlidingWindowInference
+    from adipose_amd.predictor import INFER_CPAD, HipUnetPredictor, SlidingWindowInference
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -66,7 +66,8 @@ def main():
     torch.cuda.set_device(dev)
 
     T = args.tile
-    net = AdiposeV3Net(1, T, dtype=args.dtype, device=dev, seed=865, deep_supervision=False, cpad=args.cpad)
+    cpad = args.cpad or (INFER_CPAD if args.dtype == "bf16" else None)
+    net = AdiposeV3Net(1, T, dtype=args.dtype, device=dev, seed=865, deep_supervision=False, cpad=cpad)
     pred = HipUnetPredictor(net, max_batch=args.batch)
     rng = np.random.default_rng(865)
     if args.mode == "wsi":

@@ -51,7 +51,7 @@ def build_adipose(dtype, weights, B=2, S=64, cpad=None):
 # bf16 default: channels stored 64-granular (44 -> 64, 88 -> 128, ...: tap64 / halo kernels);
 # cpad=8 keeps the 48/88/176/352 strides of the generic LDS-DMA kernels
 @pytest.mark.parametrize("dtype,cpad,S", [("f32", None, 64), ("bf16", None, 64), ("bf16", None, 128),
-                                          ("bf16", 8, 64)])
+                                          ("bf16", 8, 64), ("bf16", (8, 8, 64, 64), 64)])
 def test_adipose_forward(dtype, cpad, S, adipose_weights):
     B = 2
     x, _ = synth_batch(B, S)
@@ -76,7 +76,8 @@ def test_adipose_forward(dtype, cpad, S, adipose_weights):
 
 @pytest.mark.parametrize("dtype,cpad,S,hard_mining", [("f32", None, 64, True), ("f32", None, 64, False),
                                                       ("bf16", None, 64, True), ("bf16", None, 64, False),
-                                                      ("bf16", None, 128, True), ("bf16", 8, 64, True)])
+                                                      ("bf16", None, 128, True), ("bf16", 8, 64, True),
+                                                      ("bf16", (8, 8, 64, 64), 64, True)])
 def test_adipose_grads(dtype, cpad, S, hard_mining, adipose_weights):
     B = 2
     x, y = synth_batch(B, S, seed=4)

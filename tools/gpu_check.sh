@@ -21,6 +21,10 @@ for s in $STEPS; do
                > gpurun_out/v3_bench_cpad64.log 2>&1 &&
              timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --cpad 8 --no-cpu-baseline \
                > gpurun_out/v3_bench_cpad8.log 2>&1 ;;
+    v3mix) timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --cpad 8,8,64,64 --no-cpu-baseline \
+               > gpurun_out/v3_bench_cpad_mix.log 2>&1 &&
+           timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8,8,64,64 > gpurun_out/infer_tiles_mix.log 2>&1 &&
+           timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8,64,64,64 > gpurun_out/infer_tiles_mix2.log 2>&1 ;;
     infer) timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 > gpurun_out/infer_tiles.log 2>&1 &&
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8 > gpurun_out/infer_tiles_cpad8.log 2>&1 &&
            timeout -k 10 400 python bench_infer.py --mode wsi > gpurun_out/infer_wsi.log 2>&1 ;;
