@@ -21,6 +21,8 @@ LIB_PATH = os.path.join(PKG_DIR, "libadipose_hip.so")
 
 F32 = 0
 BF16 = 1
+FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
+ABI_VERSION = 3
 
 
 class AdpError(RuntimeError):
@@ -36,14 +38,14 @@ class ConvDesc(C.Structure):
         ("out2_stride", C.c_int), ("split_c", C.c_int),
         ("mask_stride", C.c_int), ("mask_scale", C.c_float),
         ("mask2_stride", C.c_int), ("mask2_scale", C.c_float),
-        ("accum_stride", C.c_int), ("bnr_stride", C.c_int)]
+        ("accum_stride", C.c_int), ("bnr_stride", C.c_int), ("out_fp8", C.c_int)]
 
 
 class ConvIO(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in (
         "srcA", "srcB", "bn_scaleA", "bn_shiftA", "bn_scaleB", "bn_shiftB", "W", "bias",
         "out", "out2", "addend", "mask", "mask2", "accum", "bn_sum", "bn_sqsum",
-        "bnr_z", "bnr_scale", "bnr_shift", "bnr_mean", "bnr_invstd", "bnr_dgamma", "bnr_dbeta")]
+        "bnr_z", "bnr_scale", "bnr_shift", "bnr_mean", "bnr_invstd", "bnr_dgamma", "bnr_dbeta", "w_scale")]
 
 
 _P = C.c_void_p
@@ -59,6 +61,9 @@ _SIGS = {
     "adp_conv_wgrad": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P, _I, _P, _P, _P],
     "adp_pack_weights": [_I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _P],
     "adp_maxpool2_fwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "adp_maxpool2_fwd_fp8": [_I, _I, _I, _I, _I, _P, _P, _P],
+    "adp_pack_weights_fp8": [_I, _P, _I, _P, _I, _P, _P],
+    "adp_bn_apply_fp8": [_I, _S, _I, _P, _P, _P, _P, _P],
     "adp_maxpool2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _P, _P],
     "adp_upsample2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P],
     "adp_ew_add_mask": [_I, _S, _P, _P, _P, _F, _P, _P],
@@ -110,6 +115,8 @@ def lib():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
+        if L.adp_abi_version() != ABI_VERSION:
+            raise AdpError(f"{LIB_PATH}: ABI version {L.adp_abi_version()} != {ABI_VERSION}; rebuild the library")
         _lib = L
     return _lib
 

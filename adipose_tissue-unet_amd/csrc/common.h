@@ -18,7 +18,26 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define ADP_DEV __device__ __forceinline__
 
-enum AdpDtype { ADP_F32 = 0, ADP_BF16 = 1 };
+enum AdpDtype { ADP_F32 = 0, ADP_BF16 = 1, ADP_FP8 = 2 };
+
+// ---- OCP fp8 e4m3fn (gfx950 v_cvt_*_fp8): saturating encode of 8 values into 8 bytes, decode one byte
+constexpr float FP8_MAX = 448.f;
+ADP_DEV uint2 f8x8_from_f(const float* v) {
+  float c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = fminf(fmaxf(v[j], -FP8_MAX), FP8_MAX);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], hi, true);
+  return make_uint2((unsigned)lo, (unsigned)hi);
+}
+ADP_DEV void f8x8_to_f(uint2 q, float* f) {
+  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 0); f[1] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 1);
+  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 2); f[3] = __builtin_amdgcn_cvt_f32_fp8((int)q.x, 3);
+  f[4] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 0); f[5] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 1);
+  f[6] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 2); f[7] = __builtin_amdgcn_cvt_f32_fp8((int)q.y, 3);
+}
 
 // 8-channel group as raw bytes: 16 B for bf16, 32 B for f32.
 template <typename T> struct Grp;

@@ -33,6 +33,11 @@ struct FwdArgs {
                          // of a chunk back to back: the shifted re-reads of one input window are adjacent)
   int ntile_n;           // gridDim decomposition helper
   int nblocks;
+  // fp8 (OCP e4m3fn) forward launches: operands are fp8, acc[n] is dequantised by wscale[n] (per GEMM
+  // column; activations carry no scale); out_f8 stores the output as fp8 too (else bf16)
+  int f8;
+  const float* wscale;
+  int out_f8;
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
@@ -105,7 +110,9 @@ ADP_DEV bf16x8 tr_frag_sw(const unsigned char* base, int row0, int col0, int lan
 // Applies bias, ReLU, dropout, the pixel-shuffle / split / addend / mask / accumulate store modes
 // and collects per-channel partial sums into bs/bq: BatchNorm statistics (sum, sum of squares) of the
 // stored values, or with bnr_z the BatchNorm-backward sums (db, db*xhat) of the stored gradient.
-template <int NTH, int BN>
+// F8: fp8 launch — acc * wscale[n] before the bias, fp8 or bf16 store (compiled only into the fp8
+// kernels, so the bf16 kernels keep their register budget)
+template <int NTH, int BN, bool F8 = false>
 ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int n0, int tid,
                       float (&bs)[8], float (&bq)[8]) {
   constexpr int LT = BN + 4;
@@ -116,9 +123,13 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
   const int n = n0 + cg * 8;
   if (n >= a.Nout) return;
   const int HWo = a.Ho * a.Wo;
-  float bias[8];
+  float bias[8], wsc[F8 ? 8 : 1];
 #pragma unroll
   for (int j = 0; j < 8; ++j) bias[j] = a.bias ? a.bias[a.out_mode == 1 ? (n + j) % a.Cps : n + j] : 0.f;
+  if constexpr (F8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wsc[j] = a.wscale[n + j];
+  }
   for (int row = tid / GPR; row < rows; row += RSTEP) {
     const int m = m0 + row;
     if (m >= a.M) break;
@@ -128,7 +139,8 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
     v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w; v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      v[j] += bias[j];
+      if constexpr (F8) v[j] = fmaf(v[j], wsc[j], bias[j]);
+      else v[j] += bias[j];
       if (a.relu) v[j] = fmaxf(v[j], 0.f);
     }
     if (a.drop_rate > 0.f) {
@@ -144,6 +156,12 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
       int sub = n / a.Cps, c = n - sub * a.Cps;
       int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
       size_t pix = ((size_t)nimg * (2 * a.Ho) + 2 * yo + (sub >> 1)) * (2 * a.Wo) + 2 * xo + (sub & 1);
+      if constexpr (F8) {
+        if (a.out_f8) {
+          *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(a.out) + pix * a.out_stride + c) = f8x8_from_f(v);
+          continue;
+        }
+      }
       grp_from_f(gr, v);
       grp_store(gr, reinterpret_cast<bf16*>(a.out) + pix * a.out_stride + c);
     } else if (a.out_mode == 2 && n >= a.split_c) {
@@ -160,6 +178,13 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
       continue;
     } else {
       if (!a.out) continue;
+      if constexpr (F8) {   // fp8 launches: plain store (the host rejects addend / mask / accum / BN sums)
+        if (a.out_f8) {
+          *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(a.out) + (size_t)m * a.out_stride + n) =
+              f8x8_from_f(v);
+          continue;
+        }
+      }
       float f[8];
       if (a.addend) {
         grp_load(gr, reinterpret_cast<const bf16*>(a.addend) + (size_t)m * a.addend_stride + n);

@@ -16,6 +16,13 @@
 // phases compute the quadrants (A0,B0) (A0,B1) (A1,B1) (A1,B0); a quarter is refilled with K step t+2
 // as soon as its last reader phase has passed a barrier, so two K steps of loads are in flight and
 // the only wait is one counted `s_waitcnt vmcnt` per K step (never 0 inside the loop).
+//
+// F8 (fp8 e4m3 forward, BASELINE configs[4]): the same schedule with 128-channel K steps — a 128-B LDS row
+// then holds 128 fp8 instead of 64 bf16, so staging, swizzle and barriers are unchanged — and one
+// block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales; 2x the bf16 rate) per fragment pair
+// in place of two 16x16x32 bf16 MFMAs. Each lane feeds both operands the same 32 k values (16-B chunks
+// 2*h4 and 2*h4+1 of the row), so the k order inside the instruction cancels out of the dot product.
+// The per-output-channel weight scale is applied in the epilogue (FwdArgs::wscale).
 #include "conv_common.h"
 
 namespace {
@@ -41,11 +48,16 @@ constexpr int tap64_occ() { return 2 * (WM * TM + WN * 64) * 128 <= 81920 ? 2 : 
 // measured 2-5 % slower here). BAL: one quarter-tile refill per phase (B0 of step t+1 at P0, A0/B1/A1 of
 // step t+2 at P1/P2/P3: three quarters in flight across the wait) instead of A0+B0 together at P1.
 // BNR: data-gradient launch with the fused BatchNorm-backward reduction epilogue (epi_rows_bnr).
-template <int WM, int WN, int TM, bool BAL, bool BNR>
+typedef int v8i32 __attribute__((ext_vector_type(8)));
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+
+template <int WM, int WN, int TM, bool BAL, bool BNR, bool F8>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
-  constexpr int ROWB = 128;                        // one K step of one row: 64 bf16
+  constexpr int ROWB = 128;                        // one K step of one row: 64 bf16 / 128 fp8
+  constexpr int ES = F8 ? 1 : 2;                   // bytes per element
+  constexpr int KSTEP = ROWB / ES;                 // K elements per step
   constexpr int QA = BM / 2, QB = BN / 2;          // rows per quarter-tile
   constexpr int GA = QA * 8 / NTH, GB = QB * 8 / NTH;  // glds per thread per quarter
   static_assert(GA >= 1 && GB >= 1 && GA * NTH == QA * 8 && GB * NTH == QB * 8, "quarters must split evenly");
@@ -67,7 +79,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
   const int Cin_s = a.CAs + a.CBs;
   const int Wrows = (a.Nout + 63) / 64 * 64;
-  const int nk = a.K / 64;
+  const int nk = a.K / KSTEP;
 
   // ---- per-thread staging rows: quarter h, instruction i -> quarter row q = i*(NTH/8) + tid/8
   int ry[2][GA], rx[2][GA], rn[2][GA], rc[2][GA];
@@ -83,9 +95,9 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       ry[h][i] = yo * a.stride - a.pad;
       rx[h][i] = xo * a.stride - a.pad;
       rn[h][i] = v ? n * a.Hs : -1;
-      rc[h][i] = 8 * (pos ^ swz(q));
+      rc[h][i] = 16 * (pos ^ swz(q));   // byte offset of this lane's 16-B chunk
     }
-  const bf16* bp[2][GB];
+  const unsigned char* bp[2][GB];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -93,27 +105,27 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       const int q = i * (NTH / 8) + (tid >> 3);
       const int col = (q / 32) * 64 + h * 32 + (q % 32);
       bp[h][i] = (n0 + col < Wrows)
-                     ? reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + col) * a.Kpad + 8 * (pos ^ swz(q))
+                     ? reinterpret_cast<const unsigned char*>(a.W) + ((size_t)(n0 + col) * a.Kpad) * ES + 16 * (pos ^ swz(q))
                      : nullptr;
     }
-  const bf16* srcA = reinterpret_cast<const bf16*>(a.srcA);
-  const bf16* srcB = reinterpret_cast<const bf16*>(a.srcB);
+  const unsigned char* srcA = reinterpret_cast<const unsigned char*>(a.srcA);
+  const unsigned char* srcB = reinterpret_cast<const unsigned char*>(a.srcB);
 
-  // K step -> (tap offsets, source, channel); uniform across the block
-  struct Kt { int oy, ox, cs; const bf16* base; int kt; };
+  // K step -> (tap offsets, source, channel); uniform across the block. cs = pixel stride in bytes
+  struct Kt { int oy, ox, cs; const unsigned char* base; int kt; };
   const int ntaps = a.kh * a.kw;
   auto kinfo = [&](int kt) {
     Kt r;
-    int k = kt * 64;
+    int k = kt * KSTEP;
     if (a.korder) {   // chunk-major: step kt = chunk * ntaps + tap
       const int chunk = kt / ntaps, t = kt - chunk * ntaps;
-      k = t * Cin_s + chunk * 64;
+      k = t * Cin_s + chunk * KSTEP;
     }
     const int tap = k / Cin_s, ci = k - tap * Cin_s;
     const int ty = tap / a.kw, tx = tap - ty * a.kw;
-    r.oy = ty * a.dil; r.ox = tx * a.dil; r.kt = k / 64;
-    if (ci < a.CAs) { r.base = srcA + ci; r.cs = a.CAs; }
-    else { r.base = srcB + (ci - a.CAs); r.cs = a.CBs; }
+    r.oy = ty * a.dil; r.ox = tx * a.dil; r.kt = k / KSTEP;
+    if (ci < a.CAs) { r.base = srcA + ci * ES; r.cs = a.CAs * ES; }
+    else { r.base = srcB + (ci - a.CAs) * ES; r.cs = a.CBs * ES; }
     return r;
   };
   auto issueA = [&](int h, const Kt& k, int buf) {
@@ -133,7 +145,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     unsigned char* dst = smem + buf * STAGE + (h ? OB1 : OB0) + wave * 8 * ROWB;
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
-      const void* p = bp[h][i] ? (const void*)(bp[h][i] + (size_t)k.kt * 64) : (const void*)tap64_zero_page;
+      const void* p = bp[h][i] ? (const void*)(bp[h][i] + (size_t)k.kt * ROWB) : (const void*)tap64_zero_page;
       __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
     }
   };
@@ -145,7 +157,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     for (int mi = 0; mi < MIQ; ++mi)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int q = wr * HM + mi * 16 + r16, c = 4 * s + h4;
+        const int q = wr * HM + mi * 16 + r16, c = F8 ? 2 * h4 + s : 4 * s + h4;
         fa[mi][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
       }
   };
@@ -155,7 +167,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int q = wc * 32 + ni * 16 + r16, c = 4 * s + h4;
+        const int q = wc * 32 + ni * 16 + r16, c = F8 ? 2 * h4 + s : 4 * s + h4;
         fb[ni][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
       }
   };
@@ -167,14 +179,24 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
+    if constexpr (F8) {
 #pragma unroll
       for (int mi = 0; mi < MIQ; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
-          acc[ha * MIQ + mi][hb * 2 + ni] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][s], fb[ni][s], acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
+          acc[ha * MIQ + mi][hb * 2 + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              __builtin_bit_cast(v8i32, fa[mi]), __builtin_bit_cast(v8i32, fb[ni]), acc[ha * MIQ + mi][hb * 2 + ni],
+              0, 0, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[ha * MIQ + mi][hb * 2 + ni] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][s], fb[ni][s], acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -251,7 +273,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     }
     __syncthreads();
     if constexpr (BNR) epi_rows_bnr<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
-    else epi_rows<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
+    else epi_rows<NTH, BN, F8>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
     __syncthreads();
   }
   if (a.bn_sum || a.bnr_z) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
@@ -266,14 +288,21 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
   const dim3 g(a.nblocks), b(WM * WN * 64);
-  adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s>", WM, WN, TM, bal ? "true" : "false",
+  if constexpr (TM == 64) {   // fp8: the 64-row-per-wave tiles only (the 128-row ones spill in the K loop)
+    if (a.f8) {   // inference launches: no BN-backward epilogue, default refill order
+      adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, false, false, true>", WM, WN, TM);
+      hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, false, true>), g, b, 0, s, a);
+      return;
+    }
+  }
+  adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false>", WM, WN, TM, bal ? "true" : "false",
                   a.bnr_z ? "true" : "false");
   if (a.bnr_z) {
-    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, true>), g, b, 0, s, a);
+    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, true, false>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, true, false>), g, b, 0, s, a);
   } else {
-    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, false>), g, b, 0, s, a);
+    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, false, false>), g, b, 0, s, a);
   }
 }
 
@@ -290,21 +319,24 @@ constexpr double CFG_EFF[4] = {1.0, 0.85, 0.0, 0.6};
 
 namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
-  const int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
+  int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
   // the fused BN-backward epilogue handles plain stores only (what the data-gradient launches use)
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const int Cin_s = a.CAs + a.CBs;
-  if (a.scA || a.scB || a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 ||
+  const int ks = a.f8 ? 128 : 64;   // channels per K step
+  if (a.scA || a.scB || a.CAs % ks != 0 || a.CBs % ks != 0 || a.K != a.kh * a.kw * Cin_s || a.K % ks != 0 ||
       a.Kpad != a.K)
     return 0;
   a.korder = option("tap64_korder", 0);
   int cfg = mode - 2;
+  if (a.f8 && cfg != 1 && cfg != 3) mode = 1;
   if (mode == 1) {
     // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency
     // a configuration whose N tile is less than 3/4 used is not considered
     double best = 0.0;
     for (int c = 0; c < 4; ++c) {
+      if (a.f8 && CFG_BM[c] * CFG_BN[c] > 256 * 128) continue;   // fp8: 256x128 / 256x64 tiles
       const long long tn = (a.Nout + CFG_BN[c] - 1) / CFG_BN[c], tmm = (a.M + CFG_BM[c] - 1) / CFG_BM[c];
       const long long blocks = tn * tmm, waves = (blocks + 255) / 256;
       const double colu = (double)a.Nout / (tn * CFG_BN[c]);

@@ -1010,9 +1010,8 @@ namespace {
 template <typename T>
 int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast);
 
-template <typename T>
-int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
-  FwdArgs a{};
+void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
+  a = FwdArgs{};
   a.srcA = io->srcA; a.srcB = io->srcB;
   a.scA = io->bn_scaleA; a.shA = io->bn_shiftA; a.scB = io->bn_scaleB; a.shB = io->bn_shiftB;
   a.CAs = d->CA_stride; a.CBs = d->CB_stride;
@@ -1033,6 +1032,33 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   a.bnr_sc = io->bnr_scale; a.bnr_sh = io->bnr_shift; a.bnr_mean = io->bnr_mean; a.bnr_invstd = io->bnr_invstd;
   a.bnr_dgamma = io->bnr_dgamma; a.bnr_dbeta = io->bnr_dbeta;
   a.M = d->N * d->Ho * d->Wo;
+}
+
+// fp8 e4m3 forward launch (BASELINE configs[4]): tap64 kernel only, no fallback
+int launch_fwd_f8(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
+  FwdArgs a;
+  fill_fwd_args(d, io, a);
+  a.f8 = 1;
+  a.wscale = io->w_scale;
+  a.out_f8 = d->out_fp8;
+  ADP_REQUIRE(a.wscale && a.M > 0 && a.Nout > 0 && a.Nout % 8 == 0, "adp_conv_fwd(fp8): needs w_scale and Nout % 8 == 0");
+  ADP_REQUIRE(!a.scA && !a.scB && !a.addend && !a.mask && !a.accum && !a.bn_sum && !a.bnr_z && a.drop_rate == 0.f &&
+                  (d->out_mode == 0 || d->out_mode == 1) && a.out,
+              "adp_conv_fwd(fp8): plain or pixel-shuffle store only (no BN / addend / mask / accum / dropout)");
+  ADP_REQUIRE(d->out_mode != 1 || (d->shuffle_c > 0 && d->Nout % d->shuffle_c == 0), "adp_conv_fwd: bad shuffle_c");
+  ADP_REQUIRE(a.CAs % 128 == 0 && a.CBs % 128 == 0,
+              "adp_conv_fwd(fp8): source channel strides must be multiples of 128 (one 128-channel K step per tap)");
+  if (!adp::launch_fwd_tap64(a, s)) {
+    adp::set_error("adp_conv_fwd(fp8): no fp8 kernel for this geometry (needs K == taps * Cin_s, K % 128 == 0)");
+    return -1;
+  }
+  return adp::check_launch("adp_conv_fwd");
+}
+
+template <typename T>
+int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
+  FwdArgs a;
+  fill_fwd_args(d, io, a);
   ADP_REQUIRE(a.CAs % 8 == 0 && a.CBs % 8 == 0, "adp_conv_fwd: channel strides must be multiples of 8");
   ADP_REQUIRE(a.M > 0 && a.Nout > 0, "adp_conv_fwd: empty problem");
   ADP_REQUIRE(d->out_mode != 1 || (d->shuffle_c > 0 && d->Nout % d->shuffle_c == 0), "adp_conv_fwd: bad shuffle_c");
@@ -1186,6 +1212,7 @@ extern "C" int adp_conv_fwd(int dtype, const adp_conv_desc* d, const adp_conv_io
   ADP_REQUIRE(d && io, "adp_conv_fwd: null descriptor");
   if (dtype == ADP_F32) return launch_fwd<float>(d, io, s);
   if (dtype == ADP_BF16) return launch_fwd<bf16>(d, io, s);
+  if (dtype == ADP_FP8) return launch_fwd_f8(d, io, s);
   adp::set_error("adp_conv_fwd: unknown dtype");
   return -1;
 }

@@ -303,6 +303,84 @@ __global__ void bn_apply_kernel(size_t M, int C, const T* z, const float* sc, co
   }
 }
 
+// ---------------------------------------------------------------------------- fp8 inference path
+// per-row (output channel) e4m3 quantisation of the forward weight layout: one block per row
+__global__ void pack_fp8_kernel(const float* src, int skp, unsigned char* dst, int dkp, float* scale) {
+  const int r = blockIdx.x;
+  const float* row = src + (size_t)r * skp;
+  float m = 0.f;
+  for (int k = threadIdx.x; k < skp; k += TPB) m = fmaxf(m, fabsf(row[k]));
+  __shared__ float red[TPB / 64];
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 8, 64));
+  m = fmaxf(m, __shfl_xor(m, 4, 64));
+  m = fmaxf(m, __shfl_xor(m, 2, 64));
+  m = fmaxf(m, __shfl_xor(m, 1, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float amax = 0.f;
+#pragma unroll
+  for (int w = 0; w < TPB / 64; ++w) amax = fmaxf(amax, red[w]);
+  const float sc = amax > 0.f ? amax / FP8_MAX : 1.f;
+  const float inv = 1.f / sc;
+  if (threadIdx.x == 0) scale[r] = sc;
+  for (int k8 = threadIdx.x * 8; k8 < dkp; k8 += TPB * 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = k8 + j < skp ? row[k8 + j] * inv : 0.f;
+    *reinterpret_cast<uint2*>(dst + (size_t)r * dkp + k8) = f8x8_from_f(v);
+  }
+}
+
+template <typename T>
+ADP_DEV void load8f(const T* p, float* f) {
+  Grp<T> gr;
+  grp_load(gr, p);
+  grp_to_f(gr, f);
+}
+ADP_DEV void load8f(const unsigned char* p, float* f) { f8x8_to_f(*reinterpret_cast<const uint2*>(p), f); }
+
+template <typename T>
+__global__ void bn_apply_fp8_kernel(size_t M, int C, const T* z, const float* sc, const float* sh,
+                                    unsigned char* out) {
+  const int G = C >> 3;
+  size_t total = M * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    const int g = (int)(i % G);
+    float f[8];
+    load8f(z + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[g * 8 + j], sh[g * 8 + j]), 0.f);
+    *reinterpret_cast<uint2*>(out + i * 8) = f8x8_from_f(f);
+  }
+}
+
+template <typename T>
+__global__ void maxpool_fwd_fp8_kernel(int N, int H, int W, int C, const T* src, unsigned char* dst) {
+  const int Ho = H >> 1, Wo = W >> 1, G = C >> 3;
+  size_t total = (size_t)N * Ho * Wo * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    int g = (int)(i % G);
+    size_t pix = i / G;
+    int xo = (int)(pix % Wo);
+    size_t t = pix / Wo;
+    int yo = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    float best[8], f[8];
+    const size_t base = (((size_t)n * H + 2 * yo) * W + 2 * xo) * C + g * 8;
+    load8f(src + base, best);
+    const size_t off[3] = {(size_t)C, (size_t)W * C, (size_t)W * C + C};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      load8f(src + base + off[q], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) best[j] = f[j] > best[j] ? f[j] : best[j];
+    }
+    *reinterpret_cast<uint2*>(dst + pix * C + g * 8) = f8x8_from_f(best);
+  }
+}
+
 // ------------------------------------------------------------------------------ optimizer
 // Keras 2.13 Adam.update_step: alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1);
 // v += (g^2-v)(1-b2); w -= m*alpha/(sqrt(v)+eps). AdamW first applies w -= w*wd*lr.
@@ -464,4 +542,38 @@ extern "C" int adp_adam(size_t n, float* w, const float* g, float* m, float* v, 
 extern "C" int adp_ema(size_t n, float* ema, const float* p, float d, adp_stream_t st) {
   hipLaunchKernelGGL(ema_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, n, ema, p, d);
   return adp::check_launch("adp_ema");
+}
+
+extern "C" int adp_pack_weights_fp8(int rows, const float* src, int src_kpad, void* dst, int dst_kpad, float* scale,
+                                    adp_stream_t st) {
+  ADP_REQUIRE(rows > 0 && src && dst && scale && dst_kpad % 8 == 0 && dst_kpad >= src_kpad,
+              "adp_pack_weights_fp8: bad arguments (dst_kpad % 8 == 0 and >= src_kpad)");
+  hipLaunchKernelGGL(pack_fp8_kernel, dim3(rows), dim3(TPB), 0, (hipStream_t)st, src, src_kpad, (unsigned char*)dst,
+                     dst_kpad, scale);
+  return adp::check_launch("adp_pack_weights_fp8");
+}
+
+extern "C" int adp_bn_apply_fp8(int dtype, size_t M, int C, const void* z, const float* sc, const float* sh,
+                                void* out, adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && sc && sh, "adp_bn_apply_fp8: bad arguments");
+  size_t n = M * (C / 8);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(bn_apply_fp8_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, M, C,
+                                  (const T*)z, sc, sh, (unsigned char*)out));
+  return adp::check_launch("adp_bn_apply_fp8");
+}
+
+extern "C" int adp_maxpool2_fwd_fp8(int dtype, int N, int H, int W, int C, const void* src, void* dst,
+                                    adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && H % 2 == 0 && W % 2 == 0, "adp_maxpool2_fwd_fp8: need C%8==0 and even H,W");
+  size_t n = (size_t)N * (H / 2) * (W / 2) * (C / 8);
+  hipStream_t s = (hipStream_t)st;
+  if (dtype == ADP_FP8)
+    hipLaunchKernelGGL(maxpool_fwd_fp8_kernel<unsigned char>, dim3(nblk(n)), dim3(TPB), 0, s, N, H, W, C,
+                       (const unsigned char*)src, (unsigned char*)dst);
+  else
+    DTYPE_SWITCH(dtype, T,
+                 hipLaunchKernelGGL(maxpool_fwd_fp8_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, s, N, H, W, C,
+                                    (const T*)src, (unsigned char*)dst));
+  return adp::check_launch("adp_maxpool2_fwd_fp8");
 }

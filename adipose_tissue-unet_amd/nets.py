@@ -744,6 +744,87 @@ class UNetBN(UNetEngine):
         self._train_fwd = train
         return {"main_out": a["p"]}
 
+    # ------------------------------------------------------------------ fp8 inference (configs[4])
+    def _fp8_acts(self, B):
+        """fp8 e4m3 twins of every activation at levels >= 1 (channel strides >= 128): the operands of the
+        fp8 convs. Level 0 (64 channels) and pool0 stay bf16."""
+        a = self.acts(B)
+        q = {}
+        for i in range(1, self.levels):
+            keys = [f"az{i}_1", f"az{i}_2"]
+            if i < self.levels - 1:
+                keys += [f"ay{i}_1", f"ay{i}_2", f"t{i}", f"pool{i}"]
+            for k in keys:
+                q[k] = self.buf("q/" + k, tuple(a[k].shape), ops.FP8_DTYPE)
+        return q
+
+    def pack_fp8_weights(self):
+        """fp8 forward weights + per-output-channel scales for every layer whose input channel strides are
+        multiples of 128 (one 128-channel K step per tap)."""
+        self._packed8 = {}
+        for n, l in self.layers.items():
+            if isinstance(l, Dense) and all(c % 128 == 0 for c in l.cin_s) and l.K % 128 == 0:
+                dst = self.buf("w8/" + n, (l.Npad, l.Kpad), ops.FP8_DTYPE)
+                sc = self.buf("w8s/" + n, (l.Npad,), torch.float32)
+                ops.pack_weights_fp8(self.ps.view(n + "/W"), dst, sc)
+                self._packed8[n] = (dst, sc)
+
+    def _conv_any(self, l, srcA, out, *, srcB=None):
+        """Eval conv: fp8 kernel when the operands are fp8, else the bf16 path (no BN statistics)."""
+        if srcA.dtype != ops.FP8_DTYPE:
+            return self.conv(l, srcA, out, srcB=srcB)
+        W8, ws = self._packed8[l.name]
+        if l.transpose:
+            return ops.conv_fwd(srcA, W8, l.Nout, out=out, bias=self.bias(l.name), kh=1, kw=1, pad=0, out_mode=1,
+                                shuffle_c=l.cout_s, w_scale=ws)
+        return ops.conv_fwd(srcA, W8, l.Nout, out=out, srcB=srcB, bias=self.bias(l.name) if l.bias else None,
+                            kh=l.k, kw=l.k, dil=l.dil, relu=l.relu and not l.bn, w_scale=ws)
+
+    def _bn_conv_eval(self, name, srcA, z, act, *, srcB=None):
+        l = self.layers[name]
+        s = self.st[name]
+        self._conv_any(l, srcA, z, srcB=srcB)
+        rm, rv = self.running[name]
+        ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
+                        self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
+        if act.dtype == ops.FP8_DTYPE:
+            ops.bn_apply_fp8(z, s[2], s[3], act)
+        else:
+            ops.bn_apply(z, s[2], s[3], act)
+
+    def forward_fp8(self, batch=None, *, pack=True):
+        """Eval forward with fp8 e4m3 activations and weights on every conv whose inputs have >= 128
+        channels (levels >= 1: ~78 % of the forward FLOPs); the input conv, level 0 and the head stay bf16.
+        Conv outputs (pre-BN) are bf16, BatchNorm-ReLU writes the fp8 operand of the next conv."""
+        if self.dt != torch.bfloat16:
+            raise ops.AdpError("forward_fp8 needs a bf16 network (its level-0 path)")
+        B = batch or self.B
+        a = self.acts(B)
+        q = self._fp8_acts(B)
+        if pack:
+            self.pack_forward_weights()
+            self.pack_fp8_weights()
+
+        def act(key):
+            return q.get(key, a[key])
+        Lv = self.levels
+        src = a["x"]
+        for i in range(Lv):
+            self._bn_conv_eval(f"enc{i}_conv1", src, a[f"z{i}_1"], act(f"az{i}_1"))
+            self._bn_conv_eval(f"enc{i}_conv2", act(f"az{i}_1"), a[f"z{i}_2"], act(f"az{i}_2"))
+            if i < Lv - 1:
+                ops.maxpool2_fwd(act(f"az{i}_2"), act(f"pool{i}"))
+                src = act(f"pool{i}")
+        prev = act(f"az{Lv - 1}_2")
+        for i in range(Lv - 2, -1, -1):
+            self._conv_any(self.layers[f"dec{i}_up"], prev, act(f"t{i}"))
+            self._bn_conv_eval(f"dec{i}_conv1", act(f"az{i}_2"), a[f"y{i}_1"], act(f"ay{i}_1"), srcB=act(f"t{i}"))
+            self._bn_conv_eval(f"dec{i}_conv2", act(f"ay{i}_1"), a[f"y{i}_2"], act(f"ay{i}_2"))
+            prev = act(f"ay{i}_2")
+        ops.head_fwd(prev, self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0), softmax2=False)
+        self._train_fwd = False
+        return {"main_out": a["p"]}
+
     def _bn_red(self, name, z):
         """bn_reduce argument for a dgrad launch whose output is the gradient of relu(bn_name(z))."""
         s = self.st[name]

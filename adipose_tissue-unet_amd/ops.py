@@ -13,7 +13,9 @@ import ctypes as C
 
 import torch
 
-from ._lib import BF16, F32, AdpError, ConvDesc, ConvIO, call, lib, ptr, stream_ptr
+from ._lib import BF16, F32, FP8, AdpError, ConvDesc, ConvIO, call, lib, ptr, stream_ptr
+
+FP8_DTYPE = torch.float8_e4m3fn   # storage dtype of the fp8 (OCP e4m3fn) inference tensors
 
 
 def round_up(x, m):
@@ -74,6 +76,8 @@ def dtype_code(t):
         return BF16
     if t.dtype == torch.float32:
         return F32
+    if t.dtype == FP8_DTYPE:
+        return FP8
     raise AdpError(f"unsupported dtype {t.dtype}")
 
 
@@ -141,11 +145,13 @@ def _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo
 def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=None, up=False, stride=1,
              kh=3, kw=3, dil=1, pad=None, Ho=None, Wo=None, relu=False, dropout_rate=0.0, dropout_seed=0,
              out_mode=0, shuffle_c=0, out2=None, split_c=0, addend=None, mask=None, mask_scale=1.0,
-             mask2=None, mask2_scale=1.0, accum=None, bn_stats=None, bn_reduce=None):
+             mask2=None, mask2_scale=1.0, accum=None, bn_stats=None, bn_reduce=None, w_scale=None):
     """Implicit-GEMM conv forward-shaped launch (conv, conv dgrad, convT fwd/dgrad).
 
     bn_reduce=(z, scale, shift, mean, invstd, dgamma, dbeta): fuse the BatchNorm-backward reduction
-    (bn_bwd_reduce) of the layer whose activation relu(z*scale+shift) `out` is the gradient of."""
+    (bn_bwd_reduce) of the layer whose activation relu(z*scale+shift) `out` is the gradient of.
+    fp8 launches (srcA/W torch.float8_e4m3fn): w_scale (f32, per GEMM column, from pack_weights_fp8) is
+    required; `out` may be bf16 or fp8."""
     d, io, N, Ho, Wo = _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo, nout)
     d.relu = 1 if relu else 0
     d.dropout_rate = float(dropout_rate)
@@ -168,7 +174,14 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
             io.mask2 = ptr(mask2)
     if out is not None:
         _act(out, "out")
-        _check(out.dtype == srcA.dtype, "out dtype mismatch")
+        if srcA.dtype == FP8_DTYPE:
+            _check(out.dtype in (FP8_DTYPE, torch.bfloat16), "fp8 launch: out must be bf16 or fp8")
+            _check(w_scale is not None and w_scale.dtype == torch.float32 and w_scale.numel() >= nout,
+                   "fp8 launch needs w_scale (f32, >= nout entries)")
+            d.out_fp8 = 1 if out.dtype == FP8_DTYPE else 0
+            io.w_scale = ptr(w_scale)
+        else:
+            _check(out.dtype == srcA.dtype, "out dtype mismatch")
         if out_mode != 1:
             _check(tuple(out.shape[:3]) == (N, Ho, Wo), f"out shape {tuple(out.shape)} != {(N, Ho, Wo)}")
             _check(out.shape[3] >= (split_c if out_mode == 2 else nout), "out has too few channels")
@@ -257,10 +270,32 @@ def pack_weights(src, dst, mode, *, taps=1, cin_s=0, nout=0):
          int(dst.shape[0]), int(dst.shape[1]), stream_ptr())
 
 
+def pack_weights_fp8(src, dst, scale):
+    """Forward-layout fp8 weights + per-row dequantisation scale (adp_pack_weights_fp8)."""
+    _check(src.dtype == torch.float32 and src.dim() == 2 and dst.dtype == FP8_DTYPE and dst.dim() == 2
+           and dst.shape[0] == src.shape[0] and dst.shape[1] >= src.shape[1] and dst.shape[1] % 8 == 0,
+           "pack_weights_fp8: bad tensors")
+    _check(scale.dtype == torch.float32 and scale.numel() >= src.shape[0], "pack_weights_fp8: scale size")
+    call("adp_pack_weights_fp8", int(src.shape[0]), ptr(src), int(src.shape[1]), ptr(dst), int(dst.shape[1]),
+         ptr(scale), stream_ptr())
+
+
+def bn_apply_fp8(z, scale, shift, out):
+    _check(out.shape == z.shape and out.dtype == FP8_DTYPE, "bn_apply_fp8 shapes")
+    Cs = z.shape[-1]
+    call("adp_bn_apply_fp8", dtype_code(z), z.numel() // Cs, Cs, ptr(z), ptr(scale), ptr(shift), ptr(out),
+         stream_ptr())
+    return out
+
+
 def maxpool2_fwd(src, dst, bn=None):
     _act(src, "src")
     _act(dst, "dst")
     N, H, W, Cs = src.shape
+    if dst.dtype == FP8_DTYPE:
+        _check(tuple(dst.shape) == (N, H // 2, W // 2, Cs) and bn is None, "maxpool fp8 dst shape")
+        call("adp_maxpool2_fwd_fp8", dtype_code(src), N, H, W, Cs, ptr(src), ptr(dst), stream_ptr())
+        return dst
     _check(tuple(dst.shape) == (N, H // 2, W // 2, Cs) and dst.dtype == src.dtype, "maxpool dst shape")
     call("adp_maxpool2_fwd", dtype_code(src), N, H, W, Cs, ptr(src), ptr(bn[0]) if bn else None,
          ptr(bn[1]) if bn else None, ptr(dst), stream_ptr())

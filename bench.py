@@ -20,7 +20,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-MI355X_PEAK = {"bf16": 2500.0, "f32": 157.3}   # TFLOP/s dense (MI355X_MICROARCH.md chip table)
+MI355X_PEAK = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}   # TFLOP/s dense (MI355X_MICROARCH.md chip table)
 
 
 def parse():
@@ -181,7 +181,7 @@ def main():
     # (names as rocprofv3 prints them; profiles/ holds the matching --kernel-trace --stats summary)
     dom = max(summ.items(), key=lambda kv: kv[1][2])
     (kname, dcode), (n, flops, ms) = dom
-    dname = "bf16" if dcode == 1 else "f32"
+    dname = {0: "f32", 1: "bf16", 2: "fp8"}[dcode]
     achieved = flops / (ms * 1e-3) / 1e12
     step_ms = elapsed * 1e3
     per_kernel = {k[0]: {"launches": v[0], "avg_ms": round(v[2] / v[0], 4),

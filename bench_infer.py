@@ -23,14 +23,17 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-MI355X_PEAK = {"bf16": 2500.0, "f32": 157.3}
+MI355X_PEAK = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}
+DNAME = {0: "f32", 1: "bf16", 2: "fp8"}
 # forward FLOPs of adipose_v3 per 1024^2 tile: 2 x 448.2 GMAC (counted from the layer list)
 V3_FWD_GFLOP_1024 = 896.3
 
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--mode", default="wsi", choices=["wsi", "tiles"])
+    p.add_argument("--mode", default="wsi", choices=["wsi", "tiles", "fp8"])
+    p.add_argument("--levels", type=int, default=5, help="unet_bn levels (mode fp8)")
+    p.add_argument("--train-steps", type=int, default=60, help="mode fp8: bf16 training steps before the comparison")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--size", type=int, default=8192, help="WSI side (mode wsi)")
     p.add_argument("--tile", type=int, default=1024)
@@ -44,8 +47,99 @@ def parse():
     return p.parse_args()
 
 
+def fp8_main(args):
+    """BASELINE.json configs[4]: fp8 (CDNA4 block-scaled MFMA) forward of the 1024^2 unet_bn network on one
+    GPU, Dice within 1e-2 of bf16. The network (L5, base 64, random Keras-default init, seed 865) is first
+    trained for --train-steps bf16 steps on synthetic histology tiles so that weights and BatchNorm running
+    statistics are those of a fitted model; then a held-out synthetic batch is predicted in bf16 and in fp8
+    and both are scored against its masks (calculate_pixel_metrics, threshold 0.5)."""
+    import numpy as np
+    import torch
+
+    import _adipose_pkg  # noqa: F401
+    from adipose_amd import ops
+    from adipose_amd.data import synthetic_batch
+    from adipose_amd.metrics import calculate_pixel_metrics
+    from adipose_amd.nets import UNetBN
+    from adipose_amd.trainer import LossConfig, Trainer
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    B, S = args.batch, args.tile
+    net = UNetBN(B, S, levels=args.levels, base=64, in_ch=3, dtype="bf16", device=dev, seed=865)
+    tr = Trainer(net, LossConfig(use_hard_mining=False), lr=1e-3)
+    batches = []
+    for k in range(2):
+        xs, ys = synthetic_batch(B, S, channels=3, seed=865 + k)
+        batches.append((xs.astype(np.float32), ys))
+    mean = float(np.mean([b[0].mean() for b in batches]))
+    std = float(np.mean([b[0].std() for b in batches]))
+    dev_batches = [(torch.from_numpy((x - mean) / (std + 1e-10)).to(dev), torch.from_numpy(y).to(dev))
+                   for x, y in batches]
+    t0 = time.perf_counter()
+    for i in range(args.train_steps):
+        tr.train_step(*dev_batches[i % 2])
+    torch.cuda.synchronize()
+    train_s = time.perf_counter() - t0
+    xv, yv = synthetic_batch(B, S, channels=3, seed=865 + 10_000)
+    xvd = torch.from_numpy((xv.astype(np.float32) - mean) / (std + 1e-10)).to(dev)
+    ops.prep_input(xvd, net.acts(B)["x"], mean=0.0, std=1.0)
+
+    def run(fn, steps):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        timer = ops.LaunchTimer()
+        ops.set_launch_timer(timer)
+        t = time.perf_counter()
+        for _ in range(steps):
+            out = fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t
+        ops.set_launch_timer(None)
+        return out["main_out"].clone(), el, timer.summary()
+
+    steps = max(args.steps, 5)
+    p16, el16, _ = run(lambda: net.forward(B, train=False), steps)
+    p8, el8, summ = run(lambda: net.forward_fp8(B), steps)
+    y = yv.astype(np.float32)
+    d16 = [calculate_pixel_metrics(p16[b].cpu().numpy(), y[b])["dice_score"] for b in range(B)]
+    d8 = [calculate_pixel_metrics(p8[b].cpu().numpy(), y[b])["dice_score"] for b in range(B)]
+    agree = [calculate_pixel_metrics(p8[b].cpu().numpy(), (p16[b].cpu().numpy() > 0.5).astype(np.float32))["dice_score"]
+             for b in range(B)]
+    f8 = {k: v for k, v in summ.items() if k[1] == 2}
+    dom = max(f8.items(), key=lambda kv: kv[1][2])
+    (kname, dcode), (n, flops, ms) = dom
+    achieved = flops / (ms * 1e-3) / 1e12
+    line = {
+        "metric": "1024^2 tiles/s (fp8 forward) + Dice vs bf16", "value": round(steps * B / el8, 3), "unit": "tiles/s",
+        "n_gpus": 1, "steps": steps, "warmup": args.warmup, "ms_per_step": round(el8 / steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp8 (e4m3fn)",
+        "data": "synthetic (seeded histology-like tiles, resident in HBM)",
+        "config": {"workload": f"unet_bn L{args.levels} base64 {S}x{S}x3 forward B={B} (BASELINE configs[4])",
+                   "train_steps_before_eval": args.train_steps, "train_s": round(train_s, 2),
+                   "fp8_layers": sorted(net._packed8), "batch": B},
+        "bf16_tiles_per_s": round(steps * B / el16, 3), "fp8_speedup": round(el16 / el8, 4),
+        "dice_bf16": round(float(np.mean(d16)), 5), "dice_fp8": round(float(np.mean(d8)), 5),
+        "dice_delta": round(abs(float(np.mean(d8)) - float(np.mean(d16))), 6),
+        "dice_fp8_vs_bf16_masks": round(float(np.mean(agree)), 5),
+        "max_abs_dprob": round((p8 - p16).abs().max().item(), 5),
+        "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": MI355X_PEAK["fp8"],
+                     "unit": "TFLOP/s", "frac": round(achieved / MI355X_PEAK["fp8"], 4),
+                     "avg_launch_ms": round(ms / n, 4), "launches": n,
+                     "per_kernel": {f"{k[0]} [{DNAME[k[1]]}]": {"launches": v[0], "avg_ms": round(v[2] / v[0], 4),
+                                                               "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2)}
+                                    for k, v in sorted(summ.items(), key=lambda kv: -kv[1][2])}},
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.mode == "fp8":
+        if args.batch == 8 and args.tile == 1024:
+            args.batch = 4
+        return fp8_main(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -127,7 +221,7 @@ def main():
     if rank == 0:
         dom = max(summ.items(), key=lambda kv: kv[1][2])
         (kname, dcode), (n, flops, ms) = dom
-        dname = "bf16" if dcode == 1 else "f32"
+        dname = DNAME[dcode]
         achieved = flops / (ms * 1e-3) / 1e12
         tot_ms = sum(v[2] for v in summ.values())
         # forward FLOPs executed per tile (all ranks): the wsi mode counts every rank's forwards

@@ -12,7 +12,9 @@
  *   - Calls are asynchronous on the given hipStream_t (passed as void* so the header needs no HIP
  *     include) and never allocate, free or synchronise (safe to capture in a hipGraph).
  *   - dtype: ADP_DTYPE_F32 (parity path, exact f32 MFMA) or ADP_DTYPE_BF16 (throughput path,
- *     f32 accumulation). Activations are NHWC with channel stride a multiple of 8.
+ *     f32 accumulation); ADP_DTYPE_FP8 (e4m3fn operands, block-scaled MFMA, f32 accumulation) for
+ *     forward-only launches (BASELINE.json configs[4]). Activations are NHWC with channel stride a
+ *     multiple of 8.
  *   - GEMM weights are packed [Npad][Kpad] (output-channel major, K = taps*Cin_stride contiguous,
  *     Kpad = round_up(K,32), Npad = round_up(N,64)); tap order is row-major over (ky,kx).
  */
@@ -26,7 +28,8 @@ extern "C" {
 
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
-#define ADP_ABI_VERSION 2
+#define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
+#define ADP_ABI_VERSION 3
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -51,6 +54,7 @@ typedef struct adp_conv_desc {
   float mask2_scale;
   int accum_stride;         /* accum (f32) += stored value */
   int bnr_stride;           /* channel stride of io->bnr_z */
+  int out_fp8;              /* ADP_DTYPE_FP8 launches: 1 stores the output as fp8 e4m3 (else bf16) */
 } adp_conv_desc;
 
 typedef struct adp_conv_io {
@@ -80,6 +84,8 @@ typedef struct adp_conv_io {
   const float* bnr_invstd;
   float* bnr_dgamma;
   float* bnr_dbeta;
+  /* ADP_DTYPE_FP8 launches: per-GEMM-column dequantisation scale of W (adp_pack_weights_fp8) */
+  const float* w_scale;
 } adp_conv_io;
 
 /* ---- library ---------------------------------------------------------------------------- */
@@ -99,6 +105,9 @@ int adp_set_option(const char* name, int value);
  *      Relu / ResizeNearestNeighbor / ConcatV2 / AddN / Dropout of
  *      Segmentation/train_adipose_unet_v3.py:668-710, and ConvTranspose2D of the unet_bn preset) */
 int adp_conv_fwd(int dtype, const adp_conv_desc* d, const adp_conv_io* io, adp_stream_t s);
+/* ADP_DTYPE_FP8: srcA/srcB/W fp8 e4m3, channel strides and K multiples of 128 (one 128-channel K step
+ * per tap), acc[m][n] * w_scale[n] (+ bias, ReLU) stored as bf16 or fp8 (desc.out_fp8); out_mode 0 or 1;
+ * no BatchNorm / addend / mask / accumulate / dropout epilogue terms. */
 /* dW[Npad][Kpad] (+)= sum_m dY[m][n] * X_tap(k)[m]; dB[n] (+)= sum_m dY[m][n]. f32 accumulators,
  * caller zeroes them. The gather is described by d/io exactly as for the forward launch. */
 int adp_conv_wgrad(int dtype, const adp_conv_desc* d, const adp_conv_io* io, const void* dY,
@@ -108,10 +117,17 @@ int adp_conv_wgrad(int dtype, const adp_conv_desc* d, const adp_conv_io* io, con
  * mode 1 = 3x3 flip+transpose (data-gradient of a conv), mode 2 = ConvTranspose transpose. */
 int adp_pack_weights(int dtype_out, int mode, int taps, int Cin_s, int Nout, const float* src,
                      int src_kpad, void* dst, int dst_rows, int dst_kpad, adp_stream_t s);
+/* Forward-layout fp8 weights with a per-row (output channel) scale: scale[r] = max_k |src[r][k]| / 448
+ * (1 for an all-zero row), dst[r][k] = e4m3(src[r][k] / scale[r]) (saturating, round to nearest even). */
+int adp_pack_weights_fp8(int rows, const float* src, int src_kpad, void* dst, int dst_kpad, float* scale,
+                         adp_stream_t s);
 
 /* ---- pooling / upsampling (MaxPooling2D :670,674,678; UpSampling2D grad) ------------------- */
 int adp_maxpool2_fwd(int dtype, int N, int H, int W, int C_stride, const void* src,
                      const float* bn_scale, const float* bn_shift, void* dst, adp_stream_t s);
+/* 2x2 max-pool with an fp8 e4m3 output; src of dtype dtype_in (F32, BF16 or FP8) */
+int adp_maxpool2_fwd_fp8(int dtype_in, int N, int H, int W, int C_stride, const void* src, void* dst_fp8,
+                         adp_stream_t s);
 int adp_maxpool2_bwd(int dtype, int N, int H, int W, int C_stride, const void* src,
                      const float* bn_scale, const float* bn_shift, const void* dpool,
                      const void* addend, const void* mask, float mask_scale, void* dsrc,
@@ -133,6 +149,9 @@ int adp_bn_finalize(int C, float count, const float* sum, const float* sqsum, co
 /* a = relu(z*scale + shift), the post-BatchNorm activation, materialised once per layer */
 int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* scale, const float* shift,
                  void* out, adp_stream_t s);
+/* the same activation stored as fp8 e4m3 (z of dtype dtype_in): the operand of an fp8 conv launch */
+int adp_bn_apply_fp8(int dtype_in, size_t M, int C, const void* z, const float* scale, const float* shift,
+                     void* out_fp8, adp_stream_t s);
 /* dBN = dA * (relu(z*scale+shift) > 0); dgamma += sum dBN*xhat; dbeta += sum dBN */
 int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, const void* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, float* dgamma,

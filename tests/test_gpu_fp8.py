@@ -1,0 +1,163 @@
+"""fp8 (OCP e4m3fn) inference path of BASELINE.json configs[4] (no reference code exists for it).
+
+Kernel parity: every fp8 launch is checked against a float64 CPU convolution of the SAME quantised
+operands (fp8 activations and fp8 weights dequantised with the kernel's own per-channel scales), so the
+only differences left are f32 accumulation order and the bf16 / fp8 rounding of the stored output.
+Quantisation parity: the GPU encoders (weights, BatchNorm-ReLU, max-pool) must produce the bytes torch's
+float8_e4m3fn conversion produces (round to nearest even) for in-range values.
+Network: fp8 forward vs the bf16 forward of the same unet_bn weights (acceptance of configs[4] is
+"Dice within 1e-2 of bf16"; bench_infer.py --mode fp8 measures it on a trained network).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from adipose_amd import ops
+from adipose_amd.nets import UNetBN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+F8 = ops.FP8_DTYPE
+
+
+def q8(t):
+    """host-side reference quantisation (RNE, values kept inside +-448)"""
+    return t.clamp(-448, 448).to(F8)
+
+
+def pack8(Wf):
+    """GPU per-row quantisation of an f32 [Npad][Kpad] weight matrix -> (fp8 device, scale device)."""
+    W8 = torch.empty(Wf.shape, dtype=F8, device=DEV)
+    sc = torch.empty(Wf.shape[0], dtype=torch.float32, device=DEV)
+    ops.pack_weights_fp8(Wf.to(DEV), W8, sc)
+    return W8, sc
+
+
+def ref_conv(x8, W8, sc, cout, k, dil, cin, bias=None, relu=False):
+    """float64 NHWC conv of the dequantised operands; W packed [n][tap*Cin_s + c]."""
+    x = x8.float().double().cpu().permute(0, 3, 1, 2)
+    Wd = (W8.float().double().cpu() * sc.double().cpu()[:, None])[:cout, :k * k * cin]
+    w = Wd.reshape(cout, k, k, cin).permute(0, 3, 1, 2)
+    y = F.conv2d(x, w, padding=dil * (k // 2), dilation=dil)
+    if bias is not None:
+        y = y + bias.double().cpu()[None, :, None, None]
+    if relu:
+        y = y.clamp_min(0)
+    return y.permute(0, 2, 3, 1)
+
+
+def test_pack_weights_fp8_bytes_and_scale():
+    g = torch.Generator().manual_seed(1)
+    Wf = torch.randn(192, 1152, generator=g) * 0.05
+    Wf[7] = 0.0                                         # all-zero row -> scale 1
+    W8, sc = pack8(Wf)
+    amax = Wf.abs().amax(1)
+    ref_sc = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    np.testing.assert_allclose(sc.cpu().numpy(), ref_sc.numpy(), rtol=1e-6)
+    ref = q8(Wf / sc.cpu()[:, None])
+    got = W8.cpu()
+    assert torch.equal(got.view(torch.uint8), ref.view(torch.uint8)), \
+        (got.view(torch.uint8) != ref.view(torch.uint8)).sum().item()
+
+
+@pytest.mark.parametrize("C,H", [(128, 16), (256, 32)])
+def test_bn_apply_and_maxpool_fp8(C, H):
+    g = torch.Generator().manual_seed(C)
+    z = (torch.randn(2, H, H, C, generator=g) * 3).to(torch.bfloat16)
+    scale = torch.rand(C, generator=g) + 0.5
+    shift = torch.randn(C, generator=g)
+    out = torch.empty(z.shape, dtype=F8, device=DEV)
+    ops.bn_apply_fp8(z.to(DEV), scale.to(DEV), shift.to(DEV), out)
+    ref = q8(torch.clamp_min(z.float() * scale + shift, 0))
+    # the device computes fmaf(z, scale, shift); allow a 1-ulp fp8 difference where the f32 rounding of
+    # z*scale+shift straddles an fp8 rounding boundary
+    diff = (out.cpu().view(torch.uint8).int() - ref.view(torch.uint8).int()).abs()
+    assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3
+    pooled = torch.empty(2, H // 2, H // 2, C, dtype=F8, device=DEV)
+    ops.maxpool2_fwd(out, pooled)
+    a = out.cpu().float().permute(0, 3, 1, 2)
+    refp = F.max_pool2d(a, 2).permute(0, 2, 3, 1)
+    assert torch.equal(pooled.cpu().float(), refp)
+    # bf16 source -> fp8 pooled output
+    pooled2 = torch.empty(2, H // 2, H // 2, C, dtype=F8, device=DEV)
+    ops.maxpool2_fwd(z.to(DEV), pooled2)
+    refp2 = q8(F.max_pool2d(z.float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1))
+    assert torch.equal(pooled2.cpu().view(torch.uint8), refp2.view(torch.uint8))
+
+
+@pytest.mark.parametrize("cinA,cinB,cout,dil,H,out_fp8,relu", [
+    (128, 0, 128, 1, 32, False, False),      # 256x128 tile
+    (256, 0, 64, 2, 16, False, True),        # 256x64 tile, dilation, ReLU
+    (128, 128, 128, 1, 16, True, False),     # concat sources, fp8 output
+    (512, 0, 512, 1, 8, False, False),       # wide layer
+])
+def test_fp8_conv_vs_dequantised_reference(cinA, cinB, cout, dil, H, out_fp8, relu):
+    g = torch.Generator().manual_seed(cinA + cout + H)
+    B = 2
+    xa8 = q8(torch.randn(B, H, H, cinA, generator=g).clamp_min(0) * 2)
+    xb8 = q8(torch.randn(B, H, H, cinB, generator=g)) if cinB else None
+    cin = cinA + cinB
+    K = 9 * cin
+    Wf = torch.zeros(((cout + 63) // 64 * 64, K))
+    Wf[:cout] = torch.randn(cout, K, generator=g) * (2.0 / K) ** 0.5
+    bias = torch.randn(cout, generator=g) * 0.1
+    W8, sc = pack8(Wf)
+    out = torch.zeros(B, H, H, cout, dtype=F8 if out_fp8 else torch.bfloat16, device=DEV)
+    ops.conv_fwd(xa8.to(DEV), W8, cout, out=out, srcB=None if xb8 is None else xb8.to(DEV), bias=bias.to(DEV),
+                 kh=3, kw=3, dil=dil, relu=relu, w_scale=sc)
+    torch.cuda.synchronize()
+    x_cat = xa8 if xb8 is None else torch.cat([xa8.float(), xb8.float()], -1).to(F8)
+    ref = ref_conv(x_cat, W8, sc, cout, 3, dil, cin, bias=bias, relu=relu)
+    got = out.cpu().float().double()
+    rel = 2 ** -3 if out_fp8 else 2 ** -7           # output rounding (fp8 e4m3 / bf16), relative
+    err = (got - ref).abs() - rel * ref.abs()
+    assert err.max().item() < 1e-3, err.max().item()
+
+
+def test_fp8_convtranspose_pixel_shuffle():
+    g = torch.Generator().manual_seed(7)
+    B, H, cin, cout = 2, 8, 256, 128
+    x8 = q8(torch.randn(B, H, H, cin, generator=g).clamp_min(0))
+    # packed ConvT weights: rows sub*cout + co (sub = dy*2+dx), K = cin
+    Wf = torch.randn(4 * cout, cin, generator=g) * 0.05
+    bias = torch.randn(cout, generator=g) * 0.1
+    W8, sc = pack8(Wf)
+    out = torch.zeros(B, 2 * H, 2 * H, cout, dtype=torch.bfloat16, device=DEV)
+    ops.conv_fwd(x8.to(DEV), W8, 4 * cout, out=out, bias=bias.to(DEV), kh=1, kw=1, pad=0, out_mode=1,
+                 shuffle_c=cout, w_scale=sc)
+    torch.cuda.synchronize()
+    Wd = W8.float().double().cpu() * sc.double().cpu()[:, None]
+    y = torch.einsum("bhwc,nc->bhwn", x8.float().double(), Wd)        # (B,H,W,4*cout)
+    ref = torch.zeros(B, 2 * H, 2 * H, cout, dtype=torch.float64)
+    for sub in range(4):
+        dy, dx = sub >> 1, sub & 1
+        ref[:, dy::2, dx::2, :] = y[..., sub * cout:(sub + 1) * cout] + bias.double()
+    got = out.cpu().double()
+    assert ((got - ref).abs() - 2 ** -7 * ref.abs()).max().item() < 1e-3
+
+
+def test_fp8_conv_rejects_unsupported_geometry():
+    x8 = torch.zeros(1, 8, 8, 64, dtype=F8, device=DEV)            # 64-channel stride: not a 128 K step
+    W8 = torch.zeros(64, 9 * 64, dtype=F8, device=DEV)
+    sc = torch.ones(64, device=DEV)
+    out = torch.zeros(1, 8, 8, 64, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(ops.AdpError):
+        ops.conv_fwd(x8, W8, 64, out=out, w_scale=sc)
+
+
+@pytest.mark.parametrize("S", [64, 128])
+def test_unet_bn_fp8_forward_vs_bf16(S):
+    B, L = 2, 3
+    net = UNetBN(B, S, levels=L, base=64, in_ch=3, dtype="bf16", device=DEV, seed=11)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, S, S, 3, generator=g)
+    ops.prep_input(x.to(DEV), net.acts(B)["x"], mean=0.0, std=1.0)
+    p16 = net.forward(B, train=False)["main_out"].clone()
+    p8 = net.forward_fp8(B)["main_out"].clone()
+    torch.cuda.synchronize()
+    d = (p8 - p16).abs()
+    assert d.mean().item() < 1e-2 and d.max().item() < 0.1, (d.mean().item(), d.max().item())
+    # the bf16 path is unchanged by an fp8 pass on the same buffers
+    p16b = net.forward(B, train=False)["main_out"]
+    assert torch.equal(p16b, p16)

@@ -25,6 +25,9 @@ for s in $STEPS; do
                > gpurun_out/v3_bench_cpad_mix.log 2>&1 &&
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8,8,64,64 > gpurun_out/infer_tiles_mix.log 2>&1 &&
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8,64,64,64 > gpurun_out/infer_tiles_mix2.log 2>&1 ;;
+    fp8) timeout -k 10 300 python -u -m pytest tests/test_gpu_fp8.py -x -v --timeout 120 --timeout-method thread \
+           > gpurun_out/gpu_fp8_tests.log 2>&1 &&
+         timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8.log 2>&1 ;;
     infer) timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 > gpurun_out/infer_tiles.log 2>&1 &&
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8 > gpurun_out/infer_tiles_cpad8.log 2>&1 &&
            timeout -k 10 400 python bench_infer.py --mode wsi > gpurun_out/infer_wsi.log 2>&1 ;;
