@@ -21,7 +21,8 @@
 // then holds 128 fp8 instead of 64 bf16, so staging, swizzle and barriers are unchanged — and one
 // block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales; 2x the bf16 rate) per fragment pair
 // in place of two 16x16x32 bf16 MFMAs. Each lane feeds both operands the same 32 k values (16-B chunks
-// 2*h4 and 2*h4+1 of the row), so the k order inside the instruction cancels out of the dot product.
+// h4 and h4+4 of the row: the bf16 read pattern, conflict-free under the swizzle), so the k order inside
+// the instruction cancels out of the dot product.
 // The per-output-channel weight scale is applied in the epilogue (FwdArgs::wscale).
 #include "conv_common.h"
 
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     for (int mi = 0; mi < MIQ; ++mi)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int q = wr * HM + mi * 16 + r16, c = F8 ? 2 * h4 + s : 4 * s + h4;
+        const int q = wr * HM + mi * 16 + r16, c = 4 * s + h4;
         fa[mi][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
       }
   };
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int q = wc * 32 + ni * 16 + r16, c = F8 ? 2 * h4 + s : 4 * s + h4;
+        const int q = wc * 32 + ni * 16 + r16, c = 4 * s + h4;
         fb[ni][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
       }
   };

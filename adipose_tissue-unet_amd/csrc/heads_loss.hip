@@ -391,6 +391,30 @@ __global__ void pixel_counts_kernel(size_t n, const float* pred, const float* tr
     atomicAdd(counts + threadIdx.x, v);
   }
 }
+// threshold sweep: per pixel j = #{t : pred > thr[t]} over ascending thresholds (compared in double, as
+// numpy compares a float32 map with float64 thresholds), histogram of j split by the truth bit in LDS,
+// one atomic per bin and block. tp(t) = sum_{j > t} hist[1][j], fp(t) = sum_{j > t} hist[0][j].
+struct ThrList { double t[64]; };
+__global__ void threshold_hist_kernel(size_t n, const float* pred, const float* truth, int nt, ThrList thr,
+                                      unsigned long long* hist) {
+  __shared__ unsigned int h[2][65];
+  for (int i = threadIdx.x; i < 2 * 65; i += TPB) (&h[0][0])[i] = 0;
+  __syncthreads();
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) {
+    const double p = pred[i];
+    int lo = 0, hi = nt;            // first t with !(p > thr[t]) (thresholds ascending)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (p > thr.t[mid]) lo = mid + 1; else hi = mid;
+    }
+    atomicAdd(&h[truth[i] > 0.5f ? 1 : 0][lo], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * (nt + 1); i += TPB) {
+    const unsigned int v = h[i / (nt + 1)][i % (nt + 1)];
+    if (v) atomicAdd(hist + i, (unsigned long long)v);
+  }
+}
 }  // namespace
 
 #define DTYPE_SWITCH(dtype, T, ...)                                   \
@@ -494,4 +518,17 @@ extern "C" int adp_pixel_counts(size_t n, const float* pred, const float* truth,
   hipLaunchKernelGGL(pixel_counts_kernel, dim3(nblk(n, 2048)), dim3(TPB), 0, (hipStream_t)st, n, pred, truth, thr,
                      counts);
   return adp::check_launch("adp_pixel_counts");
+}
+
+extern "C" int adp_threshold_hist(size_t n, const float* pred, const float* truth, int nthr, const double* thr,
+                                  unsigned long long* hist, adp_stream_t st) {
+  ADP_REQUIRE(nthr >= 1 && nthr <= 64 && thr && pred && truth && hist, "adp_threshold_hist: 1..64 thresholds");
+  ThrList tl;
+  for (int i = 0; i < nthr; ++i) {
+    ADP_REQUIRE(i == 0 || thr[i] >= thr[i - 1], "adp_threshold_hist: thresholds must be ascending");
+    tl.t[i] = thr[i];
+  }
+  hipLaunchKernelGGL(threshold_hist_kernel, dim3(nblk(n, 2048)), dim3(TPB), 0, (hipStream_t)st, n, pred, truth, nthr,
+                     tl, hist);
+  return adp::check_launch("adp_threshold_hist");
 }

@@ -437,6 +437,15 @@ def pixel_counts(pred, truth, thr, counts):
     call("adp_pixel_counts", pred.numel(), ptr(pred), ptr(truth), float(thr), ptr(counts), stream_ptr())
 
 
+def threshold_hist(pred, truth, thresholds, hist):
+    """hist (int64, 2*(T+1), caller zeroes) (+)= pixel histogram of #{t: pred > t} split by truth > 0.5."""
+    T = len(thresholds)
+    _check(pred.numel() == truth.numel() and pred.dtype == truth.dtype == torch.float32, "threshold_hist inputs")
+    _check(hist.dtype == torch.int64 and hist.numel() >= 2 * (T + 1), "threshold_hist: hist size")
+    arr = (C.c_double * T)(*[float(t) for t in thresholds])
+    call("adp_threshold_hist", pred.numel(), ptr(pred), ptr(truth), T, arr, ptr(hist), stream_ptr())
+
+
 def adam(param, grad, m, v, *, lr, beta1, beta2, eps, step, weight_decay=0.0, grad_scale=1.0):
     n = param.numel()
     _check(grad.numel() == n and m.numel() == n and v.numel() == n, "adam sizes")

@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 3
+#define ADP_ABI_VERSION 4 /* v4: adp_threshold_hist */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -203,6 +203,11 @@ int adp_loss_grad(int N, int H, int W, const float* p, const float* y, int smoot
 /* tp, fp, fn, tn of (pred>thr) vs (true>0.5) (full_evaluation_enhanced.py:721-785), int64 out */
 int adp_pixel_counts(size_t n, const float* pred, const float* truth, float thr,
                      unsigned long long* counts, adp_stream_t s);
+/* Threshold sweep of optimize_threshold_f1(_slide_level) (full_evaluation_enhanced.py:891-980) in one pass:
+ * thr = nthr (<= 64) ascending HOST doubles; hist[b*(nthr+1) + j] (+)= #pixels with truth bit b
+ * (truth > 0.5) and j = #{t : pred > thr[t]}. tp(t) = sum_{j>t} hist[nthr+1+j], fp(t) = sum_{j>t} hist[j]. */
+int adp_threshold_hist(size_t n, const float* pred, const float* truth, int nthr, const double* thr,
+                       unsigned long long* hist, adp_stream_t s);
 
 /* ---- optimizer (Keras Adam / AdamW, :800-806) --------------------------------------------- */
 int adp_adam(size_t n, float* param, const float* grad, float* m, float* v, float lr, float beta1,
