@@ -17,12 +17,12 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libadipose_hip.so")
+LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_hip.so")  # override: A/B timing only
 
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class AdpError(RuntimeError):
@@ -65,6 +65,7 @@ _SIGS = {
     "adp_pack_weights_fp8": [_I, _P, _I, _P, _I, _P, _P],
     "adp_bn_apply_fp8": [_I, _S, _I, _P, _P, _P, _P, _P],
     "adp_maxpool2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _P, _P],
+    "adp_maxpool2_bwd_bnr": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "adp_upsample2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P],
     "adp_ew_add_mask": [_I, _S, _P, _P, _P, _F, _P, _P],
     "adp_cast": [_I, _I, _S, _P, _P, _P],

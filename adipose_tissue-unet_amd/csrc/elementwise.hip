@@ -122,6 +122,89 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, const T* src, con
   }
 }
 
+// unet_bn encoder form of the pool backward, channel-group-stationary (thread -> channel group
+// t % G, pooled-pixel lane t / G): dsrc = route(dpool) + addend, with the BatchNorm-backward
+// reduction of the layer whose activation relu(z*scale+shift) src is fused in (dbeta += sum db,
+// dgamma += sum db*xhat over the STORED dsrc values, db = dsrc * (z*scale+shift > 0)), replacing the
+// separate bn_bwd_reduce pass over (dsrc, z).
+template <typename T>
+__global__ void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src, const T* dpool, const T* addend,
+                                       T* dsrc, const T* z, const float* sc, const float* sh, const float* mean,
+                                       const float* invstd, float* dgamma, float* dbeta) {
+  const int G = C >> 3, lanes = TPB / G;
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  const unsigned Ho = H >> 1, Wo = W >> 1, P = (unsigned)N * Ho * Wo;
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (pl < lanes) {
+    float cs[8], ch[8], mu[8], is[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = g * 8 + j;
+      cs[j] = sc[c]; ch[j] = sh[c]; mu[j] = mean[c]; is[j] = invstd[c];
+    }
+    const size_t off[4] = {0, (size_t)C, (size_t)W * C, (size_t)W * C + C};
+    for (unsigned pix = blockIdx.x * lanes + pl; pix < P; pix += gridDim.x * lanes) {
+      const unsigned xo = pix % Wo, t = pix / Wo, yo = t % Ho, n = t / Ho;
+      const size_t base = (((size_t)n * H + 2 * yo) * W + 2 * xo) * C + g * 8;
+      Grp<T> gv[4], ga[4], gz[4], gp;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) grp_load(gv[q], src + base + off[q]);
+      grp_load(gp, dpool + (size_t)pix * C + g * 8);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) grp_load(ga[q], addend + base + off[q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) grp_load(gz[q], z + base + off[q]);
+      float v[4][8], best[8], dp[8];
+      int arg[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) grp_to_f(gv[q], v[q]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { best[j] = v[0][j]; arg[j] = 0; }
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[q][j] > best[j]) { best[j] = v[q][j]; arg[j] = q; }
+      grp_to_f(gp, dp);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float o[8], ad[8], zz[8];
+        grp_to_f(ga[q], ad);
+        grp_to_f(gz[q], zz);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (arg[j] == q ? dp[j] : 0.f) + ad[j];
+        Grp<T> go;
+        grp_from_f(go, o);
+        grp_store(go, dsrc + base + off[q]);
+        grp_to_f(go, o);   // the reduction sees the stored (rounded) gradient, as bn_bwd_reduce would
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float db = fmaf(zz[j], cs[j], ch[j]) > 0.f ? o[j] : 0.f;
+          s1[j] += db;
+          s2[j] += db * (zz[j] - mu[j]) * is[j];
+        }
+      }
+    }
+  }
+  __shared__ float red[2][TPB * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x * 8 + j] = s1[j];
+    red[1][threadIdx.x * 8 + j] = s2[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += TPB) {
+    const int gg = c >> 3, j = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      a += red[0][(l * G + gg) * 8 + j];
+      b += red[1][(l * G + gg) * 8 + j];
+    }
+    atomicAdd(dbeta + c, a);
+    atomicAdd(dgamma + c, b);
+  }
+}
+
 template <typename T>
 __global__ void upsample_bwd_kernel(int N, int Hs, int Ws, int C, const T* dup, const T* addend,
                                     const T* mask, float mscale, T* dsrc) {
@@ -259,49 +342,116 @@ __global__ void bn_bwd_reduce_kernel(size_t M, int C, const T* dA, const T* z, c
   }
 }
 
-template <typename T>
+// Channel-group-stationary BatchNorm elementwise passes: thread t of a block owns channel group
+// g = t % G for its whole life and pixel lane t / G (TPB / G pixels per block row; G | TPB for every
+// C <= 2048 that is a power-of-two multiple of 8, otherwise the remainder threads idle), so its
+// per-channel coefficients sit in registers and the loop does no integer division. Two pixels per
+// iteration (all loads before any store: safe in place); U pixels per thread per iteration.
+//   dz = k*db + Q*(z - mean) + R,  k = gamma*invstd, Q = -k*invstd*dgamma/count, R = -k*dbeta/count,
+//   db = dA * (z*scale + shift > 0)            (= gamma*invstd*(db - dbeta/n - xhat*dgamma/n))
+template <typename T, int U>
 __global__ void bn_bwd_apply_kernel(size_t M, int C, const T* dA, const T* z, const float* sc,
                                     const float* sh, const float* mean, const float* invstd,
                                     const float* gamma, const float* dgamma, const float* dbeta,
                                     float inv_count, T* dz) {
-  const int G = C >> 3;
-  size_t total = M * G;
-  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
-    int g = (int)(i % G);
-    Grp<T> gr;
+  const int G = C >> 3, lanes = TPB / G;
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  if (pl >= lanes) return;
+  float s[8], h[8], mu[8], P[8], Q[8], R[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = g * 8 + j;
+    const float k = gamma[c] * invstd[c];
+    s[j] = sc[c]; h[j] = sh[c]; mu[j] = mean[c];
+    P[j] = k;
+    Q[j] = -k * invstd[c] * dgamma[c] * inv_count;
+    R[j] = -k * dbeta[c] * inv_count;
+  }
+  auto one = [&](const Grp<T>& gd, const Grp<T>& gz, Grp<T>& go) {
     float d[8], zz[8], o[8];
-    grp_load(gr, dA + i * 8); grp_to_f(gr, d);
-    grp_load(gr, z + i * 8); grp_to_f(gr, zz);
+    grp_to_f(gd, d);
+    grp_to_f(gz, zz);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      int c = g * 8 + j;
-      float a = fmaf(zz[j], sc[c], sh[c]);
-      float db = a > 0.f ? d[j] : 0.f;
-      float xh = (zz[j] - mean[c]) * invstd[c];
-      o[j] = gamma[c] * invstd[c] * (db - dbeta[c] * inv_count - xh * dgamma[c] * inv_count);
+      const float db = fmaf(zz[j], s[j], h[j]) > 0.f ? d[j] : 0.f;
+      o[j] = fmaf(P[j], db, fmaf(Q[j], zz[j] - mu[j], R[j]));
     }
-    grp_from_f(gr, o);
-    grp_store(gr, dz + i * 8);
+    grp_from_f(go, o);
+  };
+  const size_t step = (size_t)gridDim.x * lanes;
+  size_t m = (size_t)blockIdx.x * lanes + pl;
+  for (; m + (U - 1) * step < M; m += U * step) {
+    Grp<T> d[U], zz[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      grp_load(d[u], dA + (m + u * step) * C + g * 8);
+      grp_load(zz[u], z + (m + u * step) * C + g * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(d[u], zz[u], r[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) grp_store(r[u], dz + (m + u * step) * C + g * 8);
+  }
+  for (; m < M; m += step) {
+    const size_t o0 = m * C + g * 8;
+    Grp<T> d0, z0, r0;
+    grp_load(d0, dA + o0); grp_load(z0, z + o0);
+    one(d0, z0, r0);
+    grp_store(r0, dz + o0);
   }
 }
 
 // a = relu(z*scale + shift): materialised post-BN activation (lets every consumer use LDS-DMA loads)
-template <typename T>
+template <typename T, int U>
 __global__ void bn_apply_kernel(size_t M, int C, const T* z, const float* sc, const float* sh, T* out) {
-  const int G = C >> 3;
-  size_t total = M * G;
-  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
-    const int g = (int)(i % G);
-    Grp<T> gr;
+  const int G = C >> 3, lanes = TPB / G;
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  if (pl >= lanes) return;
+  float s[8], h[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = sc[g * 8 + j]; h[j] = sh[g * 8 + j]; }
+  auto one = [&](Grp<T>& gr) {
     float f[8];
-    grp_load(gr, z + i * 8);
     grp_to_f(gr, f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[g * 8 + j], sh[g * 8 + j]), 0.f);
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], s[j], h[j]), 0.f);
     grp_from_f(gr, f);
-    grp_store(gr, out + i * 8);
+  };
+  const size_t step = (size_t)gridDim.x * lanes;
+  size_t m = (size_t)blockIdx.x * lanes + pl;
+  for (; m + (U - 1) * step < M; m += U * step) {
+    Grp<T> a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) grp_load(a[u], z + (m + u * step) * C + g * 8);
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(a[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) grp_store(a[u], out + (m + u * step) * C + g * 8);
+  }
+  for (; m < M; m += step) {
+    const size_t o0 = m * C + g * 8;
+    Grp<T> a0;
+    grp_load(a0, z + o0);
+    one(a0);
+    grp_store(a0, out + o0);
   }
 }
+
+// blocks for a channel-group-stationary launch over M pixels, U pixels per thread per iteration
+// (grid caps and unrolls measured with tools/bench_ew.py at the unet_bn level shapes: bn_apply
+// U = 1 / 64K blocks 5.8-6.0 TB/s at 1024^2x64, bn_bwd_apply U = 2 / 32K blocks 5.6 TB/s)
+inline int bn_blocks(size_t M, int C, int U, int cap) {
+  const int lanes = TPB / (C / 8);
+  const size_t b = (M + (size_t)U * lanes - 1) / ((size_t)U * lanes);
+  return (int)std::max<size_t>(1, std::min<size_t>(b, (size_t)adp::option("bn_cap", cap)));
+}
+#define BN_UNROLL_SWITCH(U, dflt, ...)                \
+  do {                                                \
+    const int u_ = adp::option("bn_unroll", dflt);    \
+    if (u_ == 4) { constexpr int U = 4; __VA_ARGS__; } \
+    else if (u_ == 1) { constexpr int U = 1; __VA_ARGS__; } \
+    else { constexpr int U = 2; __VA_ARGS__; }        \
+  } while (0)
 
 // ---------------------------------------------------------------------------- fp8 inference path
 // per-row (output channel) e4m3 quantisation of the forward weight layout: one block per row
@@ -446,6 +596,25 @@ extern "C" int adp_maxpool2_bwd(int dtype, int N, int H, int W, int C, const voi
   return adp::check_launch("adp_maxpool2_bwd");
 }
 
+extern "C" int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C, const void* src, const void* dpool,
+                                    const void* addend, void* dsrc, const void* z, const float* sc, const float* sh,
+                                    const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                                    adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && H % 2 == 0 && W % 2 == 0 && src && dpool && addend && dsrc && z && sc &&
+                  sh && mean && invstd && dgamma && dbeta,
+              "adp_maxpool2_bwd_bnr: need C%8==0, C<=2048, even H,W and every operand");
+  ADP_REQUIRE((size_t)N * (H / 2) * (W / 2) < (1ull << 31), "adp_maxpool2_bwd_bnr: too many pooled pixels");
+  const int lanes = TPB / (C / 8);
+  const size_t P = (size_t)N * (H / 2) * (W / 2);
+  const int blocks = (int)std::max<size_t>(1, std::min<size_t>((P + lanes - 1) / lanes,
+                                                               (size_t)adp::option("pool_bnr_blocks", 2048)));
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(maxpool_bwd_bnr_kernel<T>, dim3(blocks), dim3(TPB), 0, (hipStream_t)st, N, H, W, C,
+                                  (const T*)src, (const T*)dpool, (const T*)addend, (T*)dsrc, (const T*)z, sc, sh,
+                                  mean, invstd, dgamma, dbeta));
+  return adp::check_launch("adp_maxpool2_bwd_bnr");
+}
+
 extern "C" int adp_upsample2_bwd(int dtype, int N, int Hs, int Ws, int C, const void* dup,
                                  const void* addend, const void* mask, float ms, void* dsrc,
                                  adp_stream_t st) {
@@ -511,22 +680,20 @@ extern "C" int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, cons
                                 const float* sh, const float* mean, const float* invstd, const float* gamma,
                                 const float* dgamma, const float* dbeta, float count, void* dz,
                                 adp_stream_t st) {
-  ADP_REQUIRE(C % 8 == 0 && count > 0, "adp_bn_bwd_apply: bad arguments");
-  size_t n = M * (C / 8);
-  DTYPE_SWITCH(dtype, T,
-               hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, M, C,
-                                  (const T*)dA, (const T*)z, sc, sh, mean, invstd, gamma, dgamma, dbeta,
-                                  1.f / count, (T*)dz));
+  ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && count > 0, "adp_bn_bwd_apply: bad arguments (C % 8 == 0, C <= 2048)");
+  BN_UNROLL_SWITCH(U, 2, DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL((bn_bwd_apply_kernel<T, U>), dim3(bn_blocks(M, C, U, 32768)), dim3(TPB), 0, (hipStream_t)st,
+                                  M, C, (const T*)dA, (const T*)z, sc, sh, mean, invstd, gamma, dgamma, dbeta,
+                                  1.f / count, (T*)dz)));
   return adp::check_launch("adp_bn_bwd_apply");
 }
 
 extern "C" int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* sc, const float* sh, void* out,
                             adp_stream_t st) {
-  ADP_REQUIRE(C % 8 == 0 && sc && sh, "adp_bn_apply: bad arguments");
-  size_t n = M * (C / 8);
-  DTYPE_SWITCH(dtype, T,
-               hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, M, C,
-                                  (const T*)z, sc, sh, (T*)out));
+  ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && sc && sh, "adp_bn_apply: bad arguments (C % 8 == 0, C <= 2048)");
+  BN_UNROLL_SWITCH(U, 1, DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL((bn_apply_kernel<T, U>), dim3(bn_blocks(M, C, U, 65536)), dim3(TPB), 0, (hipStream_t)st, M,
+                                  C, (const T*)z, sc, sh, (T*)out)));
   return adp::check_launch("adp_bn_apply");
 }
 

@@ -894,11 +894,13 @@ class UNetBN(UNetEngine):
             if i < Lv - 1:
                 # dA of enc{i}_conv2 = concat-skip part + pool backward (argmax on the activation)
                 dA2 = gb(f"dA_z{i}_2", z2)
-                ops.maxpool2_bwd(a[f"az{i}_2"], dpool, dA2, addend=skip_grad[i])
+                # pool backward + skip gradient, with enc{i}_conv2's BN-backward reduction fused in
+                ops.maxpool2_bwd(a[f"az{i}_2"], dpool, dA2, addend=skip_grad[i],
+                                 bn_reduce=self._bn_red(f"enc{i}_conv2", z2))
             else:
                 dA2 = bott_dA
             dz2 = gb(f"dz_z{i}_2", z2)
-            self._bn_bwd(f"enc{i}_conv2", dA2, z2, dz2, reduced=i == Lv - 1)
+            self._bn_bwd(f"enc{i}_conv2", dA2, z2, dz2, reduced=True)
             l2 = L[f"enc{i}_conv2"]
             self.wgrad(l2, a[f"az{i}_1"], dz2)
             dA1 = gb(f"dA_z{i}_1", z1)

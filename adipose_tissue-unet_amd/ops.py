@@ -302,13 +302,22 @@ def maxpool2_fwd(src, dst, bn=None):
     return dst
 
 
-def maxpool2_bwd(src, dpool, dsrc, *, bn=None, addend=None, mask=None, mask_scale=1.0):
+def maxpool2_bwd(src, dpool, dsrc, *, bn=None, addend=None, mask=None, mask_scale=1.0, bn_reduce=None):
+    """bn_reduce=(z, scale, shift, mean, invstd, dgamma, dbeta): fused BatchNorm-backward reduction of
+    the layer whose activation src is (adp_maxpool2_bwd_bnr; needs addend, no bn/mask)."""
     _act(src, "src")
     N, H, W, Cs = src.shape
     _check(tuple(dpool.shape) == (N, H // 2, W // 2, Cs), "dpool shape")
     _check(dsrc.shape == src.shape, "dsrc shape")
     for t in (addend, mask):
         _check(t is None or t.shape == src.shape, "addend/mask shape")
+    if bn_reduce is not None:
+        z, sc, sh, mean, inv, dg, db = bn_reduce
+        _check(bn is None and mask is None and addend is not None and z.shape == src.shape and z.dtype == src.dtype,
+               "maxpool2_bwd bn_reduce: needs addend, z like src, no bn/mask")
+        call("adp_maxpool2_bwd_bnr", dtype_code(src), N, H, W, Cs, ptr(src), ptr(dpool), ptr(addend), ptr(dsrc),
+             ptr(z), ptr(sc), ptr(sh), ptr(mean), ptr(inv), ptr(dg), ptr(db), stream_ptr())
+        return dsrc
     call("adp_maxpool2_bwd", dtype_code(src), N, H, W, Cs, ptr(src), ptr(bn[0]) if bn else None,
          ptr(bn[1]) if bn else None, ptr(dpool), ptr(addend), ptr(mask), float(mask_scale), ptr(dsrc), stream_ptr())
     return dsrc

@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 4 /* v4: adp_threshold_hist */
+#define ADP_ABI_VERSION 5 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -132,6 +132,13 @@ int adp_maxpool2_bwd(int dtype, int N, int H, int W, int C_stride, const void* s
                      const float* bn_scale, const float* bn_shift, const void* dpool,
                      const void* addend, const void* mask, float mask_scale, void* dsrc,
                      adp_stream_t s);
+/* unet_bn encoder pool backward: dsrc = route_argmax(dpool) + addend (no BN-on-load, no mask), with the
+ * BatchNorm-backward reduction of the layer whose activation src = relu(z*scale+shift) fused in:
+ * dbeta += sum db, dgamma += sum db*(z-mean)*invstd, db = dsrc*(z*scale+shift > 0) over the stored dsrc
+ * (replaces adp_maxpool2_bwd + adp_bn_bwd_reduce; train_adipose_unet_v3.py:670 MaxPooling2D grad) */
+int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C_stride, const void* src, const void* dpool,
+                         const void* addend, void* dsrc, const void* z, const float* scale, const float* shift,
+                         const float* mean, const float* invstd, float* dgamma, float* dbeta, adp_stream_t s);
 int adp_upsample2_bwd(int dtype, int N, int Hs, int Ws, int C_stride, const void* dup,
                       const void* addend, const void* mask, float mask_scale, void* dsrc,
                       adp_stream_t s);

@@ -292,6 +292,37 @@ def test_pool_upsample(dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("C", [64, 128, 1024, 48])
+def test_pool_bwd_fused_bn_reduce(dt, C):
+    """adp_maxpool2_bwd_bnr == adp_maxpool2_bwd(addend) followed by adp_bn_bwd_reduce: identical dsrc,
+    dgamma/dbeta equal up to f32 summation order (and to the CPU oracle of the BN-backward sums)."""
+    g = torch.Generator().manual_seed(C)
+    N, H = 2, 12
+    z = rb(torch.randn(N, H, H, C, generator=g), dt).to(DEV, dt).contiguous()
+    sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    mu = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    ist = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    a = torch.zeros_like(z)
+    ops.bn_apply(z, sc, sh, a)
+    dp = rb(torch.randn(N, H // 2, H // 2, C, generator=g), dt).to(DEV, dt).contiguous()
+    add = rb(torch.randn(N, H, H, C, generator=g), dt).to(DEV, dt).contiguous()
+    d1, d2 = torch.zeros_like(z), torch.zeros_like(z)
+    dg1, db1, dg2, db2 = (torch.zeros(C, device=DEV) for _ in range(4))
+    ops.maxpool2_bwd(a, dp, d1, addend=add)
+    ops.bn_bwd_reduce(d1, z, sc, sh, mu, ist, dg1, db1)
+    ops.maxpool2_bwd(a, dp, d2, addend=add, bn_reduce=(z, sc, sh, mu, ist, dg2, db2))
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
+    zf, df = z.float().cpu(), d1.float().cpu()
+    db = torch.where(zf * sc.cpu() + sh.cpu() > 0, df, torch.zeros_like(df))
+    ref_b = db.sum((0, 1, 2))
+    ref_g = (db * (zf - mu.cpu()) * ist.cpu()).sum((0, 1, 2))
+    for got, ref in ((db2, ref_b), (dg2, ref_g), (db1, ref_b), (dg1, ref_g)):
+        assert (got.cpu() - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("softmax2", [True, False])
 def test_heads(dt, softmax2):
     g = torch.Generator().manual_seed(11)
