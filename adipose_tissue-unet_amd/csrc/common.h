@@ -109,6 +109,17 @@ int check_launch(const char* what);
 int option(const char* name, int dflt);  // runtime switches set through adp_set_option
 // name of the kernel the last conv launch of this thread used (adp_last_kernel), printf-style
 void set_kernel(const char* fmt, ...);
+// Replicated per-channel accumulators for the BatchNorm sums (statistics of a conv output, or the
+// BN-backward dbeta/dgamma reductions). f32 atomics execute at the memory side and serialise per
+// address, so thousands of blocks adding into the same C floats queue behind each other (measured:
+// ~17 ns per add per address, 1.75 ms per training step); blocks add into replica (block & 63)
+// instead and stat_fold() sums the replicas into the caller's accumulators and re-zeroes them.
+// Per device, lazily allocated and zeroed; launches that use it must be ordered on one stream.
+constexpr int STAT_REPL = 64, STAT_CMAX = 2048;
+float* stat_scratch();   // [STAT_REPL][2][STAT_CMAX] f32, or nullptr (error set) if allocation failed
+// per-device growable scratch (slot 0: weight-gradient split partials); growing synchronises the device
+void* scratch(int slot, size_t bytes);
+int stat_fold(int C, float* dst0, float* dst1, hipStream_t s);   // elementwise.hip
 }  // namespace adp
 #define ADP_REQUIRE(cond, msg)          \
   do {                                  \

@@ -38,6 +38,8 @@ struct FwdArgs {
   int f8;
   const float* wscale;
   int out_f8;
+  int debug_flags;       // timing-only ablations (option "fwd_debug"): bit1 skips the BN-statistics atomics
+  float* stat;           // BatchNorm accumulator replicas (adp::stat_scratch) for bn_sum / bnr_* launches
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
@@ -52,6 +54,8 @@ struct WgradArgs {
   float* dB;            // [Nout] f32 or null
   int M, mchunk, ntile_k, ntile_n;
   int debug_flags;      // timing-only ablations (tools/bench_kernels.py): bit0 skips the dW atomics
+  float* part;          // tap64: per-split partial dW slabs [split][Nout][Kpad] (plain stores), reduced
+                        // into dW by a second launch; nullptr -> f32 atomics into dW
 };
 
 namespace {
@@ -280,6 +284,7 @@ template <int NTH, int BN>
 ADP_DEV void epi_bn_flush(const FwdArgs& a, float* red, int n0, int tid, const float (&bs)[8],
                           const float (&bq)[8]) {
   constexpr int GPR = BN / 8;
+  if (a.debug_flags & 2) return;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = bs[j]; red[tid * 16 + 8 + j] = bq[j]; }
@@ -291,8 +296,11 @@ ADP_DEV void epi_bn_flush(const FwdArgs& a, float* red, int n0, int tid, const f
     const int nn = n0 + tid;
     if (nn < a.Nout) {
       const int c = a.out_mode == 1 ? nn % a.Cps : nn;
-      atomicAdd((a.bnr_z ? a.bnr_dbeta : a.bn_sum) + c, s);
-      atomicAdd((a.bnr_z ? a.bnr_dgamma : a.bn_sq) + c, q);
+      // replica of this block (folded into bn_sum/bn_sq or bnr_dbeta/bnr_dgamma by the launcher)
+      const unsigned blk = blockIdx.x + blockIdx.y * gridDim.x;
+      float* rep = a.stat + (size_t)(blk & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+      atomicAdd(rep + c, s);
+      atomicAdd(rep + adp::STAT_CMAX + c, q);
     }
   }
 }
@@ -305,6 +313,7 @@ namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s);
 // conv_fwd_halo.hip: halo-reuse 3x3 kernel for narrow (<= 128 output channels) stride-1 layers.
 int launch_fwd_halo(FwdArgs& a, hipStream_t s);
+int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
 }

@@ -1,0 +1,152 @@
+// Input-layer forward convolution ("cin8"): one 8-channel source group (the network input, channel
+// stride 8: 3 RGB or 1 gray channel + zero pad), K = taps * 8 <= 96, N <= 64 output channels.
+// unet_bn enc0_conv1 (3 -> 64) and adipose_v3 down1_conv1 (1 -> 44, train_adipose_unet_v3.py:668).
+//
+// The layer is HBM-bound on its 64-channel output (AI ~ 9 FLOP/B), so it needs no LDS staging: the
+// whole weight matrix lives in registers as MFMA A fragments (W[co][k], 16 output channels x 32 k per
+// fragment) and each lane loads its B fragment — the 8 channels of one tap of one output pixel, one
+// 16-B load — straight from global memory (the 3x3 neighbourhood re-reads hit L1/L2). The product is
+// C^T = W X^T: lane l holds 4 consecutive output channels 4(l>>4)+i (+16 mb) of pixel l & 15, stored
+// as one 8-B vector per 16-channel block. BatchNorm statistics of the stored values are kept per lane
+// and reduced once per wave (shuffles over the 16 lanes of a channel quad, one atomic per channel into
+// the wave's replica of the BatchNorm accumulators, adp::stat_scratch).
+#include "conv_common.h"
+
+namespace {
+
+template <int KS, int UNR>
+__global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r16 = lane & 15, h4 = lane >> 4;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+  const bf16* W = reinterpret_cast<const bf16*>(a.W);
+  const bf16* src = reinterpret_cast<const bf16*>(a.srcA);
+  bf16* out = reinterpret_cast<bf16*>(a.out);
+
+  bf16x8 wf[4][KS];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[mb][ks] = *reinterpret_cast<const bf16x8*>(W + (size_t)(16 * mb + r16) * a.Kpad + 32 * ks + 8 * h4);
+  const int ntaps = a.kh * a.kw;
+  int toy[KS], tox[KS];
+  bool tval[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int t = 4 * ks + h4;
+    tval[ks] = t < ntaps;
+    const int ty = t / a.kw, tx = t - ty * a.kw;
+    toy[ks] = ty * a.dil - a.pad;
+    tox[ks] = tx * a.dil - a.pad;
+  }
+  float bias[4][4], s1[4][4], s2[4][4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = 16 * mb + 4 * h4 + i;
+      bias[mb][i] = (a.bias && co < a.Nout) ? a.bias[co] : 0.f;
+      s1[mb][i] = 0.f;
+      s2[mb][i] = 0.f;
+    }
+  const int HWo = a.Ho * a.Wo;
+  const int groups = (a.M + 15) / 16;
+  const bf16x8 zero = {};
+  for (int g0 = wave * UNR; g0 < groups; g0 += nwaves * UNR) {
+    bf16x8 xb[UNR][KS];
+    int mm[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int m = (g0 + u) * 16 + r16;
+      mm[u] = m;
+      const bool mv = g0 + u < groups && m < a.M;
+      const int mc = mv ? m : 0;
+      const int n = mc / HWo, rem = mc - n * HWo, y = rem / a.Wo, x = rem - y * a.Wo;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int yi = y + toy[ks], xi = x + tox[ks];
+        const bool ok = mv && tval[ks] && (unsigned)yi < (unsigned)a.Hs && (unsigned)xi < (unsigned)a.Ws;
+        xb[u][ks] = ok ? *reinterpret_cast<const bf16x8*>(src + ((size_t)(n * a.Hs + yi) * a.Ws + xi) * 8) : zero;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mb][ks], xb[u][ks], acc[mb], 0, 0, 0);
+      const int m = mm[u];
+      if (g0 + u >= groups || m >= a.M) continue;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int co0 = 16 * mb + 4 * h4;
+        if (co0 >= a.Nout) continue;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[mb][i] + bias[mb][i];
+          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          s1[mb][i] += v[i];
+          s2[mb][i] += v[i] * v[i];
+        }
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)v[i];
+        *reinterpret_cast<bf16x4*>(out + (size_t)m * a.out_stride + co0) = o;
+      }
+    }
+  }
+  if (!a.bn_sum || (a.debug_flags & 2)) return;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = s1[mb][i], y = s2[mb][i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+      }
+      const int co = 16 * mb + 4 * h4 + i;
+      if (r16 == 0 && co < a.Nout) {   // this wave's replica; the launcher folds them into bn_sum / bn_sq
+        float* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+        atomicAdd(rep + co, x);
+        atomicAdd(rep + adp::STAT_CMAX + co, y);
+      }
+    }
+}
+
+template <int KS>
+void launch_cin8(FwdArgs& a, hipStream_t s) {
+  constexpr int UNR = 2;
+  const int groups = (a.M + 15) / 16;
+  const int waves = std::max(1, std::min((groups + UNR - 1) / UNR, adp::option("cin8_waves", 4096)));
+  adp::set_kernel("igemm_fwd_cin8_kernel<%d, %d>", KS, UNR);
+  hipLaunchKernelGGL((igemm_fwd_cin8_kernel<KS, UNR>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+}
+
+}  // namespace
+
+namespace adp {
+// bf16 forward of an input layer: one 8-channel source, K = taps*8 <= 96, Nout <= 64 (weights packed
+// [round_up(Nout, 64)][Kpad]), plain store with bias / ReLU / BN statistics.
+int launch_fwd_cin8(FwdArgs& a, hipStream_t s) {
+  if (option("fwd_cin8", 1) == 0) return 0;
+  const int taps = a.kh * a.kw;
+  if (a.CAs != 8 || a.CBs != 0 || a.scA || a.up != 1 || a.stride != 1 || taps > 12 || a.K != taps * 8 ||
+      a.Kpad < (a.K + 31) / 32 * 32 || a.Nout > 64 || a.Nout % 8 != 0 || a.out_mode != 0 || !a.out ||
+      a.out_stride % 4 != 0 || a.addend || a.mask || a.accum || a.drop_rate > 0.f || a.bnr_z)
+    return 0;
+  const int ks = (a.K + 31) / 32;
+  if (ks == 1) launch_cin8<1>(a, s);
+  else if (ks == 2) launch_cin8<2>(a, s);
+  else launch_cin8<3>(a, s);
+  return 1;
+}
+}  // namespace adp

@@ -1032,6 +1032,17 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
   a.bnr_sc = io->bnr_scale; a.bnr_sh = io->bnr_shift; a.bnr_mean = io->bnr_mean; a.bnr_invstd = io->bnr_invstd;
   a.bnr_dgamma = io->bnr_dgamma; a.bnr_dbeta = io->bnr_dbeta;
   a.M = d->N * d->Ho * d->Wo;
+  a.debug_flags = adp::option("fwd_debug", 0);
+  a.stat = (a.bn_sum || a.bnr_z) ? adp::stat_scratch() : nullptr;
+}
+
+// after a launch whose epilogue added BatchNorm sums into the replicas: fold them into the caller's
+// accumulators (statistics: bn_sum / bn_sq; BN-backward reduction: bnr_dbeta / bnr_dgamma)
+int fold_stats(const FwdArgs& a, hipStream_t s) {
+  if (!a.stat) return 0;
+  const int C = a.out_mode == 1 ? a.Cps : a.Nout;
+  if (a.bnr_z) return adp::stat_fold(C, a.bnr_dbeta, a.bnr_dgamma, s);
+  return adp::stat_fold(C, a.bn_sum, a.bn_sq, s);
 }
 
 // fp8 e4m3 forward launch (BASELINE configs[4]): tap64 kernel only, no fallback
@@ -1067,15 +1078,25 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
                            a.bnr_dgamma && a.bnr_dbeta && a.bnr_zs == a.out_stride && a.bnr_zs % 8 == 0 &&
                            a.Nout % 8 == 0),
               "adp_conv_fwd: fused BN-backward reduction needs out_mode 0, all bnr_* pointers, z stride == out stride");
+  ADP_REQUIRE(!(a.bn_sum || a.bnr_z) || a.stat, "adp_conv_fwd: BatchNorm accumulator replicas unavailable");
+  ADP_REQUIRE(!a.stat || (d->out_mode == 1 ? d->shuffle_c : d->Nout) <= adp::STAT_CMAX,
+              "adp_conv_fwd: BatchNorm sums need <= 2048 channels");
   const int fast = adp::option("conv_fast", 2);
   if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB &&
-      (adp::launch_fwd_halo(a, s) || adp::launch_fwd_tap64(a, s)))
-    return adp::check_launch("adp_conv_fwd");
+      (adp::launch_fwd_cin8(a, s) || adp::launch_fwd_halo(a, s) || adp::launch_fwd_tap64(a, s))) {
+    if (adp::check_launch("adp_conv_fwd")) return -2;
+    return fold_stats(a, s);
+  }
   // every other kernel: plain launch, then the standalone BN-backward reduction on the stored output
   const FwdArgs bnr = a;
   a.bnr_z = nullptr;
+  if (!a.bn_sum) a.stat = nullptr;
   const int rc = launch_fwd_plain<T>(a, s, fast);
-  if (rc != 0 || !bnr.bnr_z) return rc;
+  if (rc != 0) return rc;
+  // kernels with the LDS-staged epilogue added their statistics into the replicas (the register-staged
+  // generic kernels add into bn_sum directly and leave the replicas zero)
+  if (a.stat && fold_stats(a, s) != 0) return -2;
+  if (!bnr.bnr_z) return 0;
   return adp_bn_bwd_reduce(std::is_same<T, bf16>::value ? ADP_BF16 : ADP_F32, (size_t)bnr.M, bnr.out_stride, bnr.out,
                            bnr.bnr_z, bnr.bnr_sc, bnr.bnr_sh, bnr.bnr_mean, bnr.bnr_invstd, bnr.bnr_dgamma,
                            bnr.bnr_dbeta, (adp_stream_t)s);

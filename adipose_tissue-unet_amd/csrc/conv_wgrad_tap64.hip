@@ -347,19 +347,66 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
       for (int kb = 0; kb < 4; ++kb) asm volatile("" ::"v"(acc[nb][kb]));
     return;
   }
+  // Output: each wave's 16-row blocks are re-shaped through LDS so that every store / atomic covers one
+  // whole 256-B row of dW (64 consecutive k). With several pixel splits the partial sums go to a
+  // per-split slab by plain stores and a second launch sums the slabs into dW: f32 atomics execute at
+  // the memory side at ~1.3 TB/s chip-wide, and the split partials of a step add up to ~2 GB (measured
+  // 1.7 ms of atomics per training step). The loop above ended on a barrier: the staging buffers are free.
+  constexpr int ES = 68;   // padded row stride (floats) of a wave's 16 x 64 block
+  float* blk = reinterpret_cast<float*>(smem) + wave * 16 * ES;
+  const int kk = k0 + wk * 64 + lane;
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb)
+  for (int nb = 0; nb < NB; ++nb) {
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * TNW + nb * 16 + rq + r;
-        const int kk = k0 + wk * 64 + kb * 16 + col;
-        if (n < a.Nout && kk < a.K) atomicAdd(a.dW + (size_t)n * a.Kpad + kk, acc[nb][kb][r]);
+      for (int r = 0; r < 4; ++r) blk[(rq + r) * ES + kb * 16 + col] = acc[nb][kb][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (a.part) {   // this split's partial slab: plain 256-B row stores, reduced by wgrad_reduce_kernel
+      float* slab = a.part + (size_t)split * a.Nout * a.Kpad;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int n = n0 + wn * TNW + nb * 16 + i;
+        const float v = blk[i * ES + lane];
+        if (n < a.Nout && kk < a.K) slab[(size_t)n * a.Kpad + kk] = v;
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int n = n0 + wn * TNW + nb * 16 + i;
+        const float v = blk[i * ES + lane];
+        if (n < a.Nout && kk < a.K) atomicAdd(a.dW + (size_t)n * a.Kpad + kk, v);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
 }
 
 #undef W64_BAR
+
+// dW[n][k] += sum over the splits of part[split][n][k] (n < Nout, k < K = Kpad), 4 floats per thread.
+// blockIdx.y = group of SG consecutive splits: one group adds with a plain read-modify-write, several
+// groups add their group sums with f32 atomics (SG x fewer atomic bytes than the per-block epilogue).
+constexpr int WG_SG = 32;
+__global__ void wgrad_reduce_kernel(int splits, size_t slab, const float4* part, float4* dW) {
+  const size_t n4 = slab / 4;
+  const int s0 = blockIdx.y * WG_SG, s1 = min(splits, s0 + WG_SG);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 acc = part[(size_t)s0 * n4 + i];
+    for (int s = s0 + 1; s < s1; ++s) {
+      const float4 v = part[(size_t)s * n4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if (gridDim.y == 1) {
+      float4 d = dW[i];
+      d.x += acc.x; d.y += acc.y; d.z += acc.z; d.w += acc.w;
+      dW[i] = d;
+    } else {
+      float* d = reinterpret_cast<float*>(dW + i);
+      atomicAdd(d, acc.x); atomicAdd(d + 1, acc.y); atomicAdd(d + 2, acc.z); atomicAdd(d + 3, acc.w);
+    }
+  }
+}
 
 // Pixel splits: enough blocks to fill the chip (target_blocks), but every split keeps at least
 // min_chunk pixels so that the f32 atomic epilogue (blocks x TN x TK x 4 bytes at ~1.3 TB/s) stays
@@ -379,12 +426,26 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   a.debug_flags = adp::option("wgrad_debug", 0);
   const bool two = adp::option("tap64_bar", 1) == 2;
   const dim3 grid(tiles * splits), block(WN * WK * 64);
+  // split partials: slabs + reduce launch instead of f32 atomics (Kpad == K for every tap64 launch)
+  a.part = nullptr;
+  const size_t slab = (size_t)a.Nout * a.Kpad;
+  // (measured per layer, tools/bench_kernels.py: slabs win 7-14 % on the 256x256 tiles of the >= 256-channel
+  // layers, atomics win 4-6 % on the narrow-N tiles, whose slabs are small but split ~1000 ways)
+  if (splits > 1 && adp::option("wgrad_partials", TN >= 256 ? 1 : 0) && !(a.debug_flags & 1))
+    a.part = static_cast<float*>(adp::scratch(0, slab * splits * sizeof(float)));
   adp::set_kernel("igemm_wgrad_tap64_kernel<%d, %d, %d, %s, %s>", WN, WK, TNW, two ? "true" : "false",
                   ra ? "true" : "false");
   if (ra && !two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, true>), grid, block, 0, s, a);
   else if (ra) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, true>), grid, block, 0, s, a);
   else if (!two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, false>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, false>), grid, block, 0, s, a);
+  if (a.part) {
+    const size_t n4 = slab / 4;
+    const int groups = (splits + WG_SG - 1) / WG_SG;
+    const int blocks = (int)std::min<size_t>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks, groups), dim3(256), 0, s, splits, slab,
+                       reinterpret_cast<const float4*>(a.part), reinterpret_cast<float4*>(a.dW));
+  }
 }
 
 }  // namespace

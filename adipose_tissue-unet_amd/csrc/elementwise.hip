@@ -7,6 +7,8 @@
 //   EMACallback update (ema = d*ema+(1-d)w) :455-459
 #include "common.h"
 #include "../../include/adipose_hip.h"
+#include <map>
+#include <mutex>
 
 namespace {
 
@@ -14,6 +16,11 @@ constexpr int TPB = 256;
 inline int nblk(size_t n, int cap = 8192) {
   size_t b = (n + TPB - 1) / TPB;
   return (int)(b < (size_t)cap ? (b ? b : 1) : cap);
+}
+
+// replica of this block in the BatchNorm accumulator scratch (see adp::stat_scratch)
+ADP_DEV float* stat_replica(float* scratch, unsigned block) {
+  return scratch + (size_t)(block & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
 }
 
 // ------------------------------------------------------------------------------ repacking
@@ -130,7 +137,7 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, const T* src, con
 template <typename T>
 __global__ void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src, const T* dpool, const T* addend,
                                        T* dsrc, const T* z, const float* sc, const float* sh, const float* mean,
-                                       const float* invstd, float* dgamma, float* dbeta) {
+                                       const float* invstd, float* stat) {
   const int G = C >> 3, lanes = TPB / G;
   const int g = threadIdx.x % G, pl = threadIdx.x / G;
   const unsigned Ho = H >> 1, Wo = W >> 1, P = (unsigned)N * Ho * Wo;
@@ -200,8 +207,9 @@ __global__ void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src,
       a += red[0][(l * G + gg) * 8 + j];
       b += red[1][(l * G + gg) * 8 + j];
     }
-    atomicAdd(dbeta + c, a);
-    atomicAdd(dgamma + c, b);
+    float* rep = stat_replica(stat, blockIdx.x);
+    atomicAdd(rep + c, a);                   // folded into dbeta / dgamma by stat_fold_kernel
+    atomicAdd(rep + adp::STAT_CMAX + c, b);
   }
 }
 
@@ -297,11 +305,27 @@ __global__ void bn_finalize_kernel(int C, float count, const float* sum, const f
   }
 }
 
+// dst{0,1}[c] += sum over the replicas of scratch[r][{0,1}][c]; the replicas are re-zeroed
+__global__ void stat_fold_kernel(int C, float* scratch, float* dst0, float* dst1) {
+  const int c = blockIdx.x * TPB + threadIdx.x;
+  if (c >= C) return;
+  float s0 = 0.f, s1 = 0.f;
+  for (int r = 0; r < adp::STAT_REPL; ++r) {
+    float* p = scratch + (size_t)r * 2 * adp::STAT_CMAX + c;
+    s0 += p[0];
+    s1 += p[adp::STAT_CMAX];
+    p[0] = 0.f;
+    p[adp::STAT_CMAX] = 0.f;
+  }
+  dst0[c] += s0;
+  dst1[c] += s1;
+}
+
 // per-channel sums of dBN and dBN*xhat; block = 256 threads as (pixel lane) x (channel group)
 template <typename T>
 __global__ void bn_bwd_reduce_kernel(size_t M, int C, const T* dA, const T* z, const float* sc,
                                      const float* sh, const float* mean, const float* invstd,
-                                     float* dgamma, float* dbeta) {
+                                     float* dgamma, float* dbeta, float* stat) {
   const int G = C >> 3;
   const int lanes = TPB / G;           // pixels processed per block iteration
   const int g = threadIdx.x % G, pl = threadIdx.x / G;
@@ -337,8 +361,9 @@ __global__ void bn_bwd_reduce_kernel(size_t M, int C, const T* dA, const T* z, c
       a += red[0][(l * G + gg) * 8 + j];
       b += red[1][(l * G + gg) * 8 + j];
     }
-    atomicAdd(dbeta + c, a);
-    atomicAdd(dgamma + c, b);
+    float* rep = stat_replica(stat, blockIdx.x);
+    atomicAdd(rep + c, a);
+    atomicAdd(rep + adp::STAT_CMAX + c, b);
   }
 }
 
@@ -555,6 +580,57 @@ __global__ void ema_kernel(size_t n, float* ema, const float* p, float d) {
 
 }  // namespace
 
+namespace adp {
+float* stat_scratch() {
+  static std::mutex mu;
+  static std::map<int, float*> per_dev;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { set_error("stat_scratch: hipGetDevice failed"); return nullptr; }
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = per_dev.find(dev);
+  if (it != per_dev.end()) return it->second;
+  const size_t bytes = sizeof(float) * STAT_REPL * 2 * STAT_CMAX;
+  float* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    set_error("stat_scratch: allocation of the BatchNorm accumulator replicas failed");
+    return nullptr;
+  }
+  per_dev[dev] = p;
+  return p;
+}
+void* scratch(int slot, size_t bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, std::pair<void*, size_t>> bufs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { set_error("scratch: hipGetDevice failed"); return nullptr; }
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = bufs[{dev, slot}];
+  if (e.second >= bytes) return e.first;
+  if (e.first) {   // kernels queued on any stream may still use the old buffer
+    if (hipDeviceSynchronize() != hipSuccess || hipFree(e.first) != hipSuccess) {
+      set_error("scratch: releasing the old buffer failed");
+      return nullptr;
+    }
+    e = {nullptr, 0};
+  }
+  const size_t want = bytes + bytes / 4;   // grow with headroom
+  if (hipMalloc(&e.first, want) != hipSuccess) {
+    e = {nullptr, 0};
+    set_error("scratch: hipMalloc failed");
+    return nullptr;
+  }
+  e.second = want;
+  return e.first;
+}
+int stat_fold(int C, float* dst0, float* dst1, hipStream_t s) {
+  float* sc = stat_scratch();
+  if (!sc) return -1;
+  hipLaunchKernelGGL(stat_fold_kernel, dim3((C + TPB - 1) / TPB), dim3(TPB), 0, s, C, sc, dst0, dst1);
+  return check_launch("stat_fold");
+}
+}  // namespace adp
+
 #define DTYPE_SWITCH(dtype, T, ...)                                   \
   do {                                                                \
     if ((dtype) == ADP_F32) { using T = float; __VA_ARGS__; }         \
@@ -608,11 +684,14 @@ extern "C" int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C, const
   const size_t P = (size_t)N * (H / 2) * (W / 2);
   const int blocks = (int)std::max<size_t>(1, std::min<size_t>((P + lanes - 1) / lanes,
                                                                (size_t)adp::option("pool_bnr_blocks", 2048)));
+  float* stat = adp::stat_scratch();
+  ADP_REQUIRE(stat, adp_last_error());
   DTYPE_SWITCH(dtype, T,
                hipLaunchKernelGGL(maxpool_bwd_bnr_kernel<T>, dim3(blocks), dim3(TPB), 0, (hipStream_t)st, N, H, W, C,
                                   (const T*)src, (const T*)dpool, (const T*)addend, (T*)dsrc, (const T*)z, sc, sh,
-                                  mean, invstd, dgamma, dbeta));
-  return adp::check_launch("adp_maxpool2_bwd_bnr");
+                                  mean, invstd, stat));
+  if (adp::check_launch("adp_maxpool2_bwd_bnr")) return -2;
+  return adp::stat_fold(C, dbeta, dgamma, (hipStream_t)st);
 }
 
 extern "C" int adp_upsample2_bwd(int dtype, int N, int Hs, int Ws, int C, const void* dup,
@@ -670,10 +749,13 @@ extern "C" int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, con
   ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB, "adp_bn_bwd_reduce: C must be a multiple of 8 and <= 2048");
   int lanes = TPB / (C / 8);
   int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 2048);
+  float* stat = adp::stat_scratch();
+  ADP_REQUIRE(stat, adp_last_error());
   DTYPE_SWITCH(dtype, T,
                hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, C,
-                                  (const T*)dA, (const T*)z, sc, sh, mean, invstd, dgamma, dbeta));
-  return adp::check_launch("adp_bn_bwd_reduce");
+                                  (const T*)dA, (const T*)z, sc, sh, mean, invstd, dgamma, dbeta, stat));
+  if (adp::check_launch("adp_bn_bwd_reduce")) return -2;
+  return adp::stat_fold(C, dbeta, dgamma, (hipStream_t)st);
 }
 
 extern "C" int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, const void* z, const float* sc,

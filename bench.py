@@ -36,6 +36,7 @@ def parse():
     p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-size", type=int, default=1024, help="tile size of the CPU baseline sample")
+    p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
     return p.parse_args()
 
 
@@ -116,6 +117,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    for kv in args.opt:
+        ops.set_option(kv.split("=")[0], int(kv.split("=")[1]))
     B, S = args.batch, args.size
     if args.preset == "unet_bn":
         net = UNetBN(B, S, levels=args.levels, base=64, in_ch=3, dtype=args.dtype, device=dev, seed=865)

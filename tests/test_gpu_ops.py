@@ -41,6 +41,10 @@ DTS = [torch.float32, torch.bfloat16]
 CONV_CASES = [
     # name, N, S, cin_parts, cout, dil, up
     ("first", 2, 16, [1], 44, 1, False),
+    # one 8-channel source (network input): bf16 launches take the register-resident cin8 kernel
+    ("first3_64", 2, 16, [3], 64, 1, False),
+    ("first3_ragged_dil2", 1, 13, [3], 64, 2, False),
+    ("first1_24", 3, 10, [1], 24, 1, False),
     ("plain", 2, 16, [44], 88, 2, False),
     ("dil8", 1, 32, [88], 176, 8, False),
     ("dil32", 1, 16, [64], 64, 32, False),
@@ -289,6 +293,32 @@ def test_pool_upsample(dt):
     torch.cuda.synchronize()
     ref = du.reshape(2, 8, 2, 8, 2, 48).sum((2, 4))
     assert relerr(ds, ref) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("S,cout", [(32, 64), (19, 48)])
+def test_cin8_input_layer_bn_stats(S, cout):
+    """bf16 input-layer launch (adp_conv_fwd -> igemm_fwd_cin8_kernel): output vs the oracle on
+    bf16-rounded operands, BatchNorm sums of the stored values vs a host reduction of the same
+    (pre-rounding) values, pad channels untouched."""
+    from adipose_amd._lib import lib
+    xs, kern, bias, l = make_case(2, S, [3], cout, 1, False, seed=3)
+    W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).to(torch.bfloat16).contiguous()
+    b = torch.zeros(l.cout_s, device=DEV)
+    b[:cout] = bias.to(DEV)
+    src = nhwc_pad(xs[0], l.cin_s[0], torch.bfloat16)
+    out = torch.zeros((2, S, S, l.cout_s), dtype=torch.bfloat16, device=DEV)
+    s1 = torch.zeros(l.cout_s, device=DEV)
+    s2 = torch.zeros(l.cout_s, device=DEV)
+    ops.conv_fwd(src, W, l.Nout, out=out, bias=b, relu=False, bn_stats=(s1, s2))
+    torch.cuda.synchronize()
+    assert lib().adp_last_kernel().decode().startswith("igemm_fwd_cin8_kernel")
+    ref = oracle_fwd([rb(xs[0], torch.bfloat16)], rb(kern, torch.bfloat16), bias, 1, False, relu=False)
+    assert relerr(out[..., :cout], ref) < TOL[torch.bfloat16]
+    if l.cout_s > cout:
+        assert out[..., cout:].abs().max().item() == 0.0
+    r = ref.reshape(-1, cout).double()
+    assert bool(((s1[:cout].cpu().double() - r.sum(0)).abs() <= 1e-2 * r.abs().sum(0) + 1e-3).all())
+    assert bool(((s2[:cout].cpu().double() - (r * r).sum(0)).abs() <= 1e-2 * (r * r).sum(0) + 1e-3).all())
 
 
 @pytest.mark.parametrize("dt", DTS)
