@@ -27,6 +27,15 @@ constexpr int HH = PH + 2, HW = PW + 2;         // input halo
 constexpr int HROWS = HH * HW;                  // 340 halo pixels
 constexpr int ROWB = 128;                       // 64 bf16 channels per LDS row
 
+// LDS-only barrier: this wave's LDS traffic done, then the hardware barrier. Unlike __syncthreads() it does
+// not wait for outstanding global stores / LDS-DMA prefetches (its workgroup fence drains vmcnt).
+#define LDS_BAR()                                             \
+  do {                                                        \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        \
+    __builtin_amdgcn_s_barrier();                             \
+    asm volatile("" ::: "memory");                            \
+  } while (0)
+
 #define HALO_BAR()                         \
   do {                                     \
     asm volatile("" ::: "memory");         \
@@ -223,7 +232,217 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
   if (a.bn_sum || a.bnr_z) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
 }
 
+// Persistent form for the single-chunk, <= 64-output-channel layers (Cin_s == 64, Nout <= 64: the
+// unet_bn level-0 64->64 convs and their data gradients). One block (8 waves, one patch row of 32
+// pixels each, full K) per CU walks tiles lin, lin + G, ... All nine weight taps stay resident in LDS
+// for the whole launch (the one-tile kernel's per-tap weight ring waits ~1 us per LDS-DMA fill); the
+// product is computed transposed (C^T = W X^T: a lane holds 4 consecutive output channels of one
+// pixel), so each wave stores its outputs straight from the accumulators (8-B vectors) with no LDS
+// staging and no barrier; the next tile's halo is prefetched into registers at the first tap and
+// written to the single LDS halo buffer between two barriers; BatchNorm sums stay in registers until
+// the block's last tile and go to the accumulator replicas once per wave.
+template <bool BNR>
+__global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
+  constexpr int NTH = 512, BN = 64;
+  constexpr int GH = (HROWS * 8 + NTH - 1) / NTH;           // halo chunks per thread
+  constexpr int HBUF = (GH * NTH / 8) * ROWB;
+  constexpr int GW = 9 * BN * 8 / NTH;                      // resident weight chunks per thread
+  constexpr int WTAP = BN * ROWB;
+  constexpr int OFF_W = HBUF, OFF_C = OFF_W + 9 * WTAP;
+  constexpr int SMEM = OFF_C + 5 * BN * 4;                  // + per-channel epilogue constants
+  static_assert(GW * NTH == 9 * BN * 8, "weights must split evenly");
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = patch row
+  const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
+  const int T = a.nblocks, G = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, G);
+  const int nt = lin < T ? (T - lin + G - 1) / G : 0;
+  if (nt == 0) return;
+  const int Wrows = (a.Nout + 63) / 64 * 64;
+  const bf16* srcA = reinterpret_cast<const bf16*>(a.srcA);
+
+  auto tile_origin = [&](int k, int& img, int& y0, int& x0) {
+    const int t = lin + k * G;
+    const int px = t % tx_n, r = t / tx_n;
+    y0 = (r % ty_n) * PH;
+    img = r / ty_n;
+    x0 = px * PW;
+  };
+  auto halo_src = [&](int k, int i) -> const uint4* {
+    int img, y0, x0;
+    tile_origin(k, img, y0, x0);
+    const int idx = i * NTH + tid;
+    const int hr = idx >> 3, pos = idx & 7;
+    const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
+    const bool ok = hr < HROWS && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
+    return ok ? reinterpret_cast<const uint4*>(srcA + (size_t)((img * a.Hs + gy) * a.Ws + gx) * a.CAs + 8 * (pos ^ swz(hr)))
+              : nullptr;
+  };
+
+  // ---- prologue: nine weight taps (resident), first halo, per-channel constants
+#pragma unroll
+  for (int i = 0; i < GW; ++i) {
+    const int idx = i * NTH + tid;             // chunk idx of the [tap][row q][8 chunks] image
+    const int t = idx / (BN * 8), rem = idx - t * BN * 8;
+    const int q = rem >> 3, pos = rem & 7;
+    const void* p = q < Wrows ? (const void*)(reinterpret_cast<const bf16*>(a.W) + (size_t)q * a.Kpad + t * 64 + 8 * (pos ^ swz(q)))
+                              : (const void*)halo_zero_page;
+    __builtin_amdgcn_global_load_lds(p, (lds_void*)(smem + OFF_W + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < GH; ++i) {
+    const uint4* p = halo_src(0, i);
+    __builtin_amdgcn_global_load_lds(p ? (const void*)p : (const void*)halo_zero_page,
+                                     (lds_void*)(smem + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
+  }
+  float* cst = reinterpret_cast<float*>(smem + OFF_C);      // [5][64]: bias | scale shift mean invstd
+  if (tid < BN) {
+    const bool v = tid < a.Nout;
+    cst[tid] = (!BNR && a.bias && v) ? a.bias[tid] : 0.f;
+    cst[BN + tid] = (BNR && v) ? a.bnr_sc[tid] : 0.f;
+    cst[2 * BN + tid] = (BNR && v) ? a.bnr_sh[tid] : 0.f;
+    cst[3 * BN + tid] = (BNR && v) ? a.bnr_mean[tid] : 0.f;
+    cst[4 * BN + tid] = (BNR && v) ? a.bnr_invstd[tid] : 0.f;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int r16 = lane & 15, h4 = lane >> 4;
+  const bool relu = a.relu != 0, stats = a.bn_sum != nullptr || BNR;
+  float s1[4][4], s2[4][4];
+#pragma unroll
+  for (int nf = 0; nf < 4; ++nf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { s1[nf][i] = 0.f; s2[nf][i] = 0.f; }
+
+  for (int k = 0; k < nt; ++k) {
+    const bool more = k + 1 < nt;
+    int img, y0, x0;
+    tile_origin(k, img, y0, x0);
+    const int mrow = (img * a.Ho + y0 + wave) * a.Wo + x0;   // first output pixel of this wave's row
+    uint2 zreg[2][4];
+    if constexpr (BNR) {
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf) {
+          const int c0 = nf * 16 + 4 * h4;
+          zreg[mf][nf] = c0 < a.Nout ? *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.bnr_z) +
+                                                                       (size_t)(mrow + mf * 16 + r16) * a.bnr_zs + c0)
+                                     : make_uint2(0, 0);
+        }
+    }
+    uint4 hreg[GH];
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < GH; ++i) {
+        const uint4* p = halo_src(k + 1, i);
+        hreg[i] = p ? *p : make_uint4(0, 0, 0, 0);
+      }
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3, dx = t - 3 * dy;
+      const unsigned char* Wt = smem + OFF_W + t * WTAP;
+#pragma unroll
+      for (int kq = 0; kq < 2; ++kq) {
+        const int ck = 4 * kq + h4;
+        bf16x8 fb[4], fa[2];
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf) {
+          const int q = nf * 16 + r16;
+          fb[nf] = *reinterpret_cast<const bf16x8*>(Wt + q * ROWB + ((ck ^ swz(q)) << 4));
+        }
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf) {
+          const int hr = (wave + dy) * HW + mf * 16 + r16 + dx;
+          fa[mf] = *reinterpret_cast<const bf16x8*>(smem + hr * ROWB + ((ck ^ swz(hr)) << 4));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+          for (int nf = 0; nf < 4; ++nf)   // transposed: rows = output channels, columns = pixels
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nf], fa[mf], acc[mf][nf], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // ---- epilogue from registers: lane = pixel (mf*16 + r16) x channels nf*16 + 4*h4 .. +3
+#pragma unroll
+    for (int nf = 0; nf < 4; ++nf) {
+      const int c0 = nf * 16 + 4 * h4;
+      if (c0 >= a.Nout) continue;
+      const float4 cb = *reinterpret_cast<const float4*>(cst + c0);
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf) {
+        const size_t m = (size_t)(mrow + mf * 16 + r16);
+        float v[4] = {acc[mf][nf][0] + cb.x, acc[mf][nf][1] + cb.y, acc[mf][nf][2] + cb.z, acc[mf][nf][3] + cb.w};
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (relu) v[i] = fmaxf(v[i], 0.f);
+          o[i] = (bf16)v[i];
+        }
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.out) + m * a.out_stride + c0) = o;
+        if constexpr (BNR) {
+          const float4 sc = *reinterpret_cast<const float4*>(cst + BN + c0);
+          const float4 sh = *reinterpret_cast<const float4*>(cst + 2 * BN + c0);
+          const float4 mu = *reinterpret_cast<const float4*>(cst + 3 * BN + c0);
+          const float4 is = *reinterpret_cast<const float4*>(cst + 4 * BN + c0);
+          const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+          const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+          bf16x4 zz = __builtin_bit_cast(bf16x4, zreg[mf][nf]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float g = (float)o[i], zf = (float)zz[i];   // the stored (rounded) gradient
+            const float db = fmaf(zf, scv[i], shv[i]) > 0.f ? g : 0.f;
+            s1[nf][i] += db;
+            s2[nf][i] += db * (zf - muv[i]) * isv[i];
+          }
+        } else if (stats) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { s1[nf][i] += v[i]; s2[nf][i] += v[i] * v[i]; }
+        }
+      }
+    }
+    if (more) {
+      LDS_BAR();   // every wave is done with this tile's halo
+#pragma unroll
+      for (int i = 0; i < GH; ++i)
+        *reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16) = hreg[i];
+      LDS_BAR();
+    }
+  }
+  if (!stats || (a.debug_flags & 2)) return;
+  float* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+#pragma unroll
+  for (int nf = 0; nf < 4; ++nf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = s1[nf][i], y = s2[nf][i];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        x += __shfl_xor(x, o, 64);
+        y += __shfl_xor(y, o, 64);
+      }
+      const int c = nf * 16 + 4 * h4 + i;
+      if (r16 == 0 && c < a.Nout) {
+        atomicAdd(d0 + c, x);
+        atomicAdd(d0 + adp::STAT_CMAX + c, y);
+      }
+    }
+}
+
 #undef HALO_BAR
+#undef LDS_BAR
 
 template <int WN, int KS, int TPS, int NHB>
 void launch_halo(FwdArgs& a, hipStream_t s) {
@@ -249,6 +468,17 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     return 0;
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const bool one_chunk = Cin_s == 64;
+  if (one_chunk && a.Nout <= 64 && a.out_mode == 0 && !a.addend && !a.mask && !a.accum && a.drop_rate == 0.f &&
+      a.out_stride % 8 == 0 && option("halo_persist", 1)) {
+    const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW);
+    a.ntile_n = 1;
+    a.nblocks = tiles;   // the persistent kernel reads the tile count from nblocks
+    const int grid = std::max(1, std::min(tiles, option("halo_persist_grid", 256)));
+    adp::set_kernel("igemm_fwd_halop_kernel<%s>", a.bnr_z ? "true" : "false");
+    if (a.bnr_z) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false>), dim3(grid), dim3(512), 0, s, a);
+    return 1;
+  }
   if (a.Nout <= 64) {
     if (one_chunk && mode != 2) launch_halo<1, 2, 1, 1>(a, s);   // two blocks per CU
     else launch_halo<1, 2, 2, 2>(a, s);
