@@ -1,20 +1,26 @@
 """Weight files.
 
-Reference: Keras 2.13 ``save_weights`` to ``*.weights.h5`` (weights-only HDF5; per layer
-``layers/<layer_name>/vars/{0: kernel HWIO, 1: bias}``), e.g. train_adipose_unet_v3.py:918-922,
-loaded by full_evaluation_enhanced.py:1266-1301. h5py is not installed on this image, so weights are
-stored with the same names and slot order in a safetensors container (``*.weights.safetensors``);
-genuine ``.weights.h5`` files are read when h5py is importable. Tensor name:
-``layers/<layer_name>/vars/<slot>``; metadata carries the preset and topology.
+Reference: Keras 2.13 ``save_weights`` to ``*.weights.h5`` (weights-only HDF5, saving_lib layout
+``/layers/<layer_name>/vars/{0: kernel HWIO, 1: bias}``), e.g. train_adipose_unet_v3.py:918-922, loaded by
+full_evaluation_enhanced.py:1266-1301; legacy hdf5_format ``*.h5`` files (``layer_names`` /
+``weight_names`` attributes) for the v2 pretrained weights (train_adipose_unet_v3.py:881-916).
+h5py is not installed on this image: both layouts are read and written by h5io.py (a pure-Python HDF5
+subset pinned against libhdf5-written files), so this build writes genuine ``*.weights.h5`` files under
+the reference's names. ``*.weights.safetensors`` (same ``layers/<name>/vars/<i>`` tensor names,
+earlier builds of this engine) is still read and can still be written.
 """
 from __future__ import annotations
 
 import json
 import os
+from collections import OrderedDict
 
 import numpy as np
 
-SUFFIX = ".weights.safetensors"
+from . import h5io
+
+SUFFIX = ".weights.h5"                      # what this build writes (the reference's own suffix)
+ALT_SUFFIXES = (".weights.h5", ".weights.safetensors")
 
 
 def _name(layer, i):
@@ -22,30 +28,28 @@ def _name(layer, i):
 
 
 def save_weights(net, path, weights=None):
-    from safetensors.numpy import save_file
-
+    """``*.weights.h5`` -> Keras 2.13 layout; other ``*.h5`` -> legacy hdf5_format layout;
+    ``*.safetensors`` -> safetensors with Keras tensor names."""
     wd = weights if weights is not None else net.get_weights()
-    tensors = {}
-    for layer, arrs in wd.items():
-        for i, a in enumerate(arrs):
-            tensors[_name(layer, i)] = np.ascontiguousarray(np.asarray(a, np.float32))
-    meta = {"format": "adipose_amd/keras-weights", "preset": getattr(net, "preset", ""),
-            "layers": json.dumps(list(wd.keys()))}
-    save_file(tensors, path, metadata=meta)
-    return path
+    wd = OrderedDict((k, [np.ascontiguousarray(np.asarray(a, np.float32)) for a in v]) for k, v in wd.items())
+    path = str(path)
+    if path.endswith(".safetensors"):
+        from safetensors.numpy import save_file
+        tensors = {_name(layer, i): a for layer, arrs in wd.items() for i, a in enumerate(arrs)}
+        meta = {"format": "adipose_amd/keras-weights", "preset": getattr(net, "preset", ""),
+                "layers": json.dumps(list(wd.keys()))}
+        save_file(tensors, path, metadata=meta)
+        return path
+    if path.endswith(".h5"):
+        return h5io.write_keras_weights(path, wd, fmt="keras_v3" if path.endswith(".weights.h5") else "legacy")
+    raise ValueError(f"{path}: weight files end in .weights.h5, .h5 or .safetensors")
 
 
 def read_weights(path):
-    """-> OrderedDict layer -> [arrays] from a .weights.safetensors (or .weights.h5 if h5py exists)."""
-    from collections import OrderedDict
-
+    """-> OrderedDict layer -> [arrays] (Keras slot order) from any of the supported weight files."""
+    path = str(path)
     if path.endswith(".h5"):
-        try:
-            import h5py  # noqa: F401
-        except ImportError as e:
-            raise RuntimeError(f"{path}: reading Keras HDF5 weights needs h5py, which is not installed; "
-                               f"convert to {SUFFIX}") from e
-        return _read_h5(path)
+        return h5io.read_keras_weights(path)[1]
     from safetensors import safe_open
 
     out = OrderedDict()
@@ -61,21 +65,6 @@ def read_weights(path):
                 arrs.append(f.get_tensor(_name(layer, i)))
                 i += 1
             out[layer] = arrs
-    return out
-
-
-def _read_h5(path):
-    import h5py
-    from collections import OrderedDict
-
-    out = OrderedDict()
-    with h5py.File(path, "r") as f:
-        root = f["layers"] if "layers" in f else f
-        for layer in root:
-            g = root[layer]
-            if "vars" in g:
-                v = g["vars"]
-                out[layer] = [np.asarray(v[str(i)]) for i in range(len(v))]
     return out
 
 
@@ -101,12 +90,12 @@ def resolve_weights_file(path):
     names = ["weights_best_overall", "phase2_best", "phase1_best", "best_model", "model_best", "weights_best",
              "weights_ema"]
     for n in names:
-        for suf in (SUFFIX, ".weights.h5"):
+        for suf in ALT_SUFFIXES:
             p = os.path.join(path, n + suf)
             if os.path.exists(p):
                 return p, path
     if os.path.isdir(path):
         for f in sorted(os.listdir(path)):
-            if f.endswith(SUFFIX) or f.endswith(".h5"):
+            if f.endswith(".safetensors") or f.endswith(".h5"):
                 return os.path.join(path, f), path
     raise FileNotFoundError(f"No weights files found in {path}")

@@ -40,17 +40,17 @@ from . import ops
 from .metrics import calculate_pixel_metrics, metrics_from_counts
 
 # ------------------------------------------------------------------------------ checkpoints
-_OUR_SUFFIX = ".weights.safetensors"
+_SUFFIXES = (".weights.h5", ".weights.safetensors")   # Keras 2.13 files first (this build writes them)
 _WEIGHT_CANDIDATES_BEST = ["weights_best_overall", "phase2_best", "phase1_best", "best_model", "model_best",
                            "weights_best"]
 _WEIGHT_CANDIDATES_EMA = ["weights_ema", "ema_weights_phase2", "ema_weights"]
 
 
 def _find_best_weights_in_dir(ckpt_dir: Path, use_ema: bool = False) -> Optional[Path]:
-    """:471-490 (each candidate tried with this build's suffix first, then Keras' .weights.h5)."""
+    """:471-490 (each candidate as .weights.h5, then as an earlier build's .weights.safetensors)."""
     def first(names):
         for n in names:
-            for suf in (_OUR_SUFFIX, ".weights.h5"):
+            for suf in _SUFFIXES:
                 p = ckpt_dir / (n + suf)
                 if p.exists():
                     return p
@@ -63,7 +63,7 @@ def _find_best_weights_in_dir(ckpt_dir: Path, use_ema: bool = False) -> Optional
         hit = first(_WEIGHT_CANDIDATES_BEST)
         if hit is not None:
             return hit
-    files = (sorted(ckpt_dir.glob("*" + _OUR_SUFFIX)) + sorted(ckpt_dir.glob("*.weights.h5"))
+    files = (sorted(ckpt_dir.glob("*.weights.h5")) + sorted(ckpt_dir.glob("*.weights.safetensors"))
              + sorted(ckpt_dir.glob("*.h5")))
     return files[0] if files else None
 

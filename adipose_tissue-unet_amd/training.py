@@ -13,8 +13,8 @@
   training_settings.log, phase*_best / phase*_final weights.
 
 Every step runs on the GPU through ``trainer.Trainer`` (HIP kernels); this module is host control flow.
-Weight files keep the reference's names with the ``.weights.h5`` suffix mapped to ``.weights.safetensors``
-(checkpoint.py: h5py is not installed on this image; tensor names are Keras' ``layers/<name>/vars/<i>``).
+Weight files are genuine Keras 2.13 ``*.weights.h5`` files under the reference's names (checkpoint.py /
+h5io.py: a pure-Python HDF5 writer, h5py is not installed on this image).
 """
 from __future__ import annotations
 
@@ -42,10 +42,14 @@ ENCODER_LAYERS = ["down1_conv1", "down1_conv2", "down1_pool", "down2_conv1", "do
 
 
 def weights_path(path):
-    """Reference weight-file name -> the file this build writes/reads (``*.weights.h5`` -> safetensors)."""
+    """Reference weight-file name -> the file this build writes/reads: the same name (genuine
+    ``*.weights.h5``); a ``*.weights.h5`` that does not exist but has a ``*.weights.safetensors``
+    sibling (an earlier build of this engine) resolves to the sibling."""
     p = str(path)
-    if p.endswith(".weights.h5"):
-        return p[: -len(".weights.h5")] + ckpt.SUFFIX
+    if p.endswith(".weights.h5") and not os.path.exists(p):
+        alt = p[: -len(".weights.h5")] + ".weights.safetensors"
+        if os.path.exists(alt):
+            return alt
     return p
 
 

@@ -3,7 +3,7 @@
 :307-488) on the HIP engine.
 
 Same behaviour as the reference: weights from a file or a checkpoint directory (find_weights_file
-:252-285, our `.weights.safetensors` first), z-score stats from `normalization_stats.json` next to the
+:252-285, genuine `.weights.h5` first, then an earlier build's `.weights.safetensors`), z-score stats from `normalization_stats.json` next to the
 weights (defaults 0/1 with a warning, :232-249), images of the wrong size are skipped with a warning
 (:441-444), `masks/{stem}_mask.tif` (uint8 0/1), optional `probabilities/{stem}_prob.tif` (uint8
 prob*255) and `overlays/{stem}_overlay.png`; returns 0/1. All TTA views of a tile run as one batched

@@ -60,6 +60,8 @@ def test_resolve_weights_path(tmp_path):
     (d / "weights_ema.weights.h5").write_bytes(b"")
     w, c = E.resolve_weights_path(str(d))
     assert w.endswith("phase2_best.weights.safetensors") and c == str(d)
+    (d / "phase2_best.weights.h5").write_bytes(b"")
+    assert E.resolve_weights_path(str(d))[0].endswith("phase2_best.weights.h5")
     w, _ = E.resolve_weights_path(str(d), use_ema=True)
     assert w.endswith("weights_ema.weights.h5")
     (d / "weights_best_overall.weights.safetensors").write_bytes(b"")
@@ -212,7 +214,7 @@ def _write_eval_fixture(tmp_path, S=64, n=5):
     ck.mkdir()
     net = AdiposeV3Net(1, S, dtype="f32", device="cuda", deep_supervision=False)
     net.set_weights(w)
-    save_weights(net, str(ck / "phase2_best.weights.safetensors"))
+    save_weights(net, str(ck / "phase2_best.weights.h5"))
     (ck / "normalization_stats.json").write_text(json.dumps({"mean": 127.0, "std": 50.0}))
     (ck / "training_settings.log").write_text("use_deep_supervision: False\n")
     ds = tmp_path / "val"
@@ -237,7 +239,7 @@ def test_publication_evaluation_vs_oracle(tmp_path):
     from cli.full_evaluation_enhanced import main
     from oracle import torch_ref as R
     ck, ds, w = _write_eval_fixture(tmp_path)
-    res = E.run_publication_evaluation(str(ds), str(ck / "phase2_best.weights.safetensors"), str(tmp_path / "out"),
+    res = E.run_publication_evaluation(str(ds), str(ck / "phase2_best.weights.h5"), str(tmp_path / "out"),
                                        dataset_name="val", optimize_threshold=False, save_visualizations=True,
                                        n_vis_samples=2, use_tta=True, tta_mode="basic", tile_size=64)
     assert (tmp_path / "out" / "val_comprehensive_results.csv").exists()

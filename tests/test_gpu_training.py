@@ -48,9 +48,9 @@ def test_two_phase_driver_and_cli(tmp_path):
     cdir = tmp_path / "checkpoints" / "segmentation" / "20260101_000000_adipose_v3_1024_finetune_v3"
     names = {p.name for p in cdir.iterdir()}
     for f in ["normalization_stats.json", "training_settings.log", "phase1_training.log", "phase2_training.log",
-              "phase1_best.weights.safetensors", "weights_phase1_final.weights.safetensors",
-              "phase2_best.weights.safetensors", "weights_phase2_final.weights.safetensors",
-              "weights_ema.weights.safetensors"]:
+              "phase1_best.weights.h5", "weights_phase1_final.weights.h5",
+              "phase2_best.weights.h5", "weights_phase2_final.weights.h5",
+              "weights_ema.weights.h5"]:
         assert f in names, (f, sorted(names))
     st = json.load(open(cdir / "normalization_stats.json"))
     assert st["normalization_method"] == "percentile" and st["num_training_images"] == 4

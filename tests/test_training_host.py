@@ -1,7 +1,7 @@
 """Host logic of the training surface (training.py) against the reference's formulas:
 CosineAnnealingWithWarmup (train_adipose_unet_v3.py:393-404), per-epoch EMA (:446-505),
 Keras ModelCheckpoint(save_best_only) / EarlyStopping(patience) / CSVLogger as the driver uses them
-(:1266-1300), and the .weights.h5 -> .weights.safetensors file mapping."""
+(:1266-1300), and the weight-file name resolution (genuine .weights.h5, earlier .weights.safetensors)."""
 import csv
 import math
 
@@ -82,5 +82,5 @@ def test_checkpoint_best_only_and_early_stopping(tmp_path):
 
 
 def test_weights_path_mapping():
-    assert T.weights_path("a/phase1_best.weights.h5") == "a/phase1_best.weights.safetensors"
+    assert T.weights_path("a/phase1_best.weights.h5") == "a/phase1_best.weights.h5"
     assert T.weights_path("x.weights.safetensors") == "x.weights.safetensors"
