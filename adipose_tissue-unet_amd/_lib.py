@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class AdpError(RuntimeError):
@@ -85,6 +85,14 @@ _SIGS = {
     "adp_loss_grad": [_I, _I, _I, _P, _P, _I, _F, _F, _P, _P, _F, _I, _P, _P],
     "adp_pixel_counts": [_S, _P, _P, _F, _P, _P],
     "adp_threshold_hist": [_S, _P, _P, _I, C.POINTER(C.c_double), _P, _P],
+    "adp_aug_geom": [_I, _I, _P, _P, _I, _I, _I, _P],
+    "adp_aug_photometric": [_S, _P, _P, _I, _F, _F, _P],
+    "adp_aug_noise": [_S, _P, _P, _P, _P],
+    "adp_aug_sum": [_S, _P, _P, _P],
+    "adp_aug_blur": [_I, _I, _I, _P, _P, _P, _P, _I, _P],
+    "adp_aug_scale": [_I, _I, _I, _I, _P, _P, _I, _P],
+    "adp_aug_remap": [_I, _I, _P, _P, _P, _P, C.c_double, _P, _P, _P],
+    "adp_percentile_normalize": [_S, _P, _P, C.c_double, C.c_double, _P, _P, _P],
     "adp_adam": [_S, _P, _P, _P, _P, _F, _F, _F, _F, _I, _F, _F, _P],
     "adp_ema": [_S, _P, _P, _F, _P],
     "adp_prep_input": [_I, _I, _I, _I, _I, _P, C.c_longlong, C.c_longlong, _F, _F, _I, _I, _P, _P],

@@ -115,6 +115,8 @@ class KerasLikeNet:
             raise RuntimeError("You must compile your model before training/testing. Use `model.compile(...)`.")
 
     def _dev(self, a):
+        if isinstance(a, torch.Tensor):   # device feed (TileDataset(device=...)): no host round trip
+            return a.to(self.engine.device, torch.float32).contiguous()
         return torch.as_tensor(np.asarray(a, np.float32)).to(self.engine.device)
 
     def _metrics(self):
@@ -539,15 +541,6 @@ def log_training_settings(checkpoint_dir, command_line_args, data_config, model_
     return p
 
 
-def _flip_rot_augment(img, mask, rng):
-    """Label-safe geometric augmentation (random flips and 90-degree rotations)."""
-    k = rng.randint(4)
-    img, mask = np.rot90(img, k), np.rot90(mask, k)
-    if rng.rand() < 0.5:
-        img, mask = img[:, ::-1], mask[:, ::-1]
-    return np.ascontiguousarray(img), np.ascontiguousarray(mask)
-
-
 def train_model(data_root, pretrained_weights, batch_size=2, epochs_phase1=75, epochs_phase2=150,
                 normalization_method="percentile", percentile_low=1.0, percentile_high=99.0, build_timestamp=None,
                 augmentation_level="moderate", checkpoint_suffix="", use_deep_supervision=True, use_hard_mining=True,
@@ -585,10 +578,14 @@ def train_model(data_root, pretrained_weights, batch_size=2, epochs_phase1=75, e
             "build_timestamp": build_timestamp, "version": "3.0"}
     with open(model.checkpoint_dir / "normalization_stats.json", "w") as f:
         json.dump(norm, f, indent=2)
-    augment_fn = None if augmentation_level == "none" else _flip_rot_augment
+    # the reference's pipelines (_select_augment_fn, :1056-1067) on the GPU; feed batches stay in HBM
+    from .augment import select_augment_fn
+    augment_fn, augment_label = select_augment_fn(augmentation_level)
     ds_kw = dict(mean=train_mean, std=train_std, normalization_method=normalization_method,
-                 percentile_low=percentile_low, percentile_high=percentile_high, seed=seed)
-    train_ds = TileDataset(tr_img, tr_msk, batch_size, augment=augment_fn is not None, augment_fn=augment_fn, **ds_kw)
+                 percentile_low=percentile_low, percentile_high=percentile_high, seed=seed,
+                 device=model.net.engine.device)
+    train_ds = TileDataset(tr_img, tr_msk, batch_size, augment=augment_fn is not None, augment_fn=augment_fn,
+                           augment_level=augment_label, **ds_kw)
     val_ds = TileDataset(va_img, va_msk, batch_size, augment=False, **ds_kw)
     spe = steps_per_epoch or max(1, len(train_ds) // batch_size)
     vst = validation_steps or max(1, len(val_ds) // batch_size)

@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 5 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr */
+#define ADP_ABI_VERSION 6 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -215,6 +215,30 @@ int adp_pixel_counts(size_t n, const float* pred, const float* truth, float thr,
  * (truth > 0.5) and j = #{t : pred > thr[t]}. tp(t) = sum_{j>t} hist[nthr+1+j], fp(t) = sum_{j>t} hist[j]. */
 int adp_threshold_hist(size_t n, const float* pred, const float* truth, int nthr, const double* thr,
                        unsigned long long* hist, adp_stream_t s);
+
+/* ---- training-time augmentation + normalisation of gray (H, W) f32 planes (src/utils/data.py:13-264,
+ * 398-429); random parameters are drawn by the host in the reference's RandomState order ---------- */
+/* np.rot90(k) then fliplr then flipud (random_rotation_90 / random_flip, data.py:13-29); out of place */
+int adp_aug_geom(int H, int W, const float* src, float* dst, int k, int flip_lr, int flip_ud, adp_stream_t s);
+/* mode 0 brightness clip(x*f,0,255), 1 contrast clip((x-m)*f+m,0,255), 2 gamma (x/255)^f*255 (:32-50),
+ * 3 z-score (x-m)/f (TileDataset, train_adipose_unet_v3.py:589-590) */
+int adp_aug_photometric(size_t n, const float* src, float* dst, int mode, float f, float m, adp_stream_t s);
+/* clip(x + noise, 0, 255) with noise f64 (random_gaussian_noise, :63-69) */
+int adp_aug_noise(size_t n, const float* src, const double* noise, float* dst, adp_stream_t s);
+/* *out += sum(src) in f64 (contrast's image.mean()) */
+int adp_aug_sum(size_t n, const float* src, double* out, adp_stream_t s);
+/* separable Gaussian (cv2.GaussianBlur, BORDER_REFLECT_101), taps[2r+1]; dtype64: src/tmp/dst are f64 */
+int adp_aug_blur(int dtype64, int H, int W, const void* src, void* tmp, void* dst, const float* taps, int radius,
+                 adp_stream_t s);
+/* random_scale (:72-106): cv2.resize to (Hn, Wn) (linear, or nearest for masks) + center crop / pad */
+int adp_aug_scale(int H, int W, int Hn, int Wn, const float* src, float* dst, int nearest, adp_stream_t s);
+/* elastic_transform (:109-145): remap image (linear, reflect) and mask (nearest, 0) by (x+dx*alpha, y+dy*alpha) */
+int adp_aug_remap(int H, int W, const float* src, const float* msrc, const double* dx, const double* dy, double alpha,
+                  float* dst, float* mdst, adp_stream_t s);
+/* normalize_image(method='percentile') (:398-429) with exact order statistics (radix select on the
+ * device); work >= 64 + 32768 bytes; p_out (nullable) receives (p_low, p_high) values */
+int adp_percentile_normalize(size_t n, const float* src, float* dst, double p_low, double p_high, void* work,
+                             float* p_out, adp_stream_t s);
 
 /* ---- optimizer (Keras Adam / AdamW, :800-806) --------------------------------------------- */
 int adp_adam(size_t n, float* param, const float* grad, float* m, float* v, float lr, float beta1,
