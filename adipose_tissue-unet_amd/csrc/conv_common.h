@@ -58,6 +58,16 @@ struct WgradArgs {
                         // into dW by a second launch; nullptr -> f32 atomics into dW
 };
 
+// LDS-only workgroup barrier for epilogues: this wave's LDS traffic complete, then s_barrier. Unlike
+// __syncthreads() (whose workgroup fence waits for vmcnt = 0) it does not stall behind the wave's own
+// global stores or loads still in flight; use it only where the barrier orders LDS accesses alone.
+#define ADP_LDS_BARRIER()                                     \
+  do {                                                        \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        \
+    __builtin_amdgcn_s_barrier();                             \
+    asm volatile("" ::: "memory");                            \
+  } while (0)
+
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -285,10 +295,10 @@ ADP_DEV void epi_bn_flush(const FwdArgs& a, float* red, int n0, int tid, const f
                           const float (&bq)[8]) {
   constexpr int GPR = BN / 8;
   if (a.debug_flags & 2) return;
-  __syncthreads();
+  ADP_LDS_BARRIER();
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = bs[j]; red[tid * 16 + 8 + j] = bq[j]; }
-  __syncthreads();
+  ADP_LDS_BARRIER();
   if (tid < BN) {
     const int gg = tid >> 3, j = tid & 7;
     float s = 0.f, q = 0.f;

@@ -219,7 +219,7 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
             *e = part == 0 ? acc[mf][nf][r] : *e + acc[mf][nf][r];
           }
     }
-    __syncthreads();
+    ADP_LDS_BARRIER();
   }
   float bs[8], bq[8];
 #pragma unroll

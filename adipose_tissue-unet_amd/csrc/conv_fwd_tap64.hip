@@ -272,10 +272,10 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
           for (int r = 0; r < 4; ++r)
             tile[((mt / MIQ) * HM + (mt % MIQ) * 16 + rq + r) * LT + wc * 64 + nt * 16 + col] = acc[mt][nt][r];
     }
-    __syncthreads();
+    ADP_LDS_BARRIER();
     if constexpr (BNR) epi_rows_bnr<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
     else epi_rows<NTH, BN, F8>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
-    __syncthreads();
+    ADP_LDS_BARRIER();
   }
   if (a.bn_sum || a.bnr_z) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
 }
