@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class AdpError(RuntimeError):
@@ -93,6 +93,12 @@ _SIGS = {
     "adp_aug_scale": [_I, _I, _I, _I, _P, _P, _I, _P],
     "adp_aug_remap": [_I, _I, _P, _P, _P, _P, C.c_double, _P, _P, _P],
     "adp_percentile_normalize": [_S, _P, _P, C.c_double, C.c_double, _P, _P, _P],
+    "adp_create": [_P, _I, _P],
+    "adp_destroy": [_P],
+    "adp_param_size": [_P, C.c_char_p, _I, C.POINTER(C.c_size_t)],
+    "adp_set_param": [_P, C.c_char_p, _I, _P, _S],
+    "adp_get_param": [_P, C.c_char_p, _I, _P, _S],
+    "adp_forward": [_P, _P, _I, C.c_longlong, _F, _F, _I, _P, _P],
     "adp_adam": [_S, _P, _P, _P, _P, _F, _F, _F, _F, _I, _F, _F, _P],
     "adp_ema": [_S, _P, _P, _F, _P],
     "adp_prep_input": [_I, _I, _I, _I, _I, _P, C.c_longlong, C.c_longlong, _F, _F, _I, _I, _P, _P],
@@ -105,7 +111,7 @@ _lib = None
 
 
 def exported_symbols():
-    return ["adp_last_error", "adp_last_kernel"] + list(_SIGS)
+    return ["adp_last_error", "adp_last_kernel", "adp_param_name"] + list(_SIGS)
 
 
 def lib():
@@ -121,6 +127,8 @@ def lib():
         L.adp_last_error.argtypes = []
         L.adp_last_kernel.restype = C.c_char_p
         L.adp_last_kernel.argtypes = []
+        L.adp_param_name.restype = C.c_char_p
+        L.adp_param_name.argtypes = [C.c_void_p, C.c_int]
         for name, args in _SIGS.items():
             fn = getattr(L, name)
             fn.restype = C.c_int

@@ -29,7 +29,8 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 6 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize */
+#define ADP_ABI_VERSION 7 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+                              v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -261,6 +262,33 @@ int adp_blend_accum(int H, int W, int T, int y0, int x0, const float* tile, cons
                     float* acc, float* wsum, adp_stream_t s);
 int adp_blend_finalize(size_t n, const float* acc, const float* wsum, float floor_, float* out,
                        adp_stream_t s);
+
+/* ---- handle-level engine: native adipose_v3 inference for non-Python callers ---- */
+#define ADP_PRESET_ADIPOSE_V3 0
+typedef struct adp_handle adp_handle; /* opaque: topology, packed weights, activation buffers */
+typedef struct adp_config {
+  int preset;            /* ADP_PRESET_ADIPOSE_V3 (train_adipose_unet_v3.py:660-758) */
+  int tile;              /* S (the reference hard-codes 1024), multiple of 8 */
+  int max_batch;         /* images x TTA views per forward (activation buffers are sized for it) */
+  int dtype;             /* ADP_DTYPE_F32 (the reference's fp32 numerics) or ADP_DTYPE_BF16 */
+  int deep_supervision;  /* 1: the aux_out1 / aux_out2 heads exist (checkpoint layout); inference = main_out */
+  int init_nb;           /* base width, 44 (build_model(init_nb=44)) */
+} adp_config;
+int adp_create(const adp_config* cfg, int device, adp_handle** out);
+int adp_destroy(adp_handle* h);
+/* i-th parameterised layer name (Keras layer names), NULL past the end */
+const char* adp_param_name(const adp_handle* h, int i);
+/* slot 0 = kernel (Keras HWIO for convs, (1,1,Cin,Nout) for heads), 1 = bias; n = element count */
+int adp_param_size(adp_handle* h, const char* layer, int slot, size_t* n);
+int adp_set_param(adp_handle* h, const char* layer, int slot, const float* host, size_t n);
+int adp_get_param(adp_handle* h, const char* layer, int slot, float* host, size_t n);
+/* predict_single / TTA (segmentation_inference.py:153-229): images = n device f32 (S,S) raw gray tiles
+ * img_stride floats apart (<= 0: dense); prob = n device f32 (S,S) main_out probabilities;
+ * (x - mean)/(std + 1e-10) on load; tta_mode 0 none, 1 minimal (id, flipH), 2 basic (+flipV, rot90),
+ * 3 full (8 views). Stream-ordered; the first call after adp_set_param uploads the weights
+ * (synchronous). One handle per device and thread. */
+int adp_forward(adp_handle* h, const float* images, int n, long long img_stride, float mean, float std,
+                int tta_mode, float* prob, adp_stream_t s);
 
 #ifdef __cplusplus
 }
