@@ -232,8 +232,9 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
   if (a.bn_sum || a.bnr_z) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
 }
 
-// Persistent form for the single-chunk, <= 64-output-channel layers (Cin_s == 64, Nout <= 64: the
-// unet_bn level-0 64->64 convs and their data gradients). One block (8 waves, one patch row of 32
+// Persistent form for the single-chunk layers (Cin_s == 64) with <= 64 output channels or 128 in two
+// 64-channel halves (unet_bn level-0 64->64 convs and their data gradients, enc1_conv1 64->128, the
+// split data gradient of dec0_conv1). One block (8 waves, one patch row of 32
 // pixels each, full K) per CU walks tiles lin, lin + G, ... All nine weight taps stay resident in LDS
 // for the whole launch (the one-tile kernel's per-tap weight ring waits ~1 us per LDS-DMA fill); the
 // product is computed transposed (C^T = W X^T: a lane holds 4 consecutive output channels of one
@@ -262,10 +263,19 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   const int nt = lin < T ? (T - lin + G - 1) / G : 0;
   if (nt == 0) return;
   const int Wrows = (a.Nout + 63) / 64 * 64;
+  // ntile_n = 2 (128 output channels): tile t = 2 * patch + half, the grid is even, so a block keeps
+  // one 64-channel half (its resident weights) and the two halves of a patch run side by side on one
+  // XCD (halo shared through L2). A split store (out_mode 2, split_c = 64) sends half 1 to out2.
+  const int nh = a.ntile_n == 2 ? (lin & 1) : 0, n0 = 64 * nh;
+  const int NT = a.ntile_n;
+  bf16* obase = reinterpret_cast<bf16*>(a.out_mode == 2 && nh == 1 ? a.out2 : a.out);
+  const int ostride = a.out_mode == 2 && nh == 1 ? a.out2_stride : a.out_stride;
+  const int ocol0 = a.out_mode == 2 && nh == 1 ? n0 - a.split_c : n0;
+  const int nlim = a.out_mode == 2 && nh == 0 ? a.split_c : a.Nout;
   const bf16* srcA = reinterpret_cast<const bf16*>(a.srcA);
 
   auto tile_origin = [&](int k, int& img, int& y0, int& x0) {
-    const int t = lin + k * G;
+    const int t = (lin + k * G) / NT;
     const int px = t % tx_n, r = t / tx_n;
     y0 = (r % ty_n) * PH;
     img = r / ty_n;
@@ -288,8 +298,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     const int idx = i * NTH + tid;             // chunk idx of the [tap][row q][8 chunks] image
     const int t = idx / (BN * 8), rem = idx - t * BN * 8;
     const int q = rem >> 3, pos = rem & 7;
-    const void* p = q < Wrows ? (const void*)(reinterpret_cast<const bf16*>(a.W) + (size_t)q * a.Kpad + t * 64 + 8 * (pos ^ swz(q)))
-                              : (const void*)halo_zero_page;
+    const void* p = n0 + q < Wrows
+                        ? (const void*)(reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + q) * a.Kpad + t * 64 + 8 * (pos ^ swz(q)))
+                        : (const void*)halo_zero_page;
     __builtin_amdgcn_global_load_lds(p, (lds_void*)(smem + OFF_W + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
   }
 #pragma unroll
@@ -300,12 +311,13 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   }
   float* cst = reinterpret_cast<float*>(smem + OFF_C);      // [5][64]: bias | scale shift mean invstd
   if (tid < BN) {
-    const bool v = tid < a.Nout;
-    cst[tid] = (!BNR && a.bias && v) ? a.bias[tid] : 0.f;
-    cst[BN + tid] = (BNR && v) ? a.bnr_sc[tid] : 0.f;
-    cst[2 * BN + tid] = (BNR && v) ? a.bnr_sh[tid] : 0.f;
-    cst[3 * BN + tid] = (BNR && v) ? a.bnr_mean[tid] : 0.f;
-    cst[4 * BN + tid] = (BNR && v) ? a.bnr_invstd[tid] : 0.f;
+    const int c = n0 + tid;
+    const bool v = c < a.Nout;
+    cst[tid] = (!BNR && a.bias && v) ? a.bias[c] : 0.f;
+    cst[BN + tid] = (BNR && v) ? a.bnr_sc[c] : 0.f;
+    cst[2 * BN + tid] = (BNR && v) ? a.bnr_sh[c] : 0.f;
+    cst[3 * BN + tid] = (BNR && v) ? a.bnr_mean[c] : 0.f;
+    cst[4 * BN + tid] = (BNR && v) ? a.bnr_invstd[c] : 0.f;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -330,9 +342,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
         for (int nf = 0; nf < 4; ++nf) {
           const int c0 = nf * 16 + 4 * h4;
-          zreg[mf][nf] = c0 < a.Nout ? *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.bnr_z) +
-                                                                       (size_t)(mrow + mf * 16 + r16) * a.bnr_zs + c0)
-                                     : make_uint2(0, 0);
+          zreg[mf][nf] = n0 + c0 < a.Nout ? *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.bnr_z) +
+                                                                            (size_t)(mrow + mf * 16 + r16) * a.bnr_zs + n0 + c0)
+                                          : make_uint2(0, 0);
         }
     }
     uint4 hreg[GH];
@@ -379,7 +391,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
     for (int nf = 0; nf < 4; ++nf) {
       const int c0 = nf * 16 + 4 * h4;
-      if (c0 >= a.Nout) continue;
+      if (n0 + c0 >= nlim) continue;
       const float4 cb = *reinterpret_cast<const float4*>(cst + c0);
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf) {
@@ -391,7 +403,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
           if (relu) v[i] = fmaxf(v[i], 0.f);
           o[i] = (bf16)v[i];
         }
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.out) + m * a.out_stride + c0) = o;
+        *reinterpret_cast<bf16x4*>(obase + m * ostride + ocol0 + c0) = o;
         if constexpr (BNR) {
           const float4 sc = *reinterpret_cast<const float4*>(cst + BN + c0);
           const float4 sh = *reinterpret_cast<const float4*>(cst + 2 * BN + c0);
@@ -433,7 +445,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
         x += __shfl_xor(x, o, 64);
         y += __shfl_xor(y, o, 64);
       }
-      const int c = nf * 16 + 4 * h4 + i;
+      const int c = n0 + nf * 16 + 4 * h4 + i;
       if (r16 == 0 && c < a.Nout) {
         atomicAdd(d0 + c, x);
         atomicAdd(d0 + adp::STAT_CMAX + c, y);
@@ -468,12 +480,15 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     return 0;
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const bool one_chunk = Cin_s == 64;
-  if (one_chunk && a.Nout <= 64 && a.out_mode == 0 && !a.addend && !a.mask && !a.accum && a.drop_rate == 0.f &&
-      a.out_stride % 8 == 0 && option("halo_persist", 1)) {
-    const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW);
-    a.ntile_n = 1;
+  const bool split_ok = a.out_mode == 2 && a.Nout == 128 && a.split_c == 64 && !a.mask2 && a.out2_stride % 8 == 0;
+  if (one_chunk && (a.Nout <= 64 || (a.Nout % 64 == 0 && a.Nout <= 128)) && (a.out_mode == 0 || split_ok) &&
+      !a.addend && !a.mask && !a.accum && a.drop_rate == 0.f && a.out_stride % 8 == 0 && option("halo_persist", 1)) {
+    const int halves = a.Nout > 64 ? 2 : 1;
+    const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * halves;
+    a.ntile_n = halves;
     a.nblocks = tiles;   // the persistent kernel reads the tile count from nblocks
-    const int grid = std::max(1, std::min(tiles, option("halo_persist_grid", 256)));
+    int grid = std::max(1, std::min(tiles, option("halo_persist_grid", 256)));
+    if (halves == 2) grid &= ~1;   // even grid: a block keeps one channel half
     adp::set_kernel("igemm_fwd_halop_kernel<%s>", a.bnr_z ? "true" : "false");
     if (a.bnr_z) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true>), dim3(grid), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false>), dim3(grid), dim3(512), 0, s, a);

@@ -206,6 +206,32 @@ def test_halo_fused_epilogues():
     assert relerr(db, db2) < 1e-4 and relerr(dg, dg2) < 1e-4
 
 
+@pytest.mark.parametrize("S,N", [(32, 2), (64, 3)])
+def test_persistent_halo_split_and_stats(S, N):
+    """Persistent halo kernel, 128 output channels in two halves: split store (out_mode 2, split_c 64)
+    equals the plain store sliced, BatchNorm statistics of both halves, vs the oracle."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16
+    xs, kern, bias, l = make_case(N, S, [64], 128, 1, False, seed=31)
+    W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).to(dt).contiguous()
+    x = nhwc_pad(xs[0], l.Cin_s, dt)
+    out = torch.zeros((N, S, S, 128), dtype=dt, device=DEV)
+    st = torch.zeros(2, 128, device=DEV)
+    ops.conv_fwd(x, W, 128, out=out, bias=bias.to(DEV), relu=True, bn_stats=(st[0], st[1]))
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel")
+    ref = oracle_fwd([rb(xs[0], dt)], rb(kern, dt), bias, 1, False)
+    assert relerr(out, ref) < TOL[dt]
+    r2 = ref.reshape(-1, 128)
+    assert relerr(st[0], r2.sum(0)) < 2e-2 and relerr(st[1], (r2 * r2).sum(0)) < 2e-2
+    o1 = torch.zeros((N, S, S, 64), dtype=dt, device=DEV)
+    o2 = torch.zeros((N, S, S, 72), dtype=dt, device=DEV)   # wider stride than the 64 channels stored
+    ops.conv_fwd(x, W, 128, out=o1, bias=bias.to(DEV), relu=True, out_mode=2, out2=o2, split_c=64)
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel")
+    torch.cuda.synchronize()
+    assert torch.equal(o1, out[..., :64]) and torch.equal(o2[..., :64], out[..., 64:])
+    assert o2[..., 64:].abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "128x256", "64x256"])
 @pytest.mark.parametrize("cout", [64, 192])
 @pytest.mark.parametrize("S", [23, 64], ids=["ragged", "rowaligned"])
