@@ -382,6 +382,140 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
   }
 }
 
+// Persistent halo weight-gradient kernel for the narrow full-resolution layers (3x3, stride 1, dilation
+// 1, Cin_s == 64 single source, Nout == 64, plain dY: unet_bn level-0 64->64 convs). The tap64 kernel
+// re-gathers every input pixel once per tap (9x) through LDS-DMA and pads K = 576 to three 256-wide
+// tiles (a third of its MFMAs multiply zeros). Here one block per CU walks 8 x 32 output patches; per
+// patch the 10 x 34 input halo and the 256 x 64 dY tile are moved into LDS once (LDS-DMA, double
+// buffered across patches), and wave t (9 waves) accumulates dW_t = sum_p dY[p]^T X[p + off_t] for tap
+// t in 16 accumulator tiles that stay in registers for all of the block's patches: each patch row is
+// one 32-pixel MFMA k step of transposed LDS reads (both operands with the same row permutation). The
+// block's dW partial is added once at the end (256-B rows through LDS, f32 atomics).
+__global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) {
+  constexpr int NTH = 576, RB = 128;
+  constexpr int PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
+  constexpr int HCH = HROWS * 8, DCH = PH * PW * 8;                     // 16-B chunks per image
+  constexpr int GH = (HCH + NTH - 1) / NTH, GD = (DCH + NTH - 1) / NTH;
+  constexpr int HBUF = HROWS * RB, DBUF = PH * PW * RB;
+  constexpr int STAGE = HBUF + DBUF;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap
+  const int dy = wave / 3, dx = wave - 3 * (wave / 3);
+  const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
+  const int T = a.Nimg * tx_n * ty_n, G = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, G);
+  const int nt = lin < T ? (T - lin + G - 1) / G : 0;
+  const bf16* X = reinterpret_cast<const bf16*>(a.srcA);
+  const bf16* D = reinterpret_cast<const bf16*>(a.dY);
+
+  auto issue = [&](int k, int buf) {
+    const int t = lin + k * G;
+    const int px = t % tx_n, r = t / tx_n;
+    const int y0 = (r % ty_n) * PH, img = r / ty_n, x0 = px * PW;
+    unsigned char* hb = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < GH; ++i) {
+      const int idx = i * NTH + tid;
+      if (idx < HCH) {
+        const int hr = idx >> 3, pos = idx & 7;
+        const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
+        const bool ok = gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
+        const void* p = ok ? (const void*)(X + (size_t)((img * a.Hs + gy) * a.Ws + gx) * a.CAs + 8 * (pos ^ gsw<RB>(hr)))
+                           : (const void*)wg64_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(hb + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
+      }
+    }
+    unsigned char* db = hb + HBUF;
+#pragma unroll
+    for (int i = 0; i < GD; ++i) {
+      const int idx = i * NTH + tid;
+      if (idx < DCH) {
+        const int pr = idx >> 3, pos = idx & 7;
+        const size_t m = (size_t)(img * a.Ho + y0 + (pr >> 5)) * a.Wo + x0 + (pr & 31);
+        __builtin_amdgcn_global_load_lds(D + m * a.dy_stride + 8 * (pos ^ gsw<RB>(pr)),
+                                         (lds_void*)(db + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
+      }
+    }
+  };
+  // transposed 16x32 fragment of an [row][64 bf16] LDS image whose rows row0 .. row0+31 are the 32
+  // pixels of one k step (absolute rows, so the row swizzle matches the one applied on load)
+  const int g = lane >> 4, ii = lane & 15, q = ii >> 2, pp = ii & 3;
+  const int rr0 = 16 * (g >> 1) + 4 * (g & 1) + q;
+  auto frag = [&](uint32_t img_base, int row0, int col0) {
+    const int col = col0 + 4 * pp, chunk = col >> 3, inb = (col & 7) * 2;
+    const int R0 = row0 + rr0, R1 = R0 + 8;
+    const v4s16 lo = ds_tr16(img_base + R0 * RB + ((chunk ^ gsw<RB>(R0)) << 4) + inb);
+    const v4s16 hi = ds_tr16(img_base + R1 * RB + ((chunk ^ gsw<RB>(R1)) << 4) + inb);
+    bf16x8 r;
+    const bf16* l = reinterpret_cast<const bf16*>(&lo);
+    const bf16* h = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
+    return r;
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    W64_BAR();
+  }
+  const uint32_t sbase = lds_off(smem);
+  for (int k = 0; k < nt; ++k) {
+    const int buf = k & 1;
+    if (k + 1 < nt) issue(k + 1, buf ^ 1);
+    const uint32_t hbase = sbase + buf * STAGE, dbase = hbase + HBUF;
+#pragma unroll 1
+    for (int pr = 0; pr < PH; ++pr) {
+      bf16x8 fd[4], fx[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) fd[nb] = frag(dbase, pr * PW, nb * 16);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) fx[cb] = frag(hbase, (pr + dy) * HW + dx, cb * 16);
+      lgkm_wait<0>();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+          acc[nb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[nb], fx[cb], acc[nb][cb], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next patch landed
+    W64_BAR();                                          // and nobody reads this buffer any more
+  }
+  if (a.debug_flags & 1) {
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) asm volatile("" ::"v"(acc[nb][cb]));
+    return;
+  }
+  // dW[n][tap * 64 + c] += acc: each wave's 16-row blocks through LDS into 256-B rows
+  constexpr int ES = 68;
+  float* blk = reinterpret_cast<float*>(smem) + wave * 16 * ES;
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+  const int kk = wave * a.CAs + lane;
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) blk[(rq + r) * ES + cb * 16 + col] = acc[nb][cb][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < 16; ++i) atomicAdd(a.dW + (size_t)(nb * 16 + i) * a.Kpad + kk, blk[i * ES + lane]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+}
+
 #undef W64_BAR
 
 // dW[n][k] += sum over the splits of part[split][n][k] (n < Nout, k < K = Kpad), 4 floats per thread.
@@ -456,6 +590,16 @@ namespace adp {
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   const int mode = option("wgrad_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
+  if (option("wgrad_halop", 1) && !a.scA && a.CAs == 64 && a.CBs == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
+      a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
+      a.Nout == 64 && a.dy_mode == 0 && a.K == 576 && a.Kpad == 576 && a.dy_stride % 8 == 0) {
+    const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
+    const int grid = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256)));
+    a.debug_flags = option("wgrad_debug", 0);
+    adp::set_kernel("igemm_wgrad_halop_kernel");
+    hipLaunchKernelGGL(igemm_wgrad_halop_kernel, dim3(grid), dim3(576), 0, s, a);
+    return 1;
+  }
   const int Cin_s = a.CAs + a.CBs;
   if (a.scA || a.scB || a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 ||
       a.Kpad != a.K)

@@ -257,6 +257,35 @@ def test_wgrad_tap64_configs(cfg, cout, S):
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 32, 96), (3, 16, 32)])
+def test_wgrad_persistent_halo(N, H, W):
+    """Persistent halo weight-gradient kernel (64 -> 64, 3x3: the level-0 layers) vs autograd of the
+    oracle conv, and vs the tap64 kernel on the same operands (option wgrad_halop=0)."""
+    from adipose_amd import _lib
+    cin = cout = 64
+    xs, kern, bias, l = make_case(N, H, [cin], cout, 1, False, seed=21)
+    g = torch.Generator().manual_seed(22)
+    dt = torch.bfloat16
+    x = rb(torch.randn(N, H, W, cin, generator=g), dt)
+    dZ = rb(torch.randn(N, H, W, cout, generator=g), dt)
+    kr = rb(kern, dt).clone().requires_grad_(True)
+    (R.conv2d_same(x, kr, None, relu=False) * dZ).sum().backward()
+    xd, dzd = nhwc_pad(x, l.Cin_s, dt), nhwc_pad(dZ, l.cout_s, dt)
+    dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
+    ops.conv_wgrad(xd, dzd, dW, l.Nout)
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_halop_kernel")
+    torch.cuda.synchronize()
+    assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
+    ref = torch.zeros_like(dW)
+    ops.set_option("wgrad_halop", 0)
+    try:
+        ops.conv_wgrad(xd, dzd, ref, l.Nout)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("wgrad_halop", None)
+    assert relerr(dW.cpu(), ref.cpu()) < 1e-4
+
+
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("S", [8, 64])
 def test_conv_transpose(dt, S):
