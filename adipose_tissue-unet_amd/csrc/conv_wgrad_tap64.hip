@@ -404,11 +404,18 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap
   const int dy = wave / 3, dx = wave - 3 * (wave / 3);
   const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
-  const int T = a.Nimg * tx_n * ty_n, G = gridDim.x;
-  const int lin = xcd_remap(blockIdx.x, G);
+  // work unit = (patch, 64-channel input chunk, 64-wide output block); a block keeps one
+  // (chunk, output block) combination for all of its patches (its accumulators are that dW block)
+  const int nch = (a.CAs + a.CBs) >> 6, combos = nch * (a.Nout >> 6);
+  const int T = a.Nimg * tx_n * ty_n, G = gridDim.x / combos;
+  const int lin0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int combo = lin0 % combos, lin = lin0 / combos;
+  const int ch = combo % nch, nblk = combo / nch;
   const int nt = lin < T ? (T - lin + G - 1) / G : 0;
-  const bf16* X = reinterpret_cast<const bf16*>(a.srcA);
-  const bf16* D = reinterpret_cast<const bf16*>(a.dY);
+  const bool inA = ch * 64 < a.CAs;
+  const bf16* X = reinterpret_cast<const bf16*>(inA ? a.srcA : a.srcB) + (inA ? ch * 64 : ch * 64 - a.CAs);
+  const int xcs = inA ? a.CAs : a.CBs;
+  const bf16* D = reinterpret_cast<const bf16*>(a.dY) + nblk * 64;
 
   auto issue = [&](int k, int buf) {
     const int t = lin + k * G;
@@ -422,7 +429,7 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
         const int hr = idx >> 3, pos = idx & 7;
         const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
         const bool ok = gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
-        const void* p = ok ? (const void*)(X + (size_t)((img * a.Hs + gy) * a.Ws + gx) * a.CAs + 8 * (pos ^ gsw<RB>(hr)))
+        const void* p = ok ? (const void*)(X + (size_t)((img * a.Hs + gy) * a.Ws + gx) * xcs + 8 * (pos ^ gsw<RB>(hr)))
                            : (const void*)wg64_zero_page;
         __builtin_amdgcn_global_load_lds(p, (lds_void*)(hb + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
       }
@@ -502,7 +509,8 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
   constexpr int ES = 68;
   float* blk = reinterpret_cast<float*>(smem) + wave * 16 * ES;
   const int col = lane & 15, rq = (lane >> 4) * 4;
-  const int kk = wave * a.CAs + lane;
+  const int kk = wave * (a.CAs + a.CBs) + ch * 64 + lane;
+  float* dW = a.dW + (size_t)nblk * 64 * a.Kpad;
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb) {
 #pragma unroll
@@ -511,7 +519,7 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
       for (int r = 0; r < 4; ++r) blk[(rq + r) * ES + cb * 16 + col] = acc[nb][cb][r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
-    for (int i = 0; i < 16; ++i) atomicAdd(a.dW + (size_t)(nb * 16 + i) * a.Kpad + kk, blk[i * ES + lane]);
+    for (int i = 0; i < 16; ++i) atomicAdd(dW + (size_t)(nb * 16 + i) * a.Kpad + kk, blk[i * ES + lane]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   }
 }
@@ -590,11 +598,16 @@ namespace adp {
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   const int mode = option("wgrad_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
-  if (option("wgrad_halop", 1) && !a.scA && a.CAs == 64 && a.CBs == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
+  const int hp = option("wgrad_halop", 1);   // 0 off, else every eligible shape
+  const int cin = a.CAs + a.CBs;
+  if (hp && !a.scA && !a.scB && a.CAs % 64 == 0 && a.CBs % 64 == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
       a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
-      a.Nout == 64 && a.dy_mode == 0 && a.K == 576 && a.Kpad == 576 && a.dy_stride % 8 == 0) {
+      a.Nout % 64 == 0 && a.dy_mode == 0 && a.K == 9 * cin && a.Kpad == a.K && a.dy_stride % 8 == 0 &&
+      a.dy_stride >= a.Nout) {
+    const int combos = (cin / 64) * (a.Nout / 64);
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
-    const int grid = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256)));
+    const int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
+    const int grid = per * combos;
     a.debug_flags = option("wgrad_debug", 0);
     adp::set_kernel("igemm_wgrad_halop_kernel");
     hipLaunchKernelGGL(igemm_wgrad_halop_kernel, dim3(grid), dim3(576), 0, s, a);

@@ -257,32 +257,37 @@ def test_wgrad_tap64_configs(cfg, cout, S):
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 32, 96), (3, 16, 32)])
-def test_wgrad_persistent_halo(N, H, W):
-    """Persistent halo weight-gradient kernel (64 -> 64, 3x3: the level-0 layers) vs autograd of the
-    oracle conv, and vs the tap64 kernel on the same operands (option wgrad_halop=0)."""
+@pytest.mark.parametrize("N,H,W,parts,cout", [(2, 64, 64, [64], 64), (1, 32, 96, [64], 64), (3, 16, 32, [64], 64),
+                                               (2, 32, 64, [64, 64], 64), (1, 32, 32, [128], 128),
+                                               (2, 16, 64, [128, 64], 128)])
+def test_wgrad_persistent_halo(N, H, W, parts, cout):
+    """Persistent halo weight-gradient kernel (3x3, 64-channel input chunks from one or two sources,
+    64-wide output blocks) vs autograd of the oracle conv, and vs the tap64 / glds kernels on the same
+    operands (option wgrad_halop=0)."""
     from adipose_amd import _lib
-    cin = cout = 64
-    xs, kern, bias, l = make_case(N, H, [cin], cout, 1, False, seed=21)
+    cin = sum(parts)
+    _, kern, bias, l = make_case(N, H, parts, cout, 1, False, seed=21)
     g = torch.Generator().manual_seed(22)
     dt = torch.bfloat16
-    x = rb(torch.randn(N, H, W, cin, generator=g), dt)
+    xs = [rb(torch.randn(N, H, W, c, generator=g), dt) for c in parts]
     dZ = rb(torch.randn(N, H, W, cout, generator=g), dt)
     kr = rb(kern, dt).clone().requires_grad_(True)
-    (R.conv2d_same(x, kr, None, relu=False) * dZ).sum().backward()
-    xd, dzd = nhwc_pad(x, l.Cin_s, dt), nhwc_pad(dZ, l.cout_s, dt)
+    (R.conv2d_same(torch.cat(xs, -1), kr, None, relu=False) * dZ).sum().backward()
+    xd = [x.to(DEV, dt).contiguous() for x in xs]
+    dzd = nhwc_pad(dZ, l.cout_s, dt)
+    srcB = xd[1] if len(xd) > 1 else None
     dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
-    ops.conv_wgrad(xd, dzd, dW, l.Nout)
-    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_halop_kernel")
-    torch.cuda.synchronize()
-    assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
-    ref = torch.zeros_like(dW)
-    ops.set_option("wgrad_halop", 0)
     try:
-        ops.conv_wgrad(xd, dzd, ref, l.Nout)
+        ops.conv_wgrad(xd[0], dzd, dW, l.Nout, srcB=srcB)
+        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_halop_kernel")
+        torch.cuda.synchronize()
+        ref = torch.zeros_like(dW)
+        ops.set_option("wgrad_halop", 0)
+        ops.conv_wgrad(xd[0], dzd, ref, l.Nout, srcB=srcB)
         torch.cuda.synchronize()
     finally:
         ops.set_option("wgrad_halop", None)
+    assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
     assert relerr(dW.cpu(), ref.cpu()) < 1e-4
 
 
