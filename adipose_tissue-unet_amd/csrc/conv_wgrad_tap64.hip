@@ -391,8 +391,12 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
 // t in 16 accumulator tiles that stay in registers for all of the block's patches: each patch row is
 // one 32-pixel MFMA k step of transposed LDS reads (both operands with the same row permutation). The
 // block's dW partial is added once at the end (256-B rows through LDS, f32 atomics).
-__global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) {
-  constexpr int NTH = 576, RB = 128;
+// NW = 9: one wave per tap (9 waves on 4 SIMDs: the SIMD holding 3 of them sets the pace). NW = 8: wave
+// w owns tap w and a 16 x 32 eighth of tap 8 (output block w >> 1, column blocks 2 (w & 1) + {0, 1}),
+// two waves per SIMD with 18 MFMAs each per k step.
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs a) {
+  constexpr int NTH = NW * 64, RB = 128;
   constexpr int PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
   constexpr int HCH = HROWS * 8, DCH = PH * PW * 8;                     // 16-B chunks per image
   constexpr int GH = (HCH + NTH - 1) / NTH, GD = (DCH + NTH - 1) / NTH;
@@ -463,11 +467,13 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
     return r;
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][4], acc8[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc8[0] = acc8[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nb8 = wave >> 1, cb8 = 2 * (wave & 1);
 
   if (nt > 0) {
     issue(0, 0);
@@ -481,19 +487,33 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
     const uint32_t hbase = sbase + buf * STAGE, dbase = hbase + HBUF;
 #pragma unroll 1
     for (int pr = 0; pr < PH; ++pr) {
-      bf16x8 fd[4], fx[4];
+      bf16x8 fd[4], fx[4], fd8, fx8[2];
+      if (NW == 8) {
+        fd8 = frag(dbase, pr * PW, nb8 * 16);
+        fx8[0] = frag(hbase, (pr + 2) * HW + 2, cb8 * 16);
+        fx8[1] = frag(hbase, (pr + 2) * HW + 2, cb8 * 16 + 16);
+      }
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) fd[nb] = frag(dbase, pr * PW, nb * 16);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) fx[cb] = frag(hbase, (pr + dy) * HW + dx, cb * 16);
-      lgkm_wait<0>();
-      __builtin_amdgcn_s_setprio(1);
+      // column block cb's MFMAs start as soon as its two reads (and the dY fragments) have landed
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
+      for (int cb = 0; cb < 4; ++cb) {
+        if (cb == 0) lgkm_wait<6>();
+        else if (cb == 1) lgkm_wait<4>();
+        else if (cb == 2) lgkm_wait<2>();
+        else lgkm_wait<0>();
+        __builtin_amdgcn_s_setprio(1);
+        if (NW == 8 && cb == 0) {
+          acc8[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd8, fx8[0], acc8[0], 0, 0, 0);
+          acc8[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd8, fx8[1], acc8[1], 0, 0, 0);
+        }
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
+        for (int nb = 0; nb < 4; ++nb)
           acc[nb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[nb], fx[cb], acc[nb][cb], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next patch landed
     W64_BAR();                                          // and nobody reads this buffer any more
@@ -503,6 +523,7 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) asm volatile("" ::"v"(acc[nb][cb]));
+    asm volatile("" ::"v"(acc8[0]), "v"(acc8[1]));
     return;
   }
   // dW[n][tap * 64 + c] += acc: each wave's 16-row blocks through LDS into 256-B rows
@@ -521,6 +542,13 @@ __global__ __launch_bounds__(576, 1) void igemm_wgrad_halop_kernel(WgradArgs a) 
 #pragma unroll
     for (int i = 0; i < 16; ++i) atomicAdd(dW + (size_t)(nb * 16 + i) * a.Kpad + kk, blk[i * ES + lane]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  if (NW == 8) {   // this wave's eighth of tap 8: rows nb8 * 16 + rq + r, columns cb8 * 16 + {0..31}
+    const int k8 = 8 * (a.CAs + a.CBs) + ch * 64 + cb8 * 16 + col;
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(dW + (size_t)(nb8 * 16 + rq + r) * a.Kpad + k8 + 16 * j2, acc8[j2][r]);
   }
 }
 
@@ -609,8 +637,13 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     const int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
     const int grid = per * combos;
     a.debug_flags = option("wgrad_debug", 0);
-    adp::set_kernel("igemm_wgrad_halop_kernel");
-    hipLaunchKernelGGL(igemm_wgrad_halop_kernel, dim3(grid), dim3(576), 0, s, a);
+    if (option("wgrad_halop_waves", 8) == 9) {
+      adp::set_kernel("igemm_wgrad_halop_kernel<9>");
+      hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
+    } else {
+      adp::set_kernel("igemm_wgrad_halop_kernel<8>");
+      hipLaunchKernelGGL(igemm_wgrad_halop_kernel<8>, dim3(grid), dim3(512), 0, s, a);
+    }
     return 1;
   }
   const int Cin_s = a.CAs + a.CBs;

@@ -281,14 +281,18 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.conv_wgrad(xd[0], dzd, dW, l.Nout, srcB=srcB)
         assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_halop_kernel")
         torch.cuda.synchronize()
+        ops.set_option("wgrad_halop_waves", 9)   # one wave per tap
+        dW9 = torch.zeros_like(dW)
+        ops.conv_wgrad(xd[0], dzd, dW9, l.Nout, srcB=srcB)
         ref = torch.zeros_like(dW)
         ops.set_option("wgrad_halop", 0)
         ops.conv_wgrad(xd[0], dzd, ref, l.Nout, srcB=srcB)
         torch.cuda.synchronize()
     finally:
         ops.set_option("wgrad_halop", None)
+        ops.set_option("wgrad_halop_waves", None)
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
-    assert relerr(dW.cpu(), ref.cpu()) < 1e-4
+    assert relerr(dW.cpu(), ref.cpu()) < 1e-4 and relerr(dW9.cpu(), ref.cpu()) < 1e-4
 
 
 @pytest.mark.parametrize("dt", DTS)
