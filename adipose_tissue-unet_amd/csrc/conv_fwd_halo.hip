@@ -242,16 +242,20 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 // staging and no barrier; the next tile's halo is prefetched into registers at the first tap and
 // written to the single LDS halo buffer between two barriers; BatchNorm sums stay in registers until
 // the block's last tile and go to the accumulator replicas once per wave.
-template <bool BNR>
+template <bool BNR, int NCH, int BN>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
-  constexpr int NTH = 512, BN = 64;
-  constexpr int GH = (HROWS * 8 + NTH - 1) / NTH;           // halo chunks per thread
-  constexpr int HBUF = (GH * NTH / 8) * ROWB;
-  constexpr int GW = 9 * BN * 8 / NTH;                      // resident weight chunks per thread
-  constexpr int WTAP = BN * ROWB;
+  // NCH 64-channel input chunks (1: Cin_s 64; 2: Cin_s 128 from one or two sources), BN output channels
+  // per block (64, or 32 for two chunks: 2 x 340 halo rows + 9 x 2 x 32 weight rows = 157 KiB of LDS)
+  constexpr int NTH = 512, NF = BN / 16;
+  constexpr int HCH = NCH * HROWS * 8;                      // 16-B halo chunks (all input chunks)
+  constexpr int GH = (HCH + NTH - 1) / NTH;                 // halo chunks per thread
+  constexpr int HBUF = HCH * 16;
+  constexpr int GW = 9 * NCH * BN * 8 / NTH;                // resident weight chunks per thread
+  constexpr int WTAP = NCH * BN * ROWB;
   constexpr int OFF_W = HBUF, OFF_C = OFF_W + 9 * WTAP;
   constexpr int SMEM = OFF_C + 5 * BN * 4;                  // + per-channel epilogue constants
-  static_assert(GW * NTH == 9 * BN * 8, "weights must split evenly");
+  static_assert(GW * NTH == 9 * NCH * BN * 8, "weights must split evenly");
+  static_assert(SMEM <= 160 * 1024, "LDS");
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
@@ -263,16 +267,18 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   const int nt = lin < T ? (T - lin + G - 1) / G : 0;
   if (nt == 0) return;
   const int Wrows = (a.Nout + 63) / 64 * 64;
-  // ntile_n = 2 (128 output channels): tile t = 2 * patch + half, the grid is even, so a block keeps
-  // one 64-channel half (its resident weights) and the two halves of a patch run side by side on one
-  // XCD (halo shared through L2). A split store (out_mode 2, split_c = 64) sends half 1 to out2.
-  const int nh = a.ntile_n == 2 ? (lin & 1) : 0, n0 = 64 * nh;
+  // ntile_n = NT output blocks of BN channels: tile t = NT * patch + block, the grid is a multiple of
+  // NT, so a block keeps one output block (its resident weights) and the blocks of a patch run side by
+  // side on one XCD (halo shared through L2). A split store (out_mode 2) sends channels >= split_c to
+  // out2 (split_c a multiple of BN).
   const int NT = a.ntile_n;
-  bf16* obase = reinterpret_cast<bf16*>(a.out_mode == 2 && nh == 1 ? a.out2 : a.out);
-  const int ostride = a.out_mode == 2 && nh == 1 ? a.out2_stride : a.out_stride;
-  const int ocol0 = a.out_mode == 2 && nh == 1 ? n0 - a.split_c : n0;
-  const int nlim = a.out_mode == 2 && nh == 0 ? a.split_c : a.Nout;
-  const bf16* srcA = reinterpret_cast<const bf16*>(a.srcA);
+  const int nh = lin % NT, n0 = BN * nh;
+  const bool second = a.out_mode == 2 && n0 >= a.split_c;
+  bf16* obase = reinterpret_cast<bf16*>(second ? a.out2 : a.out);
+  const int ostride = second ? a.out2_stride : a.out_stride;
+  const int ocol0 = second ? n0 - a.split_c : n0;
+  const int nlim = a.out_mode == 2 && !second ? a.split_c : a.Nout;
+  const int Cin_s = a.CAs + a.CBs;
 
   auto tile_origin = [&](int k, int& img, int& y0, int& x0) {
     const int t = (lin + k * G) / NT;
@@ -285,31 +291,39 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     int img, y0, x0;
     tile_origin(k, img, y0, x0);
     const int idx = i * NTH + tid;
-    const int hr = idx >> 3, pos = idx & 7;
+    const int cc = NCH == 1 ? 0 : idx / (HROWS * 8), rem = idx - cc * HROWS * 8;
+    const int hr = rem >> 3, pos = rem & 7;
     const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
-    const bool ok = hr < HROWS && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
-    return ok ? reinterpret_cast<const uint4*>(srcA + (size_t)((img * a.Hs + gy) * a.Ws + gx) * a.CAs + 8 * (pos ^ swz(hr)))
-              : nullptr;
+    const bool ok = idx < HCH && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
+    if (!ok) return nullptr;
+    const bool inA = cc * 64 < a.CAs;
+    const bf16* src = reinterpret_cast<const bf16*>(inA ? a.srcA : a.srcB);
+    const int cs = inA ? a.CAs : a.CBs, c0 = inA ? cc * 64 : cc * 64 - a.CAs;
+    return reinterpret_cast<const uint4*>(src + (size_t)((img * a.Hs + gy) * a.Ws + gx) * cs + c0 + 8 * (pos ^ swz(hr)));
   };
 
   // ---- prologue: nine weight taps (resident), first halo, per-channel constants
 #pragma unroll
   for (int i = 0; i < GW; ++i) {
-    const int idx = i * NTH + tid;             // chunk idx of the [tap][row q][8 chunks] image
-    const int t = idx / (BN * 8), rem = idx - t * BN * 8;
+    const int idx = i * NTH + tid;             // chunk idx of the [tap][input chunk][row q][8 chunks] image
+    const int tc = idx / (BN * 8), rem = idx - tc * BN * 8;
+    const int t = tc / NCH, cc = tc - t * NCH;
     const int q = rem >> 3, pos = rem & 7;
     const void* p = n0 + q < Wrows
-                        ? (const void*)(reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + q) * a.Kpad + t * 64 + 8 * (pos ^ swz(q)))
+                        ? (const void*)(reinterpret_cast<const bf16*>(a.W) + (size_t)(n0 + q) * a.Kpad + t * Cin_s + cc * 64 +
+                                        8 * (pos ^ swz(q)))
                         : (const void*)halo_zero_page;
     __builtin_amdgcn_global_load_lds(p, (lds_void*)(smem + OFF_W + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
   }
 #pragma unroll
   for (int i = 0; i < GH; ++i) {
-    const uint4* p = halo_src(0, i);
-    __builtin_amdgcn_global_load_lds(p ? (const void*)p : (const void*)halo_zero_page,
-                                     (lds_void*)(smem + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
+    if (i * NTH + tid < HCH) {
+      const uint4* p = halo_src(0, i);
+      __builtin_amdgcn_global_load_lds(p ? (const void*)p : (const void*)halo_zero_page,
+                                       (lds_void*)(smem + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
+    }
   }
-  float* cst = reinterpret_cast<float*>(smem + OFF_C);      // [5][64]: bias | scale shift mean invstd
+  float* cst = reinterpret_cast<float*>(smem + OFF_C);      // [5][BN]: bias | scale shift mean invstd
   if (tid < BN) {
     const int c = n0 + tid;
     const bool v = c < a.Nout;
@@ -324,9 +338,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 
   const int r16 = lane & 15, h4 = lane >> 4;
   const bool relu = a.relu != 0, stats = a.bn_sum != nullptr || BNR;
-  float s1[4][4], s2[4][4];
+  float s1[NF][4], s2[NF][4];
 #pragma unroll
-  for (int nf = 0; nf < 4; ++nf)
+  for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[nf][i] = 0.f; s2[nf][i] = 0.f; }
 
@@ -335,12 +349,12 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     int img, y0, x0;
     tile_origin(k, img, y0, x0);
     const int mrow = (img * a.Ho + y0 + wave) * a.Wo + x0;   // first output pixel of this wave's row
-    uint2 zreg[2][4];
+    uint2 zreg[2][NF];
     if constexpr (BNR) {
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf)
 #pragma unroll
-        for (int nf = 0; nf < 4; ++nf) {
+        for (int nf = 0; nf < NF; ++nf) {
           const int c0 = nf * 16 + 4 * h4;
           zreg[mf][nf] = n0 + c0 < a.Nout ? *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.bnr_z) +
                                                                             (size_t)(mrow + mf * 16 + r16) * a.bnr_zs + n0 + c0)
@@ -355,41 +369,45 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
         hreg[i] = p ? *p : make_uint4(0, 0, 0, 0);
       }
     }
-    f32x4 acc[2][4];
+    f32x4 acc[2][NF];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
     for (int t = 0; t < 9; ++t) {
       const int dy = t / 3, dx = t - 3 * dy;
-      const unsigned char* Wt = smem + OFF_W + t * WTAP;
 #pragma unroll
-      for (int kq = 0; kq < 2; ++kq) {
-        const int ck = 4 * kq + h4;
-        bf16x8 fb[4], fa[2];
+      for (int cc = 0; cc < NCH; ++cc) {
+        const unsigned char* Wt = smem + OFF_W + t * WTAP + cc * BN * ROWB;
+        const unsigned char* Hc = smem + cc * HROWS * ROWB;
 #pragma unroll
-        for (int nf = 0; nf < 4; ++nf) {
-          const int q = nf * 16 + r16;
-          fb[nf] = *reinterpret_cast<const bf16x8*>(Wt + q * ROWB + ((ck ^ swz(q)) << 4));
+        for (int kq = 0; kq < 2; ++kq) {
+          const int ck = 4 * kq + h4;
+          bf16x8 fb[NF], fa[2];
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf) {
+            const int q = nf * 16 + r16;
+            fb[nf] = *reinterpret_cast<const bf16x8*>(Wt + q * ROWB + ((ck ^ swz(q)) << 4));
+          }
+#pragma unroll
+          for (int mf = 0; mf < 2; ++mf) {
+            const int hr = (wave + dy) * HW + mf * 16 + r16 + dx;
+            fa[mf] = *reinterpret_cast<const bf16x8*>(Hc + hr * ROWB + ((ck ^ swz(hr)) << 4));
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+            for (int nf = 0; nf < NF; ++nf)   // transposed: rows = output channels, columns = pixels
+              acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nf], fa[mf], acc[mf][nf], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
         }
-#pragma unroll
-        for (int mf = 0; mf < 2; ++mf) {
-          const int hr = (wave + dy) * HW + mf * 16 + r16 + dx;
-          fa[mf] = *reinterpret_cast<const bf16x8*>(smem + hr * ROWB + ((ck ^ swz(hr)) << 4));
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int mf = 0; mf < 2; ++mf)
-#pragma unroll
-          for (int nf = 0; nf < 4; ++nf)   // transposed: rows = output channels, columns = pixels
-            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nf], fa[mf], acc[mf][nf], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
       }
     }
     // ---- epilogue from registers: lane = pixel (mf*16 + r16) x channels nf*16 + 4*h4 .. +3
 #pragma unroll
-    for (int nf = 0; nf < 4; ++nf) {
+    for (int nf = 0; nf < NF; ++nf) {
       const int c0 = nf * 16 + 4 * h4;
       if (n0 + c0 >= nlim) continue;
       const float4 cb = *reinterpret_cast<const float4*>(cst + c0);
@@ -429,14 +447,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       LDS_BAR();   // every wave is done with this tile's halo
 #pragma unroll
       for (int i = 0; i < GH; ++i)
-        *reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16) = hreg[i];
+        if (i * NTH + tid < HCH) *reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16) = hreg[i];
       LDS_BAR();
     }
   }
   if (!stats || (a.debug_flags & 2)) return;
   float* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
 #pragma unroll
-  for (int nf = 0; nf < 4; ++nf)
+  for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float x = s1[nf][i], y = s2[nf][i];
@@ -480,18 +498,31 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     return 0;
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const bool one_chunk = Cin_s == 64;
-  const bool split_ok = a.out_mode == 2 && a.Nout == 128 && a.split_c == 64 && !a.mask2 && a.out2_stride % 8 == 0;
-  if (one_chunk && (a.Nout <= 64 || (a.Nout % 64 == 0 && a.Nout <= 128)) && (a.out_mode == 0 || split_ok) &&
-      !a.addend && !a.mask && !a.accum && a.drop_rate == 0.f && a.out_stride % 8 == 0 && option("halo_persist", 1)) {
-    const int halves = a.Nout > 64 ? 2 : 1;
-    const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * halves;
-    a.ntile_n = halves;
+  const bool plain = !a.addend && !a.mask && !a.accum && a.drop_rate == 0.f && a.out_stride % 8 == 0;
+  // persistent forms: one chunk with <= 64 outputs (one block) or 128 (two 64-wide blocks); two chunks
+  // with 64 / 128 outputs in 32-wide blocks
+  int bn = 0;
+  if (one_chunk && (a.Nout <= 64 || a.Nout == 128)) bn = 64;
+  else if (Cin_s == 128 && (a.Nout == 64 || a.Nout == 128) && option("halo_persist2", 1)) bn = 32;
+  const int nt_n = bn ? (a.Nout + bn - 1) / bn : 1;
+  const bool split_ok = a.out_mode == 2 && bn && a.split_c > 0 && a.split_c % bn == 0 && a.split_c < a.Nout && !a.mask2 &&
+                        a.out2_stride % 8 == 0 && (a.Nout - a.split_c) % bn == 0;
+  if (bn && plain && (a.out_mode == 0 || split_ok) && option("halo_persist", 1)) {
+    const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * nt_n;
+    a.ntile_n = nt_n;
     a.nblocks = tiles;   // the persistent kernel reads the tile count from nblocks
     int grid = std::max(1, std::min(tiles, option("halo_persist_grid", 256)));
-    if (halves == 2) grid &= ~1;   // even grid: a block keeps one channel half
-    adp::set_kernel("igemm_fwd_halop_kernel<%s>", a.bnr_z ? "true" : "false");
-    if (a.bnr_z) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true>), dim3(grid), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false>), dim3(grid), dim3(512), 0, s, a);
+    grid -= grid % nt_n;   // a block keeps one output block
+    if (grid == 0) grid = nt_n;
+    const bool bnr = a.bnr_z != nullptr;
+    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn);
+    if (one_chunk) {
+      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 1, 64>), dim3(grid), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, 1, 64>), dim3(grid), dim3(512), 0, s, a);
+    } else {
+      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 2, 32>), dim3(grid), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, 2, 32>), dim3(grid), dim3(512), 0, s, a);
+    }
     return 1;
   }
   if (a.Nout <= 64) {

@@ -232,6 +232,68 @@ def test_persistent_halo_split_and_stats(S, N):
     assert o2[..., 64:].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("parts,cout", [([128], 64), ([64, 64], 64), ([128], 128), ([64, 64], 128)])
+@pytest.mark.parametrize("S,N", [(32, 2), (64, 1)])
+def test_persistent_halo_two_chunks(parts, cout, S, N):
+    """Persistent halo kernel with two 64-channel input chunks (one or two sources) in 32-wide output
+    blocks: output + BatchNorm statistics vs the oracle and vs the one-tile halo kernel
+    (halo_persist2=0); split store for 128 outputs; data gradient with the fused BN-backward reduction."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16
+    xs, kern, bias, l = make_case(N, S, parts, cout, 1, False, seed=41)
+    W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).to(dt).contiguous()
+    xd = [x.to(DEV, dt).contiguous() for x in xs]
+    srcB = xd[1] if len(xd) > 1 else None
+    out = torch.zeros((N, S, S, cout), dtype=dt, device=DEV)
+    st = torch.zeros(2, cout, device=DEV)
+    ops.conv_fwd(xd[0], W, cout, out=out, srcB=srcB, bias=bias.to(DEV), relu=True, bn_stats=(st[0], st[1]))
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel<false, 2, 32>")
+    ref = oracle_fwd([rb(x, dt) for x in xs], rb(kern, dt), bias, 1, False)
+    assert relerr(out, ref) < TOL[dt]
+    r2 = ref.reshape(-1, cout)
+    assert relerr(st[0], r2.sum(0)) < 2e-2 and relerr(st[1], (r2 * r2).sum(0)) < 2e-2
+    old = torch.zeros_like(out)
+    ops.set_option("halo_persist2", 0)
+    try:
+        ops.conv_fwd(xd[0], W, cout, out=old, srcB=srcB, bias=bias.to(DEV), relu=True)
+        assert "halop" not in _lib.lib().adp_last_kernel().decode()
+    finally:
+        ops.set_option("halo_persist2", None)
+    torch.cuda.synchronize()
+    assert (out.float() - old.float()).abs().max().item() <= 2 ** -6 * out.float().abs().max().item()
+    if cout == 128:
+        o1 = torch.zeros((N, S, S, 64), dtype=dt, device=DEV)
+        o2 = torch.zeros((N, S, S, 72), dtype=dt, device=DEV)
+        ops.conv_fwd(xd[0], W, 128, out=o1, srcB=srcB, bias=bias.to(DEV), relu=True, out_mode=2, out2=o2,
+                     split_c=64)
+        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel")
+        torch.cuda.synchronize()
+        assert torch.equal(o1, out[..., :64]) and torch.equal(o2[..., :64], out[..., 64:])
+    if len(parts) == 1:
+        # data gradient of a 64 -> 128 conv: dY has 128 channels (two chunks), dX 64 / 128 channels
+        g = torch.Generator().manual_seed(42)
+        dZ = torch.randn(N, S, S, 128, generator=g).to(DEV, dt)
+        Wd = (torch.randn(cout, 9 * 128, generator=g) * 0.03).to(DEV, dt)
+        z = torch.randn(N, S, S, cout, generator=g).to(DEV, dt)
+        sc, sh = (torch.rand(cout, generator=g) + 0.5).to(DEV), (torch.randn(cout, generator=g) * 0.2).to(DEV)
+        mu, ist = (torch.randn(cout, generator=g) * 0.1).to(DEV), (torch.rand(cout, generator=g) + 0.5).to(DEV)
+        dA = torch.zeros((N, S, S, cout), dtype=dt, device=DEV)
+        dg, db = torch.zeros(cout, device=DEV), torch.zeros(cout, device=DEV)
+        ops.conv_fwd(dZ, Wd, cout, out=dA, bn_reduce=(z, sc, sh, mu, ist, dg, db))
+        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel<true, 2, 32>")
+        dg2, db2 = torch.zeros_like(dg), torch.zeros_like(db)
+        ops.bn_bwd_reduce(dA, z, sc, sh, mu, ist, dg2, db2)
+        ref = torch.zeros_like(dA)
+        ops.set_option("halo_persist2", 0)
+        try:
+            ops.conv_fwd(dZ, Wd, cout, out=ref)
+        finally:
+            ops.set_option("halo_persist2", None)
+        torch.cuda.synchronize()
+        assert relerr(db, db2) < 1e-4 and relerr(dg, dg2) < 1e-4
+        assert relerr(dA, ref) < 1e-2
+
+
 @pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "128x256", "64x256"])
 @pytest.mark.parametrize("cout", [64, 192])
 @pytest.mark.parametrize("S", [23, 64], ids=["ragged", "rowaligned"])
