@@ -552,6 +552,130 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   }
 }
 
+// Weight gradient of the input layers (one 8-channel source, 3x3 stride 1, 64 outputs; K = 72): an
+// HBM-bound pass over dY (128 B per pixel) and X (16 B per pixel). Persistent, one block per CU, a
+// 3-stage LDS-DMA ring of 8 x 32 patches (34 x 10 halo of 16-B pixels + the 256 x 64 dY tile); wave w
+// takes patch row w as one 32-pixel MFMA k step for the whole 64 x 80 product: A = dY^T fragments,
+// B = "virtual" fragments whose 16 columns are two taps x 8 channels (column j = k = 8 tap + c), read
+// with ds_read_b64_tr_b16 from the halo rows of the two taps (the tenth tap column reads a zero row).
+// Wave partials meet in LDS (ds_add_f32); one f32 atomic per dW element per block.
+__global__ __launch_bounds__(512, 1) void igemm_wgrad_cin8_kernel(WgradArgs a) {
+  constexpr int NTH = 512, PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
+  constexpr int HSLOT = NTH * 16;                  // halo region: one 16-B row per thread (rows >= 340: 0)
+  constexpr int GD = PH * PW * 8 / NTH;            // dY 16-B chunks per thread
+  constexpr int STAGE = HSLOT + PH * PW * 128, NST = 3;
+  constexpr int ZROW = HROWS;                      // an all-zero halo row
+  static_assert(NST * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = patch row
+  const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
+  const int T = a.Nimg * tx_n * ty_n, G = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, G);
+  const int nt = lin < T ? (T - lin + G - 1) / G : 0;
+  const bf16* X = reinterpret_cast<const bf16*>(a.srcA);
+  const bf16* D = reinterpret_cast<const bf16*>(a.dY);
+
+  auto issue = [&](int k) {   // 1 + GD LDS-DMA instructions per thread
+    const int t = lin + k * G;
+    const int px = t % tx_n, r = t / tx_n;
+    const int y0 = (r % ty_n) * PH, img = r / ty_n, x0 = px * PW;
+    unsigned char* st = smem + (k % NST) * STAGE;
+    {
+      const int hr = tid;
+      const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
+      const bool ok = hr < HROWS && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
+      const void* p = ok ? (const void*)(X + (size_t)((img * a.Hs + gy) * a.Ws + gx) * a.CAs)
+                         : (const void*)wg64_zero_page;
+      __builtin_amdgcn_global_load_lds(p, (lds_void*)(st + wave * 64 * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < GD; ++i) {
+      const int idx = i * NTH + tid;
+      const int pr = idx >> 3, pos = idx & 7;
+      const size_t m = (size_t)(img * a.Ho + y0 + (pr >> 5)) * a.Wo + x0 + (pr & 31);
+      __builtin_amdgcn_global_load_lds(D + m * a.dy_stride + 8 * (pos ^ gsw<128>(pr)),
+                                       (lds_void*)(st + HSLOT + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
+    }
+  };
+  const int g = lane >> 4, ii = lane & 15, q = ii >> 2, pp = ii & 3;
+  const int rr0 = 16 * (g >> 1) + 4 * (g & 1) + q;
+  auto frag2 = [&](uint32_t a0, uint32_t a1) {
+    const v4s16 lo = ds_tr16(a0), hi = ds_tr16(a1);
+    bf16x8 r;
+    const bf16* l = reinterpret_cast<const bf16*>(&lo);
+    const bf16* h = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
+    return r;
+  };
+
+  f32x4 acc[4][5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) issue(0);
+  if (nt > 1) issue(1);
+  const uint32_t sbase = lds_off(smem);
+  for (int k = 0; k < nt; ++k) {
+    if (k + 2 < nt) {
+      issue(k + 2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + GD)) : "memory");
+    } else if (k + 1 < nt) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + GD) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    W64_BAR();   // patch k landed for every wave
+    const uint32_t hb = sbase + (k % NST) * STAGE, db = hb + HSLOT;
+    bf16x8 fd[4], fx[5];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {   // A = dY^T: rows = 16 output channels, k = the wave's 32 pixels
+      const int col = nb * 16 + 4 * pp, chunk = col >> 3, inb = (col & 7) * 2;
+      const int R0 = wave * PW + rr0, R1 = R0 + 8;
+      fd[nb] = frag2(db + R0 * 128 + ((chunk ^ gsw<128>(R0)) << 4) + inb,
+                     db + R1 * 128 + ((chunk ^ gsw<128>(R1)) << 4) + inb);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb) {   // B columns 16 kb .. 16 kb + 15 = taps 2 kb, 2 kb + 1 x 8 channels
+      const int tap = 2 * kb + (pp >> 1), cb = (pp & 1) * 8;
+      const int dy = tap / 3, dx = tap - 3 * (tap / 3);
+      const int h0 = tap < 9 ? (wave + dy) * HW + dx + rr0 : ZROW;
+      const int h1 = tap < 9 ? h0 + 8 : ZROW;
+      fx[kb] = frag2(hb + h0 * 16 + cb, hb + h1 * 16 + cb);
+    }
+    lgkm_wait<0>();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int kb = 0; kb < 5; ++kb)
+        acc[nb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[nb], fx[kb], acc[nb][kb], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    W64_BAR();   // stage k % NST is free for patch k + 3
+  }
+  if (nt == 0) return;
+  // wave partials -> LDS [64][80] f32 -> one atomic per element into dW[n][k], k < 72
+  float* red = reinterpret_cast<float*>(smem);
+  for (int i = tid; i < 64 * 80; i += NTH) red[i] = 0.f;
+  __syncthreads();
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(red + (nb * 16 + rq + r) * 80 + kb * 16 + col, acc[nb][kb][r]);
+  __syncthreads();
+  for (int i = tid; i < 64 * 72; i += NTH) {
+    const int n = i / 72, kk = i - n * 72;
+    atomicAdd(a.dW + (size_t)n * a.Kpad + kk, red[n * 80 + kk]);
+  }
+}
+
 #undef W64_BAR
 
 // dW[n][k] += sum over the splits of part[split][n][k] (n < Nout, k < K = Kpad), 4 floats per thread.
@@ -626,6 +750,15 @@ namespace adp {
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   const int mode = option("wgrad_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
+  if (option("wgrad_cin8", 1) && !a.scA && a.CAs == 8 && a.CBs == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
+      a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
+      a.Nout == 64 && a.dy_mode == 0 && a.K == 72 && a.Kpad >= 72 && a.dy_stride % 8 == 0 && a.dy_stride >= 64) {
+    const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
+    const int grid = std::max(1, std::min(tiles, option("wgrad_cin8_grid", 256)));
+    adp::set_kernel("igemm_wgrad_cin8_kernel");
+    hipLaunchKernelGGL(igemm_wgrad_cin8_kernel, dim3(grid), dim3(512), 0, s, a);
+    return 1;
+  }
   const int hp = option("wgrad_halop", 1);   // 0 off, else every eligible shape
   const int cin = a.CAs + a.CBs;
   if (hp && !a.scA && !a.scB && a.CAs % 64 == 0 && a.CBs % 64 == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&

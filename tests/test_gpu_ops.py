@@ -319,6 +319,36 @@ def test_wgrad_tap64_configs(cfg, cout, S):
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("N,H,W,cin", [(2, 32, 64, 3), (1, 16, 96, 1), (3, 8, 32, 8)])
+def test_wgrad_input_layer_cin8(N, H, W, cin):
+    """Input-layer weight gradient (one 8-channel source, 64 outputs): the persistent cin8 kernel vs
+    autograd of the oracle conv and vs the generic LDS-DMA kernel (option wgrad_cin8=0)."""
+    from adipose_amd import _lib
+    cout = 64
+    _, kern, bias, l = make_case(N, H, [cin], cout, 1, False, seed=51)
+    assert l.Cin_s == 8
+    g = torch.Generator().manual_seed(52)
+    dt = torch.bfloat16
+    x = rb(torch.randn(N, H, W, cin, generator=g), dt)
+    dZ = rb(torch.randn(N, H, W, cout, generator=g), dt)
+    kr = rb(kern, dt).clone().requires_grad_(True)
+    (R.conv2d_same(x, kr, None, relu=False) * dZ).sum().backward()
+    xd, dzd = nhwc_pad(x, l.Cin_s, dt), nhwc_pad(dZ, l.cout_s, dt)
+    dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
+    ops.conv_wgrad(xd, dzd, dW, l.Nout)
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_cin8_kernel")
+    ref = torch.zeros_like(dW)
+    ops.set_option("wgrad_cin8", 0)
+    try:
+        ops.conv_wgrad(xd, dzd, ref, l.Nout)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("wgrad_cin8", None)
+    assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
+    assert relerr(dW.cpu(), ref.cpu()) < 1e-4
+    assert dW[:, 72:].abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("N,H,W,parts,cout", [(2, 64, 64, [64], 64), (1, 32, 96, [64], 64), (3, 16, 32, [64], 64),
                                                (2, 32, 64, [64, 64], 64), (1, 32, 32, [128], 128),
                                                (2, 16, 64, [128, 64], 128)])
