@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class AdpError(RuntimeError):
@@ -99,6 +99,11 @@ _SIGS = {
     "adp_set_param": [_P, C.c_char_p, _I, _P, _S],
     "adp_get_param": [_P, C.c_char_p, _I, _P, _S],
     "adp_forward": [_P, _P, _I, C.c_longlong, _F, _F, _I, _P, _P],
+    "adp_train_step": [_P, _P, _P, _I, _P, _F, _P, _P],
+    "adp_set_comm": [_P, _P],
+    "adp_comm_unique_id": [_P],
+    "adp_comm_init": [_I, _P, _I, _P],
+    "adp_comm_destroy": [_P],
     "adp_adam": [_S, _P, _P, _P, _P, _F, _F, _F, _F, _I, _F, _F, _P],
     "adp_ema": [_S, _P, _P, _F, _P],
     "adp_prep_input": [_I, _I, _I, _I, _I, _P, C.c_longlong, C.c_longlong, _F, _F, _I, _I, _P, _P],

@@ -1,7 +1,9 @@
 """ctypes face of the handle-level C ABI (include/adipose_hip.h: adp_create / adp_set_param /
-adp_forward / adp_destroy; csrc/engine.cpp): the native adipose_v3 inference engine, exposed with the
-predictor seam's method surface (segmentation_inference.py:153-158 predict_single, :181-229 TTA) so that
-it can stand in for AdiposeUNet. This is also the binding a non-Python caller would write.
+adp_forward / adp_train_step / adp_set_comm / adp_destroy; csrc/engine.cpp): the native adipose_v3
+engine, exposed with the predictor seam's method surface (segmentation_inference.py:153-158
+predict_single, :181-229 TTA) so that it can stand in for AdiposeUNet, plus a native training step
+(model.net.fit's step, train_adipose_unet_v3.py:1316-1324 with compile_model's losses :780-879). This is
+also the binding a non-Python caller would write.
 """
 from __future__ import annotations
 
@@ -19,6 +21,45 @@ TTA_MODES = {None: 0, "none": 0, "minimal": 1, "basic": 2, "full": 3}
 
 class AdpConfig(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("preset", "tile", "max_batch", "dtype", "deep_supervision", "init_nb")]
+
+
+class AdpTrainCfg(C.Structure):
+    _fields_ = [("use_hard_mining", C.c_int), ("hard_example_ratio", C.c_float), ("use_label_smoothing", C.c_int),
+                ("epsilon_pos", C.c_float), ("epsilon_neg", C.c_float), ("w_main", C.c_float),
+                ("w_aux1", C.c_float), ("w_aux2", C.c_float), ("optimizer", C.c_int), ("beta1", C.c_float),
+                ("beta2", C.c_float), ("eps", C.c_float), ("weight_decay", C.c_float), ("dropout_rate", C.c_float),
+                ("freeze_encoder", C.c_int)]
+
+
+METRIC_NAMES = ("loss", "main_out_loss", "aux_out1_loss", "aux_out2_loss", "main_out_dice_coef",
+                "main_out_binary_accuracy")
+
+
+def train_cfg(*, use_hard_mining=True, hard_example_ratio=0.7, use_label_smoothing=False, epsilon_pos=0.03,
+              epsilon_neg=0.07, ds_weight_main=1.0, ds_weight_aux1=0.4, ds_weight_aux2=0.3, optimizer="adam",
+              beta1=0.9, beta2=0.999, eps=1e-7, weight_decay=0.01, dropout_rate=0.3, freeze_encoder=False):
+    """compile_model's defaults (train_adipose_unet_v3.py:780-879) as an adp_train_cfg."""
+    return AdpTrainCfg(int(use_hard_mining), hard_example_ratio, int(use_label_smoothing), epsilon_pos, epsilon_neg,
+                       ds_weight_main, ds_weight_aux1, ds_weight_aux2, 1 if optimizer.lower() == "adamw" else 0,
+                       beta1, beta2, eps, weight_decay, dropout_rate, int(freeze_encoder))
+
+
+def comm_unique_id():
+    """128-byte RCCL unique id (rank 0 creates it and shares it, e.g. through torch.distributed)."""
+    buf = (C.c_char * 128)()
+    call("adp_comm_unique_id", buf)
+    return bytes(buf)
+
+
+def comm_init(nranks, uid, rank):
+    buf = (C.c_char * 128).from_buffer_copy(uid)
+    comm = C.c_void_p()
+    call("adp_comm_init", nranks, buf, rank, C.byref(comm))
+    return comm
+
+
+def comm_destroy(comm):
+    call("adp_comm_destroy", comm)
 
 
 class NativeAdiposeV3:
@@ -91,3 +132,21 @@ class NativeAdiposeV3:
     def predict_single(self, image, mean, std):
         """segmentation_inference.py:153-158: new float32 numpy (S, S) array."""
         return self.predict_batch(image, mean, std)[0].cpu().numpy()
+
+    # ------------------------------------------------------------------------------ training
+    def set_comm(self, comm):
+        """Attach an RCCL communicator (comm_init) for data-parallel steps; None detaches."""
+        call("adp_set_comm", self._h, comm)
+
+    def train_step(self, x, y, lr, cfg=None):
+        """One native training step: x (n, S, S) normalised images, y (n, S, S) labels (host or device).
+        Returns the Keras per-batch metrics (METRIC_NAMES)."""
+        cfg = cfg or train_cfg()
+        xs = [t if isinstance(t, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(t, np.float32))
+              for t in (x, y)]
+        xd, yd = (t.to(self.device, torch.float32).contiguous() for t in xs)
+        if xd.dim() == 2:
+            xd, yd = xd[None], yd[None]
+        m = (C.c_float * 6)()
+        call("adp_train_step", self._h, ptr(xd), ptr(yd), xd.shape[0], C.byref(cfg), float(lr), m, stream_ptr())
+        return dict(zip(METRIC_NAMES, (float(v) for v in m)))

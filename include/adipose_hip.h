@@ -29,8 +29,9 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 7 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
-                              v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy */
+#define ADP_ABI_VERSION 8 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+                              v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
+                              v8: adp_train_step / adp_set_comm / adp_comm_* */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -289,6 +290,36 @@ int adp_get_param(adp_handle* h, const char* layer, int slot, float* host, size_
  * (synchronous). One handle per device and thread. */
 int adp_forward(adp_handle* h, const float* images, int n, long long img_stride, float mean, float std,
                 int tta_mode, float* prob, adp_stream_t s);
+
+/* One training step of AdiposeUNetV3 (model.net.fit, train_adipose_unet_v3.py:1316-1324) on the handle:
+ * forward with dropout -> main / deep-supervision losses and their gradients (compile_model :780-879:
+ * OHEM or BCE+Dice main head, BCE+Dice aux heads, label smoothing :244-279, weights 1.0 / 0.4 / 0.3) ->
+ * backward -> [SUM all-reduce of the gradients over the communicator of adp_set_comm] -> Adam / AdamW
+ * (Keras 2.13 update, :800-806). Frozen encoder (freeze_encoder_layers :760-772): no encoder
+ * gradients or updates. x: n device f32 (S,S) normalised images, y: n device f32 (S,S) labels in {0,1};
+ * n <= max_batch. metrics (host, 6 floats, the call synchronises the stream): loss, main_out_loss,
+ * aux_out1_loss, aux_out2_loss, main_out_dice_coef, main_out_binary_accuracy (Keras' per-batch values;
+ * with a communicator: of the global batch). The first call allocates the optimizer state (m, v = 0). */
+typedef struct adp_train_cfg {
+  int use_hard_mining;       /* OHEM main loss (--use-hard-mining, default on) */
+  float hard_example_ratio;  /* 0.7 */
+  int use_label_smoothing;
+  float epsilon_pos, epsilon_neg;          /* 0.03, 0.07 */
+  float w_main, w_aux1, w_aux2;            /* 1.0, 0.4, 0.3 */
+  int optimizer;             /* 0 Adam, 1 AdamW (weight_decay) */
+  float beta1, beta2, eps, weight_decay;   /* 0.9, 0.999, 1e-7, 0.01 */
+  float dropout_rate;        /* 0.3 (build_model dropout_rate) */
+  int freeze_encoder;        /* phase 1 */
+} adp_train_cfg;
+int adp_train_step(adp_handle* h, const float* x, const float* y, int n, const adp_train_cfg* cfg, float lr,
+                   float* metrics, adp_stream_t s);
+/* Data-parallel training: comm is an RCCL ncclComm_t (one rank per GPU); NULL detaches. RCCL is loaded
+ * at run time (librccl.so.1). The helpers create a communicator without another framework:
+ * adp_comm_unique_id fills 128 bytes on one rank, which every rank passes to adp_comm_init. */
+int adp_set_comm(adp_handle* h, void* comm);
+int adp_comm_unique_id(void* id128);
+int adp_comm_init(int nranks, const void* id128, int rank, void** comm);
+int adp_comm_destroy(void* comm);
 
 #ifdef __cplusplus
 }

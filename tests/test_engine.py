@@ -87,3 +87,99 @@ def test_engine_bf16_matches_python_bf16_predictor(weights):
     assert np.abs(got - exact).max() <= 2e-2
     eng.close()
     f32.close()
+
+
+def _train_data(seed, B=2):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((B, S, S)).astype(np.float32)
+    yy, xx = np.mgrid[0:S, 0:S]
+    y = np.stack([((yy - 20 - 8 * b) ** 2 + (xx - 30) ** 2 < 300).astype(np.float32) for b in range(B)])
+    return x, y
+
+
+def _python_trainer(weights, dtype, cpad=None, lr=1e-3, freeze=False):
+    from adipose_amd.nets import AdiposeV3Net
+    from adipose_amd.trainer import LossConfig, Trainer
+    net = AdiposeV3Net(2, S, dtype=dtype, device="cuda", deep_supervision=True, cpad=cpad)
+    net.set_weights(weights)
+    tr = Trainer(net, LossConfig(), optimizer="adam", lr=lr)
+    if freeze:
+        tr.set_frozen(net.ENCODER)
+    return net, tr
+
+
+def _compare_weights(a, b, lr, steps):
+    n_big, n_all, worst = 0, 0, 0.0
+    for k in a:
+        for u, v in zip(a[k], b[k]):
+            d = np.abs(np.asarray(u, np.float32).ravel() - np.asarray(v, np.float32).ravel())
+            n_big += int((d > 1e-6).sum())
+            n_all += d.size
+            worst = max(worst, float(d.max()))
+    # Adam's first steps move every weight by ~lr * sign(g): a gradient that is zero up to rounding may
+    # take either sign in two f32 atomic summation orders, so a few elements may differ by <= 2 lr
+    assert worst <= 2 * lr * steps + 1e-6 and n_big <= 1e-3 * n_all, (worst, n_big, n_all)
+
+
+@pytest.mark.parametrize("freeze", [False, True])
+def test_native_train_step_matches_python_f32(weights, freeze):
+    """adp_train_step (csrc/engine.cpp) vs the Python schedule (trainer.Trainer over nets.AdiposeV3Net):
+    OHEM main + BCE-Dice aux losses with dropout 0.3, Adam; per-step Keras metrics and the weights after
+    two steps; frozen encoder = no encoder update."""
+    from adipose_amd.engine import NativeAdiposeV3, train_cfg
+    lr = 1e-3
+    x, y = _train_data(7)
+    net, tr = _python_trainer(weights, "f32", lr=lr, freeze=freeze)
+    eng = NativeAdiposeV3(tile=S, max_batch=2, dtype="f32")
+    eng.set_weights(weights)
+    cfg = train_cfg(freeze_encoder=freeze)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    for step in range(2):
+        tr.train_step(xd, yd)
+        ref = tr.read_metrics()
+        got = eng.train_step(x, y, lr, cfg)
+        for k, v in got.items():
+            assert abs(v - ref[k]) <= 2e-5 * max(1.0, abs(ref[k])), (step, k, v, ref[k])
+    w_eng, w_py = eng.get_weights(), net.get_weights()
+    _compare_weights(w_eng, w_py, lr, 2)
+    if freeze:
+        for k in net.ENCODER:
+            np.testing.assert_array_equal(w_eng[k][0], np.asarray(weights[k][0], np.float32).ravel())
+    # inference after training uses the trained weights (adp_forward)
+    from adipose_amd.predictor import HipUnetPredictor
+    p_eng = eng.predict_batch(x * 50 + 127, 127.0, 50.0).cpu().numpy()
+    p_py = HipUnetPredictor(net, max_batch=2).predict_views(list(x * 50 + 127), 127.0, 50.0, [0]).cpu().numpy()
+    assert np.abs(p_eng - p_py).max() <= 1e-4
+    eng.close()
+
+
+def test_native_train_step_bf16_and_comm(weights):
+    """bf16 native step vs the Python bf16 schedule on the same channel layout; then the same step through
+    a one-rank RCCL communicator (adp_comm_unique_id / adp_comm_init / adp_set_comm: the gradient and loss
+    all-reduces run) equals the step without one."""
+    from adipose_amd.engine import NativeAdiposeV3, comm_destroy, comm_init, comm_unique_id, train_cfg
+    lr = 1e-3
+    x, y = _train_data(8)
+    net, tr = _python_trainer(weights, "bf16", cpad=(8, 8, 64, 64), lr=lr)
+    eng = NativeAdiposeV3(tile=S, max_batch=2, dtype="bf16")
+    eng.set_weights(weights)
+    tr.train_step(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+    ref = tr.read_metrics()
+    got = eng.train_step(x, y, lr, train_cfg())
+    for k, v in got.items():
+        assert abs(v - ref[k]) <= 1e-3 * max(1.0, abs(ref[k])), (k, v, ref[k])
+    a = NativeAdiposeV3(tile=S, max_batch=2, dtype="f32")
+    b = NativeAdiposeV3(tile=S, max_batch=2, dtype="f32")
+    a.set_weights(weights)
+    b.set_weights(weights)
+    comm = comm_init(1, comm_unique_id(), 0)
+    b.set_comm(comm)
+    cfg = train_cfg(dropout_rate=0.0)
+    ma, mb = a.train_step(x, y, lr, cfg), b.train_step(x, y, lr, cfg)
+    for k in ma:
+        assert abs(ma[k] - mb[k]) <= 1e-6 * max(1.0, abs(ma[k])), k
+    _compare_weights(a.get_weights(), b.get_weights(), lr, 1)
+    b.set_comm(None)
+    comm_destroy(comm)
+    for e in (eng, a, b):
+        e.close()
