@@ -160,7 +160,7 @@ def test_native_train_step_bf16_and_comm(weights):
     from adipose_amd.engine import NativeAdiposeV3, comm_destroy, comm_init, comm_unique_id, train_cfg
     lr = 1e-3
     x, y = _train_data(8)
-    net, tr = _python_trainer(weights, "bf16", cpad=(8, 8, 64, 64), lr=lr)
+    net, tr = _python_trainer(weights, "bf16", cpad=(64, 64, 64, 64), lr=lr)
     eng = NativeAdiposeV3(tile=S, max_batch=2, dtype="bf16")
     eng.set_weights(weights)
     tr.train_step(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
