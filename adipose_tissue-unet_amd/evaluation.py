@@ -15,8 +15,8 @@ Same names, arguments, return values and printed summaries as the reference:
 
 MI355X-first differences (same results): predictions stay float32 device tensors until a CPU-only
 metric needs them; the threshold search counts every threshold of the grid for a tile in ONE GPU pass
-(adp_threshold_hist) instead of one numpy pass per threshold. Boundary (EDT) and AUC metrics run on the
-host with scipy / scikit-learn as in the reference. cv2, tifffile, skimage and matplotlib are not
+(adp_threshold_hist) instead of one numpy pass per threshold, ROC / PR AUC in one sort-and-scan GPU pass
+(adp_auc_metrics). Boundary (EDT) metrics run on the host with scipy as in the reference. cv2, tifffile, skimage and matplotlib are not
 installed here: images/masks are read with PIL, skimage.morphology.binary_erosion is restated with
 scipy.ndimage (cross footprint, border_value=1, as skimage 0.21 does), and the 4-panel figure and the
 BoundaryRefiner are restated without cv2/matplotlib (their pixel output is "parity unpinned").
@@ -238,18 +238,20 @@ def calculate_boundary_metrics(pred, true, threshold: float = 0.5, spacing=(1.0,
 
 
 def calculate_auc_metrics(pred, true) -> Dict[str, float]:
-    """:847-888 (scikit-learn roc_auc_score / average_precision_score)."""
-    from sklearn.metrics import average_precision_score, roc_auc_score
-    pred_flat = _host(pred).flatten()
-    true_flat = (_host(true) > 0.5).astype(int).flatten()
-    if len(np.unique(true_flat)) < 2:
-        return {"roc_auc": np.nan, "pr_auc": np.nan}
-    try:
-        return {"roc_auc": float(roc_auc_score(true_flat, pred_flat)),
-                "pr_auc": float(average_precision_score(true_flat, pred_flat))}
-    except Exception as e:  # noqa: BLE001
-        warnings.warn(f"Error calculating AUC metrics: {e}")
-        return {"roc_auc": np.nan, "pr_auc": np.nan}
+    """:847-888 — roc_auc_score / average_precision_score of the flattened map (truth > 0.5 positive),
+    computed on the GPU (adp_auc_metrics: radix sort + scans, exact pixel counts, ties grouped by score);
+    NaN for a single-class mask."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    p = (pred if isinstance(pred, torch.Tensor) else torch.from_numpy(np.asarray(pred, np.float32)))
+    t = (true if isinstance(true, torch.Tensor) else torch.from_numpy(np.asarray(true, np.float32)))
+    p = p.to(dev, torch.float32).contiguous().reshape(-1)
+    t = t.to(dev, torch.float32).contiguous().reshape(-1)
+    if p.numel() != t.numel() or p.numel() == 0:
+        raise ValueError("calculate_auc_metrics: prediction and mask sizes differ")
+    out = torch.empty(2, dtype=torch.float64, device=dev)
+    ops.call("adp_auc_metrics", p.numel(), ops.ptr(p), ops.ptr(t), ops.ptr(out), ops.stream_ptr())
+    roc, ap = out.cpu().tolist()
+    return {"roc_auc": float(roc), "pr_auc": float(ap)}
 
 
 def optimize_threshold_f1_slide_level(predictions, ground_truths, tile_paths, threshold_range=None):

@@ -31,7 +31,7 @@ extern "C" {
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
 #define ADP_ABI_VERSION 8 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
-                              v8: adp_train_step / adp_set_comm / adp_comm_* */
+                              v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -263,6 +263,11 @@ int adp_blend_accum(int H, int W, int T, int y0, int x0, const float* tile, cons
                     float* acc, float* wsum, adp_stream_t s);
 int adp_blend_finalize(size_t n, const float* acc, const float* wsum, float floor_, float* out,
                        adp_stream_t s);
+
+/* ROC AUC and average precision of a probability map against a mask (full_evaluation_enhanced.py:847-888:
+ * roc_auc_score / average_precision_score on the flattened pixels, truth > 0.5 positive; ties grouped by
+ * identical score). out: device f64[2] = {roc_auc, pr_auc}, NaN when only one class is present. */
+int adp_auc_metrics(size_t n, const float* pred, const float* truth, double* out, adp_stream_t s);
 
 /* ---- handle-level engine: native adipose_v3 inference for non-Python callers ---- */
 #define ADP_PRESET_ADIPOSE_V3 0

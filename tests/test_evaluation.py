@@ -110,13 +110,32 @@ def test_boundary_metrics_known_answers():
     assert E.calculate_boundary_metrics(full, full) == {"hausdorff95": float("inf"), "assd": float("inf")}
 
 
+@pytest.mark.gpu
 def test_auc_metrics_edge_cases():
-    rng = np.random.default_rng(2)
+    rng = np.random.default_rng(0)
     t = (rng.random((16, 16)) > 0.5).astype(np.float32)
     m = E.calculate_auc_metrics(t, t)
     assert m["roc_auc"] == 1.0 and m["pr_auc"] == 1.0
     m = E.calculate_auc_metrics(rng.random((16, 16)), np.zeros((16, 16)))
     assert np.isnan(m["roc_auc"]) and np.isnan(m["pr_auc"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,levels", [((64, 64), 0), ((256, 256), 17), ((1024, 1024), 0), ((1024, 1024), 255),
+                                          ((3, 1000), 3)])
+def test_auc_metrics_vs_sklearn(shape, levels):
+    """GPU ROC AUC / average precision (adp_auc_metrics) vs the reference's scikit-learn calls
+    (full_evaluation_enhanced.py:873-876) on continuous scores and on quantised scores (ties)."""
+    from sklearn.metrics import average_precision_score, roc_auc_score
+    rng = np.random.default_rng(sum(shape) + levels)
+    y = (rng.random(shape) > 0.7).astype(np.float32)
+    p = np.clip(0.35 * y + 0.65 * rng.random(shape), 0, 1).astype(np.float32)
+    if levels:
+        p = (np.round(p * levels) / levels).astype(np.float32)
+    m = E.calculate_auc_metrics(p, y)
+    yt, pf = (y > 0.5).astype(int).ravel(), p.ravel()
+    assert abs(m["roc_auc"] - roc_auc_score(yt, pf)) <= 1e-9
+    assert abs(m["pr_auc"] - average_precision_score(yt, pf)) <= 1e-9
 
 
 def test_boundary_refiner_shapes_and_fixed_points():
