@@ -31,7 +31,7 @@ extern "C" {
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
 #define ADP_ABI_VERSION 8 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
-                              v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics */
+                              v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -268,6 +268,15 @@ int adp_blend_finalize(size_t n, const float* acc, const float* wsum, float floo
  * roc_auc_score / average_precision_score on the flattened pixels, truth > 0.5 positive; ties grouped by
  * identical score). out: device f64[2] = {roc_auc, pr_auc}, NaN when only one class is present. */
 int adp_auc_metrics(size_t n, const float* pred, const float* truth, double* out, adp_stream_t s);
+/* scipy.ndimage.distance_transform_edt(~(src > thr), sampling=(sy, sx)): dist (device f64 H x W) = Euclidean
+ * distance to the nearest pixel with src > thr (inf if there is none). Exact (separable lower envelope). */
+int adp_distance_transform(int H, int W, const float* src, float thr, double sy, double sx, double* dist,
+                           adp_stream_t s);
+/* calculate_boundary_metrics (full_evaluation_enhanced.py:788-844) on the GPU: out (HOST f64[2]) =
+ * {hausdorff95, assd}; 0 / 0 for two empty masks, inf for one empty mask or an empty surface. The
+ * reference's pairing is kept (each distance map is sampled at its own mask's surface). Synchronises s. */
+int adp_boundary_metrics(int H, int W, const float* pred, const float* truth, float thr, double sy, double sx,
+                         double* out, adp_stream_t s);
 
 /* ---- handle-level engine: native adipose_v3 inference for non-Python callers ---- */
 #define ADP_PRESET_ADIPOSE_V3 0

@@ -94,6 +94,7 @@ def test_load_validation_data_pairs_by_stem(tmp_path):
         E.load_validation_data(str(tmp_path / "missing"))
 
 
+@pytest.mark.gpu
 def test_boundary_metrics_known_answers():
     t = np.zeros((32, 32), np.float32)
     t[8:20, 8:20] = 1
@@ -280,3 +281,38 @@ def test_publication_evaluation_vs_oracle(tmp_path):
                "--no-visualizations", "--sliding-window", "--overlap", "0.25"])
     assert rc == 0
     assert (ck / "evaluation" / "val_original_sw_gaussian_o25" / "val_comprehensive_results.csv").exists()
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,spacing", [((64, 64), (1.0, 1.0)), ((200, 136), (1.0, 1.0)), ((96, 80), (0.5, 2.0)),
+                                           ((1024, 1024), (1.0, 1.0))])
+def test_distance_transform_vs_scipy(shape, spacing):
+    """GPU exact EDT (adp_distance_transform) vs scipy.ndimage.distance_transform_edt on sparse random
+    masks (large, non-trivial distances) with isotropic and anisotropic sampling."""
+    from scipy import ndimage
+    rng = np.random.default_rng(shape[0] + shape[1])
+    m = rng.random(shape) > 0.003   # few zeros -> long distances
+    m[rng.integers(0, shape[0]), rng.integers(0, shape[1])] = False
+    got = E.distance_transform_edt(m, sampling=spacing).cpu().numpy()
+    ref = ndimage.distance_transform_edt(m, sampling=spacing)
+    assert np.abs(got - ref).max() <= 1e-9 * max(1.0, ref.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_boundary_metrics_vs_oracle(seed):
+    """calculate_boundary_metrics on the GPU vs the line-for-line scipy restatement of :788-844."""
+    from oracle import numpy_ref as NR
+    rng = np.random.default_rng(seed)
+    H, W = 128, 96
+    yy, xx = np.mgrid[0:H, 0:W]
+    t = (((yy - 60) ** 2 + (xx - 40) ** 2) < 900).astype(np.float32)
+    p = np.clip(t * 0.8 + rng.random((H, W)) * 0.4 - 0.1, 0, 1).astype(np.float32)
+    if seed == 3:
+        t[:] = 1.0   # full mask: no surface -> inf
+    for thr in (0.3, 0.5, 0.7):
+        got = E.calculate_boundary_metrics(p, t, thr, spacing=(1.0, 1.5))
+        ref = NR.boundary_metrics(p, t, thr, spacing=(1.0, 1.5))
+        for k in ("hausdorff95", "assd"):
+            assert got[k] == ref[k] or abs(got[k] - ref[k]) <= 1e-9, (k, got, ref)
