@@ -306,19 +306,31 @@ __global__ void bn_finalize_kernel(int C, float count, const float* sum, const f
 }
 
 // dst{0,1}[c] += sum over the replicas of scratch[r][{0,1}][c]; the replicas are re-zeroed
+// block = 64 channels x 4 replica groups of STAT_REPL / 4: a thread sums 16 replicas (and zeroes them),
+// the four partial sums meet in LDS (a launch-latency-bound fold: 4x shorter dependent chain)
 __global__ void stat_fold_kernel(int C, float* scratch, float* dst0, float* dst1) {
-  const int c = blockIdx.x * TPB + threadIdx.x;
-  if (c >= C) return;
+  constexpr int RG = 4, RPER = adp::STAT_REPL / RG;
+  __shared__ float part[2][RG][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s0 = 0.f, s1 = 0.f;
-  for (int r = 0; r < adp::STAT_REPL; ++r) {
-    float* p = scratch + (size_t)r * 2 * adp::STAT_CMAX + c;
-    s0 += p[0];
-    s1 += p[adp::STAT_CMAX];
-    p[0] = 0.f;
-    p[adp::STAT_CMAX] = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int r = rg * RPER; r < (rg + 1) * RPER; ++r) {
+      float* p = scratch + (size_t)r * 2 * adp::STAT_CMAX + c;
+      s0 += p[0];
+      s1 += p[adp::STAT_CMAX];
+      p[0] = 0.f;
+      p[adp::STAT_CMAX] = 0.f;
+    }
   }
-  dst0[c] += s0;
-  dst1[c] += s1;
+  part[0][rg][cl] = s0;
+  part[1][rg][cl] = s1;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    dst0[c] += (part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]);
+    dst1[c] += (part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]);
+  }
 }
 
 // per-channel sums of dBN and dBN*xhat; block = 256 threads as (pixel lane) x (channel group)
@@ -626,7 +638,7 @@ void* scratch(int slot, size_t bytes) {
 int stat_fold(int C, float* dst0, float* dst1, hipStream_t s) {
   float* sc = stat_scratch();
   if (!sc) return -1;
-  hipLaunchKernelGGL(stat_fold_kernel, dim3((C + TPB - 1) / TPB), dim3(TPB), 0, s, C, sc, dst0, dst1);
+  hipLaunchKernelGGL(stat_fold_kernel, dim3((C + 63) / 64), dim3(256), 0, s, C, sc, dst0, dst1);
   return check_launch("stat_fold");
 }
 }  // namespace adp
