@@ -322,17 +322,16 @@ class UNetEngine:
             ops.fill(t.view(torch.float32) if t.numel() % 2 == 0 else t, 0.0)
 
     def pack_forward_weights(self):
-        """Per step: master f32 -> compute-dtype forward layout (cast) for every dense layer."""
+        """Per step: master f32 -> compute-dtype forward layout for every dense layer. The forward layout
+        of a layer is its master layout, so bf16 is ONE cast of the whole flat parameter buffer into a
+        flat mirror (one launch instead of one per layer); the layers' weights are views into it."""
+        if self.dt != torch.float32:
+            mirror = self.buf("wf/flat", (self.ps.total,))
+            ops.cast(self.ps.flat, mirror)
         for l in self.layers.values():
             if not isinstance(l, Dense):
                 continue
-            src = self.ps.view(l.name + "/W")
-            if self.dt == torch.float32:
-                self._packed[l.name] = src
-            else:
-                dst = self.buf("wf/" + l.name, (l.Npad, l.Kpad))
-                ops.pack_weights(src, dst, 0)
-                self._packed[l.name] = dst
+            self._packed[l.name] = self.ps.view(l.name + "/W", None if self.dt == torch.float32 else mirror)
 
     def pack_dgrad_weights(self, names):
         for n in names:

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Same-process A/B of two host-schedule variants of the bench step (unet_bn L5, 1024^2, B=4, bf16):
+alternating timed blocks so that clock drift and device variance hit both arms alike.
+  --variant pack: per-layer forward-weight packs (old) vs one flat cast (UNetEngine.pack_forward_weights)"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--variant", default="pack", choices=["pack"])
+    p.add_argument("--rounds", type=int, default=4)
+    p.add_argument("--steps", type=int, default=8)
+    args = p.parse_args()
+    import numpy as np
+    import torch
+
+    import _adipose_pkg  # noqa: F401
+    from adipose_amd import ops
+    from adipose_amd.data import synthetic_batch
+    from adipose_amd.nets import Dense, UNetBN, UNetEngine
+    from adipose_amd.trainer import LossConfig, Trainer
+
+    dev = torch.device("cuda", 0)
+    net = UNetBN(4, 1024, levels=5, base=64, in_ch=3, dtype="bf16", device=dev, seed=865)
+    tr = Trainer(net, LossConfig(use_hard_mining=False), lr=1e-4)
+    xs, ys = synthetic_batch(4, 1024, channels=3, seed=865)
+    x = torch.from_numpy(((xs - xs.mean()) / (xs.std() + 1e-10)).astype(np.float32)).to(dev)
+    y = torch.from_numpy(ys).to(dev)
+    new = UNetEngine.pack_forward_weights
+
+    def old(self):
+        for l in self.layers.values():
+            if isinstance(l, Dense):
+                dst = self.buf("wf_old/" + l.name, (l.Npad, l.Kpad))
+                ops.pack_weights(self.ps.view(l.name + "/W"), dst, 0)
+                self._packed[l.name] = dst
+    arms = {"A (old)": old, "B (new)": new}
+    for fn in arms.values():
+        UNetEngine.pack_forward_weights = fn
+        for _ in range(3):
+            tr.train_step(x, y)
+    res = {k: [] for k in arms}
+    for _ in range(args.rounds):
+        for k, fn in arms.items():
+            UNetEngine.pack_forward_weights = fn
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                tr.train_step(x, y)
+            torch.cuda.synchronize()
+            res[k].append((time.perf_counter() - t0) / args.steps * 1e3)
+    for k, v in res.items():
+        print(k, "ms/step", [round(t, 3) for t in v], "min", round(min(v), 3), flush=True)
+
+
+if __name__ == "__main__":
+    main()
