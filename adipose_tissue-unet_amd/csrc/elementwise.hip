@@ -42,6 +42,44 @@ __global__ void pack_kernel(int mode, int taps, int Cin_s, int Nout, const float
   }
 }
 
+// Batched data-gradient repack (modes 1/2 of pack_kernel for many layers in one launch): dst tiles of
+// 64 rows (ci) x 64 columns (k = t * Nout + co) are gathered through LDS so that both the source reads
+// (along ci) and the destination writes (along k) are coalesced; pad rows / columns are written as 0.
+struct PackJobs {
+  adp_pack_job j[ADP_PACK_MAX_JOBS];
+  int tile0[ADP_PACK_MAX_JOBS + 1];   // prefix sums of 64x64 destination tiles
+  int n;
+};
+
+template <typename To>
+__global__ __launch_bounds__(256) void pack_t_kernel(PackJobs P) {
+  __shared__ float tile[64][65];
+  int jb = 0;
+  while (jb + 1 < P.n && (int)blockIdx.x >= P.tile0[jb + 1]) ++jb;
+  const adp_pack_job& J = P.j[jb];
+  const int t_local = blockIdx.x - P.tile0[jb];
+  const int ktiles = (J.dst_kpad + 63) / 64;
+  const int r0 = (t_local / ktiles) * 64, k0 = (t_local % ktiles) * 64;
+  const float* src = J.src;
+  const int tid = threadIdx.x, KN = J.taps * J.Nout;
+  // load: thread column = ci (coalesced along the source row), 4 k rows per pass
+  for (int kk = tid >> 6; kk < 64; kk += 4) {
+    const int k = k0 + kk, ci = r0 + (tid & 63);
+    float v = 0.f;
+    if (k < KN && ci < J.Cin_s) {
+      const int t = k / J.Nout, co = k - t * J.Nout;
+      v = src[(size_t)co * J.src_kpad + (size_t)(J.taps - 1 - t) * J.Cin_s + ci];
+    }
+    tile[kk][tid & 63] = v;
+  }
+  __syncthreads();
+  To* dst = reinterpret_cast<To*>(J.dst);
+  for (int rr = tid >> 6; rr < 64; rr += 4) {
+    const int r = r0 + rr, k = k0 + (tid & 63);
+    if (r < J.dst_rows && k < J.dst_kpad) dst[(size_t)r * J.dst_kpad + k] = from_f<To>(tile[tid & 63][rr]);
+  }
+}
+
 // ------------------------------------------------------------------------------ max-pool
 template <typename T>
 ADP_DEV void load_bn(Grp<T>& g, const T* p, const float* sc, const float* sh, int c, float* f) {
@@ -660,6 +698,26 @@ extern "C" int adp_pack_weights(int dtype_out, int mode, int taps, int Cin_s, in
                hipLaunchKernelGGL(pack_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, mode, taps,
                                   Cin_s, Nout, src, src_kpad, (T*)dst, dst_rows, dst_kpad));
   return adp::check_launch("adp_pack_weights");
+}
+
+extern "C" int adp_pack_weights_batch(int dtype_out, int n, const adp_pack_job* jobs, adp_stream_t st) {
+  ADP_REQUIRE(n >= 1 && n <= ADP_PACK_MAX_JOBS && jobs, "adp_pack_weights_batch: 1..ADP_PACK_MAX_JOBS jobs");
+  PackJobs P{};
+  P.n = n;
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const adp_pack_job& J = jobs[i];
+    ADP_REQUIRE(J.src && J.dst && J.taps >= 1 && J.Cin_s > 0 && J.Nout > 0 && J.dst_rows >= J.Cin_s &&
+                    J.dst_kpad >= J.taps * J.Nout && J.src_kpad >= J.taps * J.Cin_s,
+                "adp_pack_weights_batch: job shape mismatch");
+    P.j[i] = J;
+    P.tile0[i] = tiles;
+    tiles += ((J.dst_rows + 63) / 64) * ((J.dst_kpad + 63) / 64);
+  }
+  P.tile0[n] = tiles;
+  DTYPE_SWITCH(dtype_out, T,
+               hipLaunchKernelGGL(pack_t_kernel<T>, dim3(tiles), dim3(256), 0, (hipStream_t)st, P));
+  return adp::check_launch("adp_pack_weights_batch");
 }
 
 extern "C" int adp_maxpool2_fwd(int dtype, int N, int H, int W, int C, const void* src,

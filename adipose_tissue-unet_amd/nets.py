@@ -334,15 +334,17 @@ class UNetEngine:
             self._packed[l.name] = self.ps.view(l.name + "/W", None if self.dt == torch.float32 else mirror)
 
     def pack_dgrad_weights(self, names):
+        """Flipped / transposed data-gradient weights of the named layers, batched into one launch
+        (adp_pack_weights_batch: ConvT = 1 tap over 4*C outputs, conv = 9 flipped taps)."""
+        jobs = []
         for n in names:
             l = self.layers[n]
-            src = self.ps.view(n + "/W")
             dst = self.buf("wd/" + n, (l.dNpad, l.dKpad))
-            if l.transpose:
-                ops.pack_weights(src, dst, 2, taps=1, cin_s=l.Cin_s, nout=l.Nout)
-            else:
-                ops.pack_weights(src, dst, 1, taps=l.taps, cin_s=l.Cin_s, nout=l.cout_s)
+            jobs.append((self.ps.view(n + "/W"), dst, 1 if l.transpose else l.taps, l.Cin_s,
+                         l.Nout if l.transpose else l.cout_s))
             self._packed["d/" + n] = dst
+        if jobs:
+            ops.pack_weights_batch(jobs)
 
     def Wf(self, name):
         return self._packed[name]

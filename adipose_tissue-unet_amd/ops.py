@@ -270,6 +270,33 @@ def pack_weights(src, dst, mode, *, taps=1, cin_s=0, nout=0):
          int(dst.shape[0]), int(dst.shape[1]), stream_ptr())
 
 
+class PackJob(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("taps", C.c_int), ("Cin_s", C.c_int), ("Nout", C.c_int),
+                ("src_kpad", C.c_int), ("dst_rows", C.c_int), ("dst_kpad", C.c_int)]
+
+
+PACK_MAX_JOBS = 24
+
+
+def pack_weights_batch(jobs):
+    """Data-gradient repack (pack_weights modes 1/2) of many layers in one launch per 24 layers:
+    jobs = [(src f32 [Npad][Kpad], dst [dNpad][dKpad], taps, cin_s, nout)], dst all of one dtype."""
+    for i in range(0, len(jobs), PACK_MAX_JOBS):
+        chunk = jobs[i:i + PACK_MAX_JOBS]
+        arr = (PackJob * len(chunk))()
+        dc = None
+        for k, (src, dst, taps, cin_s, nout) in enumerate(chunk):
+            _check(src.dtype == torch.float32 and src.dim() == 2 and dst.dim() == 2 and dst.is_contiguous(),
+                   "pack_weights_batch: bad tensors")
+            _check(dst.shape[0] >= cin_s and dst.shape[1] >= taps * nout and src.shape[0] >= nout
+                   and src.shape[1] >= taps * cin_s, "pack_weights_batch: shape mismatch")
+            _check(dc is None or dtype_code(dst) == dc, "pack_weights_batch: one destination dtype")
+            dc = dtype_code(dst)
+            arr[k] = PackJob(ptr(src), ptr(dst), taps, cin_s, nout, int(src.shape[1]), int(dst.shape[0]),
+                             int(dst.shape[1]))
+        call("adp_pack_weights_batch", dc, len(chunk), arr, stream_ptr())
+
+
 def pack_weights_fp8(src, dst, scale):
     """Forward-layout fp8 weights + per-row dequantisation scale (adp_pack_weights_fp8)."""
     _check(src.dtype == torch.float32 and src.dim() == 2 and dst.dtype == FP8_DTYPE and dst.dim() == 2

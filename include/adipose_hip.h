@@ -31,7 +31,7 @@ extern "C" {
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
 #define ADP_ABI_VERSION 8 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
-                              v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics */
+                              v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -119,6 +119,15 @@ int adp_conv_wgrad(int dtype, const adp_conv_desc* d, const adp_conv_io* io, con
  * mode 1 = 3x3 flip+transpose (data-gradient of a conv), mode 2 = ConvTranspose transpose. */
 int adp_pack_weights(int dtype_out, int mode, int taps, int Cin_s, int Nout, const float* src,
                      int src_kpad, void* dst, int dst_rows, int dst_kpad, adp_stream_t s);
+/* Modes 1/2 of adp_pack_weights for up to ADP_PACK_MAX_JOBS layers in one launch (LDS-tiled transpose,
+ * coalesced both ways): dst[ci][t*Nout + co] = src[co][(taps-1-t)*Cin_s + ci], zeros elsewhere. */
+#define ADP_PACK_MAX_JOBS 24
+typedef struct adp_pack_job {
+  const float* src;
+  void* dst;
+  int taps, Cin_s, Nout, src_kpad, dst_rows, dst_kpad;
+} adp_pack_job;
+int adp_pack_weights_batch(int dtype_out, int n, const adp_pack_job* jobs, adp_stream_t s);
 /* Forward-layout fp8 weights with a per-row (output channel) scale: scale[r] = max_k |src[r][k]| / 448
  * (1 for an all-zero row), dst[r][k] = e4m3(src[r][k] / scale[r]) (saturating, round to nearest even). */
 int adp_pack_weights_fp8(int rows, const float* src, int src_kpad, void* dst, int dst_kpad, float* scale,

@@ -613,3 +613,25 @@ def test_pixel_counts_and_blend():
     pb, tb = pred > 0.5, true > 0.5
     ref = [int((pb & tb).sum()), int((pb & ~tb).sum()), int((~pb & tb).sum()), int((~pb & ~tb).sum())]
     assert c.cpu().tolist() == ref
+
+
+def test_pack_weights_batch_matches_per_layer():
+    """Batched LDS-tiled data-gradient repack (adp_pack_weights_batch) == per-layer adp_pack_weights
+    (modes 1 and 2) for ragged shapes, both destination dtypes, several layers in one launch."""
+    g = torch.Generator().manual_seed(71)
+    shapes = [(9, 64, 64), (9, 48, 88), (1, 128, 256), (9, 176, 352), (9, 8, 64), (1, 64, 512)]
+    for dt in (torch.float32, torch.bfloat16):
+        jobs, refs = [], []
+        for taps, cin_s, nout in shapes:
+            Kpad, Npad = (taps * cin_s + 31) // 32 * 32, (nout + 63) // 64 * 64
+            src = torch.randn(Npad, Kpad, generator=g).to(DEV)
+            rows, dkp = (cin_s + 63) // 64 * 64 + 64, (taps * nout + 31) // 32 * 32
+            ref = torch.full((rows, dkp), 7.0, device=DEV).to(dt)
+            ops.pack_weights(src, ref, 1 if taps == 9 else 2, taps=taps, cin_s=cin_s, nout=nout)
+            got = torch.full((rows, dkp), 7.0, device=DEV).to(dt)
+            jobs.append((src, got, taps, cin_s, nout))
+            refs.append(ref)
+        ops.pack_weights_batch(jobs)
+        torch.cuda.synchronize()
+        for (_, got, *_), ref in zip(jobs, refs):
+            assert torch.equal(got, ref)
