@@ -201,6 +201,32 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     __builtin_amdgcn_s_setprio(0);
   };
 
+  bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
+  if (a.debug_flags & 4) {
+    // plain double buffering: one barrier per K step; stage t+1 is filled while stage t multiplies
+    {
+      const Kt k0 = kinfo(0);
+      issueA(0, k0, 0); issueB(0, k0, 0); issueB(1, k0, 0); issueA(1, k0, 0);
+    }
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      T64_BAR();   // stage t landed for every wave, and nobody reads buffer buf ^ 1 any more
+      if (t + 1 < nk) {
+        const Kt k1 = kinfo(t + 1);
+        issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
+      }
+      readA(buf, 0, fa);
+      readB(buf, 0, fb0);
+      mma(fa, fb0, 0, 0);
+      readB(buf, 1, fb1);
+      mma(fa, fb1, 0, 1);
+      readA(buf, 1, fa);
+      mma(fa, fb1, 1, 1);
+      mma(fa, fb0, 1, 0);
+    }
+    T64_BAR();   // the epilogue reuses the stages
+  } else {
   // ---- prologue: K step 0 and (all but B0 of) step 1 in flight, wait for step 0
   {
     const Kt k0 = kinfo(0);
@@ -218,7 +244,6 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     T64_BAR();
   }
 
-  bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     const bool n1 = t + 1 < nk, pre = t + 2 < nk;
@@ -253,6 +278,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     T64_BAR();
+  }
   }
 
   // ---- epilogue: one wave row group (TM rows x BN) at a time through LDS
