@@ -91,6 +91,37 @@ ADP_DEV void load_bn(Grp<T>& g, const T* p, const float* sc, const float* sh, in
   }
 }
 
+// act = relu(z * sc + sh) (bn_apply) and its 2x2 max-pool in one pass: each thread owns a 2x2 pixel
+// block x 8 channels (the pool of the stored bf16 values equals the rounded pool of the f32 values:
+// rounding is monotone)
+template <typename T>
+__global__ void bn_apply_pool_kernel(int N, int H, int W, int C, const T* z, const float* sc, const float* sh,
+                                     T* act, T* pool) {
+  const int Ho = H >> 1, Wo = W >> 1, G = C >> 3;
+  size_t total = (size_t)N * Ho * Wo * G;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < total; i += (size_t)gridDim.x * TPB) {
+    const int g = (int)(i % G);
+    const size_t pix = i / G;
+    const int xo = (int)(pix % Wo);
+    const size_t t = pix / Wo;
+    const int yo = (int)(t % Ho), n = (int)(t / Ho);
+    const size_t b0 = (((size_t)n * H + 2 * yo) * W + 2 * xo) * C + g * 8;
+    const size_t off[4] = {0, (size_t)C, (size_t)W * C, (size_t)W * C + C};
+    float best[8], f[8];
+    Grp<T> gr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      load_bn(gr, z + b0 + off[q], sc, sh, g * 8, f);
+      grp_from_f(gr, f);
+      grp_store(gr, act + b0 + off[q]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) best[j] = (q == 0 || f[j] > best[j]) ? f[j] : best[j];
+    }
+    grp_from_f(gr, best);
+    grp_store(gr, pool + pix * C + g * 8);
+  }
+}
+
 template <typename T>
 __global__ void maxpool_fwd_kernel(int N, int H, int W, int C, const T* src, const float* sc,
                                    const float* sh, T* dst) {
@@ -718,6 +749,16 @@ extern "C" int adp_pack_weights_batch(int dtype_out, int n, const adp_pack_job* 
   DTYPE_SWITCH(dtype_out, T,
                hipLaunchKernelGGL(pack_t_kernel<T>, dim3(tiles), dim3(256), 0, (hipStream_t)st, P));
   return adp::check_launch("adp_pack_weights_batch");
+}
+
+extern "C" int adp_bn_apply_maxpool2(int dtype, int N, int H, int W, int C, const void* z, const float* sc,
+                                     const float* sh, void* act, void* pool, adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && H % 2 == 0 && W % 2 == 0 && sc && sh, "adp_bn_apply_maxpool2: need C%8==0, even H,W");
+  size_t n = (size_t)N * (H / 2) * (W / 2) * (C / 8);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL(bn_apply_pool_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, N, H, W,
+                                  C, (const T*)z, sc, sh, (T*)act, (T*)pool));
+  return adp::check_launch("adp_bn_apply_maxpool2");
 }
 
 extern "C" int adp_maxpool2_fwd(int dtype, int N, int H, int W, int C, const void* src,

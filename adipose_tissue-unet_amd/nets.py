@@ -704,8 +704,9 @@ class UNetBN(UNetEngine):
         s = self.st[name]
         return (s[2], s[3])
 
-    def _bn_conv(self, name, srcA, out, act, *, srcB=None, train=True):
-        """conv -> BN statistics (epilogue) -> scale/shift -> act = relu(bn(out)) materialised."""
+    def _bn_conv(self, name, srcA, out, act, *, srcB=None, train=True, pool=None):
+        """conv -> BN statistics (epilogue) -> scale/shift -> act = relu(bn(out)) materialised (and, with
+        pool, its 2x2 max-pool in the same pass)."""
         l = self.layers[name]
         s = self.st[name]
         if train:
@@ -721,7 +722,10 @@ class UNetBN(UNetEngine):
             # eval: count < 0 -> (sum, sqsum) are read as (running mean, running var)
             ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                             self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
-        ops.bn_apply(out, s[2], s[3], act)
+        if pool is not None:
+            ops.bn_apply_maxpool2(out, s[2], s[3], act, pool)
+        else:
+            ops.bn_apply(out, s[2], s[3], act)
 
     def forward(self, batch=None, *, train=False, seed=0, pack=True):
         a = self.acts(batch or self.B)
@@ -731,9 +735,9 @@ class UNetBN(UNetEngine):
         src = a["x"]
         for i in range(Lv):
             self._bn_conv(f"enc{i}_conv1", src, a[f"z{i}_1"], a[f"az{i}_1"], train=train)
-            self._bn_conv(f"enc{i}_conv2", a[f"az{i}_1"], a[f"z{i}_2"], a[f"az{i}_2"], train=train)
+            self._bn_conv(f"enc{i}_conv2", a[f"az{i}_1"], a[f"z{i}_2"], a[f"az{i}_2"], train=train,
+                          pool=a[f"pool{i}"] if i < Lv - 1 else None)
             if i < Lv - 1:
-                ops.maxpool2_fwd(a[f"az{i}_2"], a[f"pool{i}"])
                 src = a[f"pool{i}"]
         prev = a[f"az{Lv - 1}_2"]
         for i in range(Lv - 2, -1, -1):

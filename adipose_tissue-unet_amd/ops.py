@@ -315,6 +315,17 @@ def bn_apply_fp8(z, scale, shift, out):
     return out
 
 
+def bn_apply_maxpool2(z, scale, shift, act, pool):
+    """act = relu(z * scale + shift) and pool = 2x2 max-pool of act, one pass (adp_bn_apply_maxpool2)."""
+    _act(z, "z")
+    N, H, W, Cs = z.shape
+    _check(act.shape == z.shape and act.dtype == z.dtype, "bn_apply_maxpool2: act shape")
+    _check(tuple(pool.shape) == (N, H // 2, W // 2, Cs) and pool.dtype == z.dtype, "bn_apply_maxpool2: pool shape")
+    call("adp_bn_apply_maxpool2", dtype_code(z), N, H, W, Cs, ptr(z), ptr(scale), ptr(shift), ptr(act), ptr(pool),
+         stream_ptr())
+    return act
+
+
 def maxpool2_fwd(src, dst, bn=None):
     _act(src, "src")
     _act(dst, "dst")

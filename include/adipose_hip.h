@@ -31,7 +31,8 @@ extern "C" {
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
 #define ADP_ABI_VERSION 8 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
-                              v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch */
+                              v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
+                              adp_bn_apply_maxpool2 */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -150,6 +151,9 @@ int adp_maxpool2_bwd(int dtype, int N, int H, int W, int C_stride, const void* s
 int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C_stride, const void* src, const void* dpool,
                          const void* addend, void* dsrc, const void* z, const float* scale, const float* shift,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, adp_stream_t s);
+/* unet_bn encoder: act = relu(z * scale + shift) (adp_bn_apply) and pool = maxpool2(act) in one pass */
+int adp_bn_apply_maxpool2(int dtype, int N, int H, int W, int C_stride, const void* z, const float* scale,
+                          const float* shift, void* act, void* pool, adp_stream_t s);
 int adp_upsample2_bwd(int dtype, int N, int Hs, int Ws, int C_stride, const void* dup,
                       const void* addend, const void* mask, float mask_scale, void* dsrc,
                       adp_stream_t s);

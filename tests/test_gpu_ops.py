@@ -635,3 +635,20 @@ def test_pack_weights_batch_matches_per_layer():
         torch.cuda.synchronize()
         for (_, got, *_), ref in zip(jobs, refs):
             assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_bn_apply_maxpool_fused(dt):
+    """adp_bn_apply_maxpool2 == adp_bn_apply followed by adp_maxpool2_fwd, bit for bit."""
+    g = torch.Generator().manual_seed(81)
+    z = (torch.randn(2, 32, 48, 64, generator=g) * 2).to(DEV, dt)
+    sc = (torch.rand(64, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(64, generator=g) * 0.5).to(DEV)
+    a1, a2 = torch.empty_like(z), torch.empty_like(z)
+    p1 = torch.empty((2, 16, 24, 64), dtype=dt, device=DEV)
+    p2 = torch.empty_like(p1)
+    ops.bn_apply(z, sc, sh, a1)
+    ops.maxpool2_fwd(a1, p1)
+    ops.bn_apply_maxpool2(z, sc, sh, a2, p2)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, a2) and torch.equal(p1, p2)

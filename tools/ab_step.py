@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Same-process A/B of two host-schedule variants of the bench step (unet_bn L5, 1024^2, B=4, bf16):
 alternating timed blocks so that clock drift and device variance hit both arms alike.
-  --variant pack: per-layer forward-weight packs (old) vs one flat cast (UNetEngine.pack_forward_weights)"""
+  --variant pack: per-layer forward-weight packs (old) vs one flat cast (UNetEngine.pack_forward_weights)
+  --variant pool: bn_apply + maxpool2_fwd (old) vs the fused adp_bn_apply_maxpool2"""
 import argparse
 import os
 import sys
@@ -13,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--variant", default="pack", choices=["pack"])
+    p.add_argument("--variant", default="pack", choices=["pack", "pool"])
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--steps", type=int, default=8)
     args = p.parse_args()
@@ -32,23 +33,33 @@ def main():
     xs, ys = synthetic_batch(4, 1024, channels=3, seed=865)
     x = torch.from_numpy(((xs - xs.mean()) / (xs.std() + 1e-10)).astype(np.float32)).to(dev)
     y = torch.from_numpy(ys).to(dev)
-    new = UNetEngine.pack_forward_weights
+    if args.variant == "pack":
+        owner, attr = UNetEngine, "pack_forward_weights"
+        new = UNetEngine.pack_forward_weights
 
-    def old(self):
-        for l in self.layers.values():
-            if isinstance(l, Dense):
-                dst = self.buf("wf_old/" + l.name, (l.Npad, l.Kpad))
-                ops.pack_weights(self.ps.view(l.name + "/W"), dst, 0)
-                self._packed[l.name] = dst
+        def old(self):
+            for l in self.layers.values():
+                if isinstance(l, Dense):
+                    dst = self.buf("wf_old/" + l.name, (l.Npad, l.Kpad))
+                    ops.pack_weights(self.ps.view(l.name + "/W"), dst, 0)
+                    self._packed[l.name] = dst
+    else:
+        owner, attr = ops, "bn_apply_maxpool2"
+        new = ops.bn_apply_maxpool2
+
+        def old(z, scale, shift, act, pool):
+            ops.bn_apply(z, scale, shift, act)
+            ops.maxpool2_fwd(act, pool)
+            return act
     arms = {"A (old)": old, "B (new)": new}
     for fn in arms.values():
-        UNetEngine.pack_forward_weights = fn
+        setattr(owner, attr, fn)
         for _ in range(3):
             tr.train_step(x, y)
     res = {k: [] for k in arms}
     for _ in range(args.rounds):
         for k, fn in arms.items():
-            UNetEngine.pack_forward_weights = fn
+            setattr(owner, attr, fn)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(args.steps):
