@@ -189,6 +189,10 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
       }
       grp_from_f(gr, v);
       grp_store(gr, reinterpret_cast<bf16*>(a.out2) + (size_t)m * a.out2_stride + c);
+      if (a.bn_sum) {   // channel sums of the out2 part too (e.g. a ConvTranspose bias gradient)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { bs[j] += v[j]; bq[j] += v[j] * v[j]; }
+      }
       continue;
     } else {
       if (!a.out) continue;

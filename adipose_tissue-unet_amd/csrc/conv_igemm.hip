@@ -140,6 +140,7 @@ ADP_DEV void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[MI][NI], int mbase, int
             v = mv > 0.f ? v * a.mask2_scale : 0.f;
           }
           reinterpret_cast<T*>(a.out2)[(size_t)m * a.out2_stride + c] = from_f<T>(v);
+          if (a.bn_sum) { bsum[ni] += v; bsq[ni] += v * v; }
           continue;
         }
         if (!a.out) continue;

@@ -367,9 +367,9 @@ class UNetEngine:
                             relu=l.relu and not l.bn, dropout_rate=dropout, dropout_seed=seed, accum=accum,
                             bn_stats=bn_stats)
 
-    def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None):
+    def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None, bias_grad=True):
         dW = self.ps.gview(l.name + "/W")
-        dB = self.ps.gview(l.name + "/b") if (l.name + "/b") in self.ps.entries else None
+        dB = self.ps.gview(l.name + "/b") if bias_grad and (l.name + "/b") in self.ps.entries else None
         if l.transpose:
             ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, bnA=bnA, kh=1, kw=1, pad=0, shuffle_c=l.cout_s)
         else:
@@ -378,9 +378,10 @@ class UNetEngine:
         self._grad_ready(l.name)
 
     def dgrad(self, l, dZ, out, *, Ho=None, Wo=None, addend=None, mask=None, mask_scale=1.0, split=False,
-              out2=None, mask2=None, mask2_scale=1.0, skip_first=False, bn_reduce=None):
+              out2=None, mask2=None, mask2_scale=1.0, skip_first=False, bn_reduce=None, bn_stats=None):
         """Data gradient of a dense layer: a forward-shaped launch over dZ with repacked weights.
-        bn_reduce: fuse the BatchNorm-backward reduction of the layer `out` is the gradient of."""
+        bn_reduce: fuse the BatchNorm-backward reduction of the layer `out` is the gradient of.
+        bn_stats: per-channel sums (and sums of squares) of the stored gradient (split stores included)."""
         Wd = self.Wd(l.name)
         if l.transpose:
             # input coord = 2*o + (dy,dx): 4 taps, stride 2, over the ConvT output gradient
@@ -396,7 +397,7 @@ class UNetEngine:
         if split:
             return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=l.k, kw=l.k, dil=l.dil, out_mode=2, out2=out2,
                                 split_c=l.cin_s[0], addend=addend, mask=mask, mask_scale=mask_scale,
-                                mask2=mask2, mask2_scale=mask2_scale)
+                                mask2=mask2, mask2_scale=mask2_scale, bn_stats=bn_stats)
         return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=l.k, kw=l.k, dil=l.dil, addend=addend, mask=mask,
                             mask_scale=mask_scale, bn_reduce=bn_reduce)
 
@@ -876,12 +877,19 @@ class UNetBN(UNetEngine):
             self.wgrad(l1, a[f"az{i}_2"], dz1, srcB=a[f"t{i}"])
             sk = gb(f"skip{i}", a[f"z{i}_2"])
             dt = gb(f"dt{i}", a[f"t{i}"])
-            self.dgrad(l1, dz1, sk, split=True, out2=dt)
+            # the ConvTranspose bias gradient (sum of dt over pixels) comes out of this launch's epilogue
+            # channel sums (channels >= split_c are dt) instead of a separate pass over dt
+            lu = L[f"dec{i}_up"]
+            tsum = self.buf(f"g/dtsum{i}", (2, l1.Cin_s), torch.float32)
+            ops.fill(tsum, 0.0)
+            self.dgrad(l1, dz1, sk, split=True, out2=dt, bn_stats=(tsum[0], tsum[1]))
+            gb_up = self.ps.gview(lu.name + "/b")
+            c0 = l1.cin_s[0]
+            ops.add_mask(gb_up, gb_up, b=tsum[0, c0:c0 + gb_up.numel()])
             skip_grad[i] = sk
             # ConvTranspose dec{i}_up reads the previous level's activation
-            lu = L[f"dec{i}_up"]
             pact = a[f"ay{i + 1}_2"] if i + 1 < Lv - 1 else a[f"az{Lv - 1}_2"]
-            self.wgrad(lu, pact, dt)
+            self.wgrad(lu, pact, dt, bias_grad=False)
             dAp = gb(f"dA_up{i}", pact)
             if i + 1 < Lv - 1:
                 red = self._bn_red(f"dec{i + 1}_conv2", a[f"y{i + 1}_2"])
