@@ -103,6 +103,7 @@ _SIGS = {
     "adp_auc_metrics": [_S, _P, _P, _P, _P],
     "adp_pack_weights_batch": [_I, _I, _P, _P],
     "adp_bn_apply_maxpool2": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "adp_head_sigmoid_bwd_bnr": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "adp_distance_transform": [_I, _I, _P, _F, C.c_double, C.c_double, _P, _P],
     "adp_boundary_metrics": [_I, _I, _P, _P, _F, C.c_double, C.c_double, _P, _P],
     "adp_set_comm": [_P, _P],

@@ -120,6 +120,8 @@ float* stat_scratch();   // [STAT_REPL][2][STAT_CMAX] f32, or nullptr (error set
 // per-device growable scratch (slot 0: weight-gradient split partials); growing synchronises the device
 void* scratch(int slot, size_t bytes);
 int stat_fold(int C, float* dst0, float* dst1, hipStream_t s);   // elementwise.hip
+// the same over replica channels [c0, c0 + C) into dst0[0..C) (and dst1 unless nullptr)
+int stat_fold_at(int c0, int C, float* dst0, float* dst1, hipStream_t s);
 }  // namespace adp
 #define ADP_REQUIRE(cond, msg)          \
   do {                                  \

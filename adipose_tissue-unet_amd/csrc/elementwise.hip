@@ -398,7 +398,7 @@ __global__ void stat_fold_kernel(int C, float* scratch, float* dst0, float* dst1
   __syncthreads();
   if (rg == 0 && c < C) {
     dst0[c] += (part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]);
-    dst1[c] += (part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]);
+    if (dst1) dst1[c] += (part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]);
   }
 }
 
@@ -704,10 +704,11 @@ void* scratch(int slot, size_t bytes) {
   e.second = want;
   return e.first;
 }
-int stat_fold(int C, float* dst0, float* dst1, hipStream_t s) {
+int stat_fold(int C, float* dst0, float* dst1, hipStream_t s) { return stat_fold_at(0, C, dst0, dst1, s); }
+int stat_fold_at(int c0, int C, float* dst0, float* dst1, hipStream_t s) {
   float* sc = stat_scratch();
   if (!sc) return -1;
-  hipLaunchKernelGGL(stat_fold_kernel, dim3((C + 63) / 64), dim3(256), 0, s, C, sc, dst0, dst1);
+  hipLaunchKernelGGL(stat_fold_kernel, dim3((C + 63) / 64), dim3(256), 0, s, C, sc + c0, dst0, dst1);
   return check_launch("stat_fold");
 }
 }  // namespace adp

@@ -39,11 +39,16 @@ __global__ void head_fwd_kernel(size_t M, int Cs, int Cin, const T* x, const flo
       float f[8];
       grp_load(gr, x + m * Cs + g);
       grp_to_f(gr, f);
+      if (sc) {   // BatchNorm+ReLU on load, rounded to T as adp_bn_apply would materialize it
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[g + j], sh[g + j]), 0.f);
+        grp_from_f(gr, f);
+        grp_to_f(gr, f);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float v = sc ? fmaxf(fmaf(f[j], sc[g + j], sh[g + j]), 0.f) : f[j];
-        z0 = fmaf(v, ws[g + j], z0);
-        if (NOUT == 2) z1 = fmaf(v, ws[Cs + g + j], z1);
+        z0 = fmaf(f[j], ws[g + j], z0);
+        if (NOUT == 2) z1 = fmaf(f[j], ws[Cs + g + j], z1);
       }
     }
     // softmax over 2 logits, channel 1 kept == 1/(1+exp(z0-z1)); sigmoid otherwise
@@ -74,11 +79,16 @@ __global__ void head_fwd_grp_kernel(size_t M, int Cs, int Cin, const T* x, const
     grp_load(gr, x + m * Cs + g * 8);
     grp_to_f(gr, f);
     float z0 = 0.f, z1 = 0.f;
+    if (sc) {   // BatchNorm+ReLU on load, rounded to T as adp_bn_apply would materialize it
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f);
+      grp_from_f(gr, f);
+      grp_to_f(gr, f);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float v = sc ? fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f) : f[j];
-      z0 = fmaf(v, w0[j], z0);
-      if (NOUT == 2) z1 = fmaf(v, w1[j], z1);
+      z0 = fmaf(f[j], w0[j], z0);
+      if (NOUT == 2) z1 = fmaf(f[j], w1[j], z1);
     }
 #pragma unroll
     for (int o = 1; o < G; o <<= 1) {
@@ -106,11 +116,15 @@ void launch_head_fwd(size_t M, int Cs, int Cin, const T* x, const float* W, cons
   }
 }
 
-// backward: block = 32 pixel lanes x 8 channel groups (Cs <= 64*8); dW reduced in LDS then atomics
-template <typename T, int NOUT>
+// backward: block = 32 pixel lanes x 8 channel groups (Cs <= 64*8); dW reduced in LDS then atomics.
+// BNR (x = the pre-BN map z, sc/sh its BatchNorm): also the BatchNorm-backward reduction of that layer
+// over the stored dx (adp_bn_bwd_reduce fused): dbeta += sum db, dgamma += sum db*(z-mean)*invstd,
+// db = dx*(z*sc+sh > 0)
+template <typename T, int NOUT, bool BNR = false>
 __global__ void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* sc,
                                 const float* sh, const float* p, const float* dp, const T* addend,
-                                const T* mask, float ms, T* dx, float* dW, float* db) {
+                                const T* mask, float ms, T* dx, float* dW, float* db, const float* bmean = nullptr,
+                                const float* binv = nullptr, float* stat = nullptr) {
   const int G = Cs >> 3;                 // groups per pixel
   const int lanes = TPB / G;
   const int g = threadIdx.x % G, pl = threadIdx.x / G;
@@ -122,7 +136,19 @@ __global__ void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const flo
     float w0 = (NOUT == 2 && c < Cin) ? W[c] : 0.f;
     wd[j] = NOUT == 2 ? w1 - w0 : w1;
   }
+  // per-channel BatchNorm coefficients of this thread's group in registers (the loop's stores through dx
+  // could alias them, so they would be re-read every pixel)
+  float s_[8], h_[8], mu[8], iv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = g * 8 + j;
+    s_[j] = sc ? sc[c] : 1.f;
+    h_[j] = sc ? sh[c] : 0.f;
+    mu[j] = BNR ? bmean[c] : 0.f;
+    iv[j] = BNR ? binv[c] : 0.f;
+  }
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float r1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float dbacc = 0.f;
   if (pl < lanes) {
     for (size_t m = (size_t)blockIdx.x * lanes + pl; m < M; m += (size_t)gridDim.x * lanes) {
@@ -134,15 +160,32 @@ __global__ void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const flo
       grp_to_f(gr, f);
       if (addend) { grp_load(gr, addend + m * Cs + g * 8); grp_to_f(gr, a); }
       if (mask) { grp_load(gr, mask + m * Cs + g * 8); grp_to_f(gr, mk); }
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = sc ? fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f) : f[j];
+      if constexpr (BNR) {   // the activation as adp_bn_apply materializes it (rounded to T)
+        Grp<T> gv;
+        grp_from_f(gv, v);
+        grp_to_f(gv, v);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float v = sc ? fmaxf(fmaf(f[j], sc[g * 8 + j], sh[g * 8 + j]), 0.f) : f[j];
-        acc[j] = fmaf(dz, v, acc[j]);
+        acc[j] = fmaf(dz, v[j], acc[j]);
         float d = dz * wd[j] + (addend ? a[j] : 0.f);
         if (mask) d = mk[j] > 0.f ? d * ms : 0.f;
         o[j] = d;
       }
       if (dx) { grp_from_f(gr, o); grp_store(gr, dx + m * Cs + g * 8); }
+      if constexpr (BNR) {   // over the stored (rounded) gradient, as adp_bn_bwd_reduce reads it
+        float os[8];
+        grp_to_f(gr, os);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = fmaf(f[j], s_[j], h_[j]) > 0.f ? os[j] : 0.f;
+          r1[j] += d;
+          r2[j] += d * (f[j] - mu[j]) * iv[j];
+        }
+      }
       if (g == 0) dbacc += dz;
     }
   }
@@ -152,18 +195,39 @@ __global__ void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const flo
   __shared__ float redb[TPB];
   redb[threadIdx.x] = dbacc;
   __syncthreads();
+  // BNR: every sum goes to this block's replica of the accumulator scratch (adp::stat_scratch; same-address
+  // f32 atomics from thousands of blocks serialise), folded by the host wrapper: row 0 [0, Cs) dbeta,
+  // row 1 [0, Cs) dgamma, row 0 [Cs, Cs + Cin) dW, row 0 Cs + Cin db
+  float* rep = BNR ? stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX : nullptr;
   for (int c = threadIdx.x; c < Cin; c += TPB) {
     int gg = c >> 3, j = c & 7;
     float s = 0.f;
     for (int l = 0; l < lanes; ++l) s += red[(l * G + gg) * 8 + j];
-    if (NOUT == 2) { atomicAdd(dW + c, -s); atomicAdd(dW + Cin + c, s); }
+    if (BNR) atomicAdd(rep + Cs + c, s);
+    else if (NOUT == 2) { atomicAdd(dW + c, -s); atomicAdd(dW + Cin + c, s); }
     else atomicAdd(dW + c, s);
   }
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int l = 0; l < lanes; ++l) s += redb[l * G];
-    if (NOUT == 2) { atomicAdd(db, -s); atomicAdd(db + 1, s); }
+    if (BNR) atomicAdd(rep + Cs + Cin, s);
+    else if (NOUT == 2) { atomicAdd(db, -s); atomicAdd(db + 1, s); }
     else atomicAdd(db, s);
+  }
+  if constexpr (BNR) {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = pass ? r2[j] : r1[j];
+      __syncthreads();
+      for (int c = threadIdx.x; c < Cs; c += TPB) {
+        const int gg = c >> 3, j = c & 7;
+        float t = 0.f;
+        for (int l = 0; l < lanes; ++l) t += red[(l * G + gg) * 8 + j];
+        atomicAdd(rep + (pass ? adp::STAT_CMAX : 0) + c, t);
+      }
+    }
   }
 }
 
@@ -461,6 +525,27 @@ extern "C" int adp_head_softmax2_bwd(int dtype, size_t M, int Cs, int Cin, const
                                      const void* addend, const void* mask, float ms, void* dx, float* dW,
                                      float* db, adp_stream_t st) {
   return head_bwd<2>(dtype, M, Cs, Cin, x, W, sc, sh, p, dp, addend, mask, ms, dx, dW, db, (hipStream_t)st);
+}
+
+extern "C" int adp_head_sigmoid_bwd_bnr(int dtype, size_t M, int Cs, int Cin, const void* z, const float* W,
+                                        const float* sc, const float* sh, const float* mean, const float* invstd,
+                                        const float* p, const float* dp, void* dx, float* dW, float* db,
+                                        float* dgamma, float* dbeta, adp_stream_t st) {
+  ADP_REQUIRE(Cs % 8 == 0 && Cs / 8 <= TPB && Cin <= Cs && z && sc && sh && mean && invstd && dx && dgamma && dbeta,
+              "adp_head_sigmoid_bwd_bnr: Cs % 8 == 0, Cin <= Cs, all BatchNorm pointers and dx");
+  ADP_REQUIRE(Cs + Cin + 1 <= adp::STAT_CMAX, "adp_head_sigmoid_bwd_bnr: Cs + Cin too large");
+  float* stat = adp::stat_scratch();
+  ADP_REQUIRE(stat, adp_last_error());
+  const int lanes = TPB / (Cs / 8);
+  const int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 4096);
+  DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL((head_bwd_kernel<T, 1, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, Cs,
+                                  Cin, (const T*)z, W, sc, sh, p, dp, (const T*)nullptr, (const T*)nullptr, 1.f,
+                                  (T*)dx, dW, db, mean, invstd, stat));
+  if (adp::check_launch("adp_head_sigmoid_bwd_bnr")) return -2;
+  if (adp::stat_fold_at(0, Cs, dbeta, dgamma, (hipStream_t)st)) return -2;
+  if (adp::stat_fold_at(Cs, Cin, dW, nullptr, (hipStream_t)st)) return -2;
+  return adp::stat_fold_at(Cs + Cin, 1, db, nullptr, (hipStream_t)st);
 }
 
 extern "C" int adp_head_sigmoid_bwd(int dtype, size_t M, int Cs, int Cin, const void* x, const float* W,

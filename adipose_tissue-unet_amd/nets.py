@@ -647,6 +647,9 @@ class UNetBN(UNetEngine):
     in training (momentum 0.1, eps 1e-5, PyTorch semantics) and running statistics in eval."""
 
     preset = "unet_bn"
+    # dec0_conv2's BatchNorm+ReLU applied on load by the head (forward) and its BatchNorm-backward
+    # reduction fused into the head backward; False: materialised activation + adp_bn_bwd_reduce
+    fuse_head_bn = True
 
     def __init__(self, batch, size, *, levels=5, base=64, in_ch=3, dtype="bf16", device="cuda", seed=865,
                  bn_eps=1e-5, bn_momentum=0.1):
@@ -707,7 +710,8 @@ class UNetBN(UNetEngine):
 
     def _bn_conv(self, name, srcA, out, act, *, srcB=None, train=True, pool=None):
         """conv -> BN statistics (epilogue) -> scale/shift -> act = relu(bn(out)) materialised (and, with
-        pool, its 2x2 max-pool in the same pass)."""
+        pool, its 2x2 max-pool in the same pass; act=None: not materialised, the consumer applies it on
+        load)."""
         l = self.layers[name]
         s = self.st[name]
         if train:
@@ -725,7 +729,7 @@ class UNetBN(UNetEngine):
                             self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
         if pool is not None:
             ops.bn_apply_maxpool2(out, s[2], s[3], act, pool)
-        else:
+        elif act is not None:
             ops.bn_apply(out, s[2], s[3], act)
 
     def forward(self, batch=None, *, train=False, seed=0, pack=True):
@@ -744,9 +748,17 @@ class UNetBN(UNetEngine):
         for i in range(Lv - 2, -1, -1):
             self.conv(self.layers[f"dec{i}_up"], prev, a[f"t{i}"])
             self._bn_conv(f"dec{i}_conv1", a[f"az{i}_2"], a[f"y{i}_1"], a[f"ay{i}_1"], srcB=a[f"t{i}"], train=train)
-            self._bn_conv(f"dec{i}_conv2", a[f"ay{i}_1"], a[f"y{i}_2"], a[f"ay{i}_2"], train=train)
+            # level 0: relu(bn(y0_2)) is only read by the head, which applies it on load (same rounding)
+            fuse = i == 0 and self.fuse_head_bn
+            self._bn_conv(f"dec{i}_conv2", a[f"ay{i}_1"], a[f"y{i}_2"], None if fuse else a[f"ay{i}_2"],
+                          train=train)
             prev = a[f"ay{i}_2"]
-        ops.head_fwd(prev, self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0), softmax2=False)
+        if self.fuse_head_bn:
+            ops.head_fwd(a["y0_2"], self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0),
+                         softmax2=False, bn=self.bnvec("dec0_conv2"))
+        else:
+            ops.head_fwd(prev, self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0),
+                         softmax2=False)
         self._train_fwd = train
         return {"main_out": a["p"]}
 
@@ -855,9 +867,19 @@ class UNetBN(UNetEngine):
             return self.buf("g/" + key, tuple(like.shape), like.dtype)
 
         # head: dA = dL/d(relu(bn(y0_2)))
+        # (dec0_conv2's BatchNorm-backward reduction over dA fused into the head backward)
         dA = gb("y0_2", a["y0_2"])
-        ops.head_bwd(a["ay0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"], self.ps.gview("head/W"),
-                     self.ps.gview("head/b"), cin=self.ch(0), softmax2=False, dx=dA)
+        s0 = self.st["dec0_conv2"]
+        if not self.fuse_head_bn:
+            ops.head_bwd(a["ay0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"],
+                         self.ps.gview("head/W"), self.ps.gview("head/b"), cin=self.ch(0), softmax2=False, dx=dA)
+            ops.bn_bwd_reduce(dA, a["y0_2"], s0[2], s0[3], s0[4], s0[5], self.ps.gview("dec0_conv2/gamma"),
+                              self.ps.gview("dec0_conv2/beta"))
+        else:
+            ops.head_bwd(a["y0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"], self.ps.gview("head/W"),
+                         self.ps.gview("head/b"), cin=self.ch(0), softmax2=False, dx=dA,
+                         bn=self.bnvec("dec0_conv2"), bn_reduce=(s0[4], s0[5], self.ps.gview("dec0_conv2/gamma"),
+                                                                 self.ps.gview("dec0_conv2/beta")))
         self._grad_ready("head")
         skip_grad = {}
         cur_dA = dA
@@ -865,8 +887,8 @@ class UNetBN(UNetEngine):
         # decoder, from level 0 down to the bottleneck
         for i in range(0, Lv - 1):
             dz = gb(f"dz_y{i}_2", a[f"y{i}_2"])
-            # level 0's dA comes from the head; deeper levels' from the ConvT dgrad (reduction fused)
-            self._bn_bwd(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz, reduced=i > 0)
+            # level 0's dA comes from the head, deeper levels' from the ConvT dgrad (reduction fused in both)
+            self._bn_bwd(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz, reduced=True)
             l2 = L[f"dec{i}_conv2"]
             self.wgrad(l2, a[f"ay{i}_1"], dz)
             dA1 = gb(f"dA_y{i}_1", a[f"y{i}_1"])

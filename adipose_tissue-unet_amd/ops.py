@@ -434,8 +434,21 @@ def head_fwd(x, W, b, p, *, cin, softmax2, bn=None):
     return p
 
 
-def head_bwd(x, W, p, dp, dW, db, *, cin, softmax2, dx=None, bn=None, addend=None, mask=None, mask_scale=1.0):
+def head_bwd(x, W, p, dp, dW, db, *, cin, softmax2, dx=None, bn=None, addend=None, mask=None, mask_scale=1.0,
+             bn_reduce=None):
+    """bn_reduce=(mean, invstd, dgamma, dbeta): x is the pre-BN map z of the layer under the head (bn its
+    scale/shift); that layer's BatchNorm-backward reduction over dx is fused (adp_head_sigmoid_bwd_bnr)."""
     _act(x, "x")
+    if bn_reduce is not None:
+        _check(not softmax2 and bn is not None and dx is not None and addend is None and mask is None,
+               "head_bwd bn_reduce: sigmoid head, bn and dx only")
+        Cs = x.shape[-1]
+        M = x.numel() // Cs
+        _check(p.numel() == M and dp.numel() == M and dx.shape == x.shape, "head grad sizes")
+        mean, invstd, dg, dbeta = bn_reduce
+        call("adp_head_sigmoid_bwd_bnr", dtype_code(x), M, Cs, cin, ptr(x), ptr(W), ptr(bn[0]), ptr(bn[1]),
+             ptr(mean), ptr(invstd), ptr(p), ptr(dp), ptr(dx), ptr(dW), ptr(db), ptr(dg), ptr(dbeta), stream_ptr())
+        return
     Cs = x.shape[-1]
     M = x.numel() // Cs
     _check(p.numel() == M and dp.numel() == M, "head grad sizes")

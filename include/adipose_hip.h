@@ -32,7 +32,7 @@ extern "C" {
 #define ADP_ABI_VERSION 8 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
-                              adp_bn_apply_maxpool2 */
+                              adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -200,6 +200,13 @@ int adp_head_sigmoid_bwd(int dtype, size_t M, int C_stride, int Cin, const void*
                          const float* bn_scale, const float* bn_shift, const float* p,
                          const float* dp, const void* addend, const void* mask, float mask_scale,
                          void* dx, float* dW, float* db, adp_stream_t s);
+/* unet_bn head backward with the BatchNorm-backward reduction of the layer under it fused (adp_bn_bwd_reduce):
+ * z = that layer's pre-BN output (the head reads relu(z*sc+sh)), dx = dL/d relu(bn(z)) stored, and
+ * dbeta += sum db, dgamma += sum db*(z-mean)*invstd with db = dx*(z*sc+sh > 0) over the stored dx */
+int adp_head_sigmoid_bwd_bnr(int dtype, size_t M, int C_stride, int Cin, const void* z, const float* W,
+                             const float* scale, const float* shift, const float* mean, const float* invstd,
+                             const float* p, const float* dp, void* dx, float* dW, float* db, float* dgamma,
+                             float* dbeta, adp_stream_t s);
 /* tf.image.resize(..., method='bilinear') (half-pixel centres, no antialias), 1 channel, f32
  * (:716-719, :723-726) and its adjoint. */
 int adp_resize_bilinear_fwd(int N, int Hs, int Ws, int Ho, int Wo, const float* src, float* dst,

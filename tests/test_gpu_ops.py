@@ -652,3 +652,39 @@ def test_bn_apply_maxpool_fused(dt):
     ops.bn_apply_maxpool2(z, sc, sh, a2, p2)
     torch.cuda.synchronize()
     assert torch.equal(a1, a2) and torch.equal(p1, p2)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_head_bn_on_load_and_fused_bn_reduce(dt):
+    """unet_bn head with dec0_conv2's BatchNorm applied on load (forward) and its BatchNorm-backward
+    reduction fused (adp_head_sigmoid_bwd_bnr) == adp_bn_apply + plain head + adp_bn_bwd_reduce: p, dx and
+    dW bit for bit (same rounding of the activation), dgamma/dbeta to f32 summation-order tolerance."""
+    g = torch.Generator().manual_seed(83)
+    M, Cs, cin = 3 * 40 * 64, 64, 48
+    z = (torch.randn(3, 40, 64, Cs, generator=g) * 2).to(DEV, dt)
+    sc = (torch.rand(Cs, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(Cs, generator=g) * 0.5).to(DEV)
+    mean = (torch.randn(Cs, generator=g) * 0.1).to(DEV)
+    inv = (torch.rand(Cs, generator=g) + 0.5).to(DEV)
+    W = (torch.randn(cin, generator=g) * 0.2).to(DEV)
+    b = torch.tensor([0.1], device=DEV)
+    dp = torch.randn(M, generator=g).to(DEV)
+    act = torch.empty_like(z)
+    ops.bn_apply(z, sc, sh, act)
+    p1, p2 = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.head_fwd(act, W, b, p1, cin=cin, softmax2=False)
+    ops.head_fwd(z, W, b, p2, cin=cin, softmax2=False, bn=(sc, sh))
+    dx1, dx2 = torch.empty_like(z), torch.empty_like(z)
+    gw1, gw2 = torch.zeros(cin, device=DEV), torch.zeros(cin, device=DEV)
+    gb1, gb2 = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    dg1, dg2, db1, db2 = (torch.zeros(Cs, device=DEV) for _ in range(4))
+    ops.head_bwd(act, W, p1, dp, gw1, gb1, cin=cin, softmax2=False, dx=dx1)
+    ops.bn_bwd_reduce(dx1, z, sc, sh, mean, inv, dg1, db1)
+    ops.head_bwd(z, W, p1, dp, gw2, gb2, cin=cin, softmax2=False, dx=dx2, bn=(sc, sh),
+                 bn_reduce=(mean, inv, dg2, db2))
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2) and torch.equal(dx1, dx2)
+    torch.testing.assert_close(gw2, gw1, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gb2, gb1, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dg2, dg1, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db2, db1, rtol=1e-4, atol=1e-3)

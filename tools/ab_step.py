@@ -2,7 +2,9 @@
 """Same-process A/B of two host-schedule variants of the bench step (unet_bn L5, 1024^2, B=4, bf16):
 alternating timed blocks so that clock drift and device variance hit both arms alike.
   --variant pack: per-layer forward-weight packs (old) vs one flat cast (UNetEngine.pack_forward_weights)
-  --variant pool: bn_apply + maxpool2_fwd (old) vs the fused adp_bn_apply_maxpool2"""
+  --variant pool: bn_apply + maxpool2_fwd (old) vs the fused adp_bn_apply_maxpool2
+  --variant head: materialised dec0_conv2 activation + adp_bn_bwd_reduce (old) vs BN-on-load head and
+                  adp_head_sigmoid_bwd_bnr (UNetBN.fuse_head_bn)"""
 import argparse
 import os
 import sys
@@ -14,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--variant", default="pack", choices=["pack", "pool"])
+    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head"])
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--steps", type=int, default=8)
     args = p.parse_args()
@@ -43,6 +45,8 @@ def main():
                     dst = self.buf("wf_old/" + l.name, (l.Npad, l.Kpad))
                     ops.pack_weights(self.ps.view(l.name + "/W"), dst, 0)
                     self._packed[l.name] = dst
+    elif args.variant == "head":
+        owner, attr, old, new = UNetBN, "fuse_head_bn", False, True
     else:
         owner, attr = ops, "bn_apply_maxpool2"
         new = ops.bn_apply_maxpool2
