@@ -650,6 +650,9 @@ class UNetBN(UNetEngine):
     # dec0_conv2's BatchNorm+ReLU applied on load by the head (forward) and its BatchNorm-backward
     # reduction fused into the head backward; False: materialised activation + adp_bn_bwd_reduce
     fuse_head_bn = True
+    # one fill of the per-step stat arena per training forward; False: a fill launch per BatchNorm layer
+    # and per ConvTranspose bias-gradient sum (tools/ab_step.py --variant stat)
+    stat_arena_fill = True
 
     def __init__(self, batch, size, *, levels=5, base=64, in_ch=3, dtype="bf16", device="cuda", seed=865,
                  bn_eps=1e-5, bn_momentum=0.1):
@@ -698,9 +701,23 @@ class UNetBN(UNetEngine):
                 a[f"pool{i}"] = self.buf(f"pool{i}", (B, s // 2, s // 2, c))
                 a[f"t{i}"] = self.buf(f"t{i}", (B, s, s, c))
         a["p"] = self.buf("p", (B, S, S), torch.float32)
-        for n, l in self.layers.items():
-            if isinstance(l, Dense) and l.bn:
-                st[n] = self.buf("bnstat/" + n, (6, l.cout_s), torch.float32)  # sum,sq,scale,shift,mean,invstd
+        # every per-step f32 accumulator in one arena, zeroed by ONE fill at the start of a training
+        # forward (instead of a fill launch per BatchNorm layer and per ConvTranspose bias-gradient sum):
+        # per BN layer (6, C) = sum, sq, scale, shift, mean, invstd; per decoder level (2, Cin_s) channel sums
+        bn = [(n, l.cout_s) for n, l in self.layers.items() if isinstance(l, Dense) and l.bn]
+        ts = [(i, self.layers[f"dec{i}_conv1"].Cin_s) for i in range(self.levels - 1)]
+        arena = self.buf("stat_arena", (sum(6 * c for _, c in bn) + sum(2 * c for _, c in ts),), torch.float32)
+        off = 0
+        for n, c in bn:
+            st[n] = arena[off:off + 6 * c].view(6, c)
+            off += 6 * c
+        self.dtsum = {}
+        for i, c in ts:
+            self.dtsum[i] = arena[off:off + 2 * c].view(2, c)
+            off += 2 * c
+        self.stat_arena = arena
+        self._dtsum_all = arena[off - sum(2 * c for _, c in ts):off]
+        self._dtsum_clean = False
         self.st = st  # batch-independent shapes: shared by every activation set
         return a
 
@@ -715,7 +732,9 @@ class UNetBN(UNetEngine):
         l = self.layers[name]
         s = self.st[name]
         if train:
-            self.zero(s[:2])
+            # s[:2] was zeroed with the whole stat arena at the start of this training forward
+            if not self.stat_arena_fill:
+                self.zero(s[:2])
             self.conv(l, srcA, out, srcB=srcB, bn_stats=(s[0], s[1]))
             count = out.shape[0] * out.shape[1] * out.shape[2]
             rm, rv = self.running[name]
@@ -736,6 +755,9 @@ class UNetBN(UNetEngine):
         a = self.acts(batch or self.B)
         if pack:
             self.pack_forward_weights()
+        if train and self.stat_arena_fill:
+            ops.fill(self.stat_arena, 0.0)
+            self._dtsum_clean = True
         Lv = self.levels
         src = a["x"]
         for i in range(Lv):
@@ -881,6 +903,9 @@ class UNetBN(UNetEngine):
                          bn=self.bnvec("dec0_conv2"), bn_reduce=(s0[4], s0[5], self.ps.gview("dec0_conv2/gamma"),
                                                                  self.ps.gview("dec0_conv2/beta")))
         self._grad_ready("head")
+        if self.stat_arena_fill and not self._dtsum_clean:   # a second backward after one training forward
+            ops.fill(self._dtsum_all, 0.0)
+        self._dtsum_clean = False
         skip_grad = {}
         cur_dA = dA
         bott_dA = None
@@ -902,8 +927,9 @@ class UNetBN(UNetEngine):
             # the ConvTranspose bias gradient (sum of dt over pixels) comes out of this launch's epilogue
             # channel sums (channels >= split_c are dt) instead of a separate pass over dt
             lu = L[f"dec{i}_up"]
-            tsum = self.buf(f"g/dtsum{i}", (2, l1.Cin_s), torch.float32)
-            ops.fill(tsum, 0.0)
+            tsum = self.dtsum[i]   # zeroed with the stat arena by the training forward
+            if not self.stat_arena_fill:
+                ops.fill(tsum, 0.0)
             self.dgrad(l1, dz1, sk, split=True, out2=dt, bn_stats=(tsum[0], tsum[1]))
             gb_up = self.ps.gview(lu.name + "/b")
             c0 = l1.cin_s[0]
