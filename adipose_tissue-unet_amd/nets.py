@@ -650,9 +650,6 @@ class UNetBN(UNetEngine):
     # dec0_conv2's BatchNorm+ReLU applied on load by the head (forward) and its BatchNorm-backward
     # reduction fused into the head backward; False: materialised activation + adp_bn_bwd_reduce
     fuse_head_bn = True
-    # one fill of the per-step stat arena per training forward; False: a fill launch per BatchNorm layer
-    # and per ConvTranspose bias-gradient sum (tools/ab_step.py --variant stat)
-    stat_arena_fill = True
 
     def __init__(self, batch, size, *, levels=5, base=64, in_ch=3, dtype="bf16", device="cuda", seed=865,
                  bn_eps=1e-5, bn_momentum=0.1):
@@ -701,12 +698,15 @@ class UNetBN(UNetEngine):
                 a[f"pool{i}"] = self.buf(f"pool{i}", (B, s // 2, s // 2, c))
                 a[f"t{i}"] = self.buf(f"t{i}", (B, s, s, c))
         a["p"] = self.buf("p", (B, S, S), torch.float32)
-        # every per-step f32 accumulator in one arena, zeroed by ONE fill at the start of a training
-        # forward (instead of a fill launch per BatchNorm layer and per ConvTranspose bias-gradient sum):
-        # per BN layer (6, C) = sum, sq, scale, shift, mean, invstd; per decoder level (2, Cin_s) channel sums
+        # the per-step f32 accumulators live in one arena of two parts, each zeroed by ONE fill (instead of a
+        # fill launch per BatchNorm layer / per ConvTranspose bias-gradient sum): the forward part, per BN
+        # layer (6, C) = sum, sq, scale, shift, mean, invstd, is filled at the start of every training
+        # forward; the backward part, per decoder level (2, Cin_s) channel sums of the concat data gradient,
+        # at the start of every backward (so a backward never depends on what the forward zeroed)
         bn = [(n, l.cout_s) for n, l in self.layers.items() if isinstance(l, Dense) and l.bn]
         ts = [(i, self.layers[f"dec{i}_conv1"].Cin_s) for i in range(self.levels - 1)]
-        arena = self.buf("stat_arena", (sum(6 * c for _, c in bn) + sum(2 * c for _, c in ts),), torch.float32)
+        nbn = sum(6 * c for _, c in bn)
+        arena = self.buf("stat_arena", (nbn + sum(2 * c for _, c in ts),), torch.float32)
         off = 0
         for n, c in bn:
             st[n] = arena[off:off + 6 * c].view(6, c)
@@ -715,9 +715,8 @@ class UNetBN(UNetEngine):
         for i, c in ts:
             self.dtsum[i] = arena[off:off + 2 * c].view(2, c)
             off += 2 * c
-        self.stat_arena = arena
-        self._dtsum_all = arena[off - sum(2 * c for _, c in ts):off]
-        self._dtsum_clean = False
+        self._stat_fwd = arena[:nbn]
+        self._stat_bwd = arena[nbn:]
         self.st = st  # batch-independent shapes: shared by every activation set
         return a
 
@@ -732,9 +731,7 @@ class UNetBN(UNetEngine):
         l = self.layers[name]
         s = self.st[name]
         if train:
-            # s[:2] was zeroed with the whole stat arena at the start of this training forward
-            if not self.stat_arena_fill:
-                self.zero(s[:2])
+            # s[:2] was zeroed with the forward part of the stat arena at the start of this training forward
             self.conv(l, srcA, out, srcB=srcB, bn_stats=(s[0], s[1]))
             count = out.shape[0] * out.shape[1] * out.shape[2]
             rm, rv = self.running[name]
@@ -755,9 +752,8 @@ class UNetBN(UNetEngine):
         a = self.acts(batch or self.B)
         if pack:
             self.pack_forward_weights()
-        if train and self.stat_arena_fill:
-            ops.fill(self.stat_arena, 0.0)
-            self._dtsum_clean = True
+        if train:
+            ops.fill(self._stat_fwd, 0.0)
         Lv = self.levels
         src = a["x"]
         for i in range(Lv):
@@ -903,9 +899,7 @@ class UNetBN(UNetEngine):
                          bn=self.bnvec("dec0_conv2"), bn_reduce=(s0[4], s0[5], self.ps.gview("dec0_conv2/gamma"),
                                                                  self.ps.gview("dec0_conv2/beta")))
         self._grad_ready("head")
-        if self.stat_arena_fill and not self._dtsum_clean:   # a second backward after one training forward
-            ops.fill(self._dtsum_all, 0.0)
-        self._dtsum_clean = False
+        ops.fill(self._stat_bwd, 0.0)
         skip_grad = {}
         cur_dA = dA
         bott_dA = None
@@ -927,9 +921,7 @@ class UNetBN(UNetEngine):
             # the ConvTranspose bias gradient (sum of dt over pixels) comes out of this launch's epilogue
             # channel sums (channels >= split_c are dt) instead of a separate pass over dt
             lu = L[f"dec{i}_up"]
-            tsum = self.dtsum[i]   # zeroed with the stat arena by the training forward
-            if not self.stat_arena_fill:
-                ops.fill(tsum, 0.0)
+            tsum = self.dtsum[i]   # zeroed with the backward part of the stat arena above
             self.dgrad(l1, dz1, sk, split=True, out2=dt, bn_stats=(tsum[0], tsum[1]))
             gb_up = self.ps.gview(lu.name + "/b")
             c0 = l1.cin_s[0]

@@ -162,20 +162,28 @@ def unet_bn_keras_weights(levels=5, base=64, in_ch=3, seed=865):
     return w
 
 
-def bn_relu_train(z, gamma, beta, eps=1e-5):
+def bn_relu_train(z, gamma, beta, eps=1e-5, record=None):
+    """record: optional list; gets {"margin": min |pre-ReLU value|, "mean", "var_unbiased"} of this layer
+    appended (test conditioning: an element within float rounding of the ReLU kink takes either
+    subgradient; running statistics: momentum updates use the unbiased batch variance)."""
     mean = z.mean(dim=(0, 1, 2))
     var = z.var(dim=(0, 1, 2), unbiased=False)
-    return F.relu((z - mean) / torch.sqrt(var + eps) * gamma + beta)
+    pre = (z - mean) / torch.sqrt(var + eps) * gamma + beta
+    if record is not None:
+        record.append({"margin": pre.detach().abs().min().item(), "mean": mean.detach().clone(),
+                       "var_unbiased": z.detach().var(dim=(0, 1, 2), unbiased=True)})
+    return F.relu(pre)
 
 
-def unet_bn_forward(x, weights, levels=5):
-    """x: (B,S,S,C_in) NHWC; training-mode BatchNorm (batch statistics). Returns (B,S,S) sigmoid."""
+def unet_bn_forward(x, weights, levels=5, record=None):
+    """x: (B,S,S,C_in) NHWC; training-mode BatchNorm (batch statistics). Returns (B,S,S) sigmoid.
+    record: optional list, receives one entry per BatchNorm layer in execution order (bn_relu_train)."""
     t = lambda a: a if torch.is_tensor(a) else torch.as_tensor(np.asarray(a))  # noqa: E731
     W = {k: [t(v) for v in vs] for k, vs in weights.items()}
 
     def blk(name, inp):
         k, g, b = W[name]
-        return bn_relu_train(conv2d_same(inp, k, None, relu=False), g, b)
+        return bn_relu_train(conv2d_same(inp, k, None, relu=False), g, b, record=record)
 
     skips = []
     h = x

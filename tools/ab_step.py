@@ -5,8 +5,8 @@ alternating timed blocks so that clock drift and device variance hit both arms a
   --variant pool: bn_apply + maxpool2_fwd (old) vs the fused adp_bn_apply_maxpool2
   --variant head: materialised dec0_conv2 activation + adp_bn_bwd_reduce (old) vs BN-on-load head and
                   adp_head_sigmoid_bwd_bnr (UNetBN.fuse_head_bn)
-  --variant stat: a fill per BatchNorm layer / ConvT bias-gradient sum (old) vs one stat-arena fill
-                  per training forward (UNetBN.stat_arena_fill)"""
+(the round-1 "stat" arm, per-layer statistic fills vs one arena fill, measured neutral:
+profiles/r01i_ab_stat_arena.txt; only the arena path remains)"""
 import argparse
 import os
 import sys
@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head", "stat"])
+    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head"])
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--steps", type=int, default=8)
     args = p.parse_args()
@@ -49,8 +49,6 @@ def main():
                     self._packed[l.name] = dst
     elif args.variant == "head":
         owner, attr, old, new = UNetBN, "fuse_head_bn", False, True
-    elif args.variant == "stat":
-        owner, attr, old, new = UNetBN, "stat_arena_fill", False, True
     else:
         owner, attr = ops, "bn_apply_maxpool2"
         new = ops.bn_apply_maxpool2
