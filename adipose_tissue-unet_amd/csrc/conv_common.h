@@ -29,8 +29,6 @@ struct FwdArgs {
   const float* bnr_sc; const float* bnr_sh; const float* bnr_mean; const float* bnr_invstd;
   float* bnr_dgamma; float* bnr_dbeta;
   int M;
-  int korder;            // tap64: 0 = K steps tap-major (k order), 1 = 64-channel-chunk-major (all taps
-                         // of a chunk back to back: the shifted re-reads of one input window are adjacent)
   int ntile_n;           // gridDim decomposition helper
   int nblocks;
   // fp8 (OCP e4m3fn) forward launches: operands are fp8, acc[n] is dequantised by wscale[n] (per GEMM

@@ -1,4 +1,4 @@
-// 8-phase LDS-DMA implicit-GEMM forward kernel ("tap64") for every layer whose channel stride is a
+// Double-buffered LDS-DMA implicit-GEMM forward kernel ("tap64") for every layer whose channel stride is a
 // multiple of 64 — all 3x3 convs of the unet_bn preset after the input layer, their data-gradients,
 // the ConvTranspose 2x2/s2 forward (1x1 + pixel-shuffle store) and data-gradient (stride-2 4-tap
 // gather). Semantics are those of igemm_fwd_kernel (conv_igemm.hip); only the schedule differs.
@@ -7,15 +7,13 @@
 // gather address of a K step is (row base pixel + tap offset) * stride + channel: a bounds test and
 // two adds, no per-lane division.
 //
-// Schedule (cf. the 256x256 8-phase GEMM template of the CDNA4 programming guide): a block of
-// WM x WN waves computes BM x BN = (WM*TM) x (WN*64); each wave a TM x 64 tile held as
-// (TM/16) x 4 accumulators of v_mfma_f32_16x16x32_bf16. Every K step (64) is staged in four
-// quarter-tiles — A0/A1 (the upper/lower TM/2 rows of every wave row group) and B0/B1 (the left/right
-// 32 columns of every wave column group) — moved HBM/L2 -> LDS by global_load_lds_dwordx4 into a
-// lane-linear image whose 16-B chunks are XOR-swizzled on the SOURCE address. Per K step t four
-// phases compute the quadrants (A0,B0) (A0,B1) (A1,B1) (A1,B0); a quarter is refilled with K step t+2
-// as soon as its last reader phase has passed a barrier, so two K steps of loads are in flight and
-// the only wait is one counted `s_waitcnt vmcnt` per K step (never 0 inside the loop).
+// Schedule: a block of WM x WN waves computes BM x BN = (WM*TM) x (WN*64); each wave a TM x 64 tile
+// held as (TM/16) x 4 accumulators of v_mfma_f32_16x16x32_bf16. Every K step (64) is staged in four
+// quarter-tiles -- A0/A1 (the upper/lower TM/2 rows of every wave row group) and B0/B1 (the left/right
+// 32 columns of every wave column group) -- moved HBM/L2 -> LDS by LDS-DMA (buffer_load ... lds) into a
+// lane-linear image whose 16-B chunks are XOR-swizzled on the SOURCE address. Two stages: after ONE
+// barrier per K step the next step's four quarters are issued into the idle stage, then the current
+// stage is multiplied as the quadrants (A0,B0) (A0,B1) (A1,B1) (A1,B0).
 //
 // F8 (fp8 e4m3 forward, BASELINE configs[4]): the same schedule with 128-channel K steps — a 128-B LDS row
 // then holds 128 fp8 instead of 64 bf16, so staging, swizzle and barriers are unchanged — and one
@@ -45,14 +43,24 @@ constexpr int cmax(int x, int y) { return x > y ? x : y; }
 template <int WM, int WN, int TM>
 constexpr int tap64_occ() { return 2 * (WM * TM + WN * 64) * 128 <= 81920 ? 2 : 1; }
 
-// One barrier per phase (a barrier between the reads and the MFMAs as well, as in the guide's template,
-// measured 2-5 % slower here). BAL: one quarter-tile refill per phase (B0 of step t+1 at P0, A0/B1/A1 of
-// step t+2 at P1/P2/P3: three quarters in flight across the wait) instead of A0+B0 together at P1.
+// BUF: operands through buffer resources (raw_ptr_buffer_load_lds): a padding tap or a weight row past
+// the matrix is an out-of-range 32-bit offset, which the buffer unit reads as zeros, so an issue is a
+// few 32-bit VALU ops (no zero page, no 64-bit address arithmetic, no scalar load of a global address
+// inside the loop). The flat-address form is kept for tensors of 2 GiB and more.
 // BNR: data-gradient launch with the fused BatchNorm-backward reduction epilogue (epi_rows_bnr).
 typedef int v8i32 __attribute__((ext_vector_type(8)));
 typedef int v4i32 __attribute__((ext_vector_type(4)));
 
-template <int WM, int WN, int TM, bool BAL, bool BNR, bool F8>
+constexpr unsigned T64_OOB = 0x80000000u;   // buffer offset beyond every resource: reads as zeros
+constexpr int T64_RSRC3 = 0x00020000;        // raw buffer descriptor word 3 (gfx9: 32-bit data format)
+
+// one 16-B-per-lane LDS-DMA piece through a buffer resource (a device function: the host pass of the
+// kernel templates then never sees the target builtin)
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
+}
+
+template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
@@ -68,7 +76,6 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   constexpr int OA1 = QA * ROWB, OB0 = BM * ROWB, OB1 = (BM + QB) * ROWB;
   constexpr int EPI = TM * (BN + 4) * 4;
   constexpr int SMEM = cmax(cmax(2 * STAGE, EPI), NTH * 16 * 4);
-  constexpr int NIN = 2 * (GA + GB);               // glds a thread issues per K step
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -83,7 +90,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   const int nk = a.K / KSTEP;
 
   // ---- per-thread staging rows: quarter h, instruction i -> quarter row q = i*(NTH/8) + tid/8
-  int ry[2][GA], rx[2][GA], rn[2][GA], rc[2][GA];
+  int ry[2][GA], rx[2][GA], rn[2][GA], rc[2][GA], pb[2][GA];   // pb: pixel of tap (0,0) (up == 1)
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -96,58 +103,79 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       ry[h][i] = yo * a.stride - a.pad;
       rx[h][i] = xo * a.stride - a.pad;
       rn[h][i] = v ? n * a.Hs : -1;
+      pb[h][i] = (n * a.Hs + ry[h][i]) * a.Ws + rx[h][i];
       rc[h][i] = 16 * (pos ^ swz(q));   // byte offset of this lane's 16-B chunk
     }
   const unsigned char* bp[2][GB];
+  unsigned bo[2][GB];   // BUF: byte offset of this lane's weight chunk (T64_OOB past the matrix)
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
       const int q = i * (NTH / 8) + (tid >> 3);
       const int col = (q / 32) * 64 + h * 32 + (q % 32);
-      bp[h][i] = (n0 + col < Wrows)
-                     ? reinterpret_cast<const unsigned char*>(a.W) + ((size_t)(n0 + col) * a.Kpad) * ES + 16 * (pos ^ swz(q))
-                     : nullptr;
+      const bool v = n0 + col < Wrows;
+      bo[h][i] = v ? (unsigned)((n0 + col) * a.Kpad * ES + 16 * (pos ^ swz(q))) : T64_OOB;
+      bp[h][i] = v ? reinterpret_cast<const unsigned char*>(a.W) + ((size_t)(n0 + col) * a.Kpad) * ES +
+                         16 * (pos ^ swz(q))
+                   : nullptr;
     }
   const unsigned char* srcA = reinterpret_cast<const unsigned char*>(a.srcA);
   const unsigned char* srcB = reinterpret_cast<const unsigned char*>(a.srcB);
+  const int npix = a.Nimg * a.Hs * a.Ws;   // (only the BUF instantiations use the resources)
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.srcA, 0, npix * a.CAs * ES, T64_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.CBs ? a.srcB : a.srcA), 0, npix * (a.CBs ? a.CBs : a.CAs) * ES, T64_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, Wrows * a.Kpad * ES, T64_RSRC3);
 
-  // K step -> (tap offsets, source, channel); uniform across the block. cs = pixel stride in bytes
-  struct Kt { int oy, ox, cs; const unsigned char* base; int kt; };
-  const int ntaps = a.kh * a.kw;
-  auto kinfo = [&](int kt) {
+  // K step -> (tap offsets, source, channel); uniform across the block, advanced incrementally (K steps
+  // run channel-chunk-fastest inside a tap, taps row-major). cs = pixel stride in bytes, cb = byte offset
+  // of the step's first channel inside its source's pixel, dpix = pixel delta of the tap (up == 1).
+  struct Kt { int oy, ox, cs, cb, srcb, dpix, kt; const unsigned char* base; };
+  int it_ci = 0, it_ty = 0, it_tx = 0, it_kt = 0;   // iterator state: the NEXT step kinfo() returns
+  auto kinfo = [&]() {
     Kt r;
-    int k = kt * KSTEP;
-    if (a.korder) {   // chunk-major: step kt = chunk * ntaps + tap
-      const int chunk = kt / ntaps, t = kt - chunk * ntaps;
-      k = t * Cin_s + chunk * KSTEP;
+    r.oy = it_ty * a.dil; r.ox = it_tx * a.dil; r.kt = it_kt;
+    r.dpix = r.oy * a.Ws + r.ox;
+    if (it_ci < a.CAs) { r.cb = it_ci * ES; r.cs = a.CAs * ES; r.srcb = 0; r.base = srcA + r.cb; }
+    else { r.cb = (it_ci - a.CAs) * ES; r.cs = a.CBs * ES; r.srcb = 1; r.base = srcB + r.cb; }
+    ++it_kt;
+    it_ci += KSTEP;
+    if (it_ci >= Cin_s) {
+      it_ci = 0;
+      if (++it_tx == a.kw) { it_tx = 0; ++it_ty; }
     }
-    const int tap = k / Cin_s, ci = k - tap * Cin_s;
-    const int ty = tap / a.kw, tx = tap - ty * a.kw;
-    r.oy = ty * a.dil; r.ox = tx * a.dil; r.kt = k / KSTEP;
-    if (ci < a.CAs) { r.base = srcA + ci * ES; r.cs = a.CAs * ES; }
-    else { r.base = srcB + (ci - a.CAs) * ES; r.cs = a.CBs * ES; }
     return r;
   };
   auto issueA = [&](int h, const Kt& k, int buf) {
     unsigned char* dst = smem + buf * STAGE + h * OA1 + wave * 8 * ROWB;
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
-      const void* p = tap64_zero_page;
       int yi = ry[h][i] + k.oy, xi = rx[h][i] + k.ox;
-      if (rn[h][i] >= 0 && (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv) {
-        if (a.up == 2) { yi >>= 1; xi >>= 1; }
-        p = k.base + (size_t)((rn[h][i] + yi) * a.Ws + xi) * k.cs + rc[h][i];
+      const bool v = rn[h][i] >= 0 && (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
+      int pix;
+      if (a.up == 2) pix = (rn[h][i] + (yi >> 1)) * a.Ws + (xi >> 1);
+      else pix = pb[h][i] + k.dpix;
+      if constexpr (BUF) {
+        const unsigned off = v ? (unsigned)(pix * k.cs + k.cb + rc[h][i]) : T64_OOB;
+        buf_lds16(k.srcb ? rsB : rsA, dst + i * (NTH / 8) * ROWB, off);
+      } else {
+        const void* p = v ? (const void*)(k.base + (size_t)pix * k.cs + rc[h][i]) : (const void*)tap64_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
       }
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
     }
   };
   auto issueB = [&](int h, const Kt& k, int buf) {
     unsigned char* dst = smem + buf * STAGE + (h ? OB1 : OB0) + wave * 8 * ROWB;
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
-      const void* p = bp[h][i] ? (const void*)(bp[h][i] + (size_t)k.kt * ROWB) : (const void*)tap64_zero_page;
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
+      if constexpr (BUF) {
+        const unsigned off = bo[h][i] == T64_OOB ? T64_OOB : bo[h][i] + (unsigned)k.kt * ROWB;
+        buf_lds16(rsW, dst + i * (NTH / 8) * ROWB, off);
+      } else {
+        const void* p = bp[h][i] ? (const void*)(bp[h][i] + (size_t)k.kt * ROWB) : (const void*)tap64_zero_page;
+        __builtin_amdgcn_global_load_lds(p, (lds_void*)(dst + i * (NTH / 8) * ROWB), 16, 0, 0);
+      }
     }
   };
 
@@ -202,84 +230,31 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   };
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
-  if (a.debug_flags & 4) {
-    // plain double buffering: one barrier per K step; stage t+1 is filled while stage t multiplies
-    {
-      const Kt k0 = kinfo(0);
-      issueA(0, k0, 0); issueB(0, k0, 0); issueB(1, k0, 0); issueA(1, k0, 0);
-    }
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      T64_BAR();   // stage t landed for every wave, and nobody reads buffer buf ^ 1 any more
-      if (t + 1 < nk) {
-        const Kt k1 = kinfo(t + 1);
-        issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
-      }
-      readA(buf, 0, fa);
-      readB(buf, 0, fb0);
-      mma(fa, fb0, 0, 0);
-      readB(buf, 1, fb1);
-      mma(fa, fb1, 0, 1);
-      readA(buf, 1, fa);
-      mma(fa, fb1, 1, 1);
-      mma(fa, fb0, 1, 0);
-    }
-    T64_BAR();   // the epilogue reuses the stages
-  } else {
-  // ---- prologue: K step 0 and (all but B0 of) step 1 in flight, wait for step 0
+  // double buffering, ONE barrier per K step: stage t+1 is filled while stage t multiplies (the earlier
+  // schedules -- a 4-barrier quarter refill with step t+2, issues interleaved with the MFMA clusters, and
+  // the guide's two-barrier ping-pong -- measured 6-20 % slower on these shapes: DESIGN.md §3)
   {
-    const Kt k0 = kinfo(0);
+    const Kt k0 = kinfo();
     issueA(0, k0, 0); issueB(0, k0, 0); issueB(1, k0, 0); issueA(1, k0, 0);
-    if (nk > 1) {
-      const Kt k1 = kinfo(1);
-      issueA(0, k1, 1);
-      if (!BAL) issueB(0, k1, 1);
-      issueB(1, k1, 1); issueA(1, k1, 1);
-      if (BAL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GA + GB) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    T64_BAR();
   }
-
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
-    const bool n1 = t + 1 < nk, pre = t + 2 < nk;
-    const Kt k2 = kinfo(pre ? t + 2 : t);
-    // P0: (A0,B0); BAL: B0 of the other buffer (read at P0 of step t-1) is dead -> step t+1
-    if (BAL && n1) issueB(0, kinfo(t + 1), buf ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    T64_BAR();   // stage t landed for every wave, and nobody reads buffer buf ^ 1 any more
+    if (t + 1 < nk) {
+      const Kt k1 = kinfo();
+      issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
+    }
     readA(buf, 0, fa);
     readB(buf, 0, fb0);
     mma(fa, fb0, 0, 0);
-    T64_BAR();
-    // P1: (A0,B1); A0 (and B0) of this buffer are dead -> refill with step t+2
-    if (pre) {
-      issueA(0, k2, buf);
-      if (!BAL) issueB(0, k2, buf);
-    }
     readB(buf, 1, fb1);
     mma(fa, fb1, 0, 1);
-    T64_BAR();
-    // P2: (A1,B1); B1 dead
-    if (pre) issueB(1, k2, buf);
     readA(buf, 1, fa);
     mma(fa, fb1, 1, 1);
-    T64_BAR();
-    // P3: (A1,B0) from registers; A1 dead. Retire step t+1 (everything issued before this step's
-    // step-t+2 refills) before the barrier that precedes its first read.
-    if (pre) issueA(1, k2, buf);
     mma(fa, fb0, 1, 0);
-    if (pre) {
-      if (BAL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GA + GB) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIN) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    T64_BAR();
   }
-  }
+  T64_BAR();   // the epilogue reuses the stages
 
   // ---- epilogue: one wave row group (TM rows x BN) at a time through LDS
   float* tile = reinterpret_cast<float*>(smem);
@@ -310,27 +285,36 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
 
 template <int WM, int WN, int TM>
 void launch_cfg(FwdArgs& a, hipStream_t s) {
-  const bool bal = adp::option("tap64_bal", 0) != 0;
   constexpr int BM = WM * TM, BN = WN * 64;
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
   const dim3 g(a.nblocks), b(WM * WN * 64);
+  // buffer-resource loads need every operand below 2 GiB (32-bit offsets, T64_OOB reserved)
+  const int es = a.f8 ? 1 : 2;
+  const size_t pix = (size_t)a.Nimg * a.Hs * a.Ws, lim = (size_t)1 << 31;
+  const bool buf = adp::option("tap64_buf", 1) && pix * a.CAs * es < lim && pix * a.CBs * es < lim &&
+                   (size_t)((a.Nout + 63) / 64 * 64) * a.Kpad * es < lim;
+#define T64_LAUNCH(BUFV, BNRV, F8V)                                                                     \
+  do {                                                                                                 \
+    adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, %s>", WM, WN, TM, BUFV ? "true" : "false", \
+                    BNRV ? "true" : "false", F8V ? "true" : "false");                                  \
+    hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, F8V>), g, b, 0, s, a);           \
+  } while (0)
   if constexpr (TM == 64) {   // fp8: the 64-row-per-wave tiles only (the 128-row ones spill in the K loop)
-    if (a.f8) {   // inference launches: no BN-backward epilogue, default refill order
-      adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, false, false, true>", WM, WN, TM);
-      hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, false, true>), g, b, 0, s, a);
+    if (a.f8) {               // inference launches: no BN-backward epilogue
+      if (buf) T64_LAUNCH(true, false, true);
+      else T64_LAUNCH(false, false, true);
       return;
     }
   }
-  adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false>", WM, WN, TM, bal ? "true" : "false",
-                  a.bnr_z ? "true" : "false");
   if (a.bnr_z) {
-    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, true, false>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, true, false>), g, b, 0, s, a);
+    if (buf) T64_LAUNCH(true, true, false);
+    else T64_LAUNCH(false, true, false);
   } else {
-    if (bal) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, false, false, false>), g, b, 0, s, a);
+    if (buf) T64_LAUNCH(true, false, false);
+    else T64_LAUNCH(false, false, false);
   }
+#undef T64_LAUNCH
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 256x128 (8 waves, 64x64),
@@ -355,7 +339,6 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   if (a.scA || a.scB || a.CAs % ks != 0 || a.CBs % ks != 0 || a.K != a.kh * a.kw * Cin_s || a.K % ks != 0 ||
       a.Kpad != a.K)
     return 0;
-  a.korder = option("tap64_korder", 0);
   int cfg = mode - 2;
   if (a.f8 && cfg != 1 && cfg != 3) mode = 1;
   if (mode == 1) {

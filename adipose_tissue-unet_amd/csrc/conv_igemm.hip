@@ -1033,7 +1033,7 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
   a.bnr_sc = io->bnr_scale; a.bnr_sh = io->bnr_shift; a.bnr_mean = io->bnr_mean; a.bnr_invstd = io->bnr_invstd;
   a.bnr_dgamma = io->bnr_dgamma; a.bnr_dbeta = io->bnr_dbeta;
   a.M = d->N * d->Ho * d->Wo;
-  a.debug_flags = adp::option("fwd_debug", 0) | (adp::option("tap64_db", 1) ? 4 : 0);
+  a.debug_flags = adp::option("fwd_debug", 0);
   a.stat = (a.bn_sum || a.bnr_z) ? adp::stat_scratch() : nullptr;
 }
 

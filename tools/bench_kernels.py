@@ -23,6 +23,8 @@ def main():
     p.add_argument("--kinds", default="fwd,wgrad")
     p.add_argument("--layers", default="", help="comma-separated substrings selecting layer shapes")
     p.add_argument("--batch", type=int, default=4)
+    p.add_argument("--blas", action="store_true",
+                   help="add a hipBLASLt (torch.matmul) dense GEMM of the same M x N x K as a reference arm")
     args = p.parse_args()
     import torch
 
@@ -52,6 +54,12 @@ def main():
         y = torch.empty(B, S, S, cout, device=dev, dtype=torch.bfloat16)
         dW = torch.zeros(((cout + 63) // 64 * 64), Kpad, device=dev)
         flops = 2.0 * B * S * S * cout * K
+        if args.blas:   # dense GEMM of the same shape: x2d (M x K) @ Wt (K x N), no im2col gather
+            a2 = torch.randn(B * S * S, K, device=dev, dtype=torch.bfloat16)
+            b2 = torch.randn(K, cout, device=dev, dtype=torch.bfloat16)
+            for _ in range(3):
+                a2 @ b2
+            bl = []
         for kind in kinds:
             for v in variants:
                 res.setdefault((name, kind, v), [])
@@ -61,6 +69,14 @@ def main():
                     ops.set_option(k_, None)      # every variant starts from the defaults
                 for k_, v_ in settings[v]:
                     ops.set_option(k_, v_)
+                if r == 0 and "fwd" in kinds:   # every variant's forward output against variant 0's
+                    ops.conv_fwd(x, W, cout, out=y)
+                    torch.cuda.synchronize()
+                    if v == 0:
+                        y0 = y.clone()
+                    else:
+                        d = (y.float() - y0.float()).abs().max().item()
+                        print(json.dumps({"layer": name, "variant": v, "fwd_max_abs_diff_vs_v0": d}), flush=True)
                 for kind in kinds:
                     fn = (lambda: ops.conv_fwd(x, W, cout, out=y)) if kind == "fwd" else \
                         (lambda: ops.conv_wgrad(x, y, dW, cout))
@@ -73,6 +89,19 @@ def main():
                     torch.cuda.synchronize()
                     ms = e0.elapsed_time(e1) / args.reps
                     res[(name, kind, v)].append(ms)
+            if args.blas:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    a2 @ b2
+                e1.record()
+                torch.cuda.synchronize()
+                bl.append(e0.elapsed_time(e1) / args.reps)
+        if args.blas:
+            ms = min(bl)
+            print(json.dumps({"layer": name, "kind": "hipblaslt_gemm", "ms": round(ms, 4),
+                              "tflops": round(flops / ms / 1e9, 1)}), flush=True)
+            del a2, b2
         for kind in kinds:
             line = {"layer": name, "kind": kind}
             for v in variants:

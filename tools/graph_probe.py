@@ -54,6 +54,18 @@ def main():
     out["eager_ms"] = (t2 - t0) * 1e3 / args.steps
     out["host_issue_ms"] = (t1 - t0) * 1e3 / args.steps
 
+    # the same with bench.py's per-launch HIP-event timer on every conv launch
+    from adipose_amd import ops
+    timer = ops.LaunchTimer()
+    ops.set_launch_timer(timer)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+    out["eager_timer_ms"] = (time.perf_counter() - t0) * 1e3 / args.steps
+    ops.set_launch_timer(None)
+
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         tr.train_step(x, y)

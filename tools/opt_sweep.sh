@@ -3,7 +3,7 @@
 # usage: bash tools/opt_sweep.sh > gpurun_out/opt_sweep.txt
 mkdir -p gpurun_out
 for r in 1 2; do
-for o in "" "--opt tap64_bal=1" "--opt tap64_korder=1" "--opt wgrad_halop_grid=512" "--opt halo_persist_grid=512"; do
+for o in "" "--opt wgrad_halop_grid=512" "--opt halo_persist_grid=512"; do
   v=$(timeout -k 10 120 python bench.py --no-cpu-baseline --steps 10 $o 2>/dev/null | grep '^{"metric"' | python -c 'import json,sys;print(json.loads(sys.stdin.read())["ms_per_step"])') || exit 1
   echo "r$r [$o] $v"
 done; done
