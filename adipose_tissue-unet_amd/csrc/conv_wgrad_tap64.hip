@@ -23,6 +23,14 @@ namespace {
 
 __device__ __attribute__((aligned(256))) uint4 wg64_zero_page[64];
 
+constexpr unsigned WG_OOB = 0x80000000u;   // buffer offset beyond every resource: reads as zeros
+constexpr int WG_RSRC3 = 0x00020000;       // raw buffer descriptor word 3 (gfx9: 32-bit data format)
+// one 16-B-per-lane LDS-DMA piece through a buffer resource (device function: the host pass of the
+// kernel templates never sees the target builtin)
+__device__ __forceinline__ void wg_buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
+}
+
 
 #define W64_BAR()                          \
   do {                                     \
@@ -402,6 +410,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   constexpr int GH = (HCH + NTH - 1) / NTH, GD = (DCH + NTH - 1) / NTH;
   constexpr int HBUF = HROWS * RB, DBUF = PH * PW * RB;
   constexpr int STAGE = HBUF + DBUF;
+  static_assert(GH + GD <= 2 * PH, "the next patch's LDS-DMA groups are spread over the 8 patch rows");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -417,38 +426,71 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   const int ch = combo % nch, nblk = combo / nch;
   const int nt = lin < T ? (T - lin + G - 1) / G : 0;
   const bool inA = ch * 64 < a.CAs;
-  const bf16* X = reinterpret_cast<const bf16*>(inA ? a.srcA : a.srcB) + (inA ? ch * 64 : ch * 64 - a.CAs);
   const int xcs = inA ? a.CAs : a.CBs;
-  const bf16* D = reinterpret_cast<const bf16*>(a.dY) + nblk * 64;
-
-  auto issue = [&](int k, int buf) {
+  // operands through buffer resources over the whole source / dY tensors (the launcher keeps each below
+  // 2 GiB): a halo pixel outside the image is an out-of-range offset and reads as zeros
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(inA ? a.srcA : a.srcB), 0, a.Nimg * a.Hs * a.Ws * xcs * 2, WG_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsD =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dY, 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
+  // per-thread constant parts of the gathers: halo group i -> (pixel delta, row/col offsets, byte offset)
+  int hy[GH], hx[GH], hpix[GH], hoff[GH], dpix[GD], doff[GD];
+  const int xc0 = (inA ? ch * 64 : ch * 64 - a.CAs) * 2;
+#pragma unroll
+  for (int i = 0; i < GH; ++i) {
+    const int idx = i * NTH + tid, hr = idx >> 3, pos = idx & 7;
+    hy[i] = hr / HW - 1;
+    hx[i] = hr % HW - 1;
+    hpix[i] = hy[i] * a.Ws + hx[i];
+    hoff[i] = xc0 + 16 * (pos ^ gsw<RB>(hr));
+  }
+#pragma unroll
+  for (int i = 0; i < GD; ++i) {
+    const int idx = i * NTH + tid, pr = idx >> 3, pos = idx & 7;
+    dpix[i] = (pr >> 5) * a.Wo + (pr & 31);
+    doff[i] = nblk * 128 + 16 * (pos ^ gsw<RB>(pr));
+  }
+  // patch k of this block -> origin (image row base, y0, x0) and the pixel indices of its (y0, x0)
+  struct Patch { int y0, x0, pbx, pbd; };
+  auto patch = [&](int k) {
+    Patch P;
     const int t = lin + k * G;
     const int px = t % tx_n, r = t / tx_n;
-    const int y0 = (r % ty_n) * PH, img = r / ty_n, x0 = px * PW;
-    unsigned char* hb = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < GH; ++i) {
-      const int idx = i * NTH + tid;
-      if (idx < HCH) {
-        const int hr = idx >> 3, pos = idx & 7;
-        const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
-        const bool ok = gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
-        const void* p = ok ? (const void*)(X + (size_t)((img * a.Hs + gy) * a.Ws + gx) * xcs + 8 * (pos ^ gsw<RB>(hr)))
-                           : (const void*)wg64_zero_page;
-        __builtin_amdgcn_global_load_lds(p, (lds_void*)(hb + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
-      }
+    const int img = r / ty_n;
+    P.y0 = (r % ty_n) * PH;
+    P.x0 = px * PW;
+    P.pbx = (img * a.Hs + P.y0) * a.Ws + P.x0;
+    P.pbd = (img * a.Ho + P.y0) * a.Wo + P.x0;
+    return P;
+  };
+  auto issue_h = [&](const Patch& P, int i, int buf) {
+    const int idx = i * NTH + tid;
+    if (i < GH - 1 || idx < HCH) {
+      const int gy = P.y0 + hy[i], gx = P.x0 + hx[i];
+      const bool ok = (unsigned)gy < (unsigned)a.Hs && (unsigned)gx < (unsigned)a.Ws;
+      const unsigned off = ok ? (unsigned)((P.pbx + hpix[i]) * xcs * 2 + hoff[i]) : WG_OOB;
+      wg_buf_lds16(rsX, smem + buf * STAGE + (size_t)(i * NTH + wave * 64) * 16, off);
     }
-    unsigned char* db = hb + HBUF;
-#pragma unroll
-    for (int i = 0; i < GD; ++i) {
-      const int idx = i * NTH + tid;
-      if (idx < DCH) {
-        const int pr = idx >> 3, pos = idx & 7;
-        const size_t m = (size_t)(img * a.Ho + y0 + (pr >> 5)) * a.Wo + x0 + (pr & 31);
-        __builtin_amdgcn_global_load_lds(D + m * a.dy_stride + 8 * (pos ^ gsw<RB>(pr)),
-                                         (lds_void*)(db + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
-      }
+  };
+  auto issue_d = [&](const Patch& P, int i, int buf) {
+    const int idx = i * NTH + tid;
+    if (i < GD - 1 || idx < DCH) {
+      const unsigned off = (unsigned)((P.pbd + dpix[i]) * a.dy_stride * 2 + doff[i]);
+      wg_buf_lds16(rsD, smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16, off);
     }
+  };
+  // the groups of the next patch issued while row pr of this one multiplies: halo first, then dY,
+  // two per row until the remaining rows can take one each
+  auto issue_row = [&](const Patch& P, int pr, int buf) {
+    constexpr int NG = GH + GD, EXTRA = NG - PH;   // rows 0 .. EXTRA-1 take two groups
+    const int g0 = pr < EXTRA ? 2 * pr : EXTRA + pr;
+    const int g1 = pr < EXTRA ? g0 + 1 : -1;
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi)
+      if (gi == g0 || gi == g1) {
+        if (gi < GH) issue_h(P, gi, buf);
+        else issue_d(P, gi - GH, buf);
+      }
   };
   // transposed 16x32 fragment of an [row][64 bf16] LDS image whose rows row0 .. row0+31 are the 32
   // pixels of one k step (absolute rows, so the row swizzle matches the one applied on load)
@@ -476,17 +518,23 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   const int nb8 = wave >> 1, cb8 = 2 * (wave & 1);
 
   if (nt > 0) {
-    issue(0, 0);
+    const Patch P0 = patch(0);
+#pragma unroll
+    for (int i = 0; i < GH; ++i) issue_h(P0, i, 0);
+#pragma unroll
+    for (int i = 0; i < GD; ++i) issue_d(P0, i, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     W64_BAR();
   }
   const uint32_t sbase = lds_off(smem);
   for (int k = 0; k < nt; ++k) {
     const int buf = k & 1;
-    if (k + 1 < nt) issue(k + 1, buf ^ 1);
+    const bool more = k + 1 < nt;
+    const Patch Pn = patch(more ? k + 1 : k);
     const uint32_t hbase = sbase + buf * STAGE, dbase = hbase + HBUF;
-#pragma unroll 1
+#pragma unroll
     for (int pr = 0; pr < PH; ++pr) {
+      if (more) issue_row(Pn, pr, buf ^ 1);
       bf16x8 fd[4], fx[4], fd8, fx8[2];
       if (NW == 8) {
         fd8 = frag(dbase, pr * PW, nb8 * 16);
@@ -764,7 +812,10 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   if (hp && !a.scA && !a.scB && a.CAs % 64 == 0 && a.CBs % 64 == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
       a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
       a.Nout % 64 == 0 && a.dy_mode == 0 && a.K == 9 * cin && a.Kpad == a.K && a.dy_stride % 8 == 0 &&
-      a.dy_stride >= a.Nout) {
+      a.dy_stride >= a.Nout &&
+      // buffer-resource offsets: every operand below 2 GiB
+      (size_t)a.Nimg * a.Hs * a.Ws * std::max(a.CAs, a.CBs) * 2 < ((size_t)1 << 31) &&
+      (size_t)a.Nimg * a.Ho * a.Wo * a.dy_stride * 2 < ((size_t)1 << 31)) {
     const int combos = (cin / 64) * (a.Nout / 64);
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
     const int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
