@@ -287,19 +287,29 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     img = r / ty_n;
     x0 = px * PW;
   };
-  auto halo_src = [&](int k, int i) -> const uint4* {
-    int img, y0, x0;
-    tile_origin(k, img, y0, x0);
+  // per-thread constant parts of the halo gather: group i -> (input chunk source, pixel delta from the
+  // tile's (y0 - 1, x0 - 1), halo row/col, channel element offset)
+  int hdy[GH], hdx[GH], hdp[GH], hce[GH], hsrc[GH];
+#pragma unroll
+  for (int i = 0; i < GH; ++i) {
     const int idx = i * NTH + tid;
     const int cc = NCH == 1 ? 0 : idx / (HROWS * 8), rem = idx - cc * HROWS * 8;
     const int hr = rem >> 3, pos = rem & 7;
-    const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
-    const bool ok = idx < HCH && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
-    if (!ok) return nullptr;
+    hdy[i] = hr / HW - 1;
+    hdx[i] = hr % HW - 1;
+    hdp[i] = hdy[i] * a.Ws + hdx[i];
     const bool inA = cc * 64 < a.CAs;
-    const bf16* src = reinterpret_cast<const bf16*>(inA ? a.srcA : a.srcB);
-    const int cs = inA ? a.CAs : a.CBs, c0 = inA ? cc * 64 : cc * 64 - a.CAs;
-    return reinterpret_cast<const uint4*>(src + (size_t)((img * a.Hs + gy) * a.Ws + gx) * cs + c0 + 8 * (pos ^ swz(hr)));
+    hsrc[i] = inA ? 0 : 1;
+    hce[i] = (inA ? cc * 64 : cc * 64 - a.CAs) + 8 * (pos ^ swz(hr));
+  }
+  auto halo_src = [&](int img, int y0, int x0, int i) -> const uint4* {
+    const int idx = i * NTH + tid;
+    const int gy = y0 + hdy[i], gx = x0 + hdx[i];
+    const bool ok = (i < GH - 1 || idx < HCH) && (unsigned)gy < (unsigned)a.Hs && (unsigned)gx < (unsigned)a.Ws;
+    if (!ok) return nullptr;
+    const bf16* src = reinterpret_cast<const bf16*>(hsrc[i] ? a.srcB : a.srcA);
+    const int cs = hsrc[i] ? a.CBs : a.CAs;
+    return reinterpret_cast<const uint4*>(src + (size_t)((img * a.Hs + y0) * a.Ws + x0 + hdp[i]) * cs + hce[i]);
   };
 
   // ---- prologue: nine weight taps (resident), first halo, per-channel constants
@@ -318,7 +328,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
   for (int i = 0; i < GH; ++i) {
     if (i * NTH + tid < HCH) {
-      const uint4* p = halo_src(0, i);
+      int img0, y00, x00;
+      tile_origin(0, img0, y00, x00);
+      const uint4* p = halo_src(img0, y00, x00, i);
       __builtin_amdgcn_global_load_lds(p ? (const void*)p : (const void*)halo_zero_page,
                                        (lds_void*)(smem + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
     }
@@ -363,9 +375,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     }
     uint4 hreg[GH];
     if (more) {
+      int img1, y01, x01;
+      tile_origin(k + 1, img1, y01, x01);
 #pragma unroll
       for (int i = 0; i < GH; ++i) {
-        const uint4* p = halo_src(k + 1, i);
+        const uint4* p = halo_src(img1, y01, x01, i);
         hreg[i] = p ? *p : make_uint4(0, 0, 0, 0);
       }
     }
@@ -374,7 +388,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
+#pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int dy = t / 3, dx = t - 3 * dy;
 #pragma unroll
