@@ -38,6 +38,7 @@ struct FwdArgs {
   int out_f8;
   int debug_flags;       // timing-only ablations (option "fwd_debug"): bit1 skips the BN-statistics atomics
   float* stat;           // BatchNorm accumulator replicas (adp::stat_scratch) for bn_sum / bnr_* launches
+  int defer_fold;        // bn_sum launch whose replica sums adp_bn_finalize_fold adds in (adp_conv_desc)
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
@@ -323,6 +324,9 @@ namespace adp {
 // conv_fwd_tap64.hip: 8-phase LDS-DMA forward kernel for layers whose channel stride is a multiple
 // of 64 (every 64-deep K step lies inside one tap). Returns 1 if it launched, 0 if not eligible.
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s);
+// conv_fwd_tap64p.hip: persistent 256x256 form of the same kernel with the tile boundary pipelined
+// (next tile's first stage in flight during a register epilogue); called by launch_fwd_tap64.
+int launch_fwd_tap64p(FwdArgs& a, hipStream_t s);
 // conv_fwd_halo.hip: halo-reuse 3x3 kernel for narrow (<= 128 output channels) stride-1 layers.
 int launch_fwd_halo(FwdArgs& a, hipStream_t s);
 int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)

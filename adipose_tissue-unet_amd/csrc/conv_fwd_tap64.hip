@@ -256,6 +256,13 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   }
   T64_BAR();   // the epilogue reuses the stages
 
+  if (a.debug_flags & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue at all
+#pragma unroll
+    for (int i = 0; i < 2 * MIQ; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   // ---- epilogue: one wave row group (TM rows x BN) at a time through LDS
   float* tile = reinterpret_cast<float*>(smem);
   constexpr int LT = BN + 4;
@@ -356,6 +363,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
     }
     if (best <= 0.0) return 0;
   }
+  if (cfg == 0 && !a.bnr_z && launch_fwd_tap64p(a, s)) return 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);
   else if (cfg == 2) launch_cfg<4, 1, 128>(a, s);

@@ -1,0 +1,402 @@
+// Persistent form of the tap64 forward-shaped kernel (conv_fwd_tap64.hip) for the 256x256 tile: one
+// 512-thread block per CU walks output tiles lin, lin + G, ... (G = grid, a multiple of the N-tile count,
+// so a block keeps one N tile), and the tile boundary is pipelined:
+//   * the first K step of tile k+1 is issued by LDS-DMA at the LAST K step of tile k (its stage is free),
+//   * the epilogue of tile k runs from registers -- the product is accumulated transposed (C^T = W X^T:
+//     a lane holds 4 consecutive output channels of one pixel) and stored as 8-B buffer stores, no LDS
+//     staging, no barrier -- while those loads land,
+//   * the next K loop waits only for the loads: every thread issues exactly EPI_OPS vector-memory
+//     instructions in an epilogue (out-of-range lanes store to an out-of-range buffer offset, which the
+//     hardware drops), so `s_waitcnt vmcnt(EPI_OPS)` retires everything older than the epilogue.
+// Per block, the non-persistent kernel paid the prologue load latency and an LDS-staged epilogue
+// (accumulators -> LDS -> 16-B stores, two row groups, four barriers) with the MFMA pipe idle: 5-17 % of
+// a 3x3 layer at K = 9216..2304 and 40-75 % of a ConvTranspose forward (K = 128..1024).
+// Epilogue forms: plain / pixel-shuffle (ConvTranspose) / channel-split store, bias, ReLU, BatchNorm
+// statistics of the stored values (bn_sum), fused BatchNorm-backward reduction (BNR); every other epilogue
+// term (addend, mask, accumulate, dropout, fp8) stays on the non-persistent kernel.
+#include "conv_common.h"
+
+namespace {
+
+constexpr unsigned P_OOB = 0x80000000u;   // buffer offset beyond every resource: loads read 0, stores drop
+constexpr int P_RSRC3 = 0x00020000;       // raw buffer descriptor word 3 (gfx9: 32-bit data format)
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void p_lds16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
+}
+__device__ __forceinline__ void p_st8(__amdgpu_buffer_rsrc_t r, unsigned off, v2u32 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
+}
+__device__ __forceinline__ v2u32 p_ld8(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+}
+
+#define P_BAR()                            \
+  do {                                     \
+    asm volatile("" ::: "memory");         \
+    __builtin_amdgcn_s_barrier();          \
+    asm volatile("" ::: "memory");         \
+  } while (0)
+
+template <bool BNR>
+__global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
+  constexpr int WN = 4, TM = 128, NTH = 512;
+  constexpr int BM = 256, BN = 256, ROWB = 128, ES = 2, KSTEP = 64;
+  constexpr int QA = BM / 2, QB = BN / 2, GA = QA * 8 / NTH, GB = QB * 8 / NTH;   // 2, 2
+  constexpr int HM = TM / 2, MIQ = TM / 32;                                       // 64, 4
+  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int OA1 = QA * ROWB, OB0 = BM * ROWB, OB1 = (BM + QB) * ROWB;
+  constexpr int EPI_OPS = 2 * MIQ * 4;   // stores per thread per epilogue (one per accumulator tile)
+  // ONE LDS object: with several, the compiler tags every LDS access with per-object alias scopes, and the
+  // waitcnt pass then drains vmcnt(0) between the LDS-DMA prefetch of stage t+1 and the fragment reads of
+  // stage t (one object: no such wait -- measured 12 % of the K loop)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE + 7 * BN * 4];
+  float (*cst)[BN] = reinterpret_cast<float (*)[BN]>(smem + 2 * STAGE);         // epilogue constants:
+                                                                                 // bias | scale shift mean invstd (BNR)
+  float (*sacc)[BN] = reinterpret_cast<float (*)[BN]>(smem + 2 * STAGE + 5 * BN * 4);   // block's BN sums
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int G = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, G);
+  const int ntiles = a.nblocks;
+  const int mine = lin < ntiles ? (ntiles - lin + G - 1) / G : 0;
+  if (mine == 0) return;   // uniform per block
+  const int n0 = (lin % a.ntile_n) * BN;
+  const int pos = lane & 7;
+  const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
+  const int Cin_s = a.CAs + a.CBs;
+  const int Wrows = (a.Nout + 63) / 64 * 64;
+  const int nk = a.K / KSTEP;
+  if (tid < BN) {   // (read in the epilogue through LDS: no vector-memory wait there)
+    const int n = n0 + tid;
+    const bool v = n < a.Nout;
+    cst[0][tid] = (!BNR && a.bias && v) ? a.bias[a.out_mode == 1 ? n % a.Cps : n] : 0.f;
+    cst[1][tid] = (BNR && v) ? a.bnr_sc[n] : 0.f;
+    cst[2][tid] = (BNR && v) ? a.bnr_sh[n] : 0.f;
+    cst[3][tid] = (BNR && v) ? a.bnr_mean[n] : 0.f;
+    cst[4][tid] = (BNR && v) ? a.bnr_invstd[n] : 0.f;
+    sacc[0][tid] = 0.f;
+    sacc[1][tid] = 0.f;
+  }
+  // (ordered before the epilogue by the first K step's barrier)
+
+  const int npix = a.Nimg * a.Hs * a.Ws;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.srcA, 0, npix * a.CAs * ES, P_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.CBs ? a.srcB : a.srcA), 0, npix * (a.CBs ? a.CBs : a.CAs) * ES, P_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, Wrows * a.Kpad * ES, P_RSRC3);
+
+  // ---- B staging (weights): fixed for the block's N tile
+  unsigned bo[2][GB];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int q = i * (NTH / 8) + (tid >> 3);
+      const int col = (q / 32) * 64 + h * 32 + (q % 32);
+      bo[h][i] = n0 + col < Wrows ? (unsigned)((n0 + col) * a.Kpad * ES + 16 * (pos ^ swz(q))) : P_OOB;
+    }
+  // ---- A staging rows of the tile being loaded: quarter h, instruction i -> quarter row q
+  int ry[2][GA], rx[2][GA], pb[2][GA];   // (up == 1 only: an invalid row has ry far out of range)
+  const int rc = 16 * (pos ^ ((tid >> 4) & 7));   // = 16 * (pos ^ swz(q)) for every staging row q of this thread
+  auto setup_rows = [&](int m0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const int q = i * (NTH / 8) + (tid >> 3);
+        const int m = m0 + (q / HM) * TM + h * HM + (q % HM);
+        const bool v = m < a.M;
+        const int mm = v ? m : 0;
+        const int n = mm / HWo, rem = mm - n * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+        ry[h][i] = v ? yo * a.stride - a.pad : -(1 << 20);
+        rx[h][i] = xo * a.stride - a.pad;
+        pb[h][i] = (n * a.Hs + yo * a.stride - a.pad) * a.Ws + rx[h][i];
+      }
+  };
+  // ---- K-step iterator of the tile being loaded (channel-chunk fastest inside a tap)
+  struct Kt { int oy, ox, cs, cb, srcb, dpix, kt; };
+  int it_ci = 0, it_ty = 0, it_tx = 0, it_kt = 0;
+  auto kreset = [&]() { it_ci = it_ty = it_tx = it_kt = 0; };
+  auto kinfo = [&]() {
+    Kt r;
+    r.oy = it_ty * a.dil; r.ox = it_tx * a.dil; r.kt = it_kt;
+    r.dpix = r.oy * a.Ws + r.ox;
+    if (it_ci < a.CAs) { r.cb = it_ci * ES; r.cs = a.CAs * ES; r.srcb = 0; }
+    else { r.cb = (it_ci - a.CAs) * ES; r.cs = a.CBs * ES; r.srcb = 1; }
+    ++it_kt;
+    it_ci += KSTEP;
+    if (it_ci >= Cin_s) {
+      it_ci = 0;
+      if (++it_tx == a.kw) { it_tx = 0; ++it_ty; }
+    }
+    return r;
+  };
+  auto issue = [&](const Kt& k, int buf) {
+    // A0 B0 B1 A1
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      unsigned char* dst = smem + buf * STAGE + h * OA1 + wave * 8 * ROWB;
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const int yi = ry[h][i] + k.oy, xi = rx[h][i] + k.ox;
+        const bool v = (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
+        const unsigned off = v ? (unsigned)((pb[h][i] + k.dpix) * k.cs + k.cb + rc) : P_OOB;
+        p_lds16(k.srcb ? rsB : rsA, dst + i * (NTH / 8) * ROWB, off);
+      }
+      unsigned char* dsb = smem + buf * STAGE + (h ? OB1 : OB0) + wave * 8 * ROWB;
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const unsigned off = bo[h][i] == P_OOB ? P_OOB : bo[h][i] + (unsigned)k.kt * ROWB;
+        p_lds16(rsW, dsb + i * (NTH / 8) * ROWB, off);
+      }
+    }
+  };
+
+  const int r16 = lane & 15, h4 = lane >> 4;
+  auto readA = [&](int buf, int h, bf16x8 (&fa)[MIQ][2]) {
+    const unsigned char* base = smem + buf * STAGE + h * OA1;
+#pragma unroll
+    for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int q = wr * HM + mi * 16 + r16, c = 4 * s + h4;
+        fa[mi][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
+      }
+  };
+  auto readB = [&](int buf, int h, bf16x8 (&fb)[2][2]) {
+    const unsigned char* base = smem + buf * STAGE + (h ? OB1 : OB0);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int q = wc * 32 + ni * 16 + r16, c = 4 * s + h4;
+        fb[ni][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
+      }
+  };
+  // acc[ha*MIQ + mi][hb*2 + ni]: transposed tile, rows = channels n0 + wc*64 + (hb*2+ni)*16 + 4*h4 + reg,
+  // column = pixel m0 + wr*TM + ha*HM + mi*16 + r16
+  f32x4 acc[2 * MIQ][4];
+  auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[ha * MIQ + mi][hb * 2 + ni] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ni][s], fa[mi][s], acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- epilogue resources
+  const bool shuffle = a.out_mode == 1, split = a.out_mode == 2;
+  const int Hq = 2 * a.Ho, Wq = 2 * a.Wo;
+  const unsigned out_bytes = shuffle ? (unsigned)(a.Nimg * Hq * Wq) * a.out_stride * ES : (unsigned)a.M * a.out_stride * ES;
+  const int out2_bytes = split ? a.M * a.out2_stride * ES : 0;
+  const __amdgpu_buffer_rsrc_t rsZ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(BNR ? a.bnr_z : a.out), 0, BNR ? a.M * a.bnr_zs * ES : 0, P_RSRC3);
+  const bool stats = BNR || a.bn_sum != nullptr;
+
+  auto epilogue = [&](int m0) {
+    // lane-derived epilogue indices made opaque here, so that the compiler cannot hoist their
+    // per-(mt, nt) offsets out of the tile loop (they would stay live across the K loop and spill)
+    int tidv = tid;
+    asm volatile("" : "+v"(tidv));
+    const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int c = n0 + wc * 64 + nt * 16 + 4 * h4;   // first of this lane's 4 channels (GEMM column)
+      const bool cv = c < a.Nout;
+      const int cl = wc * 64 + nt * 16 + 4 * h4;         // the same, relative to n0
+      const float4 b4 = *reinterpret_cast<const float4*>(&cst[0][cl]);
+      const float bias[4] = {b4.x, b4.y, b4.z, b4.w};
+      float sc[4], sh[4], mu[4], is[4];
+      if (BNR) {
+        const float4 a4 = *reinterpret_cast<const float4*>(&cst[1][cl]);
+        const float4 s4 = *reinterpret_cast<const float4*>(&cst[2][cl]);
+        const float4 m4 = *reinterpret_cast<const float4*>(&cst[3][cl]);
+        const float4 i4 = *reinterpret_cast<const float4*>(&cst[4][cl]);
+        sc[0] = a4.x; sc[1] = a4.y; sc[2] = a4.z; sc[3] = a4.w;
+        sh[0] = s4.x; sh[1] = s4.y; sh[2] = s4.z; sh[3] = s4.w;
+        mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
+        is[0] = i4.x; is[1] = i4.y; is[2] = i4.z; is[3] = i4.w;
+      }
+      // store target of the channel quad: GEMM column c -> (buffer, channel offset)
+      int sub = 0, cq = c;
+      if (shuffle) { sub = c / a.Cps; cq = c - sub * a.Cps; }
+      // (split_c % 16 == 0: the whole 16-channel block of the wave goes to one buffer -- a scalar choice
+      //  of the buffer resource, no per-lane waterfall around the store)
+      const bool second = split && __builtin_amdgcn_readfirstlane(n0 + wc * 64 + nt * 16) >= a.split_c;
+      if (second) cq = c - a.split_c;
+      const int ostr = second ? a.out2_stride : a.out_stride;
+      // the store target's resource, built from a scalar pointer choice (selecting between two resource
+      // objects makes the compiler spill them to the stack and reload per lane)
+      const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc(second ? a.out2 : a.out, 0,
+                                                                         second ? out2_bytes : (int)out_bytes, P_RSRC3);
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mt = 0; mt < 2 * MIQ; ++mt) {
+        const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
+        const bool v = cv && m < a.M;
+        float x[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[r] = acc[mt][nt][r] + bias[r];
+          if (a.relu) x[r] = fmaxf(x[r], 0.f);
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)x[r];
+        int pix = m;
+        if (shuffle) {
+          const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+          pix = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
+        }
+        const unsigned off = v ? (unsigned)((pix * ostr + cq) * ES) : P_OOB;
+        p_st8(rsO, off, __builtin_bit_cast(v2u32, o));
+        if (BNR) {
+          const bf16x4 zz = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float g = (float)o[r], zf = (float)zz[r];   // the stored (rounded) gradient
+            const float db = fmaf(zf, sc[r], sh[r]) > 0.f ? g : 0.f;
+            s1[r] += db;
+            s2[r] += db * (zf - mu[r]) * is[r];
+          }
+        } else if (stats && v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { s1[r] += x[r]; s2[r] += x[r] * x[r]; }
+        }
+      }
+      if (stats) {   // over the 16 pixel lanes of the channel quad, then into the block's LDS sums
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s1[r] += __shfl_xor(s1[r], o, 64);
+            s2[r] += __shfl_xor(s2[r], o, 64);
+          }
+        }
+        if (r16 == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            atomicAdd(&sacc[0][cl + r], s1[r]);
+            atomicAdd(&sacc[1][cl + r], s2[r]);
+          }
+        }
+      }
+    }
+  };
+
+  // ---- the pipelined tile loop (first and last K step of a tile peeled: no branches in the steady loop)
+  bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
+  auto compute = [&](int buf) {
+    readA(buf, 0, fa);
+    readB(buf, 0, fb0);
+    mma(fa, fb0, 0, 0);
+    readB(buf, 1, fb1);
+    mma(fa, fb1, 0, 1);
+    readA(buf, 1, fa);
+    mma(fa, fb1, 1, 1);
+    mma(fa, fb0, 1, 0);
+  };
+  int m0 = ((lin) / a.ntile_n) * BM;
+  setup_rows(m0);
+  kreset();
+  issue(kinfo(), 0);
+  int gs = 0;   // global K-step counter; stage = gs & 1 (the & keeps the stage index provably in {0, 1}, so
+                // the compiler can tell the LDS-DMA target stage from the stage being read and does not
+                // insert a vmcnt(0) drain before the reads)
+  for (int k = 0; k < mine; ++k) {
+    const int m0c = m0;
+#pragma unroll
+    for (int i = 0; i < 2 * MIQ; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // step 0: its stage was issued before the previous tile's EPI_OPS epilogue stores (k > 0)
+    if (k > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    P_BAR();
+    issue(kinfo(), (gs & 1) ^ 1);
+    compute(gs & 1);
+    ++gs;
+    for (int t = 1; t < nk - 1; ++t, ++gs) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      P_BAR();   // stage t landed for every wave, and nobody reads the other stage any more
+      issue(kinfo(), (gs & 1) ^ 1);
+      compute(gs & 1);
+    }
+    // last step: the next tile's first stage goes into the free stage, overlapping this tile's epilogue
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    P_BAR();
+    if (k + 1 < mine) {
+      m0 = ((lin + (k + 1) * G) / a.ntile_n) * BM;
+      setup_rows(m0);
+      kreset();
+      issue(kinfo(), (gs & 1) ^ 1);
+    }
+    compute(gs & 1);
+    ++gs;
+    if (a.debug_flags & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue
+#pragma unroll
+      for (int i = 0; i < 2 * MIQ; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+      continue;
+    }
+    epilogue(m0c);
+  }
+
+  // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
+  if (!stats || (a.debug_flags & 2)) return;
+  __syncthreads();
+  float* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+  if (tid < BN) {
+    const int n = n0 + tid;
+    if (n < a.Nout) {
+      const int c = shuffle ? n % a.Cps : n;
+      atomicAdd(rep + c, sacc[0][tid]);
+      atomicAdd(rep + adp::STAT_CMAX + c, sacc[1][tid]);
+    }
+  }
+}
+
+#undef P_BAR
+
+}  // namespace
+
+namespace adp {
+// 256x256 persistent launch for the epilogue forms it covers; 0 = not eligible (the caller falls back)
+int launch_fwd_tap64p(FwdArgs& a, hipStream_t s) {
+  if (!option("tap64_persist", 1) || a.f8 || a.K < 128) return 0;   // (two K steps at least)
+  if (a.addend || a.mask || a.mask2 || a.accum || a.drop_rate > 0.f || a.scA || a.scB) return 0;
+  if (a.up != 1) return 0;
+  if (a.out_mode == 1 && (a.Cps % 8 != 0 || a.Nout % a.Cps != 0)) return 0;
+  if (a.out_mode == 2 && (a.split_c % 16 != 0 || a.out2_stride % 8 != 0)) return 0;
+  if (a.out_stride % 8 != 0 || (a.bnr_z && a.bnr_zs % 8 != 0)) return 0;
+  const int Cin_s = a.CAs + a.CBs;
+  if (a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 || a.Kpad != a.K) return 0;
+  // buffer-resource offsets: every operand below 2 GiB
+  const size_t lim = (size_t)1 << 31, pix = (size_t)a.Nimg * a.Hs * a.Ws;
+  const size_t outb = a.out_mode == 1 ? (size_t)a.M * 4 * a.out_stride * 2 : (size_t)a.M * a.out_stride * 2;
+  if (pix * a.CAs * 2 >= lim || pix * a.CBs * 2 >= lim || outb >= lim ||
+      (size_t)((a.Nout + 63) / 64 * 64) * a.Kpad * 2 >= lim || (a.out2 && (size_t)a.M * a.out2_stride * 2 >= lim) ||
+      (a.bnr_z && (size_t)a.M * a.bnr_zs * 2 >= lim))
+    return 0;
+  a.ntile_n = (a.Nout + 255) / 256;
+  const int mt = (a.M + 255) / 256;
+  a.nblocks = mt * a.ntile_n;   // tiles; the grid is persistent
+  int grid = std::min(a.nblocks, option("tap64_persist_grid", 256));
+  grid -= grid % a.ntile_n;
+  if (grid <= 0) grid = a.ntile_n;
+  adp::set_kernel("igemm_fwd_tap64p_kernel<%s>", a.bnr_z ? "true" : "false");
+  if (a.bnr_z) hipLaunchKernelGGL(igemm_fwd_tap64p_kernel<true>, dim3(grid), dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(igemm_fwd_tap64p_kernel<false>, dim3(grid), dim3(512), 0, s, a);
+  return 1;
+}
+}  // namespace adp

@@ -1029,6 +1029,7 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
   a.mask2 = io->mask2; a.mask2_stride = d->mask2_stride; a.mask2_scale = d->mask2_scale;
   a.accum = io->accum; a.accum_stride = d->accum_stride;
   a.bn_sum = io->bn_sum; a.bn_sq = io->bn_sqsum;
+  a.defer_fold = d->bn_defer_fold && io->bn_sum && !io->bnr_z;
   a.bnr_z = io->bnr_z; a.bnr_zs = d->bnr_stride;
   a.bnr_sc = io->bnr_scale; a.bnr_sh = io->bnr_shift; a.bnr_mean = io->bnr_mean; a.bnr_invstd = io->bnr_invstd;
   a.bnr_dgamma = io->bnr_dgamma; a.bnr_dbeta = io->bnr_dbeta;
@@ -1040,7 +1041,7 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
 // after a launch whose epilogue added BatchNorm sums into the replicas: fold them into the caller's
 // accumulators (statistics: bn_sum / bn_sq; BN-backward reduction: bnr_dbeta / bnr_dgamma)
 int fold_stats(const FwdArgs& a, hipStream_t s) {
-  if (!a.stat) return 0;
+  if (!a.stat || a.defer_fold) return 0;   // (deferred: adp_bn_finalize_fold folds them)
   const int C = a.out_mode == 1 ? a.Cps : a.Nout;
   if (a.bnr_z) return adp::stat_fold(C, a.bnr_dbeta, a.bnr_dgamma, s);
   return adp::stat_fold(C, a.bn_sum, a.bn_sq, s);

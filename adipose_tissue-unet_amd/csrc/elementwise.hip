@@ -402,6 +402,51 @@ __global__ void stat_fold_kernel(int C, float* scratch, float* dst0, float* dst1
   }
 }
 
+// stat_fold_kernel + bn_finalize_kernel in one launch: the replica sums are added into sum / sq (and
+// re-zeroed), then the BatchNorm scale / shift / mean / invstd (and running statistics) of those sums
+__global__ void bn_fold_finalize_kernel(int C, float* scratch, float* sum, float* sq, float count,
+                                        const float* gamma, const float* beta, float eps, float momentum,
+                                        float* scale, float* shift, float* mean, float* invstd, float* rmean,
+                                        float* rvar) {
+  constexpr int RG = 4, RPER = adp::STAT_REPL / RG;
+  __shared__ float part[2][RG][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int r = rg * RPER; r < (rg + 1) * RPER; ++r) {
+      float* p = scratch + (size_t)r * 2 * adp::STAT_CMAX + c;
+      s0 += p[0];
+      s1 += p[adp::STAT_CMAX];
+      p[0] = 0.f;
+      p[adp::STAT_CMAX] = 0.f;
+    }
+  }
+  part[0][rg][cl] = s0;
+  part[1][rg][cl] = s1;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  const float ts = sum[c] + ((part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]));
+  const float tq = sq[c] + ((part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]));
+  sum[c] = ts;
+  sq[c] = tq;
+  // = bn_finalize_kernel (training statistics, count > 0)
+  const float mu = ts / count;
+  const float var = fmaxf(tq / count - mu * mu, 0.f);
+  const float is = rsqrtf(var + eps);
+  const float g = gamma[c] * is;
+  scale[c] = g;
+  shift[c] = beta[c] - mu * g;
+  mean[c] = mu;
+  invstd[c] = is;
+  if (rmean) {
+    const float unb = count > 1.f ? var * count / (count - 1.f) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+  }
+}
+
 // per-channel sums of dBN and dBN*xhat; block = 256 threads as (pixel lane) x (channel group)
 template <typename T>
 __global__ void bn_bwd_reduce_kernel(size_t M, int C, const T* dA, const T* z, const float* sc,
@@ -853,6 +898,19 @@ extern "C" int adp_bn_finalize(int C, float count, const float* sum, const float
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + TPB - 1) / TPB), dim3(TPB), 0, (hipStream_t)st, C, count,
                      sum, sq, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean, rvar);
   return adp::check_launch("adp_bn_finalize");
+}
+
+extern "C" int adp_bn_finalize_fold(int C, float count, float* sum, float* sq, const float* gamma, const float* beta,
+                                    float eps, float momentum, float* scale, float* shift, float* mean, float* invstd,
+                                    float* rmean, float* rvar, adp_stream_t st) {
+  ADP_REQUIRE(C > 0 && C <= adp::STAT_CMAX && count > 0 && sum && sq && gamma && beta && scale && shift && mean &&
+                  invstd,
+              "adp_bn_finalize_fold: bad arguments (training statistics, C <= 2048)");
+  float* sc = adp::stat_scratch();
+  ADP_REQUIRE(sc, adp_last_error());
+  hipLaunchKernelGGL(bn_fold_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)st, C, sc, sum, sq,
+                     count, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean, rvar);
+  return adp::check_launch("adp_bn_finalize_fold");
 }
 
 extern "C" int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, const void* z, const float* sc,

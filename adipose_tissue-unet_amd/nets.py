@@ -358,14 +358,14 @@ class UNetEngine:
 
     # conv helpers -----------------------------------------------------------------------
     def conv(self, l, srcA, out, *, srcB=None, bnA=None, bnB=None, dropout=0.0, seed=0, accum=None,
-             bn_stats=None):
+             bn_stats=None, defer_fold=False):
         if l.transpose:
             return ops.conv_fwd(srcA, self.Wf(l.name), l.Nout, out=out, bias=self.bias(l.name), kh=1, kw=1,
                                 pad=0, bnA=bnA, out_mode=1, shuffle_c=l.cout_s)
         return ops.conv_fwd(srcA, self.Wf(l.name), l.Nout, out=out, srcB=srcB, bnA=bnA, bnB=bnB,
                             bias=self.bias(l.name) if l.bias else None, up=l.up, kh=l.k, kw=l.k, dil=l.dil,
                             relu=l.relu and not l.bn, dropout_rate=dropout, dropout_seed=seed, accum=accum,
-                            bn_stats=bn_stats)
+                            bn_stats=bn_stats, defer_fold=defer_fold)
 
     def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None, bias_grad=True):
         dW = self.ps.gview(l.name + "/W")
@@ -650,6 +650,9 @@ class UNetBN(UNetEngine):
     # dec0_conv2's BatchNorm+ReLU applied on load by the head (forward) and its BatchNorm-backward
     # reduction fused into the head backward; False: materialised activation + adp_bn_bwd_reduce
     fuse_head_bn = True
+    # the training conv leaves its BatchNorm sums in the replica scratch and the finalize folds them (one
+    # launch); False: the conv's own fold launch, then the finalize
+    fuse_bn_fold = True
 
     def __init__(self, batch, size, *, levels=5, base=64, in_ch=3, dtype="bf16", device="cuda", seed=865,
                  bn_eps=1e-5, bn_momentum=0.1):
@@ -732,11 +735,13 @@ class UNetBN(UNetEngine):
         s = self.st[name]
         if train:
             # s[:2] was zeroed with the forward part of the stat arena at the start of this training forward
-            self.conv(l, srcA, out, srcB=srcB, bn_stats=(s[0], s[1]))
+            # the conv leaves its statistics in the accumulator replicas; the finalize folds them (one launch)
+            fold = self.fuse_bn_fold
+            self.conv(l, srcA, out, srcB=srcB, bn_stats=(s[0], s[1]), defer_fold=fold)
             count = out.shape[0] * out.shape[1] * out.shape[2]
             rm, rv = self.running[name]
             ops.bn_finalize(count, s[0], s[1], self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
-                            self.bn_eps, self.bn_momentum, s[2], s[3], s[4], s[5], rm, rv)
+                            self.bn_eps, self.bn_momentum, s[2], s[3], s[4], s[5], rm, rv, fold=fold)
         else:
             self.conv(l, srcA, out, srcB=srcB)
             rm, rv = self.running[name]

@@ -145,13 +145,16 @@ def _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo
 def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=None, up=False, stride=1,
              kh=3, kw=3, dil=1, pad=None, Ho=None, Wo=None, relu=False, dropout_rate=0.0, dropout_seed=0,
              out_mode=0, shuffle_c=0, out2=None, split_c=0, addend=None, mask=None, mask_scale=1.0,
-             mask2=None, mask2_scale=1.0, accum=None, bn_stats=None, bn_reduce=None, w_scale=None):
+             mask2=None, mask2_scale=1.0, accum=None, bn_stats=None, bn_reduce=None, w_scale=None,
+             defer_fold=False):
     """Implicit-GEMM conv forward-shaped launch (conv, conv dgrad, convT fwd/dgrad).
 
     bn_reduce=(z, scale, shift, mean, invstd, dgamma, dbeta): fuse the BatchNorm-backward reduction
     (bn_bwd_reduce) of the layer whose activation relu(z*scale+shift) `out` is the gradient of.
     fp8 launches (srcA/W torch.float8_e4m3fn): w_scale (f32, per GEMM column, from pack_weights_fp8) is
-    required; `out` may be bf16 or fp8."""
+    required; `out` may be bf16 or fp8.
+    defer_fold (with bn_stats): leave the statistics in the library's accumulator replicas; the next call
+    on the stream must be bn_finalize(..., fold=True) on the same two vectors."""
     d, io, N, Ho, Wo = _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo, nout)
     d.relu = 1 if relu else 0
     d.dropout_rate = float(dropout_rate)
@@ -202,6 +205,7 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
         io.accum = ptr(accum)
     if bn_stats is not None:
         io.bn_sum, io.bn_sqsum = ptr(bn_stats[0]), ptr(bn_stats[1])
+        d.bn_defer_fold = 1 if defer_fold else 0
     if bn_reduce is not None:
         z, sc, sh, mu, ist, dg, dbt = bn_reduce
         _check(out_mode == 0 and out is not None and z.shape == out.shape and z.dtype == out.dtype,
@@ -393,8 +397,16 @@ def fill(dst, value):
     call("adp_fill_f32", dst.numel(), float(value), ptr(dst), stream_ptr())
 
 
-def bn_finalize(count, ssum, ssq, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean=None, rvar=None):
+def bn_finalize(count, ssum, ssq, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean=None, rvar=None,
+                fold=False):
+    """fold=True: first add the statistics the previous conv_fwd(..., defer_fold=True) left in the
+    accumulator replicas into ssum / ssq (adp_bn_finalize_fold: one launch for fold + finalize)."""
     C_ = gamma.numel()
+    if fold:
+        _check(count > 0, "bn_finalize(fold=True) is the training form")
+        call("adp_bn_finalize_fold", C_, float(count), ptr(ssum), ptr(ssq), ptr(gamma), ptr(beta), float(eps),
+             float(momentum), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), ptr(rmean), ptr(rvar), stream_ptr())
+        return
     call("adp_bn_finalize", C_, float(count), ptr(ssum), ptr(ssq), ptr(gamma), ptr(beta), float(eps),
          float(momentum), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), ptr(rmean), ptr(rvar), stream_ptr())
 

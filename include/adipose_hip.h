@@ -29,10 +29,11 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 8 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 9 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
-                              adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr */
+                              adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
+                              v9: adp_conv_desc.bn_defer_fold + adp_bn_finalize_fold */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -58,6 +59,9 @@ typedef struct adp_conv_desc {
   int accum_stride;         /* accum (f32) += stored value */
   int bnr_stride;           /* channel stride of io->bnr_z */
   int out_fp8;              /* ADP_DTYPE_FP8 launches: 1 stores the output as fp8 e4m3 (else bf16) */
+  int bn_defer_fold;        /* 1: leave this launch's BatchNorm statistics in the library's accumulator
+                               replicas instead of adding them into io->bn_sum / bn_sqsum; the next launch
+                               on the stream must be adp_bn_finalize_fold for those two vectors */
 } adp_conv_desc;
 
 typedef struct adp_conv_io {
@@ -168,6 +172,12 @@ int adp_bn_finalize(int C, float count, const float* sum, const float* sqsum, co
                     const float* beta, float eps, float momentum, float* scale, float* shift,
                     float* mean, float* invstd, float* running_mean, float* running_var,
                     adp_stream_t s);
+/* adp_bn_finalize of statistics a conv launch left in the accumulator replicas (bn_defer_fold): first
+ * sum[c] += replicas, sqsum[c] += replicas (the replicas are re-zeroed), then the finalize; one launch in
+ * place of the fold + finalize pair. */
+int adp_bn_finalize_fold(int C, float count, float* sum, float* sqsum, const float* gamma, const float* beta,
+                         float eps, float momentum, float* scale, float* shift, float* mean, float* invstd,
+                         float* running_mean, float* running_var, adp_stream_t s);
 /* a = relu(z*scale + shift), the post-BatchNorm activation, materialised once per layer */
 int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* scale, const float* shift,
                  void* out, adp_stream_t s);

@@ -26,12 +26,13 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_error_plumbing():
     lib = _lib.lib()
-    assert lib.adp_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.adp_abi_version() == _lib.ABI_VERSION == 9
     assert isinstance(lib.adp_last_error(), bytes)
 
 
 def test_conv_desc_layout_matches_header():
-    # 15 ints, float, uint, 6 ints, float, int, float, int, int, int (out_fp8) -> 29 4-byte fields
-    assert ctypes.sizeof(_lib.ConvDesc) == 29 * 4
+    # 15 ints, float, uint, 6 ints, float, int, float, int, int, int (out_fp8), int (bn_defer_fold)
+    # -> 30 4-byte fields
+    assert ctypes.sizeof(_lib.ConvDesc) == 30 * 4
     # 16 operand pointers + 7 fused BatchNorm-backward reduction pointers + fp8 weight scales
     assert ctypes.sizeof(_lib.ConvIO) == 24 * 8

@@ -9,7 +9,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from adipose_amd import ops
+from adipose_amd import _lib, ops
 from adipose_amd.nets import Dense, Head
 from oracle import torch_ref as R
 
@@ -169,6 +169,74 @@ def test_tap64_configs(cfg):
     rs = ref.reshape(-1, cout)
     assert relerr(st[0, :cout], rs.sum(0)) < 2e-2
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
+
+
+@pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
+@pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad"])
+def test_tap64_persistent_matches(mode, grid):
+    """Persistent 256x256 tap64 kernel (conv_fwd_tap64p.hip: pipelined tile boundary, register epilogue
+    with 8-B buffer stores) vs the non-persistent kernel on the same launch: bit-identical outputs and
+    equal BatchNorm / channel sums; a 3-block grid makes every block walk many tiles (ragged last M tile,
+    partial N tile), so the cross-tile prefetch and the counted vmcnt wait are exercised."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(11)
+    kw = {}
+    if mode in ("plain", "concat", "split"):
+        N, S = 2, 23
+        parts = [128] if mode == "plain" else [64, 128]
+        cin = sum(parts)
+        nout = 320 if mode == "plain" else 256
+        srcs = [torch.randn(N, S, S, c, generator=g).to(DEV, dt) for c in parts]
+        W = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+        args = (srcs[0], W, nout)
+        if len(srcs) > 1:
+            kw["srcB"] = srcs[1]
+        outs = [torch.zeros(N, S, S, nout, dtype=dt, device=DEV)]
+        if mode == "split":
+            outs = [torch.zeros(N, S, S, 128, dtype=dt, device=DEV), torch.zeros(N, S, S, 128, dtype=dt, device=DEV)]
+            kw.update(out_mode=2, out2=outs[1], split_c=128)
+        else:
+            kw.update(bias=torch.randn(nout, generator=g).to(DEV), relu=mode == "plain")
+        stats_c = nout
+    elif mode == "convt_shuffle":   # ConvTranspose 2x2/s2 forward: 1x1 GEMM + pixel-shuffle store
+        N, S, cin, cs = 2, 19, 128, 64
+        x = torch.randn(N, S, S, cin, generator=g).to(DEV, dt)
+        W = (torch.randn(4 * cs, cin, generator=g) * 0.05).to(DEV, dt)
+        args = (x, W, 4 * cs)
+        outs = [torch.zeros(N, 2 * S, 2 * S, cs, dtype=dt, device=DEV)]
+        kw.update(bias=torch.randn(cs, generator=g).to(DEV), kh=1, kw=1, pad=0, out_mode=1, shuffle_c=cs)
+        stats_c = cs
+    else:   # ConvTranspose data gradient: stride-2 4-tap gather over the 2x-resolution gradient
+        N, S, cin, cs = 2, 21, 256, 64
+        dt_ = torch.randn(N, 2 * S, 2 * S, cs, generator=g).to(DEV, dt)
+        W = (torch.randn(cin, 4 * cs, generator=g) * 0.05).to(DEV, dt)
+        args = (dt_, W, cin)
+        outs = [torch.zeros(N, S, S, cin, dtype=dt, device=DEV)]
+        kw.update(kh=2, kw=2, dil=1, pad=0, stride=2, Ho=S, Wo=S)
+        stats_c = cin
+    res = []
+    for persist in (0, 1):
+        for o in outs:
+            o.zero_()
+        st = torch.zeros(2, stats_c, device=DEV)
+        ops.set_option("tap64_persist", persist)
+        ops.set_option("fwd_tap64", 2)   # the 256x256 configuration (small problems would pick narrower tiles)
+        if grid:
+            ops.set_option("tap64_persist_grid", grid)
+        try:
+            ops.conv_fwd(*args, out=outs[0], bn_stats=(st[0], st[1]), **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("tap64_persist", None)
+            ops.set_option("fwd_tap64", None)
+            ops.set_option("tap64_persist_grid", None)
+        res.append(([o.clone() for o in outs], st.clone(), kname))
+    assert res[0][2].startswith("igemm_fwd_tap64_kernel") and res[1][2].startswith("igemm_fwd_tap64p_kernel"), \
+        (res[0][2], res[1][2])
+    for a_, b_ in zip(res[0][0], res[1][0]):
+        assert torch.equal(a_, b_)
+    assert relerr(res[1][1], res[0][1]) < 1e-5
 
 
 def test_halo_fused_epilogues():

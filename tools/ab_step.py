@@ -5,6 +5,9 @@ alternating timed blocks so that clock drift and device variance hit both arms a
   --variant pool: bn_apply + maxpool2_fwd (old) vs the fused adp_bn_apply_maxpool2
   --variant head: materialised dec0_conv2 activation + adp_bn_bwd_reduce (old) vs BN-on-load head and
                   adp_head_sigmoid_bwd_bnr (UNetBN.fuse_head_bn)
+  --variant fold: conv-side BatchNorm statistic fold + finalize (old) vs the fold fused into the finalize
+                  (UNetBN.fuse_bn_fold)
+  --variant opt --opts "a=1;a=0": two native option settings (';'-separated, each ','-separated name=value)
 (the round-1 "stat" arm, per-layer statistic fills vs one arena fill, measured neutral:
 profiles/r01i_ab_stat_arena.txt; only the arena path remains)"""
 import argparse
@@ -18,7 +21,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head"])
+    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head", "fold", "opt"])
+    p.add_argument("--opts", default="")
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--steps", type=int, default=8)
     args = p.parse_args()
@@ -49,6 +53,16 @@ def main():
                     self._packed[l.name] = dst
     elif args.variant == "head":
         owner, attr, old, new = UNetBN, "fuse_head_bn", False, True
+    elif args.variant == "fold":
+        owner, attr, old, new = UNetBN, "fuse_bn_fold", False, True
+    elif args.variant == "opt":
+        class _Opts:   # setattr(owner, attr, settings) applies a native option setting
+            def __setattr__(self, _, st):
+                for kv in st.split(","):
+                    if kv:
+                        ops.set_option(kv.split("=")[0], int(kv.split("=")[1]))
+        owner, attr = _Opts(), "opts"
+        old, new = args.opts.split(";")
     else:
         owner, attr = ops, "bn_apply_maxpool2"
         new = ops.bn_apply_maxpool2
