@@ -3,6 +3,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -35,6 +36,22 @@ int option(const char* name, int dflt) {
   std::lock_guard<std::mutex> lk(g_opt_mu);
   auto it = opts().find(name);
   return it == opts().end() ? dflt : it->second;
+}
+int resident_grid(const void* kernel, int threads, size_t smem) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_pair(kernel, dev);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, smem) != hipSuccess) per = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  const int v = std::max(1, per) * std::max(1, cus);
+  cache[key] = v;
+  return v;
 }
 }  // namespace adp
 

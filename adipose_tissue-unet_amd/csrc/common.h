@@ -107,6 +107,10 @@ namespace adp {
 void set_error(const std::string& msg);
 int check_launch(const char* what);
 int option(const char* name, int dflt);  // runtime switches set through adp_set_option
+// blocks of `kernel` (threads per block, dynamic LDS bytes) that fit on the device at once: occupancy per
+// CU x CU count (cached per kernel and device) -- the grid of a grid-stride kernel whose blocks should all
+// be resident (no second round of blocks, no tail)
+int resident_grid(const void* kernel, int threads, size_t smem = 0);
 // name of the kernel the last conv launch of this thread used (adp_last_kernel), printf-style
 void set_kernel(const char* fmt, ...);
 // Replicated per-channel accumulators for the BatchNorm sums (statistics of a conv output, or the

@@ -27,6 +27,12 @@ constexpr int HH = PH + 2, HW = PW + 2;         // input halo
 constexpr int HROWS = HH * HW;                  // 340 halo pixels
 constexpr int ROWB = 128;                       // 64 bf16 channels per LDS row
 
+// 16-B chunk swizzle of the halo rows: c ^ (r & 7). The taps read 16 consecutive halo rows from ANY
+// base row ((wave + dy) * HW + mf * 16 + dx), and with swz(r) = (r >> 1) & 7 three bases in four put two
+// lanes of a ds_read_b128 lane group on one bank quad (8 LDS cycles instead of 4); r & 7 is conflict-free
+// for every base (the weight rows keep swz: their bases are multiples of 16).
+__device__ __forceinline__ int hswz(int r) { return r & 7; }
+
 // LDS-only barrier: this wave's LDS traffic done, then the hardware barrier. Unlike __syncthreads() it does
 // not wait for outstanding global stores / LDS-DMA prefetches (its workgroup fence drains vmcnt).
 #define LDS_BAR()                                             \
@@ -97,7 +103,7 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
   for (int i = 0; i < GH; ++i) {
     const int idx = i * NTH + tid;
     const int hr = idx >> 3, pos = idx & 7;
-    hcol[i] = 8 * (pos ^ swz(hr));
+    hcol[i] = 8 * (pos ^ hswz(hr));
     const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
     hoff[i] = (hr < HROWS && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws) ? (img * a.Hs + gy) * a.Ws + gx : -1;
   }
@@ -182,7 +188,7 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
       for (int mf = 0; mf < 4; ++mf) {
         const int prow = 2 * wm + (mf >> 1), pcol = (mf & 1) * 16 + r16;
         const int hr = (prow + dy) * HW + pcol + dx;
-        fa[mf] = *reinterpret_cast<const bf16x8*>(H + hr * ROWB + ((ck ^ swz(hr)) << 4));
+        fa[mf] = *reinterpret_cast<const bf16x8*>(H + hr * ROWB + ((ck ^ hswz(hr)) << 4));
       }
 #pragma unroll
       for (int mf = 0; mf < 4; ++mf)
@@ -300,7 +306,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     hdp[i] = hdy[i] * a.Ws + hdx[i];
     const bool inA = cc * 64 < a.CAs;
     hsrc[i] = inA ? 0 : 1;
-    hce[i] = (inA ? cc * 64 : cc * 64 - a.CAs) + 8 * (pos ^ swz(hr));
+    hce[i] = (inA ? cc * 64 : cc * 64 - a.CAs) + 8 * (pos ^ hswz(hr));
   }
   auto halo_src = [&](int img, int y0, int x0, int i) -> const uint4* {
     const int idx = i * NTH + tid;
@@ -407,7 +413,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
           for (int mf = 0; mf < 2; ++mf) {
             const int hr = (wave + dy) * HW + mf * 16 + r16 + dx;
-            fa[mf] = *reinterpret_cast<const bf16x8*>(Hc + hr * ROWB + ((ck ^ swz(hr)) << 4));
+            fa[mf] = *reinterpret_cast<const bf16x8*>(Hc + hr * ROWB + ((ck ^ hswz(hr)) << 4));
           }
           __builtin_amdgcn_s_setprio(1);
 #pragma unroll

@@ -202,9 +202,12 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, const T* src, con
 // t % G, pooled-pixel lane t / G): dsrc = route(dpool) + addend, with the BatchNorm-backward
 // reduction of the layer whose activation relu(z*scale+shift) src is fused in (dbeta += sum db,
 // dgamma += sum db*xhat over the STORED dsrc values, db = dsrc * (z*scale+shift > 0)), replacing the
-// separate bn_bwd_reduce pass over (dsrc, z).
-template <typename T>
-__global__ void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src, const T* dpool, const T* addend,
+// separate bn_bwd_reduce pass over (dsrc, z). src == nullptr: the argmax is taken over the activation
+// recomputed from z exactly as bn_apply / bn_apply_pool stored it (fmaf, fmaxf, round to T: bit-identical
+// values, so the same first maximum), which drops one of the four full-resolution streams (src, addend,
+// z, dsrc) from the pass.
+template <typename T, bool SRC>
+__global__ __launch_bounds__(TPB) void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src, const T* dpool, const T* addend,
                                        T* dsrc, const T* z, const float* sc, const float* sh, const float* mean,
                                        const float* invstd, float* stat) {
   const int G = C >> 3, lanes = TPB / G;
@@ -222,9 +225,11 @@ __global__ void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src,
     for (unsigned pix = blockIdx.x * lanes + pl; pix < P; pix += gridDim.x * lanes) {
       const unsigned xo = pix % Wo, t = pix / Wo, yo = t % Ho, n = t / Ho;
       const size_t base = (((size_t)n * H + 2 * yo) * W + 2 * xo) * C + g * 8;
-      Grp<T> gv[4], ga[4], gz[4], gp;
+      Grp<T> gv[SRC ? 4 : 1], ga[4], gz[4], gp;
+      if constexpr (SRC) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) grp_load(gv[q], src + base + off[q]);
+        for (int q = 0; q < 4; ++q) grp_load(gv[q], src + base + off[q]);
+      }
       grp_load(gp, dpool + (size_t)pix * C + g * 8);
 #pragma unroll
       for (int q = 0; q < 4; ++q) grp_load(ga[q], addend + base + off[q]);
@@ -233,7 +238,19 @@ __global__ void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src,
       float v[4][8], best[8], dp[8];
       int arg[8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) grp_to_f(gv[q], v[q]);
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (SRC) {
+          grp_to_f(gv[q], v[q]);
+        } else {   // the stored activation, recomputed
+          float f[8];
+          grp_to_f(gz[q], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], cs[j], ch[j]), 0.f);
+          Grp<T> r;
+          grp_from_f(r, f);
+          grp_to_f(r, v[q]);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) { best[j] = v[0][j]; arg[j] = 0; }
 #pragma unroll
@@ -833,7 +850,7 @@ extern "C" int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C, const
                                     const void* addend, void* dsrc, const void* z, const float* sc, const float* sh,
                                     const float* mean, const float* invstd, float* dgamma, float* dbeta,
                                     adp_stream_t st) {
-  ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && H % 2 == 0 && W % 2 == 0 && src && dpool && addend && dsrc && z && sc &&
+  ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && H % 2 == 0 && W % 2 == 0 && dpool && addend && dsrc && z && sc &&
                   sh && mean && invstd && dgamma && dbeta,
               "adp_maxpool2_bwd_bnr: need C%8==0, C<=2048, even H,W and every operand");
   ADP_REQUIRE((size_t)N * (H / 2) * (W / 2) < (1ull << 31), "adp_maxpool2_bwd_bnr: too many pooled pixels");
@@ -844,9 +861,12 @@ extern "C" int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C, const
   float* stat = adp::stat_scratch();
   ADP_REQUIRE(stat, adp_last_error());
   DTYPE_SWITCH(dtype, T,
-               hipLaunchKernelGGL(maxpool_bwd_bnr_kernel<T>, dim3(blocks), dim3(TPB), 0, (hipStream_t)st, N, H, W, C,
-                                  (const T*)src, (const T*)dpool, (const T*)addend, (T*)dsrc, (const T*)z, sc, sh,
-                                  mean, invstd, stat));
+               if (src) hipLaunchKernelGGL((maxpool_bwd_bnr_kernel<T, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st,
+                                           N, H, W, C, (const T*)src, (const T*)dpool, (const T*)addend, (T*)dsrc,
+                                           (const T*)z, sc, sh, mean, invstd, stat);
+               else hipLaunchKernelGGL((maxpool_bwd_bnr_kernel<T, false>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st,
+                                       N, H, W, C, (const T*)src, (const T*)dpool, (const T*)addend, (T*)dsrc,
+                                       (const T*)z, sc, sh, mean, invstd, stat));
   if (adp::check_launch("adp_maxpool2_bwd_bnr")) return -2;
   return adp::stat_fold(C, dbeta, dgamma, (hipStream_t)st);
 }

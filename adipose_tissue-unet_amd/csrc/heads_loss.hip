@@ -121,7 +121,7 @@ void launch_head_fwd(size_t M, int Cs, int Cin, const T* x, const float* W, cons
 // over the stored dx (adp_bn_bwd_reduce fused): dbeta += sum db, dgamma += sum db*(z-mean)*invstd,
 // db = dx*(z*sc+sh > 0)
 template <typename T, int NOUT, bool BNR = false>
-__global__ void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* sc,
+__global__ __launch_bounds__(TPB) void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* sc,
                                 const float* sh, const float* p, const float* dp, const T* addend,
                                 const T* mask, float ms, T* dx, float* dW, float* db, const float* bmean = nullptr,
                                 const float* binv = nullptr, float* stat = nullptr) {
@@ -150,43 +150,66 @@ __global__ void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const flo
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float r1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, r2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float dbacc = 0.f;
-  if (pl < lanes) {
-    for (size_t m = (size_t)blockIdx.x * lanes + pl; m < M; m += (size_t)gridDim.x * lanes) {
-      const float pm = p[m];
-      const float dz = dp[m] * pm * (1.f - pm);   // d p/d(z1-z0) for softmax2, d p/dz for sigmoid
-      Grp<T> gr;
-      float f[8], o[8], a[8], mk[8];
-      grp_load(gr, x + m * Cs + g * 8);
-      grp_to_f(gr, f);
-      if (addend) { grp_load(gr, addend + m * Cs + g * 8); grp_to_f(gr, a); }
-      if (mask) { grp_load(gr, mask + m * Cs + g * 8); grp_to_f(gr, mk); }
-      float v[8];
+  // U pixels per thread per pass, their x / p / dp loads issued before the first use (one 16-B load per
+  // thread in flight left the kernel at ~3 TB/s); addend / mask (softmax2 heads only) load per pixel
+  constexpr int U = 4;
+  auto one = [&](size_t m, float pm, float dpm, const Grp<T>& gx) {
+    const float dz = dpm * pm * (1.f - pm);   // d p/d(z1-z0) for softmax2, d p/dz for sigmoid
+    float f[8], o[8], a[8], mk[8];
+    grp_to_f(gx, f);
+    Grp<T> gt;
+    if (addend) { grp_load(gt, addend + m * Cs + g * 8); grp_to_f(gt, a); }
+    if (mask) { grp_load(gt, mask + m * Cs + g * 8); grp_to_f(gt, mk); }
+    float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = sc ? fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f) : f[j];
-      if constexpr (BNR) {   // the activation as adp_bn_apply materializes it (rounded to T)
-        Grp<T> gv;
-        grp_from_f(gv, v);
-        grp_to_f(gv, v);
-      }
+    for (int j = 0; j < 8; ++j) v[j] = sc ? fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f) : f[j];
+    if constexpr (BNR) {   // the activation as adp_bn_apply materializes it (rounded to T)
+      Grp<T> gv;
+      grp_from_f(gv, v);
+      grp_to_f(gv, v);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      acc[j] = fmaf(dz, v[j], acc[j]);
+      float d = dz * wd[j] + (addend ? a[j] : 0.f);
+      if (mask) d = mk[j] > 0.f ? d * ms : 0.f;
+      o[j] = d;
+    }
+    Grp<T> gr;
+    grp_from_f(gr, o);
+    if (dx) grp_store(gr, dx + m * Cs + g * 8);
+    if constexpr (BNR) {   // over the stored (rounded) gradient, as adp_bn_bwd_reduce reads it
+      float os[8];
+      grp_to_f(gr, os);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        acc[j] = fmaf(dz, v[j], acc[j]);
-        float d = dz * wd[j] + (addend ? a[j] : 0.f);
-        if (mask) d = mk[j] > 0.f ? d * ms : 0.f;
-        o[j] = d;
+        const float d = fmaf(f[j], s_[j], h_[j]) > 0.f ? os[j] : 0.f;
+        r1[j] += d;
+        r2[j] += d * (f[j] - mu[j]) * iv[j];
       }
-      if (dx) { grp_from_f(gr, o); grp_store(gr, dx + m * Cs + g * 8); }
-      if constexpr (BNR) {   // over the stored (rounded) gradient, as adp_bn_bwd_reduce reads it
-        float os[8];
-        grp_to_f(gr, os);
+    }
+    if (g == 0) dbacc += dz;
+  };
+  if (pl < lanes) {
+    const size_t step = (size_t)gridDim.x * lanes;
+    size_t m = (size_t)blockIdx.x * lanes + pl;
+    for (; m + (U - 1) * step < M; m += U * step) {
+      float pm[U], dpm[U];
+      Grp<T> gx[U];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = fmaf(f[j], s_[j], h_[j]) > 0.f ? os[j] : 0.f;
-          r1[j] += d;
-          r2[j] += d * (f[j] - mu[j]) * iv[j];
-        }
+      for (int u = 0; u < U; ++u) {
+        const size_t mu_ = m + u * step;
+        pm[u] = p[mu_];
+        dpm[u] = dp[mu_];
+        grp_load(gx[u], x + mu_ * Cs + g * 8);
       }
-      if (g == 0) dbacc += dz;
+#pragma unroll
+      for (int u = 0; u < U; ++u) one(m + u * step, pm[u], dpm[u], gx[u]);
+    }
+    for (; m < M; m += step) {
+      Grp<T> gx;
+      grp_load(gx, x + m * Cs + g * 8);
+      one(m, p[m], dp[m], gx);
     }
   }
   __shared__ float red[TPB * 8];
@@ -512,11 +535,13 @@ static int head_bwd(int dtype, size_t M, int Cs, int Cin, const void* x, const f
                     float ms, void* dx, float* dW, float* db, hipStream_t s) {
   ADP_REQUIRE(Cs % 8 == 0 && Cs / 8 <= TPB, "head backward: Cs must be a multiple of 8 and <= 2048");
   int lanes = TPB / (Cs / 8);
-  int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 4096);
-  DTYPE_SWITCH(dtype, T,
-               hipLaunchKernelGGL((head_bwd_kernel<T, NOUT>), dim3(blocks), dim3(TPB), 0, s, M, Cs, Cin,
-                                  (const T*)x, W, sc, sh, p, dp, (const T*)addend, (const T*)mask, ms, (T*)dx,
-                                  dW, db));
+  DTYPE_SWITCH(dtype, T, {
+    const int cap = adp::option("head_bwd_blocks",
+                                adp::resident_grid(reinterpret_cast<const void*>(&head_bwd_kernel<T, NOUT>), TPB));
+    const int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, (size_t)cap);
+    hipLaunchKernelGGL((head_bwd_kernel<T, NOUT>), dim3(blocks), dim3(TPB), 0, s, M, Cs, Cin, (const T*)x, W, sc, sh,
+                       p, dp, (const T*)addend, (const T*)mask, ms, (T*)dx, dW, db);
+  });
   return adp::check_launch("adp_head_bwd");
 }
 
@@ -537,11 +562,15 @@ extern "C" int adp_head_sigmoid_bwd_bnr(int dtype, size_t M, int Cs, int Cin, co
   float* stat = adp::stat_scratch();
   ADP_REQUIRE(stat, adp_last_error());
   const int lanes = TPB / (Cs / 8);
-  const int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 4096);
-  DTYPE_SWITCH(dtype, T,
-               hipLaunchKernelGGL((head_bwd_kernel<T, 1, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, Cs,
-                                  Cin, (const T*)z, W, sc, sh, p, dp, (const T*)nullptr, (const T*)nullptr, 1.f,
-                                  (T*)dx, dW, db, mean, invstd, stat));
+  // every block resident at once (measured at level 0: 233 us with 2 blocks per CU, 286 us with 4096)
+  DTYPE_SWITCH(dtype, T, {
+    const int cap = adp::option("head_bwd_blocks",
+                                adp::resident_grid(reinterpret_cast<const void*>(&head_bwd_kernel<T, 1, true>), TPB));
+    const int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, (size_t)cap);
+    hipLaunchKernelGGL((head_bwd_kernel<T, 1, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, Cs, Cin,
+                       (const T*)z, W, sc, sh, p, dp, (const T*)nullptr, (const T*)nullptr, 1.f, (T*)dx, dW, db, mean,
+                       invstd, stat);
+  });
   if (adp::check_launch("adp_head_sigmoid_bwd_bnr")) return -2;
   if (adp::stat_fold_at(0, Cs, dbeta, dgamma, (hipStream_t)st)) return -2;
   if (adp::stat_fold_at(Cs, Cin, dW, nullptr, (hipStream_t)st)) return -2;

@@ -344,9 +344,13 @@ def maxpool2_fwd(src, dst, bn=None):
     return dst
 
 
-def maxpool2_bwd(src, dpool, dsrc, *, bn=None, addend=None, mask=None, mask_scale=1.0, bn_reduce=None):
+def maxpool2_bwd(src, dpool, dsrc, *, bn=None, addend=None, mask=None, mask_scale=1.0, bn_reduce=None,
+                 argmax_from_z=True):
     """bn_reduce=(z, scale, shift, mean, invstd, dgamma, dbeta): fused BatchNorm-backward reduction of
-    the layer whose activation src is (adp_maxpool2_bwd_bnr; needs addend, no bn/mask)."""
+    the layer whose activation src = relu(z*scale+shift) is (adp_maxpool2_bwd_bnr; needs addend, no
+    bn/mask). argmax_from_z: the kernel recomputes src from z instead of reading it (bit-identical when
+    src was stored by bn_apply / bn_apply_maxpool2 with the same scale/shift; src then only gives the
+    shape)."""
     _act(src, "src")
     N, H, W, Cs = src.shape
     _check(tuple(dpool.shape) == (N, H // 2, W // 2, Cs), "dpool shape")
@@ -357,7 +361,8 @@ def maxpool2_bwd(src, dpool, dsrc, *, bn=None, addend=None, mask=None, mask_scal
         z, sc, sh, mean, inv, dg, db = bn_reduce
         _check(bn is None and mask is None and addend is not None and z.shape == src.shape and z.dtype == src.dtype,
                "maxpool2_bwd bn_reduce: needs addend, z like src, no bn/mask")
-        call("adp_maxpool2_bwd_bnr", dtype_code(src), N, H, W, Cs, ptr(src), ptr(dpool), ptr(addend), ptr(dsrc),
+        call("adp_maxpool2_bwd_bnr", dtype_code(src), N, H, W, Cs, None if argmax_from_z else ptr(src), ptr(dpool),
+             ptr(addend), ptr(dsrc),
              ptr(z), ptr(sc), ptr(sh), ptr(mean), ptr(inv), ptr(dg), ptr(db), stream_ptr())
         return dsrc
     call("adp_maxpool2_bwd", dtype_code(src), N, H, W, Cs, ptr(src), ptr(bn[0]) if bn else None,

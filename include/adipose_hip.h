@@ -151,7 +151,9 @@ int adp_maxpool2_bwd(int dtype, int N, int H, int W, int C_stride, const void* s
 /* unet_bn encoder pool backward: dsrc = route_argmax(dpool) + addend (no BN-on-load, no mask), with the
  * BatchNorm-backward reduction of the layer whose activation src = relu(z*scale+shift) fused in:
  * dbeta += sum db, dgamma += sum db*(z-mean)*invstd, db = dsrc*(z*scale+shift > 0) over the stored dsrc
- * (replaces adp_maxpool2_bwd + adp_bn_bwd_reduce; train_adipose_unet_v3.py:670 MaxPooling2D grad) */
+ * (replaces adp_maxpool2_bwd + adp_bn_bwd_reduce; train_adipose_unet_v3.py:670 MaxPooling2D grad).
+ * src may be NULL: the argmax then runs over relu(z*scale+shift) recomputed and rounded to dtype, the
+ * values adp_bn_apply / adp_bn_apply_maxpool2 store (one full-resolution read less) */
 int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C_stride, const void* src, const void* dpool,
                          const void* addend, void* dsrc, const void* z, const float* scale, const float* shift,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, adp_stream_t s);

@@ -561,13 +561,15 @@ def test_pool_bwd_fused_bn_reduce(dt, C):
     ops.bn_apply(z, sc, sh, a)
     dp = rb(torch.randn(N, H // 2, H // 2, C, generator=g), dt).to(DEV, dt).contiguous()
     add = rb(torch.randn(N, H, H, C, generator=g), dt).to(DEV, dt).contiguous()
-    d1, d2 = torch.zeros_like(z), torch.zeros_like(z)
-    dg1, db1, dg2, db2 = (torch.zeros(C, device=DEV) for _ in range(4))
+    d1, d2, d3 = torch.zeros_like(z), torch.zeros_like(z), torch.zeros_like(z)
+    dg1, db1, dg2, db2, dg3, db3 = (torch.zeros(C, device=DEV) for _ in range(6))
     ops.maxpool2_bwd(a, dp, d1, addend=add)
     ops.bn_bwd_reduce(d1, z, sc, sh, mu, ist, dg1, db1)
-    ops.maxpool2_bwd(a, dp, d2, addend=add, bn_reduce=(z, sc, sh, mu, ist, dg2, db2))
+    ops.maxpool2_bwd(a, dp, d2, addend=add, bn_reduce=(z, sc, sh, mu, ist, dg2, db2), argmax_from_z=False)
+    ops.maxpool2_bwd(a, dp, d3, addend=add, bn_reduce=(z, sc, sh, mu, ist, dg3, db3))   # argmax from z
     torch.cuda.synchronize()
-    assert torch.equal(d1, d2)
+    assert torch.equal(d1, d2) and torch.equal(d1, d3)
+    assert torch.equal(dg2, dg3) and torch.equal(db2, db3)
     zf, df = z.float().cpu(), d1.float().cpu()
     db = torch.where(zf * sc.cpu() + sh.cpu() > 0, df, torch.zeros_like(df))
     ref_b = db.sum((0, 1, 2))

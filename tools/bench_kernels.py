@@ -20,7 +20,8 @@ def main():
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--variants", default="conv_fast=2,fwd_tap64=0;conv_fast=2,fwd_tap64=1")
-    p.add_argument("--kinds", default="fwd,wgrad")
+    p.add_argument("--kinds", default="fwd,wgrad", help="fwd, fwd_stats, bnr (data gradient with the fused "
+                   "BatchNorm-backward reduction), wgrad")
     p.add_argument("--layers", default="", help="comma-separated substrings selecting layer shapes")
     p.add_argument("--batch", type=int, default=4)
     p.add_argument("--blas", action="store_true",
@@ -53,6 +54,12 @@ def main():
         W = (torch.randn(((cout + 63) // 64 * 64), Kpad, device=dev) * 0.02).to(torch.bfloat16)
         y = torch.empty(B, S, S, cout, device=dev, dtype=torch.bfloat16)
         dW = torch.zeros(((cout + 63) // 64 * 64), Kpad, device=dev)
+        # BatchNorm operands: forward statistics (fwd_stats) and the data gradient's fused BN-backward
+        # reduction (bnr: z = the pre-BN output of the layer below, same shape as y)
+        st = (torch.zeros(cout, device=dev), torch.zeros(cout, device=dev))
+        z = torch.randn(B, S, S, cout, device=dev).to(torch.bfloat16)
+        vec = [torch.rand(cout, device=dev) + 0.5 for _ in range(4)]
+        bnr = (z, vec[0], vec[1], vec[2], vec[3], torch.zeros(cout, device=dev), torch.zeros(cout, device=dev))
         flops = 2.0 * B * S * S * cout * K
         if args.blas:   # dense GEMM of the same shape: x2d (M x K) @ Wt (K x N), no im2col gather
             a2 = torch.randn(B * S * S, K, device=dev, dtype=torch.bfloat16)
@@ -78,8 +85,10 @@ def main():
                         d = (y.float() - y0.float()).abs().max().item()
                         print(json.dumps({"layer": name, "variant": v, "fwd_max_abs_diff_vs_v0": d}), flush=True)
                 for kind in kinds:
-                    fn = (lambda: ops.conv_fwd(x, W, cout, out=y)) if kind == "fwd" else \
-                        (lambda: ops.conv_wgrad(x, y, dW, cout))
+                    fn = {"fwd": lambda: ops.conv_fwd(x, W, cout, out=y),
+                          "fwd_stats": lambda: ops.conv_fwd(x, W, cout, out=y, bn_stats=st),
+                          "bnr": lambda: ops.conv_fwd(x, W, cout, out=y, bn_reduce=bnr),
+                          "wgrad": lambda: ops.conv_wgrad(x, y, dW, cout)}[kind]
                     fn()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
