@@ -326,7 +326,7 @@ namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s);
 // conv_fwd_tap64p.hip: persistent 256x256 form of the same kernel with the tile boundary pipelined
 // (next tile's first stage in flight during a register epilogue); called by launch_fwd_tap64.
-int launch_fwd_tap64p(FwdArgs& a, hipStream_t s);
+int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile);   // tile: tap64 config 0 (256x256) / 1 (256x128)
 // conv_fwd_halo.hip: halo-reuse 3x3 kernel for narrow (<= 128 output channels) stride-1 layers.
 int launch_fwd_halo(FwdArgs& a, hipStream_t s);
 int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)

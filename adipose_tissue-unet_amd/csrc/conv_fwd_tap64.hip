@@ -363,7 +363,9 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
     }
     if (best <= 0.0) return 0;
   }
-  if (cfg == 0 && !a.bnr_z && launch_fwd_tap64p(a, s)) return 1;
+  // the persistent kernel for the 256x256 and 256x128 tiles (BNR launches: option tap64p_bnr)
+  if ((cfg == 0 || cfg == 1) && !a.f8 && (!a.bnr_z || option("tap64p_bnr", 1)) && launch_fwd_tap64p(a, s, cfg))
+    return 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);
   else if (cfg == 2) launch_cfg<4, 1, 128>(a, s);

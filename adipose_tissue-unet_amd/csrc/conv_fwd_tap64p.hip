@@ -33,6 +33,23 @@ __device__ __forceinline__ v2u32 p_ld8(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
 }
 
+// epilogue constant read (ds_read_b128 + its own lgkmcnt wait) as inline asm: the compiler's form of an
+// LDS read after the LDS-DMA prefetch of the next stages gets a vmcnt(0) in front -- it cannot tell the
+// constants from the stages being written -- which drained the whole prefetch at every tile's epilogue
+__device__ __forceinline__ float4 p_lds_f4(const float* p) {
+  float4 r;
+  const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
+
+// the block's BatchNorm sums: LDS float add as inline asm for the same reason (no lgkmcnt wait: nothing
+// reads sacc before the final barrier, which is preceded by an explicit lgkmcnt(0))
+__device__ __forceinline__ void p_lds_add(float* p, float v) {
+  const unsigned addr = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)p;
+  asm volatile("ds_add_f32 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
 #define P_BAR()                            \
   do {                                     \
     asm volatile("" ::: "memory");         \
@@ -40,22 +57,34 @@ __device__ __forceinline__ v2u32 p_ld8(__amdgpu_buffer_rsrc_t r, unsigned off) {
     asm volatile("" ::: "memory");         \
   } while (0)
 
-template <bool BNR>
+// BM x BN tile, NST-stage LDS ring. 8 waves: WN = BN / 64 along N, WM = 8 / WN along M, a wave owns TM
+// pixels x 64 channels. The K steps of ALL the block's tiles form one stream: the loader runs NST - 1 steps
+// ahead of the multiply, across tile boundaries, so with NST = 3 two stages are in flight while a third
+// multiplies (the small-K ConvTranspose / N = 128 shapes, whose tiles are only 2..18 steps long).
+template <int BM, int BN, int NST, bool BNR>
+constexpr int tap64p_lds() { return NST * (BM + BN) * 128 + 7 * BN * 4; }
+
+template <int BM, int BN, int NST, bool BNR>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
-  constexpr int WN = 4, TM = 128, NTH = 512;
-  constexpr int BM = 256, BN = 256, ROWB = 128, ES = 2, KSTEP = 64;
-  constexpr int QA = BM / 2, QB = BN / 2, GA = QA * 8 / NTH, GB = QB * 8 / NTH;   // 2, 2
-  constexpr int HM = TM / 2, MIQ = TM / 32;                                       // 64, 4
+  constexpr int NTH = 512, ROWB = 128, ES = 2, KSTEP = 64;
+  constexpr int WN = BN / 64, WM = 8 / WN, TM = BM / WM;
+  static_assert(WN * WM == 8 && TM % 32 == 0 && TM >= 64, "wave layout");
+  constexpr int QA = BM / 2, QB = BN / 2, GA = QA * 8 / NTH, GB = QB * 8 / NTH;
+  static_assert(GA >= 1 && GB >= 1, "staging split");
+  constexpr int HM = TM / 2, MIQ = TM / 32;
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int OA1 = QA * ROWB, OB0 = BM * ROWB, OB1 = (BM + QB) * ROWB;
-  constexpr int EPI_OPS = 2 * MIQ * 4;   // stores per thread per epilogue (one per accumulator tile)
+  constexpr int LOPS = 2 * GA + 2 * GB;                    // LDS-DMA pieces per thread per stage
+  constexpr int EPI_OPS = 2 * MIQ * 4 * (BNR ? 2 : 1);     // vector-memory ops per thread per epilogue
+  // (vmcnt holds 0..63: a larger count is clamped, which only waits for more)
+  constexpr int VM_EPI = (NST - 2) * LOPS + EPI_OPS < 63 ? (NST - 2) * LOPS + EPI_OPS : 63;
   // ONE LDS object: with several, the compiler tags every LDS access with per-object alias scopes, and the
   // waitcnt pass then drains vmcnt(0) between the LDS-DMA prefetch of stage t+1 and the fragment reads of
   // stage t (one object: no such wait -- measured 12 % of the K loop)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE + 7 * BN * 4];
-  float (*cst)[BN] = reinterpret_cast<float (*)[BN]>(smem + 2 * STAGE);         // epilogue constants:
-                                                                                 // bias | scale shift mean invstd (BNR)
-  float (*sacc)[BN] = reinterpret_cast<float (*)[BN]>(smem + 2 * STAGE + 5 * BN * 4);   // block's BN sums
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[tap64p_lds<BM, BN, NST, BNR>()];
+  float (*cst)[BN] = reinterpret_cast<float (*)[BN]>(smem + NST * STAGE);   // epilogue constants:
+                                                                           // bias | scale shift mean invstd (BNR)
+  float (*sacc)[BN] = reinterpret_cast<float (*)[BN]>(smem + NST * STAGE + 5 * BN * 4);   // block's BN sums
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WN, wc = wave % WN;
@@ -99,7 +128,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       const int col = (q / 32) * 64 + h * 32 + (q % 32);
       bo[h][i] = n0 + col < Wrows ? (unsigned)((n0 + col) * a.Kpad * ES + 16 * (pos ^ swz(q))) : P_OOB;
     }
-  // ---- A staging rows of the tile being loaded: quarter h, instruction i -> quarter row q
+  // ---- A staging rows of the tile being LOADED: quarter h, instruction i -> quarter row q
   int ry[2][GA], rx[2][GA], pb[2][GA];   // (up == 1 only: an invalid row has ry far out of range)
   const int rc = 16 * (pos ^ ((tid >> 4) & 7));   // = 16 * (pos ^ swz(q)) for every staging row q of this thread
   auto setup_rows = [&](int m0) {
@@ -120,7 +149,6 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // ---- K-step iterator of the tile being loaded (channel-chunk fastest inside a tap)
   struct Kt { int oy, ox, cs, cb, srcb, dpix, kt; };
   int it_ci = 0, it_ty = 0, it_tx = 0, it_kt = 0;
-  auto kreset = [&]() { it_ci = it_ty = it_tx = it_kt = 0; };
   auto kinfo = [&]() {
     Kt r;
     r.oy = it_ty * a.dil; r.ox = it_tx * a.dil; r.kt = it_kt;
@@ -154,6 +182,19 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         p_lds16(rsW, dsb + i * (NTH / 8) * ROWB, off);
       }
     }
+  };
+  // the loader: the next K step of the block's stream (tile lk, step lt) into stage ls
+  int lk = 0, lt = 0, ls = 0;
+  auto tile_m0 = [&](int k) { return ((lin + k * G) / a.ntile_n) * BM; };
+  auto load_next = [&]() {
+    if (lk >= mine) return;   // stream exhausted (uniform)
+    if (lt == 0) {
+      setup_rows(tile_m0(lk));
+      it_ci = it_ty = it_tx = it_kt = 0;
+    }
+    issue(kinfo(), ls);
+    ls = ls == NST - 1 ? 0 : ls + 1;
+    if (++lt == nk) { lt = 0; ++lk; }
   };
 
   const int r16 = lane & 15, h4 = lane >> 4;
@@ -213,18 +254,27 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       const int c = n0 + wc * 64 + nt * 16 + 4 * h4;   // first of this lane's 4 channels (GEMM column)
       const bool cv = c < a.Nout;
       const int cl = wc * 64 + nt * 16 + 4 * h4;         // the same, relative to n0
-      const float4 b4 = *reinterpret_cast<const float4*>(&cst[0][cl]);
+      const float4 b4 = p_lds_f4(&cst[0][cl]);
       const float bias[4] = {b4.x, b4.y, b4.z, b4.w};
       float sc[4], sh[4], mu[4], is[4];
-      if (BNR) {
-        const float4 a4 = *reinterpret_cast<const float4*>(&cst[1][cl]);
-        const float4 s4 = *reinterpret_cast<const float4*>(&cst[2][cl]);
-        const float4 m4 = *reinterpret_cast<const float4*>(&cst[3][cl]);
-        const float4 i4 = *reinterpret_cast<const float4*>(&cst[4][cl]);
+      // BNR: the 2*MIQ z quads of this channel group, all loaded before the first store of the group (a
+      // load behind a store waits for it: vmcnt retires in order)
+      bf16x4 zq[BNR ? 2 * MIQ : 1];
+      if constexpr (BNR) {
+        const float4 a4 = p_lds_f4(&cst[1][cl]);
+        const float4 s4 = p_lds_f4(&cst[2][cl]);
+        const float4 m4 = p_lds_f4(&cst[3][cl]);
+        const float4 i4 = p_lds_f4(&cst[4][cl]);
         sc[0] = a4.x; sc[1] = a4.y; sc[2] = a4.z; sc[3] = a4.w;
         sh[0] = s4.x; sh[1] = s4.y; sh[2] = s4.z; sh[3] = s4.w;
         mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
         is[0] = i4.x; is[1] = i4.y; is[2] = i4.z; is[3] = i4.w;
+#pragma unroll
+        for (int mt = 0; mt < 2 * MIQ; ++mt) {
+          const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
+          const bool v = cv && m < a.M;
+          zq[mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+        }
       }
       // store target of the channel quad: GEMM column c -> (buffer, channel offset)
       int sub = 0, cq = c;
@@ -259,11 +309,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         }
         const unsigned off = v ? (unsigned)((pix * ostr + cq) * ES) : P_OOB;
         p_st8(rsO, off, __builtin_bit_cast(v2u32, o));
-        if (BNR) {
-          const bf16x4 zz = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+        if constexpr (BNR) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float g = (float)o[r], zf = (float)zz[r];   // the stored (rounded) gradient
+            const float g = (float)o[r], zf = (float)zq[mt][r];   // the stored (rounded) gradient
             const float db = fmaf(zf, sc[r], sh[r]) > 0.f ? g : 0.f;
             s1[r] += db;
             s2[r] += db * (zf - mu[r]) * is[r];
@@ -285,15 +334,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         if (r16 == 0) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            atomicAdd(&sacc[0][cl + r], s1[r]);
-            atomicAdd(&sacc[1][cl + r], s2[r]);
+            p_lds_add(&sacc[0][cl + r], s1[r]);
+            p_lds_add(&sacc[1][cl + r], s2[r]);
           }
         }
       }
     }
   };
 
-  // ---- the pipelined tile loop (first and last K step of a tile peeled: no branches in the steady loop)
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   auto compute = [&](int buf) {
     readA(buf, 0, fa);
@@ -305,48 +353,37 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     mma(fa, fb1, 1, 1);
     mma(fa, fb0, 1, 0);
   };
-  int m0 = ((lin) / a.ntile_n) * BM;
-  setup_rows(m0);
-  kreset();
-  issue(kinfo(), 0);
-  int gs = 0;   // global K-step counter; stage = gs & 1 (the & keeps the stage index provably in {0, 1}, so
-                // the compiler can tell the LDS-DMA target stage from the stage being read and does not
-                // insert a vmcnt(0) drain before the reads)
+  // ---- the stream: prologue fills NST - 1 stages; step gs waits for its stage, issues step gs + NST - 1
+  // into the stage step gs - 1 read (every wave is past this step's barrier, so nobody reads it), multiplies.
+  // The wait counts what was issued after the stage: the NST - 2 younger stages and, when a tile ended
+  // inside that window, its EPI_OPS epilogue ops; near the end of the stream (fewer younger stages) it
+  // drains everything.
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i) load_next();
+  const int total = mine * nk;
+  int gs = 0, cs = 0, last_epi = -NST;   // step, its stage, step of the latest epilogue
   for (int k = 0; k < mine; ++k) {
-    const int m0c = m0;
+    const int m0c = tile_m0(k);
 #pragma unroll
     for (int i = 0; i < 2 * MIQ; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // step 0: its stage was issued before the previous tile's EPI_OPS epilogue stores (k > 0)
-    if (k > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    P_BAR();
-    issue(kinfo(), (gs & 1) ^ 1);
-    compute(gs & 1);
-    ++gs;
-    for (int t = 1; t < nk - 1; ++t, ++gs) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      P_BAR();   // stage t landed for every wave, and nobody reads the other stage any more
-      issue(kinfo(), (gs & 1) ^ 1);
-      compute(gs & 1);
+    for (int t = 0; t < nk; ++t, ++gs) {
+      if (gs + NST - 2 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
+      P_BAR();   // stage cs landed for every wave, and nobody reads the stage being refilled any more
+      load_next();
+      compute(cs);
+      cs = cs == NST - 1 ? 0 : cs + 1;
     }
-    // last step: the next tile's first stage goes into the free stage, overlapping this tile's epilogue
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    P_BAR();
-    if (k + 1 < mine) {
-      m0 = ((lin + (k + 1) * G) / a.ntile_n) * BM;
-      setup_rows(m0);
-      kreset();
-      issue(kinfo(), (gs & 1) ^ 1);
-    }
-    compute(gs & 1);
-    ++gs;
+    last_epi = gs - 1;
     if (a.debug_flags & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue
 #pragma unroll
       for (int i = 0; i < 2 * MIQ; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+      last_epi = -NST;   // (no epilogue ops were issued)
       continue;
     }
     epilogue(m0c);
@@ -354,6 +391,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
 
   // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
   if (!stats || (a.debug_flags & 2)) return;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
   float* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
   if (tid < BN) {
@@ -371,8 +409,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
 }  // namespace
 
 namespace adp {
-// 256x256 persistent launch for the epilogue forms it covers; 0 = not eligible (the caller falls back)
-int launch_fwd_tap64p(FwdArgs& a, hipStream_t s) {
+// persistent launch for the epilogue forms it covers; 0 = not eligible (the caller falls back).
+// Tile / ring (option tap64p_cfg, 0 = from the tap64 tile choice): 1 = 256x256 / 2 stages,
+// 2 = 256x128 / 3 stages, 3 = 128x256 / 3 stages.
+int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   if (!option("tap64_persist", 1) || a.f8 || a.K < 128) return 0;   // (two K steps at least)
   if (a.addend || a.mask || a.mask2 || a.accum || a.drop_rate > 0.f || a.scA || a.scB) return 0;
   if (a.up != 1) return 0;
@@ -388,15 +428,34 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s) {
       (size_t)((a.Nout + 63) / 64 * 64) * a.Kpad * 2 >= lim || (a.out2 && (size_t)a.M * a.out2_stride * 2 >= lim) ||
       (a.bnr_z && (size_t)a.M * a.bnr_zs * 2 >= lim))
     return 0;
-  a.ntile_n = (a.Nout + 255) / 256;
-  const int mt = (a.M + 255) / 256;
+  // auto (tools/bench_kernels.py, bench_convt.py; profiles/r02_tap64p_cfg_ab.txt): the tap64 256x128 choice
+  // -> 256x128 / 3 stages; 256x256 -> 256x256 / 2 stages for K >= 512 (3x3 layers: +3-7 % over tap64) and
+  // 128x256 / 3 stages for the short ConvTranspose K of 128..256 (+8-15 % over 256x256); the fused BN-backward
+  // reduction only on the 256x128 form (its z loads wait behind the prefetch stream, which costs the
+  // 256x256 form 5-8 % against tap64's LDS-staged epilogue)
+  int cfg = option("tap64p_cfg", 0);
+  if (cfg < 1 || cfg > 3) {
+    if (a.bnr_z && tile != 1 && option("tap64p_bnr", 1) < 2) return 0;
+    cfg = tile == 1 ? 2 : (a.K <= 256 ? 3 : 1);
+  }
+  const int BM = cfg == 3 ? 128 : 256, BN = cfg == 2 ? 128 : 256;
+  a.ntile_n = (a.Nout + BN - 1) / BN;
+  const int mt = (a.M + BM - 1) / BM;
   a.nblocks = mt * a.ntile_n;   // tiles; the grid is persistent
   int grid = std::min(a.nblocks, option("tap64_persist_grid", 256));
   grid -= grid % a.ntile_n;
   if (grid <= 0) grid = a.ntile_n;
-  adp::set_kernel("igemm_fwd_tap64p_kernel<%s>", a.bnr_z ? "true" : "false");
-  if (a.bnr_z) hipLaunchKernelGGL(igemm_fwd_tap64p_kernel<true>, dim3(grid), dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(igemm_fwd_tap64p_kernel<false>, dim3(grid), dim3(512), 0, s, a);
+  const bool bnr = a.bnr_z != nullptr;
+  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
+#define P_LAUNCH(BM_, BN_, NST_)                                                                           \
+  do {                                                                                                     \
+    if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, false>), dim3(grid), dim3(512), 0, s, a);   \
+  } while (0)
+  if (cfg == 1) P_LAUNCH(256, 256, 2);
+  else if (cfg == 2) P_LAUNCH(256, 128, 3);
+  else P_LAUNCH(128, 256, 3);
+#undef P_LAUNCH
   return 1;
 }
 }  // namespace adp

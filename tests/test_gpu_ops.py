@@ -171,21 +171,25 @@ def test_tap64_configs(cfg):
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("cfg", [1, 2, 3], ids=["256x256x2", "256x128x3", "128x256x3"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
-@pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad"])
-def test_tap64_persistent_matches(mode, grid):
-    """Persistent 256x256 tap64 kernel (conv_fwd_tap64p.hip: pipelined tile boundary, register epilogue
-    with 8-B buffer stores) vs the non-persistent kernel on the same launch: bit-identical outputs and
-    equal BatchNorm / channel sums; a 3-block grid makes every block walk many tiles (ragged last M tile,
-    partial N tile), so the cross-tile prefetch and the counted vmcnt wait are exercised."""
+@pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad", "bnr"])
+def test_tap64_persistent_matches(mode, grid, cfg):
+    """Persistent tap64 kernel (conv_fwd_tap64p.hip: one K-step stream over the block's tiles through an
+    NST-stage LDS ring, register epilogue with 8-B buffer stores) in its three tile / ring forms vs the
+    non-persistent kernel on the same launch: bit-identical outputs and equal BatchNorm sums (statistics,
+    or the fused BatchNorm-backward reduction for bnr); a 3-block grid makes every block walk many tiles
+    (ragged last M tile, partial N tile), so the cross-tile prefetch and the counted vmcnt waits are
+    exercised."""
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(11)
     kw = {}
-    if mode in ("plain", "concat", "split"):
+    bnr = None
+    if mode in ("plain", "concat", "split", "bnr"):
         N, S = 2, 23
-        parts = [128] if mode == "plain" else [64, 128]
+        parts = [128] if mode in ("plain", "bnr") else [64, 128]
         cin = sum(parts)
-        nout = 320 if mode == "plain" else 256
+        nout = 320 if mode in ("plain", "bnr") else 256
         srcs = [torch.randn(N, S, S, c, generator=g).to(DEV, dt) for c in parts]
         W = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
         args = (srcs[0], W, nout)
@@ -195,6 +199,10 @@ def test_tap64_persistent_matches(mode, grid):
         if mode == "split":
             outs = [torch.zeros(N, S, S, 128, dtype=dt, device=DEV), torch.zeros(N, S, S, 128, dtype=dt, device=DEV)]
             kw.update(out_mode=2, out2=outs[1], split_c=128)
+        elif mode == "bnr":   # data gradient with the fused BatchNorm-backward reduction of the layer below
+            z = torch.randn(N, S, S, nout, generator=g).to(DEV, dt)
+            vec = [(torch.rand(nout, generator=g) + 0.5).to(DEV) for _ in range(4)]
+            bnr = (z, vec[0], vec[1] - 1.0, vec[2] - 1.0, vec[3])
         else:
             kw.update(bias=torch.randn(nout, generator=g).to(DEV), relu=mode == "plain")
         stats_c = nout
@@ -221,16 +229,19 @@ def test_tap64_persistent_matches(mode, grid):
         st = torch.zeros(2, stats_c, device=DEV)
         ops.set_option("tap64_persist", persist)
         ops.set_option("fwd_tap64", 2)   # the 256x256 configuration (small problems would pick narrower tiles)
+        ops.set_option("tap64p_cfg", cfg)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
-            ops.conv_fwd(*args, out=outs[0], bn_stats=(st[0], st[1]), **kw)
+            if bnr is not None:
+                ops.conv_fwd(*args, out=outs[0], bn_reduce=bnr + (st[1], st[0]), **kw)
+            else:
+                ops.conv_fwd(*args, out=outs[0], bn_stats=(st[0], st[1]), **kw)
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            ops.set_option("tap64_persist", None)
-            ops.set_option("fwd_tap64", None)
-            ops.set_option("tap64_persist_grid", None)
+            for o_ in ("tap64_persist", "fwd_tap64", "tap64_persist_grid", "tap64p_cfg"):
+                ops.set_option(o_, None)
         res.append(([o.clone() for o in outs], st.clone(), kname))
     assert res[0][2].startswith("igemm_fwd_tap64_kernel") and res[1][2].startswith("igemm_fwd_tap64p_kernel"), \
         (res[0][2], res[1][2])
