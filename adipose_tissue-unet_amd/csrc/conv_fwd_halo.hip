@@ -16,6 +16,8 @@
 // K loop: step s = chunk * ceil(9/TPS) + j covers taps j*TPS ..; at step s the block issues the weights
 // of step s+2 (and, at a chunk's first step, the next chunk's halo) and retires step s+1 with one
 // counted vmcnt before the step's barrier. The 64-channel layers take two taps per step.
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace {
@@ -248,7 +250,10 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 // staging and no barrier; the next tile's halo is prefetched into registers at the first tap and
 // written to the single LDS halo buffer between two barriers; BatchNorm sums stay in registers until
 // the block's last tile and go to the accumulator replicas once per wave.
-template <bool BNR, int NCH, int BN>
+#ifndef HALOP_VALU_PER_MFMA
+#define HALOP_VALU_PER_MFMA 8
+#endif
+template <bool BNR, int NCH, int BN, bool PIPE>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   // NCH 64-channel input chunks (1: Cin_s 64; 2: Cin_s 128 from one or two sources), BN output channels
   // per block (64, or 32 for two chunks: 2 x 340 halo rows + 9 x 2 x 32 weight rows = 157 KiB of LDS)
@@ -263,6 +268,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   static_assert(GW * NTH == 9 * NCH * BN * 8, "weights must split evenly");
   static_assert(SMEM <= 160 * 1024, "LDS");
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int v2u32_h __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -293,29 +299,21 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     img = r / ty_n;
     x0 = px * PW;
   };
-  // per-thread constant parts of the halo gather: group i -> (input chunk source, pixel delta from the
-  // tile's (y0 - 1, x0 - 1), halo row/col, channel element offset)
-  int hdy[GH], hdx[GH], hdp[GH], hce[GH], hsrc[GH];
-#pragma unroll
-  for (int i = 0; i < GH; ++i) {
-    const int idx = i * NTH + tid;
-    const int cc = NCH == 1 ? 0 : idx / (HROWS * 8), rem = idx - cc * HROWS * 8;
-    const int hr = rem >> 3, pos = rem & 7;
-    hdy[i] = hr / HW - 1;
-    hdx[i] = hr % HW - 1;
-    hdp[i] = hdy[i] * a.Ws + hdx[i];
-    const bool inA = cc * 64 < a.CAs;
-    hsrc[i] = inA ? 0 : 1;
-    hce[i] = (inA ? cc * 64 : cc * 64 - a.CAs) + 8 * (pos ^ hswz(hr));
-  }
+  // halo gather of group i: chunk idx = i * NTH + tid -> (input chunk cc, halo row hr, 16-B position pos);
+  // derived per call (a few VALU per group and tile) instead of held in 5 x GH registers per thread, which
+  // the pipelined epilogue needs. pos = tid & 7 for every group (NTH and HROWS * 8 are multiples of 8).
   auto halo_src = [&](int img, int y0, int x0, int i) -> const uint4* {
     const int idx = i * NTH + tid;
-    const int gy = y0 + hdy[i], gx = x0 + hdx[i];
+    const int cc = NCH == 1 ? 0 : (idx >= HROWS * 8 ? 1 : 0), hr = (idx - cc * HROWS * 8) >> 3;
+    const int hy = hr / HW, hx = hr - hy * HW;
+    const int gy = y0 + hy - 1, gx = x0 + hx - 1;
     const bool ok = (i < GH - 1 || idx < HCH) && (unsigned)gy < (unsigned)a.Hs && (unsigned)gx < (unsigned)a.Ws;
     if (!ok) return nullptr;
-    const bf16* src = reinterpret_cast<const bf16*>(hsrc[i] ? a.srcB : a.srcA);
-    const int cs = hsrc[i] ? a.CBs : a.CAs;
-    return reinterpret_cast<const uint4*>(src + (size_t)((img * a.Hs + y0) * a.Ws + x0 + hdp[i]) * cs + hce[i]);
+    const bool inA = cc * 64 < a.CAs;
+    const bf16* src = reinterpret_cast<const bf16*>(inA ? a.srcA : a.srcB);
+    const int cs = inA ? a.CAs : a.CBs;
+    return reinterpret_cast<const uint4*>(src + (size_t)((img * a.Hs + gy) * a.Ws + gx) * cs +
+                                          (inA ? cc * 64 : cc * 64 - a.CAs) + 8 * ((tid & 7) ^ hswz(hr)));
   };
 
   // ---- prologue: nine weight taps (resident), first halo, per-channel constants
@@ -362,23 +360,76 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[nf][i] = 0.f; s2[nf][i] = 0.f; }
 
-  for (int k = 0; k < nt; ++k) {
+  // the store target as a buffer resource: a lane whose channel quad lies past nlim stores to an
+  // out-of-range offset (dropped) instead of branching around the store, so the epilogue has no divergent
+  // control flow and its units can sit between the MFMAs of the next tile (PIPE)
+  const __amdgpu_buffer_rsrc_t rsO =
+      __builtin_amdgcn_make_buffer_rsrc((void*)obase, 0, a.M * ostride * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsZ = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNR ? a.bnr_z : a.out), 0, BNR ? a.M * a.bnr_zs * 2 : 0, 0x00020000);
+  // BNR: the z quads of one accumulator tile
+  auto load_z = [&](int mrow_, uint2 (&zr)[2][NF]) {
+#pragma unroll
+    for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf) {
+        const int c0 = nf * 16 + 4 * h4;
+        const unsigned off = n0 + c0 < a.Nout ? (unsigned)(((mrow_ + mf * 16 + r16) * a.bnr_zs + n0 + c0) * 2) : 0x80000000u;
+        zr[mf][nf] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rsZ, off, 0, 0));
+      }
+  };
+  // epilogue of accumulator tile (mf, nf): lane = pixel mrow_ + mf*16 + r16, channels nf*16 + 4*h4 .. +3
+  auto epi_unit = [&](int mf, int nf, const f32x4& av, uint2 zv, int mrow_) {
+    const int c0 = nf * 16 + 4 * h4;
+    const bool cv = n0 + c0 < nlim;
+    const float4 cb = *reinterpret_cast<const float4*>(cst + c0);
+    const int m = mrow_ + mf * 16 + r16;
+    float v[4] = {av[0] + cb.x, av[1] + cb.y, av[2] + cb.z, av[3] + cb.w};
+    bf16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (relu) v[i] = fmaxf(v[i], 0.f);
+      o[i] = (bf16)v[i];
+    }
+    const unsigned off = cv ? (unsigned)((m * ostride + ocol0 + c0) * 2) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_h, o), rsO, off, 0, 0);
+    if constexpr (BNR) {
+      const float4 sc = *reinterpret_cast<const float4*>(cst + BN + c0);
+      const float4 sh = *reinterpret_cast<const float4*>(cst + 2 * BN + c0);
+      const float4 mu = *reinterpret_cast<const float4*>(cst + 3 * BN + c0);
+      const float4 is = *reinterpret_cast<const float4*>(cst + 4 * BN + c0);
+      const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+      const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+      bf16x4 zz = __builtin_bit_cast(bf16x4, zv);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float g = (float)o[i], zf = (float)zz[i];   // the stored (rounded) gradient
+        const float db = fmaf(zf, scv[i], shv[i]) > 0.f ? g : 0.f;   // (z = 0 past nlim: sc = sh = 0 there)
+        s1[nf][i] += db;
+        s2[nf][i] += db * (zf - muv[i]) * isv[i];
+      }
+    } else if (stats) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x = cv ? v[i] : 0.f;
+        s1[nf][i] += x;
+        s2[nf][i] += x * x;
+      }
+    }
+  };
+
+  f32x4 acc[2][NF], accp[2][NF];   // this tile's / the previous tile's accumulators (PIPE)
+  uint2 zreg[2][NF];
+  int mrowp = 0;
+  // one tile: prefetch the next tile's halo into registers, nine taps, then (PIPE) nothing -- the
+  // previous tile's epilogue units run between this tile's taps -- or (!PIPE) this tile's epilogue
+  auto run_tile = [&](int k, auto with_prev) {
+    constexpr bool EPI_PREV = decltype(with_prev)::value;
     const bool more = k + 1 < nt;
     int img, y0, x0;
     tile_origin(k, img, y0, x0);
     const int mrow = (img * a.Ho + y0 + wave) * a.Wo + x0;   // first output pixel of this wave's row
-    uint2 zreg[2][NF];
-    if constexpr (BNR) {
-#pragma unroll
-      for (int mf = 0; mf < 2; ++mf)
-#pragma unroll
-        for (int nf = 0; nf < NF; ++nf) {
-          const int c0 = nf * 16 + 4 * h4;
-          zreg[mf][nf] = n0 + c0 < a.Nout ? *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.bnr_z) +
-                                                                            (size_t)(mrow + mf * 16 + r16) * a.bnr_zs + n0 + c0)
-                                          : make_uint2(0, 0);
-        }
-    }
+    if constexpr (BNR) load_z(EPI_PREV ? mrowp : mrow, zreg);
     uint4 hreg[GH];
     if (more) {
       int img1, y01, x01;
@@ -389,7 +440,6 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
         hreg[i] = p ? *p : make_uint4(0, 0, 0, 0);
       }
     }
-    f32x4 acc[2][NF];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -415,53 +465,42 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
             const int hr = (wave + dy) * HW + mf * 16 + r16 + dx;
             fa[mf] = *reinterpret_cast<const bf16x8*>(Hc + hr * ROWB + ((ck ^ hswz(hr)) << 4));
           }
-          __builtin_amdgcn_s_setprio(1);
+          // previous tile's epilogue unit u in tap u + 1 (the z loads had a tap's time to land), its VALU
+          // spread between this step's MFMAs
+          constexpr bool unit_here = EPI_PREV;
+          const bool with_unit = unit_here && cc == 0 && kq == 0 && t >= 1 && t - 1 < 2 * NF;
+          if (with_unit) {
+            const int u = t - 1, mf = u & 1, nf = u >> 1;
+            epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
+          }
+          if (!with_unit) __builtin_amdgcn_s_setprio(1);   // (setprio would split the interleave region)
 #pragma unroll
           for (int mf = 0; mf < 2; ++mf)
 #pragma unroll
             for (int nf = 0; nf < NF; ++nf)   // transposed: rows = output channels, columns = pixels
               acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nf], fa[mf], acc[mf][nf], 0, 0, 0);
-          __builtin_amdgcn_s_setprio(0);
+          if (!with_unit) __builtin_amdgcn_s_setprio(0);
+          if (with_unit) {
+#pragma unroll
+            for (int i = 0; i < 2 * NF; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, HALOP_VALU_PER_MFMA, 0);   // then VALU
+            }
+          }
         }
       }
     }
-    // ---- epilogue from registers: lane = pixel (mf*16 + r16) x channels nf*16 + 4*h4 .. +3
+    if constexpr (PIPE) {
 #pragma unroll
-    for (int nf = 0; nf < NF; ++nf) {
-      const int c0 = nf * 16 + 4 * h4;
-      if (n0 + c0 >= nlim) continue;
-      const float4 cb = *reinterpret_cast<const float4*>(cst + c0);
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int mf = 0; mf < 2; ++mf) {
-        const size_t m = (size_t)(mrow + mf * 16 + r16);
-        float v[4] = {acc[mf][nf][0] + cb.x, acc[mf][nf][1] + cb.y, acc[mf][nf][2] + cb.z, acc[mf][nf][3] + cb.w};
-        bf16x4 o;
+        for (int j = 0; j < NF; ++j) accp[i][j] = acc[i][j];
+      mrowp = mrow;
+    } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (relu) v[i] = fmaxf(v[i], 0.f);
-          o[i] = (bf16)v[i];
-        }
-        *reinterpret_cast<bf16x4*>(obase + m * ostride + ocol0 + c0) = o;
-        if constexpr (BNR) {
-          const float4 sc = *reinterpret_cast<const float4*>(cst + BN + c0);
-          const float4 sh = *reinterpret_cast<const float4*>(cst + 2 * BN + c0);
-          const float4 mu = *reinterpret_cast<const float4*>(cst + 3 * BN + c0);
-          const float4 is = *reinterpret_cast<const float4*>(cst + 4 * BN + c0);
-          const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
-          const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
-          bf16x4 zz = __builtin_bit_cast(bf16x4, zreg[mf][nf]);
+      for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float g = (float)o[i], zf = (float)zz[i];   // the stored (rounded) gradient
-            const float db = fmaf(zf, scv[i], shv[i]) > 0.f ? g : 0.f;
-            s1[nf][i] += db;
-            s2[nf][i] += db * (zf - muv[i]) * isv[i];
-          }
-        } else if (stats) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) { s1[nf][i] += v[i]; s2[nf][i] += v[i] * v[i]; }
-        }
-      }
+        for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, acc[mf][nf], zreg[mf][nf], mrow);
     }
     if (more) {
       LDS_BAR();   // every wave is done with this tile's halo
@@ -470,6 +509,15 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
         if (i * NTH + tid < HCH) *reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16) = hreg[i];
       LDS_BAR();
     }
+  };
+  run_tile(0, std::false_type{});
+  for (int k = 1; k < nt; ++k) run_tile(k, std::integral_constant<bool, PIPE>{});
+  if constexpr (PIPE) {   // the last tile's epilogue
+    if constexpr (BNR) load_z(mrowp, zreg);
+#pragma unroll
+    for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
   }
   if (!stats || (a.debug_flags & 2)) return;
   float* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
@@ -527,7 +575,10 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   const int nt_n = bn ? (a.Nout + bn - 1) / bn : 1;
   const bool split_ok = a.out_mode == 2 && bn && a.split_c > 0 && a.split_c % bn == 0 && a.split_c < a.Nout && !a.mask2 &&
                         a.out2_stride % 8 == 0 && (a.Nout - a.split_c) % bn == 0;
-  if (bn && plain && (a.out_mode == 0 || split_ok) && option("halo_persist", 1)) {
+  const size_t lim = (size_t)1 << 31;   // the persistent form stores / reads z through buffer resources
+  const bool fits = (size_t)a.M * a.out_stride * 2 < lim && (!a.out2 || (size_t)a.M * a.out2_stride * 2 < lim) &&
+                    (!a.bnr_z || (size_t)a.M * a.bnr_zs * 2 < lim);
+  if (bn && plain && fits && (a.out_mode == 0 || split_ok) && option("halo_persist", 1)) {
     const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * nt_n;
     a.ntile_n = nt_n;
     a.nblocks = tiles;   // the persistent kernel reads the tile count from nblocks
@@ -535,14 +586,28 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     grid -= grid % nt_n;   // a block keeps one output block
     if (grid == 0) grid = nt_n;
     const bool bnr = a.bnr_z != nullptr;
-    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn);
+    // PIPE (option halop_pipe): the epilogue of tile k runs between the MFMAs of tile k+1 (not for the
+    // BN-backward reduction launches: their z quads and sums do not fit the registers next to two
+    // accumulator sets)
+    // (one-chunk launches only by default: +8 % on the 64 -> 64 forward; the two-chunk form has twice the
+    // MFMA work per epilogue and lost 2-5 % to the extra registers -- profiles/r02_halop_pipe_ab.txt)
+    const int pm = option("halop_pipe", 1);
+    const bool pipe = !bnr && (pm == 2 || (pm == 1 && one_chunk));
+    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
+                    pipe ? "true" : "false");
+#define HALOP_LAUNCH(B_, NCH_, BN_)                                                                          \
+  do {                                                                                                       \
+    if (pipe) hipLaunchKernelGGL((igemm_fwd_halop_kernel<B_, NCH_, BN_, true>), dim3(grid), dim3(512), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_fwd_halop_kernel<B_, NCH_, BN_, false>), dim3(grid), dim3(512), 0, s, a);     \
+  } while (0)
     if (one_chunk) {
-      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 1, 64>), dim3(grid), dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, 1, 64>), dim3(grid), dim3(512), 0, s, a);
+      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 1, 64, false>), dim3(grid), dim3(512), 0, s, a);
+      else HALOP_LAUNCH(false, 1, 64);
     } else {
-      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 2, 32>), dim3(grid), dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, 2, 32>), dim3(grid), dim3(512), 0, s, a);
+      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 2, 32, false>), dim3(grid), dim3(512), 0, s, a);
+      else HALOP_LAUNCH(false, 2, 32);
     }
+#undef HALOP_LAUNCH
     return 1;
   }
   if (a.Nout <= 64) {

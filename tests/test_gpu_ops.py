@@ -311,6 +311,52 @@ def test_persistent_halo_split_and_stats(S, N):
     assert o2[..., 64:].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
+@pytest.mark.parametrize("parts,cout,split", [([64], 64, False), ([64], 128, True), ([64, 64], 128, False),
+                                              ([128], 64, False)])
+def test_halop_pipelined_epilogue_matches(parts, cout, split, grid):
+    """Persistent halo kernel with the epilogue of tile k between the MFMAs of tile k+1 (halop_pipe=2)
+    vs the tile-serial form: bit-identical outputs (plain or split store) and equal BatchNorm sums; a
+    3-block grid gives every block many tiles, so the carried accumulators and the last tile's epilogue
+    after the loop are exercised."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16
+    N, S = 2, 64
+    g = torch.Generator().manual_seed(53)
+    xs = [torch.randn(N, S, S, c, generator=g).to(DEV, dt) for c in parts]
+    cin = sum(parts)
+    W = (torch.randn(cout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(cout, generator=g).to(DEV)
+    res = []
+    for pipe in (0, 1):
+        ops.set_option("halop_pipe", 2 * pipe)   # 2: every (non-BNR) form pipelined
+        if grid:
+            ops.set_option("halo_persist_grid", grid)
+        try:
+            st = torch.zeros(2, cout, device=DEV)
+            kw = dict(srcB=xs[1] if len(xs) > 1 else None, bias=bias, relu=True, bn_stats=(st[0], st[1]))
+            if split:
+                o1 = torch.zeros(N, S, S, 64, dtype=dt, device=DEV)
+                o2 = torch.zeros(N, S, S, cout - 64, dtype=dt, device=DEV)
+                ops.conv_fwd(xs[0], W, cout, out=o1, out_mode=2, out2=o2, split_c=64, **kw)
+                outs = [o1, o2]
+            else:
+                o = torch.zeros(N, S, S, cout, dtype=dt, device=DEV)
+                ops.conv_fwd(xs[0], W, cout, out=o, **kw)
+                outs = [o]
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("halop_pipe", None)
+            ops.set_option("halo_persist_grid", None)
+        assert kname.startswith("igemm_fwd_halop_kernel") and kname.endswith("true>" if pipe else "false>"), kname
+        res.append((outs, st))
+    for a_, b_ in zip(res[0][0], res[1][0]):
+        assert torch.equal(a_, b_)
+    if not split:   # (the split launch carries no statistics request)
+        assert relerr(res[1][1], res[0][1]) < 1e-5
+
+
 @pytest.mark.parametrize("parts,cout", [([128], 64), ([64, 64], 64), ([128], 128), ([64, 64], 128)])
 @pytest.mark.parametrize("S,N", [(32, 2), (64, 1)])
 def test_persistent_halo_two_chunks(parts, cout, S, N):
@@ -326,7 +372,7 @@ def test_persistent_halo_two_chunks(parts, cout, S, N):
     out = torch.zeros((N, S, S, cout), dtype=dt, device=DEV)
     st = torch.zeros(2, cout, device=DEV)
     ops.conv_fwd(xd[0], W, cout, out=out, srcB=srcB, bias=bias.to(DEV), relu=True, bn_stats=(st[0], st[1]))
-    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel<false, 2, 32>")
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel<false, 2, 32")
     ref = oracle_fwd([rb(x, dt) for x in xs], rb(kern, dt), bias, 1, False)
     assert relerr(out, ref) < TOL[dt]
     r2 = ref.reshape(-1, cout)
@@ -359,7 +405,7 @@ def test_persistent_halo_two_chunks(parts, cout, S, N):
         dA = torch.zeros((N, S, S, cout), dtype=dt, device=DEV)
         dg, db = torch.zeros(cout, device=DEV), torch.zeros(cout, device=DEV)
         ops.conv_fwd(dZ, Wd, cout, out=dA, bn_reduce=(z, sc, sh, mu, ist, dg, db))
-        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel<true, 2, 32>")
+        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel<true, 2, 32")
         dg2, db2 = torch.zeros_like(dg), torch.zeros_like(db)
         ops.bn_bwd_reduce(dA, z, sc, sh, mu, ist, dg2, db2)
         ref = torch.zeros_like(dA)
