@@ -253,8 +253,12 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 #ifndef HALOP_VALU_PER_MFMA
 #define HALOP_VALU_PER_MFMA 8
 #endif
-template <bool BNR, int NCH, int BN, bool PIPE>
+// EPI (non-BNR launches): 0 plain store, 1 + BatchNorm statistics, 2 + ReLU, 3 + ReLU + statistics of the
+// stored values -- compile-time, so the
+// epilogue carries no per-element selects for the launch-uniform flags
+template <bool BNR, int NCH, int BN, bool PIPE, int EPI>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
+  static_assert(!BNR || EPI == 0, "the BN-backward reduction launch stores the plain product");
   // NCH 64-channel input chunks (1: Cin_s 64; 2: Cin_s 128 from one or two sources), BN output channels
   // per block (64, or 32 for two chunks: 2 x 340 halo rows + 9 x 2 x 32 weight rows = 157 KiB of LDS)
   constexpr int NTH = 512, NF = BN / 16;
@@ -346,14 +350,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     cst[tid] = (!BNR && a.bias && v) ? a.bias[c] : 0.f;
     cst[BN + tid] = (BNR && v) ? a.bnr_sc[c] : 0.f;
     cst[2 * BN + tid] = (BNR && v) ? a.bnr_sh[c] : 0.f;
-    cst[3 * BN + tid] = (BNR && v) ? a.bnr_mean[c] : 0.f;
+    cst[3 * BN + tid] = (BNR && v) ? -a.bnr_mean[c] * a.bnr_invstd[c] : 0.f;   // xhat = z * invstd + this
     cst[4 * BN + tid] = (BNR && v) ? a.bnr_invstd[c] : 0.f;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int r16 = lane & 15, h4 = lane >> 4;
-  const bool relu = a.relu != 0, stats = a.bn_sum != nullptr || BNR;
+  constexpr bool stats = BNR || EPI == 1 || EPI == 3;
   float s1[NF][4], s2[NF][4];
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf)
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     bf16x4 o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (relu) v[i] = fmaxf(v[i], 0.f);
+      if constexpr (EPI >= 2) v[i] = fmaxf(v[i], 0.f);
       o[i] = (bf16)v[i];
     }
     const unsigned off = cv ? (unsigned)((m * ostride + ocol0 + c0) * 2) : 0x80000000u;
@@ -396,24 +400,24 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     if constexpr (BNR) {
       const float4 sc = *reinterpret_cast<const float4*>(cst + BN + c0);
       const float4 sh = *reinterpret_cast<const float4*>(cst + 2 * BN + c0);
-      const float4 mu = *reinterpret_cast<const float4*>(cst + 3 * BN + c0);
+      const float4 nm = *reinterpret_cast<const float4*>(cst + 3 * BN + c0);
       const float4 is = *reinterpret_cast<const float4*>(cst + 4 * BN + c0);
       const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
-      const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+      const float nmv[4] = {nm.x, nm.y, nm.z, nm.w}, isv[4] = {is.x, is.y, is.z, is.w};
       bf16x4 zz = __builtin_bit_cast(bf16x4, zv);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float g = (float)o[i], zf = (float)zz[i];   // the stored (rounded) gradient
         const float db = fmaf(zf, scv[i], shv[i]) > 0.f ? g : 0.f;   // (z = 0 past nlim: sc = sh = 0 there)
         s1[nf][i] += db;
-        s2[nf][i] += db * (zf - muv[i]) * isv[i];
+        s2[nf][i] = fmaf(db, fmaf(zf, isv[i], nmv[i]), s2[nf][i]);   // db * (z - mean) * invstd
       }
-    } else if (stats) {
+    } else if constexpr (EPI == 1 || EPI == 3) {
+      // (no channel mask: channels past nlim accumulate zero products and the final flush skips them)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float x = cv ? v[i] : 0.f;
-        s1[nf][i] += x;
-        s2[nf][i] += x * x;
+        s1[nf][i] += v[i];
+        s2[nf][i] = fmaf(v[i], v[i], s2[nf][i]);
       }
     }
   };
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
   }
-  if (!stats || (a.debug_flags & 2)) return;
+  if (!stats || (a.debug_flags & 2)) return;   // (uniform)
   float* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf)
@@ -593,20 +597,26 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     // MFMA work per epilogue and lost 2-5 % to the extra registers -- profiles/r02_halop_pipe_ab.txt)
     const int pm = option("halop_pipe", 1);
     const bool pipe = !bnr && (pm == 2 || (pm == 1 && one_chunk));
-    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
-                    pipe ? "true" : "false");
-#define HALOP_LAUNCH(B_, NCH_, BN_)                                                                          \
-  do {                                                                                                       \
-    if (pipe) hipLaunchKernelGGL((igemm_fwd_halop_kernel<B_, NCH_, BN_, true>), dim3(grid), dim3(512), 0, s, a); \
-    else hipLaunchKernelGGL((igemm_fwd_halop_kernel<B_, NCH_, BN_, false>), dim3(grid), dim3(512), 0, s, a);     \
+    const int epi = bnr ? 0 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
+    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
+                    pipe ? "true" : "false", epi);
+#define HALOP_LAUNCH(NCH_, BN_)                                                                             \
+  do {                                                                                                      \
+    if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0>), dim3(grid), dim3(512), 0, s, a); \
+    else if (pipe) {                                                                                        \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 3>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 0>), dim3(grid), dim3(512), 0, s, a); \
+    } else {                                                                                                \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0>), dim3(grid), dim3(512), 0, s, a); \
+    }                                                                                                       \
   } while (0)
-    if (one_chunk) {
-      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 1, 64, false>), dim3(grid), dim3(512), 0, s, a);
-      else HALOP_LAUNCH(false, 1, 64);
-    } else {
-      if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, 2, 32, false>), dim3(grid), dim3(512), 0, s, a);
-      else HALOP_LAUNCH(false, 2, 32);
-    }
+    if (one_chunk) HALOP_LAUNCH(1, 64);
+    else HALOP_LAUNCH(2, 32);
 #undef HALOP_LAUNCH
     return 1;
   }

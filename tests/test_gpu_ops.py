@@ -294,14 +294,20 @@ def test_persistent_halo_split_and_stats(S, N):
     xs, kern, bias, l = make_case(N, S, [64], 128, 1, False, seed=31)
     W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).to(dt).contiguous()
     x = nhwc_pad(xs[0], l.Cin_s, dt)
+    # BatchNorm statistics of the pre-activation output (the unet_bn form: no ReLU on the conv)
     out = torch.zeros((N, S, S, 128), dtype=dt, device=DEV)
     st = torch.zeros(2, 128, device=DEV)
-    ops.conv_fwd(x, W, 128, out=out, bias=bias.to(DEV), relu=True, bn_stats=(st[0], st[1]))
+    ops.conv_fwd(x, W, 128, out=out, bias=bias.to(DEV), bn_stats=(st[0], st[1]))
     assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel")
-    ref = oracle_fwd([rb(xs[0], dt)], rb(kern, dt), bias, 1, False)
+    ref = oracle_fwd([rb(xs[0], dt)], rb(kern, dt), bias, 1, False, relu=False)
     assert relerr(out, ref) < TOL[dt]
     r2 = ref.reshape(-1, 128)
     assert relerr(st[0], r2.sum(0)) < 2e-2 and relerr(st[1], (r2 * r2).sum(0)) < 2e-2
+    # ReLU epilogue, plain and split store
+    out = torch.zeros((N, S, S, 128), dtype=dt, device=DEV)
+    ops.conv_fwd(x, W, 128, out=out, bias=bias.to(DEV), relu=True)
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_halop_kernel")
+    assert relerr(out, oracle_fwd([rb(xs[0], dt)], rb(kern, dt), bias, 1, False)) < TOL[dt]
     o1 = torch.zeros((N, S, S, 64), dtype=dt, device=DEV)
     o2 = torch.zeros((N, S, S, 72), dtype=dt, device=DEV)   # wider stride than the 64 channels stored
     ops.conv_fwd(x, W, 128, out=o1, bias=bias.to(DEV), relu=True, out_mode=2, out2=o2, split_c=64)
@@ -311,10 +317,11 @@ def test_persistent_halo_split_and_stats(S, N):
     assert o2[..., 64:].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("epi", ["stats", "relu"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
 @pytest.mark.parametrize("parts,cout,split", [([64], 64, False), ([64], 128, True), ([64, 64], 128, False),
                                               ([128], 64, False)])
-def test_halop_pipelined_epilogue_matches(parts, cout, split, grid):
+def test_halop_pipelined_epilogue_matches(parts, cout, split, grid, epi):
     """Persistent halo kernel with the epilogue of tile k between the MFMAs of tile k+1 (halop_pipe=2)
     vs the tile-serial form: bit-identical outputs (plain or split store) and equal BatchNorm sums; a
     3-block grid gives every block many tiles, so the carried accumulators and the last tile's epilogue
@@ -334,7 +341,8 @@ def test_halop_pipelined_epilogue_matches(parts, cout, split, grid):
             ops.set_option("halo_persist_grid", grid)
         try:
             st = torch.zeros(2, cout, device=DEV)
-            kw = dict(srcB=xs[1] if len(xs) > 1 else None, bias=bias, relu=True, bn_stats=(st[0], st[1]))
+            kw = dict(srcB=xs[1] if len(xs) > 1 else None, bias=bias, relu=epi == "relu",
+                      bn_stats=(st[0], st[1]) if epi == "stats" else None)
             if split:
                 o1 = torch.zeros(N, S, S, 64, dtype=dt, device=DEV)
                 o2 = torch.zeros(N, S, S, cout - 64, dtype=dt, device=DEV)
@@ -349,11 +357,12 @@ def test_halop_pipelined_epilogue_matches(parts, cout, split, grid):
         finally:
             ops.set_option("halop_pipe", None)
             ops.set_option("halo_persist_grid", None)
-        assert kname.startswith("igemm_fwd_halop_kernel") and kname.endswith("true>" if pipe else "false>"), kname
+        # igemm_fwd_halop_kernel<BNR, NCH, BN, PIPE, EPI>
+        assert kname.startswith("igemm_fwd_halop_kernel") and kname.split(", ")[3] == ("true" if pipe else "false"), kname
         res.append((outs, st))
     for a_, b_ in zip(res[0][0], res[1][0]):
         assert torch.equal(a_, b_)
-    if not split:   # (the split launch carries no statistics request)
+    if epi == "stats":
         assert relerr(res[1][1], res[0][1]) < 1e-5
 
 
