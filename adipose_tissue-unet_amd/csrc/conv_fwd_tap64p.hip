@@ -75,9 +75,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int OA1 = QA * ROWB, OB0 = BM * ROWB, OB1 = (BM + QB) * ROWB;
   constexpr int LOPS = 2 * GA + 2 * GB;                    // LDS-DMA pieces per thread per stage
-  constexpr int EPI_OPS = 2 * MIQ * 4 * (BNR ? 2 : 1);     // vector-memory ops per thread per epilogue
+  constexpr bool ZALL = BNR && MIQ == 2;                     // (see load_zall)
+  constexpr int EPI_OPS = 2 * MIQ * 4 * (BNR && !ZALL ? 2 : 1);   // vector-memory ops per thread per epilogue
   // (vmcnt holds 0..63: a larger count is clamped, which only waits for more)
   constexpr int VM_EPI = (NST - 2) * LOPS + EPI_OPS < 63 ? (NST - 2) * LOPS + EPI_OPS : 63;
+  constexpr int VM_Z = (NST - 2) * LOPS + 4 * 2 * MIQ < 63 ? (NST - 2) * LOPS + 4 * 2 * MIQ : 63;
   // ONE LDS object: with several, the compiler tags every LDS access with per-object alias scopes, and the
   // waitcnt pass then drains vmcnt(0) between the LDS-DMA prefetch of stage t+1 and the fragment reads of
   // stage t (one object: no such wait -- measured 12 % of the K loop)
@@ -243,6 +245,28 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       __builtin_amdgcn_make_buffer_rsrc((void*)(BNR ? a.bnr_z : a.out), 0, BNR ? a.M * a.bnr_zs * ES : 0, P_RSRC3);
   const bool stats = BNR || a.bn_sum != nullptr;
 
+  // BNR with TM = 64: every z quad of the tile (16 loads, 32 registers) is issued in the K loop, right
+  // after the tile's last LDS-DMA step and BEFORE the next tile's first one: vmcnt retires in order, so
+  // the epilogue's wait for z then does not wait for the prefetch of the next tile (z loaded inside the
+  // epilogue drained the whole ring at every tile), and the four channel groups' stores of a pixel row
+  // follow each other closely (with z waits between them the partial lines were written twice: 2.1x the
+  // output bytes, PMC WRITE_SIZE)
+  bf16x4 zall[ZALL ? 4 : 1][ZALL ? 2 * MIQ : 1];
+  auto load_zall = [&](int m0) {
+    int tidv = tid;
+    asm volatile("" : "+v"(tidv));
+    const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int c = n0 + wc * 64 + nt * 16 + 4 * h4;
+#pragma unroll
+      for (int mt = 0; mt < 2 * MIQ; ++mt) {
+        const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
+        const bool v = c < a.Nout && m < a.M;
+        zall[nt][mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+      }
+    }
+  };
   auto epilogue = [&](int m0) {
     // lane-derived epilogue indices made opaque here, so that the compiler cannot hoist their
     // per-(mt, nt) offsets out of the tile loop (they would stay live across the K loop and spill)
@@ -259,7 +283,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       float sc[4], sh[4], mu[4], is[4];
       // BNR: the 2*MIQ z quads of this channel group, all loaded before the first store of the group (a
       // load behind a store waits for it: vmcnt retires in order)
-      bf16x4 zq[BNR ? 2 * MIQ : 1];
+      bf16x4 zq[BNR && !ZALL ? 2 * MIQ : 1];
       if constexpr (BNR) {
         const float4 a4 = p_lds_f4(&cst[1][cl]);
         const float4 s4 = p_lds_f4(&cst[2][cl]);
@@ -269,11 +293,13 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         sh[0] = s4.x; sh[1] = s4.y; sh[2] = s4.z; sh[3] = s4.w;
         mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
         is[0] = i4.x; is[1] = i4.y; is[2] = i4.z; is[3] = i4.w;
+        if constexpr (!ZALL) {
 #pragma unroll
-        for (int mt = 0; mt < 2 * MIQ; ++mt) {
-          const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
-          const bool v = cv && m < a.M;
-          zq[mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+          for (int mt = 0; mt < 2 * MIQ; ++mt) {
+            const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
+            const bool v = cv && m < a.M;
+            zq[mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+          }
         }
       }
       // store target of the channel quad: GEMM column c -> (buffer, channel offset)
@@ -312,7 +338,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         if constexpr (BNR) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float g = (float)o[r], zf = (float)zq[mt][r];   // the stored (rounded) gradient
+            const float g = (float)o[r], zf = (float)(ZALL ? zall[nt][mt][r] : zq[ZALL ? 0 : mt][r]);   // stored gradient
             const float db = fmaf(zf, sc[r], sh[r]) > 0.f ? g : 0.f;
             s1[r] += db;
             s2[r] += db * (zf - mu[r]) * is[r];
@@ -368,11 +394,24 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     for (int i = 0; i < 2 * MIQ; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bool zissued = false;
+    int zstep = -NST;   // step whose barrier preceded this tile's z loads
     for (int t = 0; t < nk; ++t, ++gs) {
+      // ops younger than stage cs: the NST - 2 stages issued after it, an epilogue in the window, and the
+      // z loads when they went out at the previous step (after cs, before that step's stage); a count
+      // that is too small only waits longer, so the combinations are covered by the smaller constant
       if (gs + NST - 2 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
+      else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
       P_BAR();   // stage cs landed for every wave, and nobody reads the stage being refilled any more
+      if constexpr (ZALL) {
+        if (!zissued && lk > k) {   // the loader is past this tile: z before the next tile's first stage
+          load_zall(m0c);
+          zissued = true;
+          zstep = gs;
+        }
+      }
       load_next();
       compute(cs);
       cs = cs == NST - 1 ? 0 : cs + 1;
