@@ -237,17 +237,26 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     const Kt k0 = kinfo();
     issueA(0, k0, 0); issueB(0, k0, 0); issueB(1, k0, 0); issueA(1, k0, 0);
   }
+  // staggered issue (option tap64p_stagger, shared with the persistent kernel): the waves on the second
+  // half of the SIMDs (waves w and w + NW/2 share one) issue their LDS-DMA pieces after their first MFMA
+  // cluster, so one wave of each SIMD multiplies while the other issues
+  constexpr int NW = WM * WN;
+  const bool late = a.stagger && NW == 8 && ((__builtin_amdgcn_readfirstlane(wave) >> 2) & 1);
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     T64_BAR();   // stage t landed for every wave, and nobody reads buffer buf ^ 1 any more
-    if (t + 1 < nk) {
-      const Kt k1 = kinfo();
-      issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
-    }
+    auto issue_next = [&]() {
+      if (t + 1 < nk) {
+        const Kt k1 = kinfo();
+        issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
+      }
+    };
+    if (!late) issue_next();
     readA(buf, 0, fa);
     readB(buf, 0, fb0);
     mma(fa, fb0, 0, 0);
+    if (late) issue_next();
     readB(buf, 1, fb1);
     mma(fa, fb1, 0, 1);
     readA(buf, 1, fa);
@@ -337,6 +346,7 @@ constexpr double CFG_EFF[4] = {1.0, 0.85, 0.0, 0.6};
 
 namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
+  a.stagger = option("tap64p_stagger", 1);
   int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
   // the fused BN-backward epilogue handles plain stores only (what the data-gradient launches use)

@@ -188,8 +188,16 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // the loader: the next K step of the block's stream (tile lk, step lt) into stage ls
   int lk = 0, lt = 0, ls = 0;
   auto tile_m0 = [&](int k) { return ((lin + k * G) / a.ntile_n) * BM; };
+  const bool no_dma = (a.debug_flags & 32) != 0;   // timing-only ablation (fwd_debug bit 5): the K loop
+                                                    // multiplies whatever the prologue loaded
+  int nissued = 0;
   auto load_next = [&]() {
     if (lk >= mine) return;   // stream exhausted (uniform)
+    if (no_dma && nissued >= NST - 1) {   // (keep the loader's bookkeeping, issue nothing)
+      if (++lt == nk) { lt = 0; ++lk; }
+      return;
+    }
+    ++nissued;
     if (lt == 0) {
       setup_rows(tile_m0(lk));
       it_ci = it_ty = it_tx = it_kt = 0;
@@ -369,10 +377,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   };
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
-  auto compute = [&](int buf) {
+  // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
+  // cluster instead of right after the barrier. Waves w and w + 4 share a SIMD, so one of them multiplies
+  // while the other issues (the issue of a piece costs the issuing wave 60-185 cycles); with every wave
+  // issuing after the barrier the DMA issue and the MFMAs serialised on each SIMD (the no-DMA ablation
+  // runs the K loop 20 % faster)
+  const bool late = a.stagger && ((__builtin_amdgcn_readfirstlane(wave) >> 2) & 1);
+  auto compute = [&](int buf, bool issue_late) {
     readA(buf, 0, fa);
     readB(buf, 0, fb0);
     mma(fa, fb0, 0, 0);
+    if (issue_late) load_next();
     readB(buf, 1, fb1);
     mma(fa, fb1, 0, 1);
     readA(buf, 1, fa);
@@ -412,8 +427,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           zstep = gs;
         }
       }
-      load_next();
-      compute(cs);
+      if (!late) load_next();
+      compute(cs, late);
       cs = cs == NST - 1 ? 0 : cs + 1;
     }
     last_epi = gs - 1;
@@ -472,6 +487,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // 128x256 / 3 stages for the short ConvTranspose K of 128..256 (+8-15 % over 256x256); the fused BN-backward
   // reduction only on the 256x128 form (its z loads wait behind the prefetch stream, which costs the
   // 256x256 form 5-8 % against tap64's LDS-staged epilogue)
+  a.stagger = option("tap64p_stagger", 1);
   int cfg = option("tap64p_cfg", 0);
   if (cfg < 1 || cfg > 3) {
     if (a.bnr_z && tile != 1 && option("tap64p_bnr", 1) < 2) return 0;
