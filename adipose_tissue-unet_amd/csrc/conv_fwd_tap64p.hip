@@ -165,6 +165,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     }
     return r;
   };
+  const bool l2_only = (a.debug_flags & 256) != 0;   // (fwd_debug bit 8)
   auto issue = [&](const Kt& k, int buf) {
     // A0 B0 B1 A1
 #pragma unroll
@@ -174,7 +175,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       for (int i = 0; i < GA; ++i) {
         const int yi = ry[h][i] + k.oy, xi = rx[h][i] + k.ox;
         const bool v = (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
-        const unsigned off = v ? (unsigned)((pb[h][i] + k.dpix) * k.cs + k.cb + rc) : P_OOB;
+        unsigned off = v ? (unsigned)((pb[h][i] + k.dpix) * k.cs + k.cb + rc) : P_OOB;
+        if (l2_only && v) off &= 0x3FFF0u;   // timing-only ablation: the A gather from a 256-KiB window
         p_lds16(k.srcb ? rsB : rsA, dst + i * (NTH / 8) * ROWB, off);
       }
       unsigned char* dsb = smem + buf * STAGE + (h ? OB1 : OB0) + wave * 8 * ROWB;
@@ -382,6 +384,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // while the other issues (the issue of a piece costs the issuing wave 60-185 cycles); with every wave
   // issuing after the barrier the DMA issue and the MFMAs serialised on each SIMD (the no-DMA ablation
   // runs the K loop 20 % faster)
+  // (issuing each wave's step in two halves spread over the clusters measured 5-9 % slower:
+  //  profiles/r02_stagger_ab.txt)
   const bool late = a.stagger && ((__builtin_amdgcn_readfirstlane(wave) >> 2) & 1);
   auto compute = [&](int buf, bool issue_late) {
     readA(buf, 0, fa);
