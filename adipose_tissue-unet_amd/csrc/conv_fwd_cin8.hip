@@ -122,13 +122,21 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
     }
 }
 
-template <int KS>
-void launch_cin8(FwdArgs& a, hipStream_t s) {
-  constexpr int UNR = 2;
+template <int KS, int UNR>
+void launch_cin8_u(FwdArgs& a, hipStream_t s) {
   const int groups = (a.M + 15) / 16;
-  const int waves = std::max(1, std::min((groups + UNR - 1) / UNR, adp::option("cin8_waves", 4096)));
+  // (4 groups per pass on 2048 waves: 0.255 -> 0.239 ms at unet_bn's 1024^2 x 4 input layer,
+  //  profiles/r02_cin8_ab.txt)
+  const int waves = std::max(1, std::min((groups + UNR - 1) / UNR, adp::option("cin8_waves", 2048)));
   adp::set_kernel("igemm_fwd_cin8_kernel<%d, %d>", KS, UNR);
   hipLaunchKernelGGL((igemm_fwd_cin8_kernel<KS, UNR>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+}
+template <int KS>
+void launch_cin8(FwdArgs& a, hipStream_t s) {
+  const int unr = adp::option("cin8_unr", 4);
+  if (unr == 4) launch_cin8_u<KS, 4>(a, s);
+  else if (unr == 1) launch_cin8_u<KS, 1>(a, s);
+  else launch_cin8_u<KS, 2>(a, s);
 }
 
 }  // namespace

@@ -37,7 +37,8 @@ def main():
     # (name, S, Cin, Cout): 3x3 convs of unet_bn L5 (one per (level, shape) class)
     shapes = [("L0 64->64", 1024, 64, 64), ("L0 128->64", 1024, 128, 64), ("L1 128->128", 512, 128, 128),
               ("L2 256->256", 256, 256, 256), ("L3 512->512", 128, 512, 512), ("L4 1024->1024", 64, 1024, 1024),
-              ("L3 1024->512", 128, 1024, 512), ("L4 1024->512", 64, 1024, 512), ("L1 256->128", 512, 256, 128)]
+              ("L3 1024->512", 128, 1024, 512), ("L4 1024->512", 64, 1024, 512), ("L1 256->128", 512, 256, 128),
+              ("L0 in8->64", 1024, 8, 64)]   # the input layer (8-channel source: cin8 kernels)
     if args.layers:
         keys = args.layers.split(",")
         shapes = [sh for sh in shapes if any(k in sh[0] for k in keys)]
