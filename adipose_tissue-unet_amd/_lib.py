@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class AdpError(RuntimeError):
@@ -48,6 +48,11 @@ class ConvIO(C.Structure):
         "bnr_z", "bnr_scale", "bnr_shift", "bnr_mean", "bnr_invstd", "bnr_dgamma", "bnr_dbeta", "w_scale")]
 
 
+class BnBwdArgs(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "dA", "z", "scale", "shift", "mean", "invstd", "gamma", "dgamma", "dbeta")] + [("count", C.c_float)]
+
+
 _P = C.c_void_p
 _I = C.c_int
 _F = C.c_float
@@ -59,6 +64,7 @@ _SIGS = {
     "adp_set_option": [C.c_char_p, _I],
     "adp_conv_fwd": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P],
     "adp_conv_wgrad": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P, _I, _P, _P, _P],
+    "adp_conv_wgrad_bn": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), C.POINTER(BnBwdArgs), _P, _I, _P, _P, _P],
     "adp_pack_weights": [_I, _I, _I, _I, _I, _P, _I, _P, _I, _I, _P],
     "adp_maxpool2_fwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "adp_maxpool2_fwd_fp8": [_I, _I, _I, _I, _I, _P, _P, _P],
@@ -75,6 +81,7 @@ _SIGS = {
     "adp_bn_apply": [_I, _S, _I, _P, _P, _P, _P, _P],
     "adp_bn_bwd_reduce":[_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "adp_bn_bwd_apply": [_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P],
+    "adp_bn_bwd_apply_head": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P],
     "adp_head_softmax2_fwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "adp_head_softmax2_bwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P],
     "adp_head_sigmoid_fwd": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P],

@@ -56,6 +56,12 @@ struct WgradArgs {
   int debug_flags;      // timing-only ablations (tools/bench_kernels.py): bit0 skips the dW atomics
   float* part;          // tap64: per-split partial dW slabs [split][Nout][Kpad] (plain stores), reduced
                         // into dW by a second launch; nullptr -> f32 atomics into dW
+  // fused BatchNorm-backward apply (adp_conv_wgrad_bn): dY = bn_bwd_apply(bna_dA, bna_z) of the layer's
+  // BatchNorm, computed on load and stored into dY (all three [M][dy_stride]); bna_dA == nullptr: plain dY
+  const void* bna_dA; const void* bna_z;
+  const float* bna_sc; const float* bna_sh; const float* bna_mean; const float* bna_invstd;
+  const float* bna_gamma; const float* bna_dgamma; const float* bna_dbeta;
+  float bna_inv_count;
 };
 
 // LDS-only workgroup barrier for epilogues: this wave's LDS traffic complete, then s_barrier. Unlike
@@ -333,4 +339,6 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s);
 int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
+// the persistent halo weight-gradient kernel takes this launch with the BatchNorm-backward apply fused
+bool wgrad_bna_fusable(const WgradArgs& a);
 }

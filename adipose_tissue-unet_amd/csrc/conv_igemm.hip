@@ -1147,7 +1147,7 @@ int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
 
 template <typename T>
 int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, int dy_stride,
-                 float* dW, float* dB, hipStream_t s) {
+                 float* dW, float* dB, hipStream_t s, const adp_bn_bwd_args* bn = nullptr) {
   WgradArgs a{};
   a.srcA = io->srcA; a.srcB = io->srcB;
   a.scA = io->bn_scaleA; a.shA = io->bn_shiftA; a.scB = io->bn_scaleB; a.shB = io->bn_shiftB;
@@ -1161,6 +1161,19 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
   ADP_REQUIRE(a.CAs % 8 == 0 && a.CBs % 8 == 0 && a.Nout % 8 == 0,
               "adp_conv_wgrad: channel strides and Nout must be multiples of 8");
   ADP_REQUIRE(d->out_mode != 2, "adp_conv_wgrad: split-store descriptors are dgrad-only");
+  if (bn) {   // adp_conv_wgrad_bn: fused into the halo kernel, else the apply launch first
+    a.bna_dA = bn->dA; a.bna_z = bn->z;
+    a.bna_sc = bn->scale; a.bna_sh = bn->shift; a.bna_mean = bn->mean; a.bna_invstd = bn->invstd;
+    a.bna_gamma = bn->gamma; a.bna_dgamma = bn->dgamma; a.bna_dbeta = bn->dbeta;
+    a.bna_inv_count = 1.f / bn->count;
+    if (!(std::is_same<T, bf16>::value && adp::option("conv_fast", 2) == 2 && adp::wgrad_bna_fusable(a))) {
+      a.bna_dA = nullptr;
+      if (adp_bn_bwd_apply(std::is_same<T, bf16>::value ? ADP_BF16 : ADP_F32, (size_t)a.M, dy_stride, bn->dA, bn->z,
+                           bn->scale, bn->shift, bn->mean, bn->invstd, bn->gamma, bn->dgamma, bn->dbeta, bn->count,
+                           const_cast<void*>(dY), s))
+        return -2;
+    }
+  }
   if (std::is_same<T, bf16>::value && adp::option("conv_fast", 2) == 2 && !a.scA && !a.scB) {
     if (!adp::launch_wgrad_tap64(a, s)) {
       const int TN = (a.Nout <= 64 && adp::option("wgrad_glds_tn64", 1)) ? 64 : 128, TK = TN == 64 ? 256 : 128;
@@ -1237,6 +1250,20 @@ extern "C" int adp_conv_fwd(int dtype, const adp_conv_desc* d, const adp_conv_io
   if (dtype == ADP_BF16) return launch_fwd<bf16>(d, io, s);
   if (dtype == ADP_FP8) return launch_fwd_f8(d, io, s);
   adp::set_error("adp_conv_fwd: unknown dtype");
+  return -1;
+}
+
+extern "C" int adp_conv_wgrad_bn(int dtype, const adp_conv_desc* d, const adp_conv_io* io, const adp_bn_bwd_args* bn,
+                                 void* dY, int dy_stride, float* dW, float* dB, adp_stream_t st) {
+  hipStream_t s = (hipStream_t)st;
+  ADP_REQUIRE(d && io && bn && bn->dA && bn->z && dY && dW, "adp_conv_wgrad_bn: null argument");
+  ADP_REQUIRE(bn->scale && bn->shift && bn->mean && bn->invstd && bn->gamma && bn->dgamma && bn->dbeta && bn->count > 0,
+              "adp_conv_wgrad_bn: BatchNorm vectors and count");
+  ADP_REQUIRE(d->out_mode == 0 && dy_stride == d->Nout && dy_stride % 8 == 0,
+              "adp_conv_wgrad_bn: plain [M][Nout] gradient (dA, z, dY share the channel stride)");
+  if (dtype == ADP_F32) return launch_wgrad<float>(d, io, dY, dy_stride, dW, dB, s, bn);
+  if (dtype == ADP_BF16) return launch_wgrad<bf16>(d, io, dY, dy_stride, dW, dB, s, bn);
+  adp::set_error("adp_conv_wgrad_bn: unknown dtype");
   return -1;
 }
 

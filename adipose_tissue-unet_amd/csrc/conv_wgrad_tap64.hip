@@ -69,6 +69,23 @@ ADP_DEV v4s16 ds_tr16(uint32_t lds_addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
   return r;
 }
+typedef unsigned v4u32_w __attribute__((ext_vector_type(4)));
+// LDS float4 read / 16-B write as inline asm: the compiler would put a vmcnt(0) (every LDS-DMA in flight)
+// in front of a plain access to the LDS object the DMA writes; the reader waits itself
+ADP_DEV float4 wg_lds_f4(uint32_t lds_addr) {
+  float4 r;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_addr) : "memory");
+  return r;
+}
+typedef unsigned v2u32_w __attribute__((ext_vector_type(2)));
+ADP_DEV v2u32_w wg_lds_r8(uint32_t lds_addr) {
+  v2u32_w r;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_addr) : "memory");
+  return r;
+}
+ADP_DEV void wg_lds_w16(uint32_t lds_addr, v4u32_w v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr), "v"(v) : "memory");
+}
 ADP_DEV uint32_t lds_off(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
@@ -402,7 +419,16 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
 // NW = 9: one wave per tap (9 waves on 4 SIMDs: the SIMD holding 3 of them sets the pace). NW = 8: wave
 // w owns tap w and a 16 x 32 eighth of tap 8 (output block w >> 1, column blocks 2 (w & 1) + {0, 1}),
 // two waves per SIMD with 18 MFMAs each per k step.
-template <int NW>
+//
+// BNA (adp_conv_wgrad_bn, NW = 8): the dY tile is not read but computed, adp_bn_bwd_apply of the layer's
+// BatchNorm fused. At the first two rows of a patch each thread moves its 4 16-B groups of dA (into the
+// next stage's dY image) and of z (into the next stage's halo image, free until its halo is issued) by
+// LDS-DMA with the dY swizzle; at row BNA_ROW it waits for its own pieces, applies
+// dY = P*dA*(z*s+h > 0) + Q*(z - mean) + R in place (the apply kernel's arithmetic and bf16 rounding; the
+// thread's channel group is fixed, so its constants are 8 LDS words each) and -- blocks of input chunk 0
+// only -- stores dY for the data-gradient launch; the halo groups follow at rows BNA_ROW..7. No barrier
+// and no long-lived registers: every thread reads back only the LDS slots its own DMA wrote.
+template <int NW, bool BNA = false>
 __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs a) {
   constexpr int NTH = NW * 64, RB = 128;
   constexpr int PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
@@ -411,7 +437,9 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   constexpr int HBUF = HROWS * RB, DBUF = PH * PW * RB;
   constexpr int STAGE = HBUF + DBUF;
   static_assert(GH + GD <= 2 * PH, "the next patch's LDS-DMA groups are spread over the 8 patch rows");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+  static_assert(!BNA || (NW == 8 && GD * NTH == DCH), "BNA: 8 waves, whole dY groups");
+  constexpr int BNA_ROW = 3;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE + (BNA ? 6 * 64 * 4 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap
@@ -433,6 +461,10 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
       (void*)(inA ? a.srcA : a.srcB), 0, a.Nimg * a.Hs * a.Ws * xcs * 2, WG_RSRC3);
   const __amdgpu_buffer_rsrc_t rsD =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.dY, 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsBA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNA ? a.bna_dA : a.dY), 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsBZ = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(BNA ? a.bna_z : a.dY), 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
   // per-thread constant parts of the gathers: halo group i -> (pixel delta, row/col offsets, byte offset)
   int hy[GH], hx[GH], hpix[GH], hoff[GH], dpix[GD], doff[GD];
   const int xc0 = (inA ? ch * 64 : ch * 64 - a.CAs) * 2;
@@ -476,12 +508,33 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     const int idx = i * NTH + tid;
     if (i < GD - 1 || idx < DCH) {
       const unsigned off = (unsigned)((P.pbd + dpix[i]) * a.dy_stride * 2 + doff[i]);
-      wg_buf_lds16(rsD, smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16, off);
+      if constexpr (BNA) {   // dA -> the dY image, z -> the (still unused) halo image of the stage
+        wg_buf_lds16(rsBA, smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16, off);
+        wg_buf_lds16(rsBZ, smem + buf * STAGE + (size_t)(i * NTH + wave * 64) * 16, off);
+      } else {
+        wg_buf_lds16(rsD, smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16, off);
+      }
     }
   };
   // the groups of the next patch issued while row pr of this one multiplies: halo first, then dY,
-  // two per row until the remaining rows can take one each
+  // two per row until the remaining rows can take one each (BNA: halo only, rows 2..7)
   auto issue_row = [&](const Patch& P, int pr, int buf) {
+    if constexpr (BNA) {   // rows 0-1: dA / z groups; rows BNA_ROW..7: the halo, two per row first
+      constexpr int HR = PH - BNA_ROW, EXTRA = GH - HR;
+      if (pr < 2) {
+#pragma unroll
+        for (int i = 0; i < GD; ++i)
+          if (i / (GD / 2) == pr) issue_d(P, i, buf);
+      } else if (pr >= BNA_ROW) {
+        const int r = pr - BNA_ROW;
+        const int g0 = r < EXTRA ? 2 * r : EXTRA + r;
+        const int g1 = r < EXTRA ? g0 + 1 : -1;
+#pragma unroll
+        for (int gi = 0; gi < GH; ++gi)
+          if (gi == g0 || gi == g1) issue_h(P, gi, buf);
+      }
+      return;
+    }
     constexpr int NG = GH + GD, EXTRA = NG - PH;   // rows 0 .. EXTRA-1 take two groups
     const int g0 = pr < EXTRA ? 2 * pr : EXTRA + pr;
     const int g1 = pr < EXTRA ? g0 + 1 : -1;
@@ -496,9 +549,13 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   // pixels of one k step (absolute rows, so the row swizzle matches the one applied on load)
   const int g = lane >> 4, ii = lane & 15, q = ii >> 2, pp = ii & 3;
   const int rr0 = 16 * (g >> 1) + 4 * (g & 1) + q;
+  // BNA: the lane terms are re-derived per patch from an opaque copy of the lane id, so that the
+  // fragment addresses of the 8 unrolled rows are not hoisted out of the patch loop (they would hold
+  // the registers the apply needs)
+  int fpp = pp, frr0 = rr0;
   auto frag = [&](uint32_t img_base, int row0, int col0) {
-    const int col = col0 + 4 * pp, chunk = col >> 3, inb = (col & 7) * 2;
-    const int R0 = row0 + rr0, R1 = R0 + 8;
+    const int col = col0 + 4 * fpp, chunk = col >> 3, inb = (col & 7) * 2;
+    const int R0 = row0 + frr0, R1 = R0 + 8;
     const v4s16 lo = ds_tr16(img_base + R0 * RB + ((chunk ^ gsw<RB>(R0)) << 4) + inb);
     const v4s16 hi = ds_tr16(img_base + R1 * RB + ((chunk ^ gsw<RB>(R1)) << 4) + inb);
     bf16x8 r;
@@ -508,6 +565,67 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
     return r;
   };
+
+  // ---- BNA: per-channel constants of this output block in LDS ([6][64]: scale, shift, mean, P, Q, R, as
+  // bn_bwd_apply_kernel forms them); the thread's slots hold source channel group bcg for all its groups
+  // (the swizzle gsw(pr) depends on row bits its rows share)
+  float* bk = reinterpret_cast<float*>(smem + 2 * STAGE);
+  const uint32_t sbase = lds_off(smem);
+  const int bcg = (tid & 7) ^ gsw<RB>(tid >> 3);
+  auto bna_apply = [&](const Patch& P, int buf) {
+    if constexpr (BNA) {
+      uint32_t og[GD][4];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {   // 4 channels at a time: bounds the registers held
+        float c[6][4];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const float4 v = wg_lds_f4(sbase + 2 * STAGE + (q * 64 + bcg * 8 + 4 * half) * 4);
+          c[q][0] = v.x; c[q][1] = v.y; c[q][2] = v.z; c[q][3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < GD; ++i) {
+          const uint32_t slot = (uint32_t)(i * NTH + tid) * 16 + 8 * half;
+          const v2u32_w dv = wg_lds_r8(sbase + buf * STAGE + HBUF + slot);
+          const v2u32_w zv = wg_lds_r8(sbase + buf * STAGE + slot);
+          const bf16* d = reinterpret_cast<const bf16*>(&dv);
+          const bf16* zz = reinterpret_cast<const bf16*>(&zv);
+          bf16 o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {   // bn_bwd_apply_kernel's arithmetic and rounding
+            const float zf = (float)zz[j];
+            const float db = fmaf(zf, c[0][j], c[1][j]) > 0.f ? (float)d[j] : 0.f;
+            o[j] = (bf16)fmaf(c[3][j], db, fmaf(c[4][j], zf - c[2][j], c[5][j]));
+          }
+          const uint32_t* ow = reinterpret_cast<const uint32_t*>(o);
+          og[i][2 * half] = ow[0];
+          og[i][2 * half + 1] = ow[1];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < GD; ++i) {
+        const v4u32_w ov = {og[i][0], og[i][1], og[i][2], og[i][3]};
+        wg_lds_w16(sbase + buf * STAGE + HBUF + (uint32_t)(i * NTH + tid) * 16, ov);
+        if (ch == 0)
+          __builtin_amdgcn_raw_buffer_store_b128(ov, rsD, (unsigned)((P.pbd + dpix[i]) * a.dy_stride * 2 + doff[i]), 0, 0);
+      }
+      // this thread's z slots are overwritten by its own halo DMA next: the reads above are complete
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  };
+  if constexpr (BNA) {
+    if (tid < 64) {
+      const int cc = nblk * 64 + tid;
+      const float k = a.bna_gamma[cc] * a.bna_invstd[cc];
+      bk[0 * 64 + tid] = a.bna_sc[cc];
+      bk[1 * 64 + tid] = a.bna_sh[cc];
+      bk[2 * 64 + tid] = a.bna_mean[cc];
+      bk[3 * 64 + tid] = k;
+      bk[4 * 64 + tid] = -k * a.bna_invstd[cc] * a.bna_dgamma[cc] * a.bna_inv_count;
+      bk[5 * 64 + tid] = -k * a.bna_dbeta[cc] * a.bna_inv_count;
+    }
+    __syncthreads();
+  }
 
   f32x4 acc[4][4], acc8[2];
 #pragma unroll
@@ -519,21 +637,39 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
 
   if (nt > 0) {
     const Patch P0 = patch(0);
+    if constexpr (BNA) {
+#pragma unroll
+      for (int i = 0; i < GD; ++i) issue_d(P0, i, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bna_apply(P0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < GH; ++i) issue_h(P0, i, 0);
+    if constexpr (!BNA) {
 #pragma unroll
-    for (int i = 0; i < GD; ++i) issue_d(P0, i, 0);
+      for (int i = 0; i < GD; ++i) issue_d(P0, i, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     W64_BAR();
   }
-  const uint32_t sbase = lds_off(smem);
   for (int k = 0; k < nt; ++k) {
     const int buf = k & 1;
     const bool more = k + 1 < nt;
     const Patch Pn = patch(more ? k + 1 : k);
+    if constexpr (BNA) {
+      int lz = lane;
+      asm volatile("" : "+v"(lz));
+      const int g_ = lz >> 4, i_ = lz & 15;
+      fpp = i_ & 3;
+      frr0 = 16 * (g_ >> 1) + 4 * (g_ & 1) + (i_ >> 2);
+    }
     const uint32_t hbase = sbase + buf * STAGE, dbase = hbase + HBUF;
 #pragma unroll
     for (int pr = 0; pr < PH; ++pr) {
+      if (BNA && more && pr == BNA_ROW) {   // this thread's dA / z pieces (rows 0-1) have landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bna_apply(Pn, buf ^ 1);
+      }
       if (more) issue_row(Pn, pr, buf ^ 1);
       bf16x8 fd[4], fx[4], fd8, fx8[2];
       if (NW == 8) {
@@ -793,6 +929,26 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
 }  // namespace
 
 namespace adp {
+// shapes of the persistent halo weight-gradient kernel
+static bool halop_ok(const WgradArgs& a) {
+  const int cin = a.CAs + a.CBs;
+  return option("wgrad_halop", 1) && !a.scA && !a.scB && a.CAs % 64 == 0 && a.CBs % 64 == 0 && a.kh == 3 &&
+         a.kw == 3 && a.dil == 1 && a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws &&
+         a.Ho % 8 == 0 && a.Wo % 32 == 0 && a.Nout % 64 == 0 && a.dy_mode == 0 && a.K == 9 * cin &&
+         a.Kpad == a.K && a.dy_stride % 8 == 0 && a.dy_stride >= a.Nout &&
+         // buffer-resource offsets: every operand below 2 GiB
+         (size_t)a.Nimg * a.Hs * a.Ws * std::max(a.CAs, a.CBs) * 2 < ((size_t)1 << 31) &&
+         (size_t)a.Nimg * a.Ho * a.Wo * a.dy_stride * 2 < ((size_t)1 << 31);
+}
+
+// BatchNorm-backward apply fused into the halo weight gradient: every block of input chunk c recomputes
+// its output block's dY tile, so only layers with at most wgrad_bna_maxch (default 2) 64-channel input
+// chunks take it (levels 0-1 of unet_bn; deeper layers re-read dA/z once per chunk)
+bool wgrad_bna_fusable(const WgradArgs& a) {
+  return a.bna_dA && a.bna_z && option("wgrad_bna", 1) && option("wgrad_halop_waves", 8) == 8 && halop_ok(a) &&
+         (a.CAs + a.CBs) / 64 <= option("wgrad_bna_maxch", 2);
+}
+
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 128x256 (8 waves, 64x64),
 // 2 = 64x256 (4 waves, 64x64, two blocks per CU)
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
@@ -807,25 +963,21 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(igemm_wgrad_cin8_kernel, dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
-  const int hp = option("wgrad_halop", 1);   // 0 off, else every eligible shape
   const int cin = a.CAs + a.CBs;
-  if (hp && !a.scA && !a.scB && a.CAs % 64 == 0 && a.CBs % 64 == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
-      a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
-      a.Nout % 64 == 0 && a.dy_mode == 0 && a.K == 9 * cin && a.Kpad == a.K && a.dy_stride % 8 == 0 &&
-      a.dy_stride >= a.Nout &&
-      // buffer-resource offsets: every operand below 2 GiB
-      (size_t)a.Nimg * a.Hs * a.Ws * std::max(a.CAs, a.CBs) * 2 < ((size_t)1 << 31) &&
-      (size_t)a.Nimg * a.Ho * a.Wo * a.dy_stride * 2 < ((size_t)1 << 31)) {
+  if (halop_ok(a)) {   // option wgrad_halop: 0 off, else every eligible shape
     const int combos = (cin / 64) * (a.Nout / 64);
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
     const int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
     const int grid = per * combos;
     a.debug_flags = option("wgrad_debug", 0);
-    if (option("wgrad_halop_waves", 8) == 9) {
-      adp::set_kernel("igemm_wgrad_halop_kernel<9>");
+    if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
+      adp::set_kernel("igemm_wgrad_halop_kernel<8, true>");
+      hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true>), dim3(grid), dim3(512), 0, s, a);
+    } else if (option("wgrad_halop_waves", 8) == 9) {
+      adp::set_kernel("igemm_wgrad_halop_kernel<9, false>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
     } else {
-      adp::set_kernel("igemm_wgrad_halop_kernel<8>");
+      adp::set_kernel("igemm_wgrad_halop_kernel<8, false>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<8>, dim3(grid), dim3(512), 0, s, a);
     }
     return 1;

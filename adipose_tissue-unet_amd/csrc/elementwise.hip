@@ -569,6 +569,93 @@ __global__ void bn_bwd_apply_kernel(size_t M, int C, const T* dA, const T* z, co
   }
 }
 
+// an empty asm that uses the loaded values: every load before it is issued before any math after it
+__device__ __forceinline__ void ew_pin(float a, float b, const Grp<bf16>& g) {
+  asm volatile("" ::"v"(a), "v"(b), "v"(g.v.x), "v"(g.v.y), "v"(g.v.z), "v"(g.v.w));
+}
+__device__ __forceinline__ void ew_pin(float a, float b, const Grp<float>& g) {
+  asm volatile("" ::"v"(a), "v"(b), "v"(g.v[0].x), "v"(g.v[0].y), "v"(g.v[0].z), "v"(g.v[0].w));
+  asm volatile("" ::"v"(g.v[1].x), "v"(g.v[1].y), "v"(g.v[1].z), "v"(g.v[1].w));
+}
+
+// adp_bn_bwd_apply of the layer under the sigmoid head with dA recomputed instead of read:
+// dA = T(dp * p * (1 - p) * W[c]) (0 for c >= Cin), rounded exactly as adp_head_sigmoid_bwd_bnr stores
+// it, so that launch need not store dA (one map write and one read fewer). Same thread layout and
+// arithmetic as bn_bwd_apply_kernel; every load of a pass is issued before its arithmetic.
+template <typename T, int U>
+__global__ void bn_bwd_apply_head_kernel(size_t M, int C, int Cin, const T* z, const float* W, const float* p,
+                                         const float* dp, const float* sc, const float* sh, const float* mean,
+                                         const float* invstd, const float* gamma, const float* dgamma,
+                                         const float* dbeta, float inv_count, T* dz) {
+  const int G = C >> 3, lanes = TPB / G;
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  if (pl >= lanes) return;
+  float s[8], h[8], mu[8], P[8], Q[8], R[8], wd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = g * 8 + j;
+    const float k = gamma[c] * invstd[c];
+    s[j] = sc[c]; h[j] = sh[c]; mu[j] = mean[c];
+    P[j] = k;
+    Q[j] = -k * invstd[c] * dgamma[c] * inv_count;
+    R[j] = -k * dbeta[c] * inv_count;
+  }
+  // head weights as two 16-B loads (Cin % 8 == 0): a per-channel conditional load here made the
+  // compiler split the whole coefficient prologue into 64 single-dword loads behind branches (6x slower)
+  if (g * 8 < Cin) {
+    const float4 w0 = reinterpret_cast<const float4*>(W)[2 * g], w1 = reinterpret_cast<const float4*>(W)[2 * g + 1];
+    wd[0] = w0.x; wd[1] = w0.y; wd[2] = w0.z; wd[3] = w0.w;
+    wd[4] = w1.x; wd[5] = w1.y; wd[6] = w1.z; wd[7] = w1.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wd[j] = 0.f;
+  }
+  auto one = [&](float pm, float dpm, const Grp<T>& gz, Grp<T>& go) {
+    const float dl = dpm * pm * (1.f - pm);
+    float dv[8], d[8], zz[8], o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dv[j] = dl * wd[j] + 0.f;   // the head backward's expression (no addend)
+    Grp<T> gd;
+    grp_from_f(gd, dv);
+    grp_to_f(gd, d);
+    grp_to_f(gz, zz);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float db = fmaf(zz[j], s[j], h[j]) > 0.f ? d[j] : 0.f;
+      o[j] = fmaf(P[j], db, fmaf(Q[j], zz[j] - mu[j], R[j]));
+    }
+    grp_from_f(go, o);
+  };
+  const size_t step = (size_t)gridDim.x * lanes;
+  size_t m = (size_t)blockIdx.x * lanes + pl;
+  for (; m + (U - 1) * step < M; m += U * step) {
+    Grp<T> zz[U], r[U];
+    float pm[U], dpm[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      grp_load(zz[u], z + (m + u * step) * C + g * 8);
+      pm[u] = p[m + u * step];
+      dpm[u] = dp[m + u * step];
+    }
+    // pin every load of the pass ahead of the arithmetic (left alone, the compiler sinks the later
+    // pixels' loads below the earlier pixels' math: one pixel in flight per wave, 2.2 TB/s)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      ew_pin(pm[u], dpm[u], zz[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(pm[u], dpm[u], zz[u], r[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) grp_store(r[u], dz + (m + u * step) * C + g * 8);
+  }
+  for (; m < M; m += step) {
+    const size_t o0 = m * C + g * 8;
+    Grp<T> z0, r0;
+    grp_load(z0, z + o0);
+    one(p[m], dp[m], z0, r0);
+    grp_store(r0, dz + o0);
+  }
+}
+
 // a = relu(z*scale + shift): materialised post-BN activation (lets every consumer use LDS-DMA loads)
 template <typename T, int U>
 __global__ void bn_apply_kernel(size_t M, int C, const T* z, const float* sc, const float* sh, T* out) {
@@ -958,6 +1045,21 @@ extern "C" int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, cons
                                   M, C, (const T*)dA, (const T*)z, sc, sh, mean, invstd, gamma, dgamma, dbeta,
                                   1.f / count, (T*)dz)));
   return adp::check_launch("adp_bn_bwd_apply");
+}
+
+extern "C" int adp_bn_bwd_apply_head(int dtype, size_t M, int C, int Cin, const float* W, const float* p,
+                                     const float* dp, const void* z, const float* sc, const float* sh,
+                                     const float* mean, const float* invstd, const float* gamma,
+                                     const float* dgamma, const float* dbeta, float count, void* dz,
+                                     adp_stream_t st) {
+  ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && Cin <= C && Cin % 8 == 0 && count > 0 && W && p && dp &&
+                  ((uintptr_t)W & 15) == 0,
+              "adp_bn_bwd_apply_head: bad arguments (C % 8 == 0, C <= 2048, Cin <= C, Cin % 8 == 0, W 16-B aligned)");
+  BN_UNROLL_SWITCH(U, 2, DTYPE_SWITCH(dtype, T,
+               hipLaunchKernelGGL((bn_bwd_apply_head_kernel<T, U>), dim3(bn_blocks(M, C, U, 32768)), dim3(TPB), 0,
+                                  (hipStream_t)st, M, C, Cin, (const T*)z, W, p, dp, sc, sh, mean, invstd, gamma,
+                                  dgamma, dbeta, 1.f / count, (T*)dz)));
+  return adp::check_launch("adp_bn_bwd_apply_head");
 }
 
 extern "C" int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* sc, const float* sh, void* out,

@@ -556,8 +556,8 @@ extern "C" int adp_head_sigmoid_bwd_bnr(int dtype, size_t M, int Cs, int Cin, co
                                         const float* sc, const float* sh, const float* mean, const float* invstd,
                                         const float* p, const float* dp, void* dx, float* dW, float* db,
                                         float* dgamma, float* dbeta, adp_stream_t st) {
-  ADP_REQUIRE(Cs % 8 == 0 && Cs / 8 <= TPB && Cin <= Cs && z && sc && sh && mean && invstd && dx && dgamma && dbeta,
-              "adp_head_sigmoid_bwd_bnr: Cs % 8 == 0, Cin <= Cs, all BatchNorm pointers and dx");
+  ADP_REQUIRE(Cs % 8 == 0 && Cs / 8 <= TPB && Cin <= Cs && z && sc && sh && mean && invstd && dgamma && dbeta,
+              "adp_head_sigmoid_bwd_bnr: Cs % 8 == 0, Cin <= Cs, all BatchNorm pointers");
   ADP_REQUIRE(Cs + Cin + 1 <= adp::STAT_CMAX, "adp_head_sigmoid_bwd_bnr: Cs + Cin too large");
   float* stat = adp::stat_scratch();
   ADP_REQUIRE(stat, adp_last_error());

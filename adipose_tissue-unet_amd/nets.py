@@ -367,14 +367,14 @@ class UNetEngine:
                             relu=l.relu and not l.bn, dropout_rate=dropout, dropout_seed=seed, accum=accum,
                             bn_stats=bn_stats, defer_fold=defer_fold)
 
-    def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None, bias_grad=True):
+    def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None, bias_grad=True, bn_apply=None):
         dW = self.ps.gview(l.name + "/W")
         dB = self.ps.gview(l.name + "/b") if bias_grad and (l.name + "/b") in self.ps.entries else None
         if l.transpose:
             ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, bnA=bnA, kh=1, kw=1, pad=0, shuffle_c=l.cout_s)
         else:
             ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, srcB=srcB, bnA=bnA, bnB=bnB, up=l.up, kh=l.k, kw=l.k,
-                           dil=l.dil)
+                           dil=l.dil, bn_apply=bn_apply)
         self._grad_ready(l.name)
 
     def dgrad(self, l, dZ, out, *, Ho=None, Wo=None, addend=None, mask=None, mask_scale=1.0, split=False,
@@ -653,6 +653,13 @@ class UNetBN(UNetEngine):
     # the training conv leaves its BatchNorm sums in the replica scratch and the finalize folds them (one
     # launch); False: the conv's own fold launch, then the finalize
     fuse_bn_fold = True
+    # with fuse_head_bn: the head backward stores no dA for dec0_conv2; that layer's BatchNorm-backward
+    # apply recomputes it from p, dL/dp and the head weights (adp_bn_bwd_apply_head, bit-identical dz)
+    head_recompute_dA = True
+    # each layer's BatchNorm-backward apply (dz from dA, z) handed to its weight-gradient launch
+    # (adp_conv_wgrad_bn: computed inside the halo weight-gradient kernel on levels 0-1, which also stores
+    # dz for the data gradient); False: adp_bn_bwd_apply, then the weight gradient re-reads dz
+    fuse_bn_wgrad = True
 
     def __init__(self, batch, size, *, levels=5, base=64, in_ch=3, dtype="bf16", device="cuda", seed=865,
                  bn_eps=1e-5, bn_momentum=0.1):
@@ -871,6 +878,18 @@ class UNetBN(UNetEngine):
         s = self.st[name]
         return (z, s[2], s[3], s[4], s[5], self.ps.gview(name + "/gamma"), self.ps.gview(name + "/beta"))
 
+    def _bn_bwd_wgrad(self, name, dA, z, dz, l, srcA, srcB=None):
+        """_bn_bwd(reduced=True) of layer `name` followed by the weight gradient of conv l over its dz."""
+        if not self.fuse_bn_wgrad:
+            self._bn_bwd(name, dA, z, dz, reduced=True)
+            self.wgrad(l, srcA, dz, srcB=srcB)
+            return
+        s = self.st[name]
+        count = z.shape[0] * z.shape[1] * z.shape[2]
+        self.wgrad(l, srcA, dz, srcB=srcB,
+                   bn_apply=(dA, z, s[2], s[3], s[4], s[5], self.ps.view(name + "/gamma"),
+                             self.ps.gview(name + "/gamma"), self.ps.gview(name + "/beta"), count))
+
     def _bn_bwd(self, name, dA, z, dz, reduced=False):
         """dA: gradient wrt relu(bn(z)) -> dz, and gamma/beta grads (already summed by the producer of
         dA when reduced=True)."""
@@ -891,7 +910,8 @@ class UNetBN(UNetEngine):
 
         # head: dA = dL/d(relu(bn(y0_2)))
         # (dec0_conv2's BatchNorm-backward reduction over dA fused into the head backward)
-        dA = gb("y0_2", a["y0_2"])
+        recompute = self.fuse_head_bn and self.head_recompute_dA
+        dA = None if recompute else gb("y0_2", a["y0_2"])
         s0 = self.st["dec0_conv2"]
         if not self.fuse_head_bn:
             ops.head_bwd(a["ay0_2"], self.ps.view("head/W"), a["p"], grads_out["main_out"],
@@ -912,15 +932,23 @@ class UNetBN(UNetEngine):
         for i in range(0, Lv - 1):
             dz = gb(f"dz_y{i}_2", a[f"y{i}_2"])
             # level 0's dA comes from the head, deeper levels' from the ConvT dgrad (reduction fused in both)
-            self._bn_bwd(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz, reduced=True)
+            if cur_dA is None:   # level 0, head_recompute_dA
+                s2 = self.st["dec0_conv2"]
+                y = a["y0_2"]
+                ops.bn_bwd_apply_head(self.ps.view("head/W"), a["p"], grads_out["main_out"], y, s2[2], s2[3], s2[4],
+                                      s2[5], self.ps.view("dec0_conv2/gamma"), self.ps.gview("dec0_conv2/gamma"),
+                                      self.ps.gview("dec0_conv2/beta"), y.shape[0] * y.shape[1] * y.shape[2], dz,
+                                      cin=self.ch(0))
             l2 = L[f"dec{i}_conv2"]
-            self.wgrad(l2, a[f"ay{i}_1"], dz)
+            if cur_dA is None:
+                self.wgrad(l2, a[f"ay{i}_1"], dz)
+            else:
+                self._bn_bwd_wgrad(f"dec{i}_conv2", cur_dA, a[f"y{i}_2"], dz, l2, a[f"ay{i}_1"])
             dA1 = gb(f"dA_y{i}_1", a[f"y{i}_1"])
             self.dgrad(l2, dz, dA1, bn_reduce=self._bn_red(f"dec{i}_conv1", a[f"y{i}_1"]))
             dz1 = gb(f"dz_y{i}_1", a[f"y{i}_1"])
-            self._bn_bwd(f"dec{i}_conv1", dA1, a[f"y{i}_1"], dz1, reduced=True)
             l1 = L[f"dec{i}_conv1"]
-            self.wgrad(l1, a[f"az{i}_2"], dz1, srcB=a[f"t{i}"])
+            self._bn_bwd_wgrad(f"dec{i}_conv1", dA1, a[f"y{i}_1"], dz1, l1, a[f"az{i}_2"], srcB=a[f"t{i}"])
             sk = gb(f"skip{i}", a[f"z{i}_2"])
             dt = gb(f"dt{i}", a[f"t{i}"])
             # the ConvTranspose bias gradient (sum of dt over pixels) comes out of this launch's epilogue
@@ -958,16 +986,14 @@ class UNetBN(UNetEngine):
             else:
                 dA2 = bott_dA
             dz2 = gb(f"dz_z{i}_2", z2)
-            self._bn_bwd(f"enc{i}_conv2", dA2, z2, dz2, reduced=True)
             l2 = L[f"enc{i}_conv2"]
-            self.wgrad(l2, a[f"az{i}_1"], dz2)
+            self._bn_bwd_wgrad(f"enc{i}_conv2", dA2, z2, dz2, l2, a[f"az{i}_1"])
             dA1 = gb(f"dA_z{i}_1", z1)
             self.dgrad(l2, dz2, dA1, bn_reduce=self._bn_red(f"enc{i}_conv1", z1))
             dz1 = gb(f"dz_z{i}_1", z1)
-            self._bn_bwd(f"enc{i}_conv1", dA1, z1, dz1, reduced=True)
             l1 = L[f"enc{i}_conv1"]
             src = a["x"] if i == 0 else a[f"pool{i - 1}"]
-            self.wgrad(l1, src, dz1)
+            self._bn_bwd_wgrad(f"enc{i}_conv1", dA1, z1, dz1, l1, src)
             if i > 0:
                 dpool = gb(f"dpool{i - 1}", a[f"pool{i - 1}"])
                 self.dgrad(l1, dz1, dpool)

@@ -13,7 +13,7 @@ import ctypes as C
 
 import torch
 
-from ._lib import BF16, F32, FP8, AdpError, ConvDesc, ConvIO, call, lib, ptr, stream_ptr
+from ._lib import BF16, F32, FP8, AdpError, BnBwdArgs, ConvDesc, ConvIO, call, lib, ptr, stream_ptr
 
 FP8_DTYPE = torch.float8_e4m3fn   # storage dtype of the fp8 (OCP e4m3fn) inference tensors
 
@@ -221,8 +221,11 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
 
 
 def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up=False, stride=1, kh=3, kw=3,
-               dil=1, pad=None, Ho=None, Wo=None, shuffle_c=0):
-    """dW (+)= X_tap^T dY (f32 accumulators, caller zeroes). shuffle_c>0: dY is a ConvT output."""
+               dil=1, pad=None, Ho=None, Wo=None, shuffle_c=0, bn_apply=None):
+    """dW (+)= X_tap^T dY (f32 accumulators, caller zeroes). shuffle_c>0: dY is a ConvT output.
+    bn_apply=(dA, z, scale, shift, mean, invstd, gamma, dgamma, dbeta, count): dY is first computed as
+    bn_bwd_apply(dA, z, ...) and stored (adp_conv_wgrad_bn: fused into the weight-gradient launch where the
+    halo kernel takes the shape, bit-identical to bn_bwd_apply + conv_wgrad)."""
     Wdummy = torch.empty(0)
     _act(srcA, "srcA")
     _act(dY, "dY")
@@ -257,6 +260,16 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     del Wdummy
     dc = dtype_code(srcA)
     flops = 2.0 * N * Ho * Wo * nout * K
+    if bn_apply is not None:
+        dA, z, sc, sh, mu, ist, gam, dg, dbt, count = bn_apply
+        _check(not shuffle_c and dA.shape == z.shape == dY.shape and dY.shape[3] == nout and
+               dA.dtype == z.dtype == dY.dtype, "bn_apply: dA, z, dY of one [N, Ho, Wo, nout] shape")
+        bn = BnBwdArgs(ptr(dA), ptr(z), ptr(sc), ptr(sh), ptr(mu), ptr(ist), ptr(gam), ptr(dg), ptr(dbt),
+                       float(count))
+        _timed(dc, flops,
+               lambda: call("adp_conv_wgrad_bn", dc, C.byref(d), C.byref(io), C.byref(bn), ptr(dY),
+                            int(dY.shape[3]), ptr(dW), ptr(dB), stream_ptr()))
+        return
     _timed(dc, flops,
            lambda: call("adp_conv_wgrad", dc, C.byref(d), C.byref(io), ptr(dY), int(dY.shape[3]), ptr(dW),
                         ptr(dB), stream_ptr()))
@@ -439,6 +452,18 @@ def bn_bwd_apply(dA, z, scale, shift, mean, invstd, gamma, dgamma, dbeta, count,
          ptr(invstd), ptr(gamma), ptr(dgamma), ptr(dbeta), float(count), ptr(dz), stream_ptr())
 
 
+def bn_bwd_apply_head(W, p, dp, z, scale, shift, mean, invstd, gamma, dgamma, dbeta, count, dz, *, cin):
+    """adp_bn_bwd_apply with dA = dp*p*(1-p)*W[c] recomputed from the sigmoid head (the dx the fused head
+    backward would have stored: it then runs with dx=None)."""
+    _check(z.shape == dz.shape, "bn bwd shapes")
+    Cs = z.shape[-1]
+    M = z.numel() // Cs
+    _check(p.numel() == M and dp.numel() == M and W.numel() == cin and cin <= Cs, "head grad sizes")
+    call("adp_bn_bwd_apply_head", dtype_code(z), M, Cs, cin, ptr(W), ptr(p), ptr(dp), ptr(z), ptr(scale),
+         ptr(shift), ptr(mean), ptr(invstd), ptr(gamma), ptr(dgamma), ptr(dbeta), float(count), ptr(dz),
+         stream_ptr())
+
+
 def head_fwd(x, W, b, p, *, cin, softmax2, bn=None):
     _act(x, "x")
     Cs = x.shape[-1]
@@ -457,11 +482,11 @@ def head_bwd(x, W, p, dp, dW, db, *, cin, softmax2, dx=None, bn=None, addend=Non
     scale/shift); that layer's BatchNorm-backward reduction over dx is fused (adp_head_sigmoid_bwd_bnr)."""
     _act(x, "x")
     if bn_reduce is not None:
-        _check(not softmax2 and bn is not None and dx is not None and addend is None and mask is None,
-               "head_bwd bn_reduce: sigmoid head, bn and dx only")
+        _check(not softmax2 and bn is not None and addend is None and mask is None,
+               "head_bwd bn_reduce: sigmoid head and bn only")
         Cs = x.shape[-1]
         M = x.numel() // Cs
-        _check(p.numel() == M and dp.numel() == M and dx.shape == x.shape, "head grad sizes")
+        _check(p.numel() == M and dp.numel() == M and (dx is None or dx.shape == x.shape), "head grad sizes")
         mean, invstd, dg, dbeta = bn_reduce
         call("adp_head_sigmoid_bwd_bnr", dtype_code(x), M, Cs, cin, ptr(x), ptr(W), ptr(bn[0]), ptr(bn[1]),
              ptr(mean), ptr(invstd), ptr(p), ptr(dp), ptr(dx), ptr(dW), ptr(db), ptr(dg), ptr(dbeta), stream_ptr())

@@ -29,11 +29,12 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 9 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 10 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
-                              v9: adp_conv_desc.bn_defer_fold + adp_bn_finalize_fold */
+                              v9: adp_conv_desc.bn_defer_fold + adp_bn_finalize_fold;
+                              v10: adp_bn_bwd_apply_head, adp_head_sigmoid_bwd_bnr with dx = NULL, adp_conv_wgrad_bn */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -119,6 +120,20 @@ int adp_conv_fwd(int dtype, const adp_conv_desc* d, const adp_conv_io* io, adp_s
  * caller zeroes them. The gather is described by d/io exactly as for the forward launch. */
 int adp_conv_wgrad(int dtype, const adp_conv_desc* d, const adp_conv_io* io, const void* dY,
                    int dy_stride, float* dW, float* dB, adp_stream_t s);
+/* The BatchNorm backward of the layer this conv feeds (adp_bn_bwd_apply's arguments): dY of the weight
+ * gradient is dz = bn_bwd_apply(dA, z) (dgamma / dbeta already reduced). */
+typedef struct adp_bn_bwd_args {
+  const void* dA;      /* gradient wrt relu(z*scale + shift), [M][dy_stride] */
+  const void* z;       /* the layer's pre-BatchNorm output, [M][dy_stride] */
+  const float *scale, *shift, *mean, *invstd, *gamma, *dgamma, *dbeta;
+  float count;
+} adp_bn_bwd_args;
+/* adp_bn_bwd_apply(bn -> dY) followed by adp_conv_wgrad(dY), as one launch where the persistent halo
+ * weight-gradient kernel takes the shape (3x3 stride-1 layers with <= 2 64-channel input chunks): dz is
+ * computed while the weight gradient loads its tiles and stored into dY (for the data-gradient launch),
+ * bit-identical to the two-launch form, which runs otherwise. */
+int adp_conv_wgrad_bn(int dtype, const adp_conv_desc* d, const adp_conv_io* io, const adp_bn_bwd_args* bn,
+                      void* dY, int dy_stride, float* dW, float* dB, adp_stream_t s);
 
 /* Repack f32 master weights into the launch layout: mode 0 = cast only (forward);
  * mode 1 = 3x3 flip+transpose (data-gradient of a conv), mode 2 = ConvTranspose transpose. */
@@ -194,6 +209,13 @@ int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, const void* z, 
                      const float* shift, const float* mean, const float* invstd,
                      const float* gamma, const float* dgamma, const float* dbeta, float count,
                      void* dz, adp_stream_t s);
+/* adp_bn_bwd_apply of the layer under the unet_bn sigmoid head with dA recomputed instead of read:
+ * dA[m][c] = dtype(dp[m] * p[m] * (1 - p[m]) * W[c]) (0 for c >= Cin; Cin % 8 == 0, W 16-B aligned), the value adp_head_sigmoid_bwd_bnr
+ * stores, so that launch can run with dx = NULL (one full-resolution write and read fewer; bit-identical dz) */
+int adp_bn_bwd_apply_head(int dtype, size_t M, int C, int Cin, const float* W, const float* p, const float* dp,
+                          const void* z, const float* scale, const float* shift, const float* mean,
+                          const float* invstd, const float* gamma, const float* dgamma, const float* dbeta,
+                          float count, void* dz, adp_stream_t s);
 
 /* ---- heads (Conv2D(2,1,softmax)[...,1] :729-731; Conv2D(1,1,sigmoid) :715,722) ------------- */
 /* p = softmax(W x + b)[1] = sigmoid(z1 - z0); W f32 [2][Cin], b f32 [2] */
@@ -214,7 +236,8 @@ int adp_head_sigmoid_bwd(int dtype, size_t M, int C_stride, int Cin, const void*
                          void* dx, float* dW, float* db, adp_stream_t s);
 /* unet_bn head backward with the BatchNorm-backward reduction of the layer under it fused (adp_bn_bwd_reduce):
  * z = that layer's pre-BN output (the head reads relu(z*sc+sh)), dx = dL/d relu(bn(z)) stored, and
- * dbeta += sum db, dgamma += sum db*(z-mean)*invstd with db = dx*(z*sc+sh > 0) over the stored dx */
+ * dbeta += sum db, dgamma += sum db*(z-mean)*invstd with db = dx*(z*sc+sh > 0) over the (rounded) dx;
+ * dx may be NULL (the sums are the same; adp_bn_bwd_apply_head then recomputes dx) */
 int adp_head_sigmoid_bwd_bnr(int dtype, size_t M, int C_stride, int Cin, const void* z, const float* W,
                              const float* scale, const float* shift, const float* mean, const float* invstd,
                              const float* p, const float* dp, void* dx, float* dW, float* db, float* dgamma,

@@ -483,6 +483,40 @@ def test_wgrad_input_layer_cin8(N, H, W, cin):
     assert dW[:, 72:].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("N,H,W,parts,cout,dtn,fused", [
+    (2, 64, 64, [64], 64, "bf16", True), (1, 32, 96, [64], 64, "bf16", True),
+    (2, 32, 64, [64, 64], 64, "bf16", True), (1, 32, 32, [128], 128, "bf16", True),
+    (1, 16, 64, [64], 128, "bf16", True), (2, 16, 64, [128, 64], 128, "bf16", False),
+    (1, 16, 32, [64], 64, "f32", False)])
+def test_wgrad_bn_apply_fused(N, H, W, parts, cout, dtn, fused):
+    """adp_conv_wgrad_bn (BatchNorm-backward apply computed inside the halo weight-gradient kernel, dz
+    stored for the data gradient) == adp_bn_bwd_apply + adp_conv_wgrad: dz bit for bit, dW to f32
+    summation order; shapes the fused kernel does not take run the two launches."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16 if dtn == "bf16" else torch.float32
+    g = torch.Generator().manual_seed(31)
+    xs = [(torch.randn(N, H, W, c, generator=g)).to(DEV, dt) for c in parts]
+    z = (torch.randn(N, H, W, cout, generator=g) * 2).to(DEV, dt)
+    dA = torch.randn(N, H, W, cout, generator=g).to(DEV, dt)
+    vec = lambda: (torch.rand(cout, generator=g) + 0.5).to(DEV)   # noqa: E731
+    sc, sh, mu, ist, gam = vec(), vec() - 1.0, vec() - 1.0, vec(), vec()
+    dg, db = torch.randn(cout, generator=g).to(DEV), torch.randn(cout, generator=g).to(DEV)
+    count = N * H * W
+    K = 9 * sum(parts)
+    srcB = xs[1] if len(xs) > 1 else None
+    dz1, dz2 = torch.full_like(z, 7.0), torch.full_like(z, 7.0)
+    dW1 = torch.zeros((cout, K), device=DEV)
+    dW2 = torch.zeros_like(dW1)
+    ops.bn_bwd_apply(dA, z, sc, sh, mu, ist, gam, dg, db, count, dz1)
+    ops.conv_wgrad(xs[0], dz1, dW1, cout, srcB=srcB)
+    ops.conv_wgrad(xs[0], dz2, dW2, cout, srcB=srcB, bn_apply=(dA, z, sc, sh, mu, ist, gam, dg, db, count))
+    kname = _lib.lib().adp_last_kernel().decode()
+    torch.cuda.synchronize()
+    assert (kname == "igemm_wgrad_halop_kernel<8, true>") == fused, kname
+    assert torch.equal(dz1, dz2)
+    assert relerr(dW2.cpu(), dW1.cpu()) < 1e-5
+
+
 @pytest.mark.parametrize("N,H,W,parts,cout", [(2, 64, 64, [64], 64), (1, 32, 96, [64], 64), (3, 16, 32, [64], 64),
                                                (2, 32, 64, [64, 64], 64), (1, 32, 32, [128], 128),
                                                (2, 16, 64, [128, 64], 128)])
@@ -820,6 +854,42 @@ def test_head_bn_on_load_and_fused_bn_reduce(dt):
                  bn_reduce=(mean, inv, dg2, db2))
     torch.cuda.synchronize()
     assert torch.equal(p1, p2) and torch.equal(dx1, dx2)
+    torch.testing.assert_close(gw2, gw1, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gb2, gb1, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dg2, dg1, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db2, db1, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_bn_bwd_apply_head_recompute(dt):
+    """adp_bn_bwd_apply_head (dA recomputed from the sigmoid head) == adp_head_sigmoid_bwd_bnr's stored dx
+    fed to adp_bn_bwd_apply, bit for bit; the fused head backward with dx=None leaves the same sums."""
+    g = torch.Generator().manual_seed(84)
+    Cs, cin = 64, 48
+    shape = (2, 24, 96, Cs)
+    M = shape[0] * shape[1] * shape[2]
+    z = (torch.randn(*shape, generator=g) * 2).to(DEV, dt)
+    sc = (torch.rand(Cs, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(Cs, generator=g) * 0.5).to(DEV)
+    mean = (torch.randn(Cs, generator=g) * 0.1).to(DEV)
+    inv = (torch.rand(Cs, generator=g) + 0.5).to(DEV)
+    gam = (torch.rand(Cs, generator=g) + 0.5).to(DEV)
+    W = (torch.randn(cin, generator=g) * 0.2).to(DEV)
+    b = torch.tensor([0.1], device=DEV)
+    dp = torch.randn(M, generator=g).to(DEV)
+    p = torch.empty(M, device=DEV)
+    ops.head_fwd(z, W, b, p, cin=cin, softmax2=False, bn=(sc, sh))
+    dx = torch.empty_like(z)
+    gw1, gw2 = torch.zeros(cin, device=DEV), torch.zeros(cin, device=DEV)
+    gb1, gb2 = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    dg1, dg2, db1, db2 = (torch.zeros(Cs, device=DEV) for _ in range(4))
+    ops.head_bwd(z, W, p, dp, gw1, gb1, cin=cin, softmax2=False, dx=dx, bn=(sc, sh), bn_reduce=(mean, inv, dg1, db1))
+    ops.head_bwd(z, W, p, dp, gw2, gb2, cin=cin, softmax2=False, dx=None, bn=(sc, sh), bn_reduce=(mean, inv, dg2, db2))
+    dz1, dz2 = torch.empty_like(z), torch.empty_like(z)
+    ops.bn_bwd_apply(dx, z, sc, sh, mean, inv, gam, dg1, db1, M, dz1)
+    ops.bn_bwd_apply_head(W, p, dp, z, sc, sh, mean, inv, gam, dg1, db1, M, dz2, cin=cin)
+    torch.cuda.synchronize()
+    assert torch.equal(dz1, dz2)
     torch.testing.assert_close(gw2, gw1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(gb2, gb1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dg2, dg1, rtol=1e-4, atol=1e-3)

@@ -7,6 +7,9 @@ alternating timed blocks so that clock drift and device variance hit both arms a
                   adp_head_sigmoid_bwd_bnr (UNetBN.fuse_head_bn)
   --variant fold: conv-side BatchNorm statistic fold + finalize (old) vs the fold fused into the finalize
                   (UNetBN.fuse_bn_fold)
+  --variant headdA: head backward storing dA (old) vs dA recomputed by adp_bn_bwd_apply_head
+                  (UNetBN.head_recompute_dA)
+  --variant bnwgrad: adp_bn_bwd_apply + weight gradient (old) vs adp_conv_wgrad_bn (UNetBN.fuse_bn_wgrad)
   --variant opt --opts "a=1;a=0": two native option settings (';'-separated, each ','-separated name=value)
 (the round-1 "stat" arm, per-layer statistic fills vs one arena fill, measured neutral:
 profiles/r01i_ab_stat_arena.txt; only the arena path remains)"""
@@ -21,7 +24,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head", "fold", "opt"])
+    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head", "fold", "headdA", "bnwgrad", "opt"])
     p.add_argument("--opts", default="")
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--steps", type=int, default=8)
@@ -55,6 +58,10 @@ def main():
         owner, attr, old, new = UNetBN, "fuse_head_bn", False, True
     elif args.variant == "fold":
         owner, attr, old, new = UNetBN, "fuse_bn_fold", False, True
+    elif args.variant == "headdA":
+        owner, attr, old, new = UNetBN, "head_recompute_dA", False, True
+    elif args.variant == "bnwgrad":
+        owner, attr, old, new = UNetBN, "fuse_bn_wgrad", False, True
     elif args.variant == "opt":
         class _Opts:   # setattr(owner, attr, settings) applies a native option setting
             def __setattr__(self, _, st):

@@ -53,6 +53,10 @@ def main():
         table = {
             "head_bwd_bnr": (lambda: ops.head_bwd(z, Wh, pr, dpr, gw, gb, cin=C, softmax2=False, dx=out, bn=(sc, sh),
                                                   bn_reduce=(mu, ist, dg, db)), 2 * E + 8 * M),
+            "head_bwd_bnr_nodx": (lambda: ops.head_bwd(z, Wh, pr, dpr, gw, gb, cin=C, softmax2=False, dx=None,
+                                                       bn=(sc, sh), bn_reduce=(mu, ist, dg, db)), E + 8 * M),
+            "bn_bwd_apply_head": (lambda: ops.bn_bwd_apply_head(Wh, pr, dpr, z, sc, sh, mu, ist, gam, dg, db, float(M),
+                                                                out, cin=C), 2 * E + 8 * M),
             "pool_bwd_bnr": (lambda: ops.maxpool2_bwd(act, dpool, out, addend=add,
                                                       bn_reduce=(z, sc, sh, mu, ist, dg, db)), 3 * E + E // 4),
             "pool_bwd_bnr_src": (lambda: ops.maxpool2_bwd(act, dpool, out, addend=add, argmax_from_z=False,
