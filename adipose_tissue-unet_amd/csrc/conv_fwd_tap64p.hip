@@ -61,20 +61,36 @@ __device__ __forceinline__ void p_lds_add(float* p, float v) {
 // pixels x 64 channels. The K steps of ALL the block's tiles form one stream: the loader runs NST - 1 steps
 // ahead of the multiply, across tile boundaries, so with NST = 3 two stages are in flight while a third
 // multiplies (the small-K ConvTranspose / N = 128 shapes, whose tiles are only 2..18 steps long).
-template <int BM, int BN, int NST, bool BNR>
-constexpr int tap64p_lds() { return NST * (BM + BN) * 128 + 7 * BN * 4; }
+// HALO (3x3 stride-1 'same' layers, 8 x 32 output patches, BM = BN = 256, NST = 2): the A operand is not
+// gathered per tap but read from the 10 x 34 input halo of the patch, moved into LDS once per 64-channel
+// chunk (a two-slot ring beside the weight stages). The K stream of a tile is chunk-major (chunk c: taps
+// 0..8 over the same halo), each step stages only the weight rows of its (tap, chunk), and the halo of the
+// NEXT chunk of the stream -- the next tile's first chunk at a tile's last one -- goes out one 16-B group
+// per step at the steps of taps 1..6 (its slot was freed by the previous chunk's last step). LDS-DMA
+// pieces per thread per step: 4 weight + <= 1 halo, against 4 + 4 gathered A pieces (their issue is what
+// the K loop waits on: profiles/r02_stagger_ab.txt).
+constexpr int P_HROWS = 340;   // 10 x 34 halo pixels of an 8 x 32 patch
+template <int BM, int BN, int NST, bool BNR, bool HALO = false>
+constexpr int tap64p_lds() {
+  return HALO ? NST * BN * 128 + 2 * P_HROWS * 128 + 7 * BN * 4 : NST * (BM + BN) * 128 + 7 * BN * 4;
+}
+__device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_halo.hip: conflict-free)
 
-template <int BM, int BN, int NST, bool BNR>
+template <int BM, int BN, int NST, bool BNR, bool HALO = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   constexpr int NTH = 512, ROWB = 128, ES = 2, KSTEP = 64;
   constexpr int WN = BN / 64, WM = 8 / WN, TM = BM / WM;
   static_assert(WN * WM == 8 && TM % 32 == 0 && TM >= 64, "wave layout");
+  static_assert(!HALO || (BM == 256 && BN == 256 && NST == 2 && !BNR), "halo form: 256x256, 2 stages");
   constexpr int QA = BM / 2, QB = BN / 2, GA = QA * 8 / NTH, GB = QB * 8 / NTH;
   static_assert(GA >= 1 && GB >= 1, "staging split");
   constexpr int HM = TM / 2, MIQ = TM / 32;
-  constexpr int STAGE = (BM + BN) * ROWB;
-  constexpr int OA1 = QA * ROWB, OB0 = BM * ROWB, OB1 = (BM + QB) * ROWB;
-  constexpr int LOPS = 2 * GA + 2 * GB;                    // LDS-DMA pieces per thread per stage
+  constexpr int STAGE = (HALO ? BN : BM + BN) * ROWB;
+  constexpr int OA1 = QA * ROWB, OB0 = HALO ? 0 : BM * ROWB, OB1 = (HALO ? QB : BM + QB) * ROWB;
+  constexpr int HBUF = P_HROWS * ROWB, OH = NST * STAGE;   // halo slots (HALO)
+  constexpr int GH = (P_HROWS * 8 + NTH - 1) / NTH;        // halo groups per chunk (the last one partial)
+  static_assert(!HALO || GH <= 8, "halo groups ride on taps 1..8");
+  constexpr int LOPS = HALO ? 2 * GB : 2 * GA + 2 * GB;   // LDS-DMA pieces per thread per stage (HALO: + halo)
   constexpr bool ZALL = BNR && MIQ == 2;                     // (see load_zall)
   constexpr int EPI_OPS = 2 * MIQ * 4 * (BNR && !ZALL ? 2 : 1);   // vector-memory ops per thread per epilogue
   // (vmcnt holds 0..63: a larger count is clamped, which only waits for more)
@@ -83,10 +99,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // ONE LDS object: with several, the compiler tags every LDS access with per-object alias scopes, and the
   // waitcnt pass then drains vmcnt(0) between the LDS-DMA prefetch of stage t+1 and the fragment reads of
   // stage t (one object: no such wait -- measured 12 % of the K loop)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[tap64p_lds<BM, BN, NST, BNR>()];
-  float (*cst)[BN] = reinterpret_cast<float (*)[BN]>(smem + NST * STAGE);   // epilogue constants:
-                                                                           // bias | scale shift mean invstd (BNR)
-  float (*sacc)[BN] = reinterpret_cast<float (*)[BN]>(smem + NST * STAGE + 5 * BN * 4);   // block's BN sums
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[tap64p_lds<BM, BN, NST, BNR, HALO>()];
+  constexpr int OC = NST * STAGE + (HALO ? 2 * HBUF : 0);
+  float (*cst)[BN] = reinterpret_cast<float (*)[BN]>(smem + OC);   // epilogue constants:
+                                                                  // bias | scale shift mean invstd (BNR)
+  float (*sacc)[BN] = reinterpret_cast<float (*)[BN]>(smem + OC + 5 * BN * 4);   // block's BN sums
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WN, wc = wave % WN;
@@ -189,11 +206,76 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   };
   // the loader: the next K step of the block's stream (tile lk, step lt) into stage ls
   int lk = 0, lt = 0, ls = 0;
-  auto tile_m0 = [&](int k) { return ((lin + k * G) / a.ntile_n) * BM; };
+  // HALO: tile -> 8 x 32 patch (image, y0, x0); its first output pixel is the tile's "m0" and pixel p of the
+  // tile (p = 32 * patch row + column) is output pixel m0 + (p >> 5) * Wo + (p & 31)
+  const int ptx = HALO ? a.Wo / 32 : 1, pty = HALO ? a.Ho / 8 : 1;
+  struct PatchO { int img, y0, x0; };
+  auto patch_of = [&](int k) {
+    const int t = (lin + k * G) / a.ntile_n;
+    PatchO P;
+    P.x0 = (t % ptx) * 32;
+    const int r = t / ptx;
+    P.y0 = (r % pty) * 8;
+    P.img = r / pty;
+    return P;
+  };
+  auto tile_m0 = [&](int k) {
+    if constexpr (HALO) {
+      const PatchO P = patch_of(k);
+      return (P.img * a.Ho + P.y0) * a.Wo + P.x0;
+    }
+    return ((lin + k * G) / a.ntile_n) * BM;
+  };
+  auto pix = [&](int m0, int p) { return HALO ? m0 + (p >> 5) * a.Wo + (p & 31) : m0 + p; };
   const bool no_dma = (a.debug_flags & 32) != 0;   // timing-only ablation (fwd_debug bit 5): the K loop
                                                     // multiplies whatever the prologue loaded
   int nissued = 0;
+  // HALO: one 16-B group g of the halo of chunk c of tile k into slot `slot`; returns whether this wave
+  // issued an instruction (the last group covers 160 of 512 threads: waves 3-7 skip it)
+  const int nch = Cin_s / 64;
+  auto issue_halo = [&](int k, int c, int g, int slot) {
+    const int idx = g * NTH + tid;
+    if (g == GH - 1 && __builtin_amdgcn_readfirstlane(g * NTH + wave * 64) >= P_HROWS * 8) return false;
+    if (idx < P_HROWS * 8) {
+      const PatchO P = patch_of(k);
+      const int hr = idx >> 3, hp = idx & 7;
+      const int yi = P.y0 - 1 + hr / 34, xi = P.x0 - 1 + hr % 34;
+      const int ci = c * 64;
+      const bool srcb = ci >= a.CAs;
+      const int cs = (srcb ? a.CBs : a.CAs) * ES, cb = (srcb ? ci - a.CAs : ci) * ES;
+      const bool v = (unsigned)yi < (unsigned)a.Hs && (unsigned)xi < (unsigned)a.Ws;
+      const unsigned off = v ? (unsigned)(((P.img * a.Hs + yi) * a.Ws + xi) * cs + cb + 16 * (hp ^ p_hswz(hr))) : P_OOB;
+      p_lds16(srcb ? rsB : rsA, smem + OH + slot * HBUF + (size_t)(g * NTH + wave * 64) * 16, off);
+    }
+    return true;
+  };
+  bool hg_last = false;   // HALO: the latest load_next issued a halo group after its weights (wave-uniform)
+  auto load_next_halo = [&]() {
+    hg_last = false;
+    if (lk >= mine) return;
+    const int c = lt / 9, tp = lt - 9 * c;
+    {   // weights of (tap tp, chunk c): GEMM K rows kt = tp * nch + c
+      const unsigned kt = (unsigned)(tp * nch + c);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        unsigned char* dsb = smem + ls * STAGE + (h ? OB1 : OB0) + wave * 8 * ROWB;
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+          const unsigned off = bo[h][i] == P_OOB ? P_OOB : bo[h][i] + kt * ROWB;
+          p_lds16(rsW, dsb + i * (NTH / 8) * ROWB, off);
+        }
+      }
+    }
+    if (tp >= 1 && tp <= GH) {   // one group of the next chunk of the stream
+      const int e = lk * nch + c;   // stream index of this chunk; the next one goes to slot (e + 1) & 1
+      const int nk2 = c + 1 < nch ? lk : lk + 1, nc2 = c + 1 < nch ? c + 1 : 0;
+      if (nk2 < mine) hg_last = issue_halo(nk2, nc2, tp - 1, (e + 1) & 1);
+    }
+    ls = ls == NST - 1 ? 0 : ls + 1;
+    if (++lt == nk) { lt = 0; ++lk; }
+  };
   auto load_next = [&]() {
+    if constexpr (HALO) { load_next_halo(); return; }
     if (lk >= mine) return;   // stream exhausted (uniform)
     if (no_dma && nissued >= NST - 1) {   // (keep the loader's bookkeeping, issue nothing)
       if (++lt == nk) { lt = 0; ++lk; }
@@ -218,6 +300,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       for (int s = 0; s < 2; ++s) {
         const int q = wr * HM + mi * 16 + r16, c = 4 * s + h4;
         fa[mi][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
+      }
+  };
+  auto readA_halo = [&](int slot, int dy, int dx, int h, bf16x8 (&fa)[MIQ][2]) {
+    const unsigned char* base = smem + OH + slot * HBUF;
+#pragma unroll
+    for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int p = wr * TM + h * HM + mi * 16 + r16;   // tile pixel: patch row p >> 5, column p & 31
+        const int hr = ((p >> 5) + dy) * 34 + (p & 31) + dx, c = 4 * s + h4;
+        fa[mi][s] = *reinterpret_cast<const bf16x8*>(base + hr * ROWB + ((c ^ p_hswz(hr)) << 4));
       }
   };
   auto readB = [&](int buf, int h, bf16x8 (&fb)[2][2]) {
@@ -271,7 +364,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       const int c = n0 + wc * 64 + nt * 16 + 4 * h4;
 #pragma unroll
       for (int mt = 0; mt < 2 * MIQ; ++mt) {
-        const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
+        const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
         const bool v = c < a.Nout && m < a.M;
         zall[nt][mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
       }
@@ -306,7 +399,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         if constexpr (!ZALL) {
 #pragma unroll
           for (int mt = 0; mt < 2 * MIQ; ++mt) {
-            const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
+            const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
             const bool v = cv && m < a.M;
             zq[mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
           }
@@ -327,7 +420,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int mt = 0; mt < 2 * MIQ; ++mt) {
-        const int m = m0 + wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16;
+        const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
         const bool v = cv && m < a.M;
         float x[4];
 #pragma unroll
@@ -387,14 +480,19 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // (issuing each wave's step in two halves spread over the clusters measured 5-9 % slower:
   //  profiles/r02_stagger_ab.txt)
   const bool late = a.stagger && ((__builtin_amdgcn_readfirstlane(wave) >> 2) & 1);
+  int hslot = 0, hdy = 0, hdx = 0;   // HALO: halo slot and tap of the step being multiplied
+  auto rA = [&](int buf, int h) {
+    if constexpr (HALO) readA_halo(hslot, hdy, hdx, h, fa);
+    else readA(buf, h, fa);
+  };
   auto compute = [&](int buf, bool issue_late) {
-    readA(buf, 0, fa);
+    rA(buf, 0);
     readB(buf, 0, fb0);
     mma(fa, fb0, 0, 0);
     if (issue_late) load_next();
     readB(buf, 1, fb1);
     mma(fa, fb1, 0, 1);
-    readA(buf, 1, fa);
+    rA(buf, 1);
     mma(fa, fb1, 1, 1);
     mma(fa, fb0, 1, 0);
   };
@@ -403,6 +501,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // The wait counts what was issued after the stage: the NST - 2 younger stages and, when a tile ended
   // inside that window, its EPI_OPS epilogue ops; near the end of the stream (fewer younger stages) it
   // drains everything.
+  if constexpr (HALO) {   // the first chunk's whole halo ahead of the stream
+#pragma unroll
+    for (int g = 0; g < GH; ++g) issue_halo(0, 0, g, 0);
+  }
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i) load_next();
   const int total = mine * nk;
@@ -419,7 +521,22 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       // ops younger than stage cs: the NST - 2 stages issued after it, an epilogue in the window, and the
       // z loads when they went out at the previous step (after cs, before that step's stage); a count
       // that is too small only waits longer, so the combinations are covered by the smaller constant
-      if (gs + NST - 2 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (HALO, NST = 2: the stage's weights plus, when this wave issued one, a halo group after them; the
+      // halo of a chunk was issued before the weights of the chunk's first step, so it has landed too)
+      if constexpr (HALO) {
+        if (last_epi > gs - NST) {
+          if (hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS + 1 < 63 ? EPI_OPS + 1 : 63) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS) : "memory");
+        } else if (hg_last) {
+          asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const int c = t / 9, tp = t - 9 * c;
+        hslot = (k * nch + c) & 1;
+        hdy = tp / 3;
+        hdx = tp - 3 * hdy;
+      } else if (gs + NST - 2 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
       else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
@@ -505,7 +622,16 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   grid -= grid % a.ntile_n;
   if (grid <= 0) grid = a.ntile_n;
   const bool bnr = a.bnr_z != nullptr;
-  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
+  // the halo form (option tap64p_halo): 3x3 stride-1 'same' layers whose output tiles into 8 x 32 patches
+  const bool halo = cfg == 1 && !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&
+                    a.dil == 1 && a.pad == 1 && a.stride == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 &&
+                    a.Wo % 32 == 0;
+  if (halo) {
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true>");
+    hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);
+    return 1;
+  }
+  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
 #define P_LAUNCH(BM_, BN_, NST_)                                                                           \
   do {                                                                                                     \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \

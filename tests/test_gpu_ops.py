@@ -171,6 +171,58 @@ def test_tap64_configs(cfg):
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
+@pytest.mark.parametrize("mode", ["plain", "one_chunk", "concat", "split"])
+def test_tap64p_halo_matches(mode, grid):
+    """Halo form of the persistent 256x256 forward (A operand read from a 10x34 halo moved into LDS once per
+    64-channel chunk, chunk-major K stream, next chunk's halo issued one group per step) vs a float64
+    reference convolution of the same bf16 operands, and vs the gathered form (tap64p_halo=0) to within the
+    bf16 rounding of a different f32 summation order; BatchNorm sums to 1e-4. Ragged N tile (320), 1-3
+    input chunks from one or two sources, split store; 3 / 7-block grids walk many patches per block."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(12)
+    N, H, W_ = 2, 32, 64
+    parts = {"plain": [128], "one_chunk": [64], "concat": [64, 128], "split": [128, 64]}[mode]
+    nout = {"plain": 320, "one_chunk": 256, "concat": 256, "split": 256}[mode]
+    cin = sum(parts)
+    srcs = [torch.randn(N, H, W_, c, generator=g).to(DEV, dt) for c in parts]
+    Wt = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV)
+    x = torch.cat([t.double() for t in srcs], -1).permute(0, 3, 1, 2)
+    wk = Wt[:nout].double().view(nout, 3, 3, cin).permute(0, 3, 1, 2)
+    ref = F.conv2d(x, wk, padding=1).permute(0, 2, 3, 1) + bias.double()
+    relu = mode != "split"
+    if relu:
+        ref = ref.clamp_min(0.0)
+    res = []
+    for halo in (1, 0):
+        outs = [torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)]
+        kw = dict(srcB=srcs[1] if len(srcs) > 1 else None, bias=bias, relu=relu)
+        if mode == "split":
+            outs = [torch.zeros(N, H, W_, 128, dtype=dt, device=DEV), torch.zeros(N, H, W_, nout - 128, dtype=dt, device=DEV)]
+            kw.update(out_mode=2, out2=outs[1], split_c=128)
+        st = torch.zeros(2, nout, device=DEV)
+        ops.set_option("fwd_tap64", 2)   # the 256x256 configuration
+        ops.set_option("tap64p_halo", halo)
+        if grid:
+            ops.set_option("tap64_persist_grid", grid)
+        try:
+            ops.conv_fwd(srcs[0], Wt, nout, out=outs[0], bn_stats=(st[0], st[1]), **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for o_ in ("fwd_tap64", "tap64p_halo", "tap64_persist_grid"):
+                ops.set_option(o_, None)
+        assert kname == "igemm_fwd_tap64p_kernel<256, 256, 2, false, %s>" % ("true" if halo else "false"), kname
+        res.append((torch.cat(outs, -1).double(), st.double()))
+    (yh, sh_), (yg, sg) = res
+    assert (yh - ref).abs().max().item() < 0.02 * ref.abs().max().item()
+    assert (yh - yg).abs().max().item() <= 0.01 * ref.abs().max().item()
+    torch.testing.assert_close(sh_, sg, rtol=1e-4, atol=1e-2)
+    rf = ref.reshape(-1, nout)
+    torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
+
+
 @pytest.mark.parametrize("cfg", [1, 2, 3], ids=["256x256x2", "256x128x3", "128x256x3"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
 @pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad", "bnr"])
