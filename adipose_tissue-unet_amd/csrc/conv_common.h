@@ -76,6 +76,18 @@ struct WgradArgs {
 
 namespace {
 
+// sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), every lane receives it: xor-1 and xor-2 quad
+// permutes, then the half-row and row mirrors (after the quad steps the lanes of a quad hold equal values,
+// so a mirror adds exactly what xor 4 / xor 8 would) -- the butterfly of __shfl_xor(v, 1..8) term for term,
+// as four DPP-modified VALU adds instead of four ds_bpermute round trips through the LDS pipe
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
 typedef __attribute__((address_space(3))) void lds_void;
 typedef short v4s16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s16 lds_v4s16;

@@ -107,12 +107,7 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float x = s1[mb][i], y = s2[mb][i];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        x += __shfl_xor(x, o, 64);
-        y += __shfl_xor(y, o, 64);
-      }
+      const float x = row16_sum(s1[mb][i]), y = row16_sum(s2[mb][i]);
       const int co = 16 * mb + 4 * h4 + i;
       if (r16 == 0 && co < a.Nout) {   // this wave's replica; the launcher folds them into bn_sum / bn_sq
         float* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;

@@ -529,12 +529,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float x = s1[nf][i], y = s2[nf][i];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        x += __shfl_xor(x, o, 64);
-        y += __shfl_xor(y, o, 64);
-      }
+      const float x = row16_sum(s1[nf][i]), y = row16_sum(s2[nf][i]);
       const int c = n0 + nf * 16 + 4 * h4 + i;
       if (r16 == 0 && c < a.Nout) {
         atomicAdd(d0 + c, x);

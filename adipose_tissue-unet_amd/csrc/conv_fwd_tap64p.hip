@@ -253,6 +253,12 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   auto load_next_halo = [&]() {
     hg_last = false;
     if (lk >= mine) return;
+    if (no_dma && nissued >= NST - 1) {   // (timing-only ablation, fwd_debug bit 5: bookkeeping only)
+      ls = ls == NST - 1 ? 0 : ls + 1;
+      if (++lt == nk) { lt = 0; ++lk; }
+      return;
+    }
+    ++nissued;
     const int c = lt / 9, tp = lt - 9 * c;
     {   // weights of (tap tp, chunk c): GEMM K rows kt = tp * nch + c
       const unsigned kt = (unsigned)(tp * nch + c);
@@ -454,11 +460,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       if (stats) {   // over the 16 pixel lanes of the channel quad, then into the block's LDS sums
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            s1[r] += __shfl_xor(s1[r], o, 64);
-            s2[r] += __shfl_xor(s2[r], o, 64);
-          }
+          s1[r] = row16_sum(s1[r]);
+          s2[r] = row16_sum(s2[r]);
         }
         if (r16 == 0) {
 #pragma unroll
@@ -524,7 +527,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       // (HALO, NST = 2: the stage's weights plus, when this wave issued one, a halo group after them; the
       // halo of a chunk was issued before the weights of the chunk's first step, so it has landed too)
       if constexpr (HALO) {
-        if (last_epi > gs - NST) {
+        if (a.debug_flags & 64) {   // timing-only ablation (fwd_debug bit 6): LDS-DMA issued, never waited for
+        } else if (last_epi > gs - NST) {
           if (hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS + 1 < 63 ? EPI_OPS + 1 : 63) : "memory");
           else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS) : "memory");
         } else if (hg_last) {
