@@ -442,7 +442,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
           pix = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
         }
-        const unsigned off = v ? (unsigned)((pix * ostr + cq) * ES) : P_OOB;
+        // (timing-only ablation, fwd_debug bit 7: every store to an out-of-range offset, dropped)
+        const unsigned off = v && !(a.debug_flags & 128) ? (unsigned)((pix * ostr + cq) * ES) : P_OOB;
         p_st8(rsO, off, __builtin_bit_cast(v2u32, o));
         if constexpr (BNR) {
 #pragma unroll
