@@ -615,6 +615,11 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
 #undef HALOP_LAUNCH
     return 1;
   }
+  // 128 outputs from more than two input chunks (unet_bn dec1_conv1, 256 -> 128): the 256x128 halo form of
+  // the persistent tap64 kernel takes plain launches (917 vs 852 TF with statistics,
+  // profiles/r02_tap64p_halo_ab.txt)
+  if (a.Nout == 128 && Cin_s > 128 && !a.bnr_z && plain && a.out_mode != 1 && option("halo_defer_tap64p", 1))
+    return 0;
   if (a.Nout <= 64) {
     if (one_chunk && mode != 2) launch_halo<1, 2, 1, 1>(a, s);   // two blocks per CU
     else launch_halo<1, 2, 2, 2>(a, s);

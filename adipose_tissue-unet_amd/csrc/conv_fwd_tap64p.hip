@@ -81,7 +81,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   constexpr int NTH = 512, ROWB = 128, ES = 2, KSTEP = 64;
   constexpr int WN = BN / 64, WM = 8 / WN, TM = BM / WM;
   static_assert(WN * WM == 8 && TM % 32 == 0 && TM >= 64, "wave layout");
-  static_assert(!HALO || (BM == 256 && BN == 256 && NST == 2 && !BNR), "halo form: 256x256, 2 stages");
+  static_assert(!HALO || (!BNR && BM == 256 && ((BN == 256 && NST == 2) || (BN == 128 && NST == 3))),
+                "halo form: 256x256 / 2 stages or 256x128 / 3 stages, no BN-backward reduction");
   constexpr int QA = BM / 2, QB = BN / 2, GA = QA * 8 / NTH, GB = QB * 8 / NTH;
   static_assert(GA >= 1 && GB >= 1, "staging split");
   constexpr int HM = TM / 2, MIQ = TM / 32;
@@ -89,7 +90,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   constexpr int OA1 = QA * ROWB, OB0 = HALO ? 0 : BM * ROWB, OB1 = (HALO ? QB : BM + QB) * ROWB;
   constexpr int HBUF = P_HROWS * ROWB, OH = NST * STAGE;   // halo slots (HALO)
   constexpr int GH = (P_HROWS * 8 + NTH - 1) / NTH;        // halo groups per chunk (the last one partial)
-  static_assert(!HALO || GH <= 8, "halo groups ride on taps 1..8");
+  // HALO: group g of the next chunk's halo rides on the loader step of tap g + NST - 1 (the compute is then
+  // past the barrier of the chunk's first step, so the slot's previous chunk is no longer read)
+  static_assert(!HALO || GH + NST - 1 <= 9, "halo groups ride on taps NST-1 .. 8");
   constexpr int LOPS = HALO ? 2 * GB : 2 * GA + 2 * GB;   // LDS-DMA pieces per thread per stage (HALO: + halo)
   constexpr bool ZALL = BNR && MIQ == 2;                     // (see load_zall)
   constexpr int EPI_OPS = 2 * MIQ * 4 * (BNR && !ZALL ? 2 : 1);   // vector-memory ops per thread per epilogue
@@ -272,10 +275,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         }
       }
     }
-    if (tp >= 1 && tp <= GH) {   // one group of the next chunk of the stream
+    if (tp >= NST - 1 && tp < NST - 1 + GH) {   // one group of the next chunk of the stream
       const int e = lk * nch + c;   // stream index of this chunk; the next one goes to slot (e + 1) & 1
       const int nk2 = c + 1 < nch ? lk : lk + 1, nc2 = c + 1 < nch ? c + 1 : 0;
-      if (nk2 < mine) hg_last = issue_halo(nk2, nc2, tp - 1, (e + 1) & 1);
+      if (nk2 < mine) hg_last = issue_halo(nk2, nc2, tp - (NST - 1), (e + 1) & 1);
     }
     ls = ls == NST - 1 ? 0 : ls + 1;
     if (++lt == nk) { lt = 0; ++lk; }
@@ -528,14 +531,18 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       // (HALO, NST = 2: the stage's weights plus, when this wave issued one, a halo group after them; the
       // halo of a chunk was issued before the weights of the chunk's first step, so it has landed too)
       if constexpr (HALO) {
+        // NST = 3: the younger stage's weights are counted, its halo groups not (a smaller count only
+        // waits longer)
         if (a.debug_flags & 64) {   // timing-only ablation (fwd_debug bit 6): LDS-DMA issued, never waited for
+        } else if (gs + NST - 2 >= total) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (last_epi > gs - NST) {
-          if (hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS + 1 < 63 ? EPI_OPS + 1 : 63) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI_OPS) : "memory");
-        } else if (hg_last) {
+          if (NST == 2 && hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI + 1 < 63 ? VM_EPI + 1 : 63) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
+        } else if (NST == 2 && hg_last) {
           asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
         }
         const int c = t / 9, tp = t - 9 * c;
         hslot = (k * nch + c) & 1;
@@ -628,12 +635,17 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   if (grid <= 0) grid = a.ntile_n;
   const bool bnr = a.bnr_z != nullptr;
   // the halo form (option tap64p_halo): 3x3 stride-1 'same' layers whose output tiles into 8 x 32 patches
-  const bool halo = cfg == 1 && !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&
-                    a.dil == 1 && a.pad == 1 && a.stride == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 &&
-                    a.Wo % 32 == 0;
-  if (halo) {
+  const bool halo_shape = !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&
+                          a.dil == 1 && a.pad == 1 && a.stride == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 &&
+                          a.Wo % 32 == 0;
+  if (halo_shape && cfg == 1) {
     adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);
+    return 1;
+  }
+  if (halo_shape && cfg == 2 && option("tap64p_halo128", 1)) {
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true>");
+    hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
   adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");

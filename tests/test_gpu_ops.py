@@ -171,9 +171,10 @@ def test_tap64_configs(cfg):
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("tile", [256, 128], ids=["256x256x2", "256x128x3"])
 @pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
 @pytest.mark.parametrize("mode", ["plain", "one_chunk", "concat", "split"])
-def test_tap64p_halo_matches(mode, grid):
+def test_tap64p_halo_matches(mode, grid, tile):
     """Halo form of the persistent 256x256 forward (A operand read from a 10x34 halo moved into LDS once per
     64-channel chunk, chunk-major K stream, next chunk's halo issued one group per step) vs a float64
     reference convolution of the same bf16 operands, and vs the gathered form (tap64p_halo=0) to within the
@@ -184,6 +185,8 @@ def test_tap64p_halo_matches(mode, grid):
     N, H, W_ = 2, 32, 64
     parts = {"plain": [128], "one_chunk": [64], "concat": [64, 128], "split": [128, 64]}[mode]
     nout = {"plain": 320, "one_chunk": 256, "concat": 256, "split": 256}[mode]
+    if tile == 128:
+        nout = {"plain": 192, "one_chunk": 128, "concat": 128, "split": 256}[mode]
     cin = sum(parts)
     srcs = [torch.randn(N, H, W_, c, generator=g).to(DEV, dt) for c in parts]
     Wt = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
@@ -202,7 +205,8 @@ def test_tap64p_halo_matches(mode, grid):
             outs = [torch.zeros(N, H, W_, 128, dtype=dt, device=DEV), torch.zeros(N, H, W_, nout - 128, dtype=dt, device=DEV)]
             kw.update(out_mode=2, out2=outs[1], split_c=128)
         st = torch.zeros(2, nout, device=DEV)
-        ops.set_option("fwd_tap64", 2)   # the 256x256 configuration
+        ops.set_option("fwd_tap64", 2 if tile == 256 else 3)   # the 256x256 / 256x128 configuration
+        ops.set_option("fwd_halo", 0)   # (the <= 128-output halo kernels would take the narrow shapes)
         ops.set_option("tap64p_halo", halo)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
@@ -211,9 +215,10 @@ def test_tap64p_halo_matches(mode, grid):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("fwd_tap64", "tap64p_halo", "tap64_persist_grid"):
+            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid"):
                 ops.set_option(o_, None)
-        assert kname == "igemm_fwd_tap64p_kernel<256, 256, 2, false, %s>" % ("true" if halo else "false"), kname
+        assert kname == "igemm_fwd_tap64p_kernel<256, %d, %d, false, %s>" % (
+            tile, 2 if tile == 256 else 3, "true" if halo else "false"), kname
         res.append((torch.cat(outs, -1).double(), st.double()))
     (yh, sh_), (yg, sg) = res
     assert (yh - ref).abs().max().item() < 0.02 * ref.abs().max().item()
