@@ -428,7 +428,7 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
 // thread's channel group is fixed, so its constants are 8 LDS words each) and -- blocks of input chunk 0
 // only -- stores dY for the data-gradient launch; the halo groups follow at rows BNA_ROW..7. No barrier
 // and no long-lived registers: every thread reads back only the LDS slots its own DMA wrote.
-template <int NW, bool BNA = false>
+template <int NW, bool BNA = false, int SPR = 8>
 __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs a) {
   constexpr int NTH = NW * 64, RB = 128;
   constexpr int PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
@@ -525,6 +525,10 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
 #pragma unroll
         for (int i = 0; i < GD; ++i)
           if (i / (GD / 2) == pr) issue_d(P, i, buf);
+      } else if (SPR != PH && pr >= BNA_ROW) {   // two halo groups a row from BNA_ROW on
+#pragma unroll
+        for (int gi = 0; gi < GH; ++gi)
+          if (gi / 2 == pr - BNA_ROW) issue_h(P, gi, buf);
       } else if (pr >= BNA_ROW) {
         const int r = pr - BNA_ROW;
         const int g0 = r < EXTRA ? 2 * r : EXTRA + r;
@@ -535,15 +539,26 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
       }
       return;
     }
-    constexpr int NG = GH + GD, EXTRA = NG - PH;   // rows 0 .. EXTRA-1 take two groups
-    const int g0 = pr < EXTRA ? 2 * pr : EXTRA + pr;
-    const int g1 = pr < EXTRA ? g0 + 1 : -1;
+    constexpr int NG = GH + GD;
+    if constexpr (SPR == PH) {   // over all 8 rows: rows 0 .. EXTRA-1 take two groups
+      constexpr int EXTRA = NG - PH;
+      const int g0 = pr < EXTRA ? 2 * pr : EXTRA + pr;
+      const int g1 = pr < EXTRA ? g0 + 1 : -1;
 #pragma unroll
-    for (int gi = 0; gi < NG; ++gi)
-      if (gi == g0 || gi == g1) {
-        if (gi < GH) issue_h(P, gi, buf);
-        else issue_d(P, gi - GH, buf);
-      }
+      for (int gi = 0; gi < NG; ++gi)
+        if (gi == g0 || gi == g1) {
+          if (gi < GH) issue_h(P, gi, buf);
+          else issue_d(P, gi - GH, buf);
+        }
+    } else {   // over rows 0 .. SPR-1, ceil(NG / SPR) groups a row: the last rows give the DMA slack
+      constexpr int PER = (NG + SPR - 1) / SPR;
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi)
+        if (gi / PER == pr) {
+          if (gi < GH) issue_h(P, gi, buf);
+          else issue_d(P, gi - GH, buf);
+        }
+    }
   };
   // transposed 16x32 fragment of an [row][64 bf16] LDS image whose rows row0 .. row0+31 are the 32
   // pixels of one k step (absolute rows, so the row swizzle matches the one applied on load)
@@ -971,14 +986,27 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     const int grid = per * combos;
     a.debug_flags = option("wgrad_debug", 0);
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
-      adp::set_kernel("igemm_wgrad_halop_kernel<8, true>");
-      hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true>), dim3(grid), dim3(512), 0, s, a);
+      if (option("wgrad_halop_spread", 4) == 8) {
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8>");
+        hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 8>), dim3(grid), dim3(512), 0, s, a);
+      } else {   // halo groups two a row over rows 3-5
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4>");
+        hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 4>), dim3(grid), dim3(512), 0, s, a);
+      }
     } else if (option("wgrad_halop_waves", 8) == 9) {
       adp::set_kernel("igemm_wgrad_halop_kernel<9, false>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
     } else {
-      adp::set_kernel("igemm_wgrad_halop_kernel<8, false>");
-      hipLaunchKernelGGL(igemm_wgrad_halop_kernel<8>, dim3(grid), dim3(512), 0, s, a);
+      // the next patch's loads over rows 0-3 (3 groups a row) leave 4 rows of DMA slack before the patch
+      // barrier: +1-3 % on every level but 0 64->64 against rows 0-7, step -0.3 %
+      // (profiles/r02_wgrad_spread_ab.txt); option wgrad_halop_spread=8 keeps the all-rows schedule
+      if (option("wgrad_halop_spread", 4) == 8) {
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 8>");
+        hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 8>), dim3(grid), dim3(512), 0, s, a);
+      } else {
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4>");
+        hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4>), dim3(grid), dim3(512), 0, s, a);
+      }
     }
     return 1;
   }
