@@ -76,6 +76,7 @@ _SIGS = {
     "adp_ew_add_mask": [_I, _S, _P, _P, _P, _F, _P, _P],
     "adp_cast": [_I, _I, _S, _P, _P, _P],
     "adp_fill_f32": [_S, _F, _P, _P],
+    "adp_sum_bf16": [_I, _P, _S, _P, _P],
     "adp_bn_finalize": [_I, _F, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P],
     "adp_bn_finalize_fold": [_I, _F, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P],
     "adp_bn_apply": [_I, _S, _I, _P, _P, _P, _P, _P],

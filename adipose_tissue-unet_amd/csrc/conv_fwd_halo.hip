@@ -310,13 +310,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     const int idx = i * NTH + tid;
     const int cc = NCH == 1 ? 0 : (idx >= HROWS * 8 ? 1 : 0), hr = (idx - cc * HROWS * 8) >> 3;
     const int hy = hr / HW, hx = hr - hy * HW;
-    const int gy = y0 + hy - 1, gx = x0 + hx - 1;
-    const bool ok = (i < GH - 1 || idx < HCH) && (unsigned)gy < (unsigned)a.Hs && (unsigned)gx < (unsigned)a.Ws;
+    // (gy, gx) in the conv's input grid = the source upsampled x a.up (nearest: source (gy >> 1, gx >> 1))
+    const int gy = y0 + hy - 1, gx = x0 + hx - 1, us = a.up >> 1;
+    const bool ok = (i < GH - 1 || idx < HCH) && (unsigned)gy < (unsigned)(a.Hs << us) && (unsigned)gx < (unsigned)(a.Ws << us);
     if (!ok) return nullptr;
     const bool inA = cc * 64 < a.CAs;
     const bf16* src = reinterpret_cast<const bf16*>(inA ? a.srcA : a.srcB);
     const int cs = inA ? a.CAs : a.CBs;
-    return reinterpret_cast<const uint4*>(src + (size_t)((img * a.Hs + gy) * a.Ws + gx) * cs +
+    return reinterpret_cast<const uint4*>(src + (size_t)((img * a.Hs + (gy >> us)) * a.Ws + (gx >> us)) * cs +
                                           (inA ? cc * 64 : cc * 64 - a.CAs) + 8 * ((tid & 7) ^ hswz(hr)));
   };
 
@@ -559,8 +560,9 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   const int mode = option("fwd_halo", 1);   // 0 off, 1 auto, 2 = no single-buffer form (A/B)
   if (mode == 0) return 0;
   const int Cin_s = a.CAs + a.CBs;
-  if (a.scA || a.scB || a.kh != 3 || a.kw != 3 || a.dil != 1 || a.pad != 1 || a.stride != 1 || a.up != 1 ||
-      a.Ho != a.Hs || a.Wo != a.Ws || a.Ho % PH != 0 || a.Wo % PW != 0 || a.CAs % 64 != 0 || a.CBs % 64 != 0 ||
+  // up = 2 (nearest upsample folded into the gather): the persistent forms only
+  if (a.scA || a.scB || a.kh != 3 || a.kw != 3 || a.dil != 1 || a.pad != 1 || a.stride != 1 || (a.up != 1 && a.up != 2) ||
+      a.Ho != a.Hs * a.up || a.Wo != a.Ws * a.up || a.Ho % PH != 0 || a.Wo % PW != 0 || a.CAs % 64 != 0 || a.CBs % 64 != 0 ||
       a.K != 9 * Cin_s || a.Kpad != a.K || a.Nout > 128)
     return 0;
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
@@ -577,7 +579,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   const size_t lim = (size_t)1 << 31;   // the persistent form stores / reads z through buffer resources
   const bool fits = (size_t)a.M * a.out_stride * 2 < lim && (!a.out2 || (size_t)a.M * a.out2_stride * 2 < lim) &&
                     (!a.bnr_z || (size_t)a.M * a.bnr_zs * 2 < lim);
-  if (bn && plain && fits && (a.out_mode == 0 || split_ok) && option("halo_persist", 1)) {
+  if (bn && plain && fits && (a.out_mode == 0 || split_ok) && option("halo_persist", 1) && (a.up == 1 || !a.bnr_z)) {
     const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * nt_n;
     a.ntile_n = nt_n;
     a.nblocks = tiles;   // the persistent kernel reads the tile count from nblocks
@@ -620,6 +622,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   // profiles/r02_tap64p_halo_ab.txt)
   if (a.Nout == 128 && Cin_s > 128 && !a.bnr_z && plain && a.out_mode != 1 && option("halo_defer_tap64p", 1))
     return 0;
+  if (a.up != 1) return 0;   // (the non-persistent halo kernels gather at the source resolution)
   if (a.Nout <= 64) {
     if (one_chunk && mode != 2) launch_halo<1, 2, 1, 1>(a, s);   // two blocks per CU
     else launch_halo<1, 2, 2, 2>(a, s);

@@ -242,12 +242,16 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     if (idx < P_HROWS * 8) {
       const PatchO P = patch_of(k);
       const int hr = idx >> 3, hp = idx & 7;
+      // (yi, xi) in the conv's input grid, which is the source upsampled x up (nearest: source pixel
+      // (yi >> 1, xi >> 1) for up = 2, the UpSampling2D of train_adipose_unet_v3.py:691 folded in)
       const int yi = P.y0 - 1 + hr / 34, xi = P.x0 - 1 + hr % 34;
       const int ci = c * 64;
       const bool srcb = ci >= a.CAs;
       const int cs = (srcb ? a.CBs : a.CAs) * ES, cb = (srcb ? ci - a.CAs : ci) * ES;
-      const bool v = (unsigned)yi < (unsigned)a.Hs && (unsigned)xi < (unsigned)a.Ws;
-      const unsigned off = v ? (unsigned)(((P.img * a.Hs + yi) * a.Ws + xi) * cs + cb + 16 * (hp ^ p_hswz(hr))) : P_OOB;
+      const bool v = (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
+      const int us = a.up >> 1;
+      const unsigned off =
+          v ? (unsigned)(((P.img * a.Hs + (yi >> us)) * a.Ws + (xi >> us)) * cs + cb + 16 * (hp ^ p_hswz(hr))) : P_OOB;
       p_lds16(srcb ? rsB : rsA, smem + OH + slot * HBUF + (size_t)(g * NTH + wave * 64) * 16, off);
     }
     return true;
@@ -602,7 +606,7 @@ namespace adp {
 int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   if (!option("tap64_persist", 1) || a.f8 || a.K < 128) return 0;   // (two K steps at least)
   if (a.addend || a.mask || a.mask2 || a.accum || a.drop_rate > 0.f || a.scA || a.scB) return 0;
-  if (a.up != 1) return 0;
+  if (a.up != 1 && (a.up != 2 || a.bnr_z)) return 0;   // up = 2: the halo form only (below)
   if (a.out_mode == 1 && (a.Cps % 8 != 0 || a.Nout % a.Cps != 0)) return 0;
   if (a.out_mode == 2 && (a.split_c % 16 != 0 || a.out2_stride % 8 != 0)) return 0;
   if (a.out_stride % 8 != 0 || (a.bnr_z && a.bnr_zs % 8 != 0)) return 0;
@@ -636,8 +640,9 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   const bool bnr = a.bnr_z != nullptr;
   // the halo form (option tap64p_halo): 3x3 stride-1 'same' layers whose output tiles into 8 x 32 patches
   const bool halo_shape = !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&
-                          a.dil == 1 && a.pad == 1 && a.stride == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 &&
-                          a.Wo % 32 == 0;
+                          a.dil == 1 && a.pad == 1 && a.stride == 1 && a.Ho == a.Hs * a.up && a.Wo == a.Ws * a.up &&
+                          a.Ho % 8 == 0 && a.Wo % 32 == 0;
+  if (a.up != 1 && !(halo_shape && (cfg == 1 || (cfg == 2 && option("tap64p_halo128", 1))))) return 0;
   if (halo_shape && cfg == 1) {
     adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);

@@ -364,6 +364,26 @@ __global__ void cast_kernel(size_t n, const Ti* src, To* dst) {
     dst[i] = from_f<To>(to_f(src[i]));
 }
 
+// out = bf16(sum_k src_k) over 8-element groups, the f32 sum taken in source order from 0: the value
+// an f32 accumulator zeroed and then accumulated by each producer's epilogue (the bf16-rounded value
+// it stored) holds, rounded once (the dilated bottleneck's Add, train_adipose_unet_v3.py:688)
+struct SumSrcs { const bf16* p[8]; };
+__global__ void sum_bf16_kernel(size_t g, int nsrc, SumSrcs S, bf16* out) {
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < g; i += (size_t)gridDim.x * TPB) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, f[8];
+    for (int k = 0; k < nsrc; ++k) {
+      Grp<bf16> gr;
+      grp_load(gr, S.p[k] + i * 8);
+      grp_to_f(gr, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    Grp<bf16> go;
+    grp_from_f(go, acc);
+    grp_store(go, out + i * 8);
+  }
+}
+
 __global__ void fill_kernel(size_t n, float v, float* dst) {
   for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) dst[i] = v;
 }
@@ -991,6 +1011,21 @@ extern "C" int adp_cast(int di, int dout, size_t n, const void* src, void* dst, 
     hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(nblk(n)), dim3(TPB), 0, s, n, (const bf16*)src, (bf16*)dst);
   else { adp::set_error("adp_cast: bad dtype"); return -1; }
   return adp::check_launch("adp_cast");
+}
+
+extern "C" int adp_sum_bf16(int nsrc, const void* const* srcs, size_t n, void* out, adp_stream_t st) {
+  if (nsrc < 1 || nsrc > 8 || n % 8 != 0 || !srcs || !out) {
+    adp::set_error("adp_sum_bf16: 1..8 sources, n a multiple of 8");
+    return -1;
+  }
+  SumSrcs S{};
+  for (int k = 0; k < nsrc; ++k) {
+    if (!srcs[k] || (reinterpret_cast<uintptr_t>(srcs[k]) & 15)) { adp::set_error("adp_sum_bf16: source not 16-B aligned"); return -1; }
+    S.p[k] = (const bf16*)srcs[k];
+  }
+  const size_t g = n / 8;
+  hipLaunchKernelGGL(sum_bf16_kernel, dim3(nblk(g)), dim3(TPB), 0, (hipStream_t)st, g, nsrc, S, (bf16*)out);
+  return adp::check_launch("adp_sum_bf16");
 }
 
 extern "C" int adp_fill_f32(size_t n, float v, float* dst, adp_stream_t st) {

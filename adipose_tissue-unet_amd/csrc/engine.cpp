@@ -460,16 +460,21 @@ struct adp_handle {
     CL(conv("down3_conv1", N, b("p2"), sz[2], nullptr, b("d3a"), nullptr, s));
     CL(conv("down3_conv2", N, b("d3a"), sz[2], nullptr, b("d3"), nullptr, s));
     CL(adp_maxpool2_fwd(dt, N, sz[2], sz[2], ch[2], b("d3"), nullptr, nullptr, b("p3"), s));
+    // the bottleneck Add: f32 accumulates in the dilated convs' epilogues; bf16 sums the six stored maps
+    // in one pass (adp_sum_bf16: the same f32 sum, rounded once; keeps the convs on the persistent kernel)
     const size_t nsum = (size_t)N * sz[3] * sz[3] * ch[3];
-    CL(adp_fill_f32(nsum, 0.f, b<float>("dsum_f"), s));
+    const bool f32 = dt == ADP_DTYPE_F32;
+    if (f32) CL(adp_fill_f32(nsum, 0.f, b<float>("dsum_f"), s));
     const char* dl[6] = {"dl1", "dl2", "dl3", "dl4", "dl5", "dl6"};
     const char* dn[6] = {"dilate1", "dilate2", "dilate3", "dilate4", "dilate5", "dilate6"};
     for (int i = 0; i < 6; ++i)
-      CL(conv(dn[i], N, i ? b(dl[i - 1]) : b("p3"), sz[3], nullptr, b(dl[i]), b<float>("dsum_f"), s,
+      CL(conv(dn[i], N, i ? b(dl[i - 1]) : b("p3"), sz[3], nullptr, b(dl[i]), f32 ? b<float>("dsum_f") : nullptr, s,
               i == 0 ? r : 0.f, sd + 1));
-    void* dsum = b("dsum_f");
-    if (dt != ADP_DTYPE_F32) {
-      CL(adp_cast(ADP_DTYPE_F32, dt, nsum, b("dsum_f"), b("dsum"), s));
+    void* dsum = f32 ? b("dsum_f") : nullptr;
+    if (!f32) {
+      const void* maps[6];
+      for (int i = 0; i < 6; ++i) maps[i] = b(dl[i]);
+      CL(adp_sum_bf16(6, maps, nsum, b("dsum"), s));
       dsum = b("dsum");
     }
     CL(conv("up3_conv1", N, dsum, sz[3], nullptr, b("u3a"), nullptr, s));
@@ -678,7 +683,7 @@ extern "C" int adp_create(const adp_config* cfg, int device, adp_handle** out) {
     rc = rc || act(per_level[l][0], l, l) || act(per_level[l][1], l, l) || act(per_level[l][2], l + 1, l);
   }
   for (int i = 1; i <= 6 && !rc; ++i) rc = act(("dl" + std::to_string(i)).c_str(), 3, 3);
-  if (!rc) rc = h->alloc("dsum_f", B * h->sz[3] * h->sz[3] * h->ch[3] * 4);
+  if (!rc && cfg->dtype == ADP_DTYPE_F32) rc = h->alloc("dsum_f", B * h->sz[3] * h->sz[3] * h->ch[3] * 4);
   if (!rc && cfg->dtype != ADP_DTYPE_F32) rc = act("dsum", 3, 3);
   const char* ups[3][3] = {{"u3a", "u3b", "u3"}, {"u2a", "u2b", "u2"}, {"u1a", "u1b", "u1"}};
   for (int u = 0; u < 3 && !rc; ++u)

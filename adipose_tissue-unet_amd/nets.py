@@ -420,7 +420,8 @@ class AdiposeV3Net(UNetEngine):
         # the generic LDS-DMA kernels. f32 (parity) uses 8 everywhere.
         if cpad is None:
             cpad = 64 if dtype == "bf16" else 8
-        self.cpad = tuple(cpad) if isinstance(cpad, (tuple, list)) else (int(cpad),) * 4
+        cpad = tuple(cpad) if isinstance(cpad, (tuple, list)) else (int(cpad),)
+        self.cpad = cpad * 4 if len(cpad) == 1 else cpad   # one granule: every level
         assert size % 8 == 0, "adipose_v3 needs S % 8 == 0 (3 poolings)"
         super().__init__(batch, size, dtype=dtype, device=device, seed=seed)
 
@@ -472,8 +473,7 @@ class AdiposeV3Net(UNetEngine):
         a["p3"] = self.buf("p3", (B, s[3], s[3], c[2]))
         for i in range(1, 7):
             a[f"dl{i}"] = self.buf(f"dl{i}", (B, s[3], s[3], c[3]))
-        a["dsum_f"] = self.buf("dsum_f", (B, s[3], s[3], c[3]), torch.float32)
-        a["dsum"] = a["dsum_f"] if self.dt == torch.float32 else self.buf("dsum", (B, s[3], s[3], c[3]))
+        a["dsum"] = self.buf("dsum", (B, s[3], s[3], c[3]))   # f32 networks: the accumulator itself
         for lvl, (sz, cc) in zip((3, 2, 1), ((s[2], c[2]), (s[1], c[1]), (s[0], c[0]))):
             for j in ("a", "b", ""):
                 a[f"u{lvl}{j}"] = self.buf(f"u{lvl}{j}", (B, sz, sz, cc))
@@ -503,12 +503,18 @@ class AdiposeV3Net(UNetEngine):
         self.conv(L["down3_conv1"], a["p2"], a["d3a"])
         self.conv(L["down3_conv2"], a["d3a"], a["d3"])
         ops.maxpool2_fwd(a["d3"], a["p3"])
-        self.zero(a["dsum_f"])
-        self.conv(L["dilate1"], a["p3"], a["dl1"], dropout=r, seed=sd + 1, accum=a["dsum_f"])
+        # the Add of the six dilated outputs: f32 networks accumulate in the convs' epilogues; bf16 ones sum
+        # the six stored maps in one pass (the same f32 sum of the same bf16 values, rounded once), which
+        # keeps the dilated convs on the persistent kernel (no read-modify-write epilogue) and moves
+        # 7 x 4 bytes per element less than accumulate + cast
+        acc = a["dsum"] if self.dt == torch.float32 else None
+        if acc is not None:
+            self.zero(acc)
+        self.conv(L["dilate1"], a["p3"], a["dl1"], dropout=r, seed=sd + 1, accum=acc)
         for i in range(2, 7):
-            self.conv(L[f"dilate{i}"], a[f"dl{i - 1}"], a[f"dl{i}"], accum=a["dsum_f"])
-        if self.dt != torch.float32:
-            ops.cast(a["dsum_f"], a["dsum"])
+            self.conv(L[f"dilate{i}"], a[f"dl{i - 1}"], a[f"dl{i}"], accum=acc)
+        if acc is None:
+            ops.sum_bf16([a[f"dl{i}"] for i in range(1, 7)], a["dsum"])
         self.conv(L["up3_conv1"], a["dsum"], a["u3a"])
         self.conv(L["up3_conv2"], a["d3"], a["u3b"], srcB=a["u3a"])
         self.conv(L["up3_conv3"], a["u3b"], a["u3"], dropout=r, seed=sd + 2)

@@ -410,6 +410,17 @@ def cast(src, dst):
     return dst
 
 
+def sum_bf16(srcs, out):
+    """out = bf16(sum(srcs)) (f32 sum in list order): adp_sum_bf16."""
+    import ctypes
+    _check(1 <= len(srcs) <= 8, "sum_bf16: 1..8 sources")
+    _check(out.dtype == torch.bfloat16 and all(t.dtype == torch.bfloat16 and t.shape == out.shape and t.is_contiguous()
+                                                for t in srcs), "sum_bf16: same-shape contiguous bf16 maps")
+    arr = (ctypes.c_void_p * len(srcs))(*[ptr(t) for t in srcs])
+    call("adp_sum_bf16", len(srcs), ctypes.cast(arr, ctypes.c_void_p).value, out.numel(), ptr(out), stream_ptr())
+    return out
+
+
 def fill(dst, value):
     _check(dst.dtype == torch.float32, "fill is f32")
     call("adp_fill_f32", dst.numel(), float(value), ptr(dst), stream_ptr())

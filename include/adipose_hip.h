@@ -183,6 +183,10 @@ int adp_ew_add_mask(int dtype, size_t n, const void* a, const void* b, const voi
                     float mask_scale, void* out, adp_stream_t s);
 int adp_cast(int dtype_in, int dtype_out, size_t n, const void* src, void* dst, adp_stream_t s);
 int adp_fill_f32(size_t n, float value, float* dst, adp_stream_t s);
+/* out = bf16(sum of nsrc (1..8) bf16 maps of n elements, f32 sum in source order): the dilated
+   bottleneck's Add (train_adipose_unet_v3.py:688) as one pass after its six convs; n % 8 == 0, srcs is a
+   host array of 16-B aligned device pointers */
+int adp_sum_bf16(int nsrc, const void* const* srcs, size_t n, void* out, adp_stream_t s);
 
 /* ---- BatchNorm (unet_bn preset; training-mode batch statistics) -------------------------- */
 int adp_bn_finalize(int C, float count, const float* sum, const float* sqsum, const float* gamma,

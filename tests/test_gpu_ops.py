@@ -228,9 +228,57 @@ def test_tap64p_halo_matches(mode, grid, tile):
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
 
 
+@pytest.mark.parametrize("form", ["halop_1ch", "halop_2ch", "tap64p_256", "tap64p_128"])
+@pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
+def test_upsample_gather_halo_forms(form, grid):
+    """Nearest-x2 upsample folded into the halo gathers of the persistent forward kernels (adipose_v3's
+    UpSampling2D + 3x3 conv, train_adipose_unet_v3.py:691-692): halop (one / two 64-channel chunks) and the
+    256x256 / 256x128 halo forms of tap64p, vs a float64 convolution of the upsampled bf16 operands and
+    vs the non-persistent tap64 kernel's gather (different f32 summation order: within bf16 rounding);
+    BatchNorm sums to 1e-4."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(13)
+    N, Hs, Ws = 2, 16, 32
+    cin, nout, kern = {"halop_1ch": (64, 64, "igemm_fwd_halop_kernel<false, 1, 64"),
+                       "halop_2ch": (128, 64, "igemm_fwd_halop_kernel<false, 2, 32"),
+                       "tap64p_256": (128, 256, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true>"),
+                       "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true>")}[form]
+    x = torch.randn(N, Hs, Ws, cin, generator=g).to(DEV, dt)
+    Wt = (torch.randn(nout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV)
+    xu = x.double().repeat_interleave(2, 1).repeat_interleave(2, 2).permute(0, 3, 1, 2)
+    wk = Wt.double().view(nout, 3, 3, cin).permute(0, 3, 1, 2)
+    ref = (F.conv2d(xu, wk, padding=1).permute(0, 2, 3, 1) + bias.double()).clamp_min(0.0)
+    res = []
+    for persist in (1, 0):
+        out = torch.zeros(N, 2 * Hs, 2 * Ws, nout, dtype=dt, device=DEV)
+        st = torch.zeros(2, nout, device=DEV)
+        opts = {"halo_persist": persist, "tap64_persist": persist}
+        if form.startswith("tap64p"):   # the 256x256 / 256x128 configuration (small M picks narrow tiles)
+            opts.update(fwd_halo=0, fwd_tap64=2 if form == "tap64p_256" else 3)
+        if grid:
+            opts.update(tap64_persist_grid=grid, halo_persist_grid=grid)
+        for k_, v_ in opts.items():
+            ops.set_option(k_, v_)
+        try:
+            ops.conv_fwd(x, Wt, nout, out=out, bias=bias, relu=True, up=True, bn_stats=(st[0], st[1]))
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for k_ in opts:
+                ops.set_option(k_, None)
+        res.append((out.double(), st.double(), kname))
+    (yp, sp, kp), (yn, sn, kn) = res
+    assert kp.startswith(kern), kp
+    assert not kn.startswith("igemm_fwd_halop") and not kn.startswith("igemm_fwd_tap64p"), kn
+    assert (yp - ref).abs().max().item() < 0.02 * ref.abs().max().item()
+    assert (yp - yn).abs().max().item() <= 0.01 * ref.abs().max().item()
+    torch.testing.assert_close(sp, sn, rtol=1e-4, atol=1e-2)
+
+
 @pytest.mark.parametrize("cfg", [1, 2, 3], ids=["256x256x2", "256x128x3", "128x256x3"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
-@pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad", "bnr"])
+@pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad", "bnr", "dilated"])
 def test_tap64_persistent_matches(mode, grid, cfg):
     """Persistent tap64 kernel (conv_fwd_tap64p.hip: one K-step stream over the block's tiles through an
     NST-stage LDS ring, register epilogue with 8-B buffer stores) in its three tile / ring forms vs the
@@ -242,11 +290,11 @@ def test_tap64_persistent_matches(mode, grid, cfg):
     g = torch.Generator().manual_seed(11)
     kw = {}
     bnr = None
-    if mode in ("plain", "concat", "split", "bnr"):
+    if mode in ("plain", "concat", "split", "bnr", "dilated"):
         N, S = 2, 23
-        parts = [128] if mode in ("plain", "bnr") else [64, 128]
+        parts = [128] if mode in ("plain", "bnr", "dilated") else [64, 128]
         cin = sum(parts)
-        nout = 320 if mode in ("plain", "bnr") else 256
+        nout = 320 if mode in ("plain", "bnr", "dilated") else 256
         srcs = [torch.randn(N, S, S, c, generator=g).to(DEV, dt) for c in parts]
         W = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
         args = (srcs[0], W, nout)
@@ -260,8 +308,10 @@ def test_tap64_persistent_matches(mode, grid, cfg):
             z = torch.randn(N, S, S, nout, generator=g).to(DEV, dt)
             vec = [(torch.rand(nout, generator=g) + 0.5).to(DEV) for _ in range(4)]
             bnr = (z, vec[0], vec[1] - 1.0, vec[2] - 1.0, vec[3])
-        else:
-            kw.update(bias=torch.randn(nout, generator=g).to(DEV), relu=mode == "plain")
+        else:   # dilated: the adipose_v3 bottleneck's 'same' 3x3 with dilation 4 (gather form, not halo)
+            kw.update(bias=torch.randn(nout, generator=g).to(DEV), relu=mode in ("plain", "dilated"))
+            if mode == "dilated":
+                kw.update(dil=4, pad=4)
         stats_c = nout
     elif mode == "convt_shuffle":   # ConvTranspose 2x2/s2 forward: 1x1 GEMM + pixel-shuffle store
         N, S, cin, cs = 2, 19, 128, 64
@@ -569,7 +619,7 @@ def test_wgrad_bn_apply_fused(N, H, W, parts, cout, dtn, fused):
     ops.conv_wgrad(xs[0], dz2, dW2, cout, srcB=srcB, bn_apply=(dA, z, sc, sh, mu, ist, gam, dg, db, count))
     kname = _lib.lib().adp_last_kernel().decode()
     torch.cuda.synchronize()
-    assert (kname == "igemm_wgrad_halop_kernel<8, true>") == fused, kname
+    assert kname.startswith("igemm_wgrad_halop_kernel<8, true") == fused, kname
     assert torch.equal(dz1, dz2)
     assert relerr(dW2.cpu(), dW1.cpu()) < 1e-5
 
@@ -598,6 +648,10 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.conv_wgrad(xd[0], dzd, dW, l.Nout, srcB=srcB)
         assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_halop_kernel")
         torch.cuda.synchronize()
+        ops.set_option("wgrad_halop_spread", 8)   # next patch's loads over all 8 patch rows
+        dWs = torch.zeros_like(dW)
+        ops.conv_wgrad(xd[0], dzd, dWs, l.Nout, srcB=srcB)
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 8>"
         ops.set_option("wgrad_halop_waves", 9)   # one wave per tap
         dW9 = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dW9, l.Nout, srcB=srcB)
@@ -608,8 +662,10 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     finally:
         ops.set_option("wgrad_halop", None)
         ops.set_option("wgrad_halop_waves", None)
+        ops.set_option("wgrad_halop_spread", None)
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
     assert relerr(dW.cpu(), ref.cpu()) < 1e-4 and relerr(dW9.cpu(), ref.cpu()) < 1e-4
+    assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
 
 @pytest.mark.parametrize("dt", DTS)
@@ -647,6 +703,23 @@ def test_conv_transpose(dt, S):
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < tol
     assert relerr(dB, br.grad) < tol
     assert relerr(dX, xr.grad) < tol
+
+
+def test_sum_bf16_matches_accumulate():
+    """adp_sum_bf16 (the bottleneck Add as one pass) == an f32 accumulator zeroed, += each bf16 map in
+    order, cast to bf16 (the accumulate-epilogue path): bit for bit."""
+    g = torch.Generator().manual_seed(5)
+    maps = [(torch.randn(2, 16, 16, 384, generator=g) * (k + 1)).to(DEV, torch.bfloat16) for k in range(6)]
+    acc = torch.zeros(maps[0].shape, device=DEV)
+    for m in maps:
+        acc += m.float()
+    out = torch.full_like(maps[0], 7.0)
+    ops.sum_bf16(maps, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, acc.to(torch.bfloat16))
+    one = torch.empty_like(out)
+    ops.sum_bf16(maps[:1], one)
+    assert torch.equal(one, maps[0])
 
 
 @pytest.mark.parametrize("dt", DTS)
