@@ -357,6 +357,11 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
       a.Kpad != a.K)
     return 0;
   int cfg = mode - 2;
+  // fp8: the persistent halo forms first (256x256 when a 256-wide N tile is at least 3/4 used, else 256x128)
+  if (a.f8 && (mode == 1 || cfg == 0 || cfg == 1)) {
+    const int t = mode == 1 ? ((a.Nout % 256 == 0 || (a.Nout > 256 && a.Nout % 256 >= 192)) ? 0 : 1) : cfg;
+    if (launch_fwd_tap64p(a, s, t)) return 1;
+  }
   if (a.f8 && cfg != 1 && cfg != 3) mode = 1;
   if (mode == 1) {
     // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency

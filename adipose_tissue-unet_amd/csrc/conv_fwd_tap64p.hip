@@ -22,6 +22,7 @@ constexpr unsigned P_OOB = 0x80000000u;   // buffer offset beyond every resource
 constexpr int P_RSRC3 = 0x00020000;       // raw buffer descriptor word 3 (gfx9: 32-bit data format)
 typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef int v8i32 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void p_lds16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
@@ -76,9 +77,15 @@ constexpr int tap64p_lds() {
 }
 __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_halo.hip: conflict-free)
 
-template <int BM, int BN, int NST, bool BNR, bool HALO = false>
+// F8 (halo form, fp8 e4m3 operands, BASELINE configs[4]): the same byte schedule with 128-channel K steps
+// (a 128-B row is 128 fp8 channels); the two 16-B fragments a lane reads per row are one 32-B operand of
+// v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales; A and B share the permutation of K), and the
+// epilogue multiplies by the per-column weight scale; bf16 output, plain store, no BatchNorm sums.
+template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
-  constexpr int NTH = 512, ROWB = 128, ES = 2, KSTEP = 64;
+  static_assert(!F8 || !BNR, "fp8: no BN-backward reduction");
+  constexpr int NTH = 512, ROWB = 128, ES = F8 ? 1 : 2, KSTEP = F8 ? 128 : 64;
+  constexpr int OES = 2;   // output / z element bytes (bf16)
   constexpr int WN = BN / 64, WM = 8 / WN, TM = BM / WM;
   static_assert(WN * WM == 8 && TM % 32 == 0 && TM >= 64, "wave layout");
   static_assert(!HALO || (!BNR && BM == 256 && ((BN == 256 && NST == 2) || (BN == 128 && NST == 3))),
@@ -125,7 +132,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     const int n = n0 + tid;
     const bool v = n < a.Nout;
     cst[0][tid] = (!BNR && a.bias && v) ? a.bias[a.out_mode == 1 ? n % a.Cps : n] : 0.f;
-    cst[1][tid] = (BNR && v) ? a.bnr_sc[n] : 0.f;
+    cst[1][tid] = (BNR && v) ? a.bnr_sc[n] : (F8 && v) ? a.wscale[n] : 0.f;
     cst[2][tid] = (BNR && v) ? a.bnr_sh[n] : 0.f;
     cst[3][tid] = (BNR && v) ? a.bnr_mean[n] : 0.f;
     cst[4][tid] = (BNR && v) ? a.bnr_invstd[n] : 0.f;
@@ -235,7 +242,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   int nissued = 0;
   // HALO: one 16-B group g of the halo of chunk c of tile k into slot `slot`; returns whether this wave
   // issued an instruction (the last group covers 160 of 512 threads: waves 3-7 skip it)
-  const int nch = Cin_s / 64;
+  const int nch = Cin_s / KSTEP;
   auto issue_halo = [&](int k, int c, int g, int slot) {
     const int idx = g * NTH + tid;
     if (g == GH - 1 && __builtin_amdgcn_readfirstlane(g * NTH + wave * 64) >= P_HROWS * 8) return false;
@@ -245,13 +252,13 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       // (yi, xi) in the conv's input grid, which is the source upsampled x up (nearest: source pixel
       // (yi >> 1, xi >> 1) for up = 2, the UpSampling2D of train_adipose_unet_v3.py:691 folded in)
       const int yi = P.y0 - 1 + hr / 34, xi = P.x0 - 1 + hr % 34;
-      const int ci = c * 64;
+      const int ci = c * KSTEP;
       const bool srcb = ci >= a.CAs;
       const int cs = (srcb ? a.CBs : a.CAs) * ES, cb = (srcb ? ci - a.CAs : ci) * ES;
-      const bool v = (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
-      const int us = a.up >> 1;
-      const unsigned off =
-          v ? (unsigned)(((P.img * a.Hs + (yi >> us)) * a.Ws + (xi >> us)) * cs + cb + 16 * (hp ^ p_hswz(hr))) : P_OOB;
+      // (bounds on the source coordinates: an arithmetic shift keeps -1 negative)
+      const int sy = yi >> (a.up >> 1), sx = xi >> (a.up >> 1);
+      const bool v = (unsigned)sy < (unsigned)a.Hs && (unsigned)sx < (unsigned)a.Ws;
+      const unsigned off = v ? (unsigned)(((P.img * a.Hs + sy) * a.Ws + sx) * cs + cb + 16 * (hp ^ p_hswz(hr))) : P_OOB;
       p_lds16(srcb ? rsB : rsA, smem + OH + slot * HBUF + (size_t)(g * NTH + wave * 64) * 16, off);
     }
     return true;
@@ -341,6 +348,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   f32x4 acc[2 * MIQ][4];
   auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
+#pragma unroll
+      for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[ha * MIQ + mi][hb * 2 + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              __builtin_bit_cast(v8i32, fb[ni]), __builtin_bit_cast(v8i32, fa[mi]), acc[ha * MIQ + mi][hb * 2 + ni],
+              0, 0, 0, 127, 0, 127);
+      __builtin_amdgcn_s_setprio(0);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -355,10 +373,12 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // ---- epilogue resources
   const bool shuffle = a.out_mode == 1, split = a.out_mode == 2;
   const int Hq = 2 * a.Ho, Wq = 2 * a.Wo;
-  const unsigned out_bytes = shuffle ? (unsigned)(a.Nimg * Hq * Wq) * a.out_stride * ES : (unsigned)a.M * a.out_stride * ES;
-  const int out2_bytes = split ? a.M * a.out2_stride * ES : 0;
+  const bool o8 = F8 && a.out_f8;   // fp8 output (the ConvTranspose forwards of UNetBN.forward_fp8)
+  const int oes = o8 ? 1 : OES;
+  const unsigned out_bytes = shuffle ? (unsigned)(a.Nimg * Hq * Wq) * a.out_stride * oes : (unsigned)a.M * a.out_stride * oes;
+  const int out2_bytes = split ? a.M * a.out2_stride * OES : 0;
   const __amdgpu_buffer_rsrc_t rsZ =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(BNR ? a.bnr_z : a.out), 0, BNR ? a.M * a.bnr_zs * ES : 0, P_RSRC3);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(BNR ? a.bnr_z : a.out), 0, BNR ? a.M * a.bnr_zs * OES : 0, P_RSRC3);
   const bool stats = BNR || a.bn_sum != nullptr;
 
   // BNR with TM = 64: every z quad of the tile (16 loads, 32 registers) is issued in the K loop, right
@@ -379,7 +399,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       for (int mt = 0; mt < 2 * MIQ; ++mt) {
         const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
         const bool v = c < a.Nout && m < a.M;
-        zall[nt][mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+        zall[nt][mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * OES) : P_OOB));
       }
     }
   };
@@ -396,6 +416,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       const int cl = wc * 64 + nt * 16 + 4 * h4;         // the same, relative to n0
       const float4 b4 = p_lds_f4(&cst[0][cl]);
       const float bias[4] = {b4.x, b4.y, b4.z, b4.w};
+      float wsc[4] = {1.f, 1.f, 1.f, 1.f};
+      if constexpr (F8) {
+        const float4 w4 = p_lds_f4(&cst[1][cl]);
+        wsc[0] = w4.x; wsc[1] = w4.y; wsc[2] = w4.z; wsc[3] = w4.w;
+      }
       float sc[4], sh[4], mu[4], is[4];
       // BNR: the 2*MIQ z quads of this channel group, all loaded before the first store of the group (a
       // load behind a store waits for it: vmcnt retires in order)
@@ -414,7 +439,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           for (int mt = 0; mt < 2 * MIQ; ++mt) {
             const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
             const bool v = cv && m < a.M;
-            zq[mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * ES) : P_OOB));
+            zq[mt] = __builtin_bit_cast(bf16x4, p_ld8(rsZ, v ? (unsigned)((m * a.bnr_zs + c) * OES) : P_OOB));
           }
         }
       }
@@ -438,7 +463,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         float x[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          x[r] = acc[mt][nt][r] + bias[r];
+          x[r] = F8 ? fmaf(acc[mt][nt][r], wsc[r], bias[r]) : acc[mt][nt][r] + bias[r];
           if (a.relu) x[r] = fmaxf(x[r], 0.f);
         }
         bf16x4 o;
@@ -450,8 +475,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           pix = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
         }
         // (timing-only ablation, fwd_debug bit 7: every store to an out-of-range offset, dropped)
-        const unsigned off = v && !(a.debug_flags & 128) ? (unsigned)((pix * ostr + cq) * ES) : P_OOB;
-        p_st8(rsO, off, __builtin_bit_cast(v2u32, o));
+        const unsigned off = v && !(a.debug_flags & 128) ? (unsigned)((pix * ostr + cq) * oes) : P_OOB;
+        if (o8) {   // 4 channels -> 4 e4m3 bytes (f8x8_from_f's saturating encode)
+          float c8[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) c8[r] = fminf(fmaxf(x[r], -FP8_MAX), FP8_MAX);
+          int q = __builtin_amdgcn_cvt_pk_fp8_f32(c8[0], c8[1], 0, false);
+          q = __builtin_amdgcn_cvt_pk_fp8_f32(c8[2], c8[3], q, true);
+          __builtin_amdgcn_raw_buffer_store_b32((unsigned)q, rsO, off, 0, 0);
+        } else {
+          p_st8(rsO, off, __builtin_bit_cast(v2u32, o));
+        }
         if constexpr (BNR) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -604,7 +638,11 @@ namespace adp {
 // Tile / ring (option tap64p_cfg, 0 = from the tap64 tile choice): 1 = 256x256 / 2 stages,
 // 2 = 256x128 / 3 stages, 3 = 128x256 / 3 stages.
 int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
-  if (!option("tap64_persist", 1) || a.f8 || a.K < 128) return 0;   // (two K steps at least)
+  if (!option("tap64_persist", 1) || a.K < 128) return 0;   // (two bf16 K steps / one fp8 step at least)
+  // fp8: the halo forms with a plain bf16 store (the eval convs of UNetBN.forward_fp8)
+  if (a.f8 && (!option("tap64p_f8", 1) || a.out_mode == 2 || a.bn_sum || a.bnr_z ||
+               a.CAs % 128 != 0 || a.CBs % 128 != 0))
+    return 0;
   if (a.addend || a.mask || a.mask2 || a.accum || a.drop_rate > 0.f || a.scA || a.scB) return 0;
   if (a.up != 1 && (a.up != 2 || a.bnr_z)) return 0;   // up = 2: the halo form only (below)
   if (a.out_mode == 1 && (a.Cps % 8 != 0 || a.Nout % a.Cps != 0)) return 0;
@@ -643,17 +681,34 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
                           a.dil == 1 && a.pad == 1 && a.stride == 1 && a.Ho == a.Hs * a.up && a.Wo == a.Ws * a.up &&
                           a.Ho % 8 == 0 && a.Wo % 32 == 0;
   if (a.up != 1 && !(halo_shape && (cfg == 1 || (cfg == 2 && option("tap64p_halo128", 1))))) return 0;
+  if (a.f8 && !(halo_shape && (cfg == 1 || cfg == 2))) {   // gather form (ConvTranspose, fp8 output)
+    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, true>", BM, BN, cfg == 1 ? 2 : 3);
+    if (cfg == 1) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, false, true>), dim3(grid), dim3(512), 0, s, a);
+    else if (cfg == 2) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, false, true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<128, 256, 3, false, false, true>), dim3(grid), dim3(512), 0, s, a);
+    return 1;
+  }
+  if (a.f8) {
+    if (cfg == 1) {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true>), dim3(grid), dim3(512), 0, s, a);
+    } else {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true>), dim3(grid), dim3(512), 0, s, a);
+    }
+    return 1;
+  }
   if (halo_shape && cfg == 1) {
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
   if (halo_shape && cfg == 2 && option("tap64p_halo128", 1)) {
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
-  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
+  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
 #define P_LAUNCH(BM_, BN_, NST_)                                                                           \
   do {                                                                                                     \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \

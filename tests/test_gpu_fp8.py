@@ -115,26 +115,85 @@ def test_fp8_conv_vs_dequantised_reference(cinA, cinB, cout, dil, H, out_fp8, re
     assert err.max().item() < 1e-3, err.max().item()
 
 
-def test_fp8_convtranspose_pixel_shuffle():
-    g = torch.Generator().manual_seed(7)
-    B, H, cin, cout = 2, 8, 256, 128
+@pytest.mark.parametrize("cinA,cinB,cout,H,W,relu,kern", [
+    (128, 0, 128, 16, 64, False, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true>"),
+    (512, 0, 512, 8, 32, False, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true>"),
+    (256, 256, 256, 16, 32, True, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true>"),
+    (256, 0, 320, 8, 64, False, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true>"),   # ragged N tile
+])
+def test_fp8_persistent_halo_form(cinA, cinB, cout, H, W, relu, kern):
+    """fp8 halo form of the persistent forward kernel (128-channel K steps, one 32-B MFMA operand per
+    row pair, per-column weight scale in the epilogue) vs the dequantised reference and vs the
+    non-persistent fp8 tap64 kernel (option tap64p_f8=0) on the same operands."""
+    from adipose_amd import _lib
+    g = torch.Generator().manual_seed(cinA + cout + W)
+    B = 2
+    xa8 = q8(torch.randn(B, H, W, cinA, generator=g).clamp_min(0) * 2)
+    xb8 = q8(torch.randn(B, H, W, cinB, generator=g)) if cinB else None
+    cin = cinA + cinB
+    K = 9 * cin
+    Wf = torch.zeros(((cout + 63) // 64 * 64, K))
+    Wf[:cout] = torch.randn(cout, K, generator=g) * (2.0 / K) ** 0.5
+    bias = torch.randn(cout, generator=g) * 0.1
+    W8, sc = pack8(Wf)
+    outs = []
+    for persist in (1, 0):
+        out = torch.zeros(B, H, W, cout, dtype=torch.bfloat16, device=DEV)
+        ops.set_option("tap64p_f8", persist)
+        try:
+            ops.conv_fwd(xa8.to(DEV), W8, cout, out=out, srcB=None if xb8 is None else xb8.to(DEV),
+                         bias=bias.to(DEV), kh=3, kw=3, relu=relu, w_scale=sc)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("tap64p_f8", None)
+        assert (kname == kern) == bool(persist), kname
+        outs.append(out.cpu().float().double())
+    x_cat = xa8 if xb8 is None else torch.cat([xa8.float(), xb8.float()], -1).to(F8)
+    ref = ref_conv(x_cat, W8, sc, cout, 3, 1, cin, bias=bias, relu=relu)
+    for got in outs:
+        err = (got - ref).abs() - 2 ** -7 * ref.abs()
+        assert err.max().item() < 1e-3, err.max().item()
+    assert ((outs[0] - outs[1]).abs() - 2 ** -7 * ref.abs()).max().item() < 1e-3
+
+
+@pytest.mark.parametrize("cin,cout,H,out_fp8", [(256, 128, 8, False), (128, 64, 16, True), (256, 128, 12, True),
+                                                 (512, 256, 8, True), (1024, 512, 4, False)])
+def test_fp8_convtranspose_pixel_shuffle(cin, cout, H, out_fp8):
+    """fp8 ConvTranspose 2x2/s2 forward (1x1 GEMM + pixel-shuffle store, bf16 or fp8 output): the persistent
+    gather form (tap64p, one to eight 128-channel K steps, 128x256 / 256x256 tiles) vs the dequantised
+    reference, and bit for bit vs the non-persistent fp8 tap64 kernel (option tap64p_f8=0: same K order)."""
+    from adipose_amd import _lib
+    g = torch.Generator().manual_seed(7 + cin + H)
+    B = 2
     x8 = q8(torch.randn(B, H, H, cin, generator=g).clamp_min(0))
     # packed ConvT weights: rows sub*cout + co (sub = dy*2+dx), K = cin
     Wf = torch.randn(4 * cout, cin, generator=g) * 0.05
     bias = torch.randn(cout, generator=g) * 0.1
     W8, sc = pack8(Wf)
-    out = torch.zeros(B, 2 * H, 2 * H, cout, dtype=torch.bfloat16, device=DEV)
-    ops.conv_fwd(x8.to(DEV), W8, 4 * cout, out=out, bias=bias.to(DEV), kh=1, kw=1, pad=0, out_mode=1,
-                 shuffle_c=cout, w_scale=sc)
-    torch.cuda.synchronize()
+    outs = []
+    for persist in (1, 0):
+        out = torch.zeros(B, 2 * H, 2 * H, cout, dtype=F8 if out_fp8 else torch.bfloat16, device=DEV)
+        ops.set_option("tap64p_f8", persist)
+        try:
+            ops.conv_fwd(x8.to(DEV), W8, 4 * cout, out=out, bias=bias.to(DEV), kh=1, kw=1, pad=0, out_mode=1,
+                         shuffle_c=cout, w_scale=sc)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("tap64p_f8", None)
+        assert kname.startswith("igemm_fwd_tap64p_kernel") == bool(persist), kname
+        outs.append(out.cpu())
+    assert torch.equal(outs[0].view(torch.uint8), outs[1].view(torch.uint8))
     Wd = W8.float().double().cpu() * sc.double().cpu()[:, None]
     y = torch.einsum("bhwc,nc->bhwn", x8.float().double(), Wd)        # (B,H,W,4*cout)
     ref = torch.zeros(B, 2 * H, 2 * H, cout, dtype=torch.float64)
     for sub in range(4):
         dy, dx = sub >> 1, sub & 1
         ref[:, dy::2, dx::2, :] = y[..., sub * cout:(sub + 1) * cout] + bias.double()
-    got = out.cpu().double()
-    assert ((got - ref).abs() - 2 ** -7 * ref.abs()).max().item() < 1e-3
+    got = outs[0].float().double()
+    rel = 2 ** -3 if out_fp8 else 2 ** -7
+    assert ((got - ref).abs() - rel * ref.abs()).max().item() < 1e-3
 
 
 def test_fp8_conv_rejects_unsupported_geometry():

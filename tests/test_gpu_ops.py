@@ -217,7 +217,7 @@ def test_tap64p_halo_matches(mode, grid, tile):
         finally:
             for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid"):
                 ops.set_option(o_, None)
-        assert kname == "igemm_fwd_tap64p_kernel<256, %d, %d, false, %s>" % (
+        assert kname == "igemm_fwd_tap64p_kernel<256, %d, %d, false, %s, false>" % (
             tile, 2 if tile == 256 else 3, "true" if halo else "false"), kname
         res.append((torch.cat(outs, -1).double(), st.double()))
     (yh, sh_), (yg, sg) = res
@@ -241,8 +241,8 @@ def test_upsample_gather_halo_forms(form, grid):
     N, Hs, Ws = 2, 16, 32
     cin, nout, kern = {"halop_1ch": (64, 64, "igemm_fwd_halop_kernel<false, 1, 64"),
                        "halop_2ch": (128, 64, "igemm_fwd_halop_kernel<false, 2, 32"),
-                       "tap64p_256": (128, 256, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true>"),
-                       "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true>")}[form]
+                       "tap64p_256": (128, 256, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>"),
+                       "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false>")}[form]
     x = torch.randn(N, Hs, Ws, cin, generator=g).to(DEV, dt)
     Wt = (torch.randn(nout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
     bias = torch.randn(nout, generator=g).to(DEV)
