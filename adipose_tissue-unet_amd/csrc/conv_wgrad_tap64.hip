@@ -466,6 +466,10 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   const __amdgpu_buffer_rsrc_t rsBZ = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(BNA ? a.bna_z : a.dY), 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
   // per-thread constant parts of the gathers: halo group i -> (pixel delta, row/col offsets, byte offset)
+  // up = 2 (nearest-x2 upsample folded into the input gather, adipose_v3's up*_conv1): halo pixel (y0 + hy,
+  // x0 + hx) of the conv's input grid is source pixel ((y0 + hy) >> 1, (x0 + hx) >> 1) = (y0 / 2 + (hy >> 1), ...)
+  // for the even patch origins, so the per-thread part of the gather stays a constant pixel delta
+  const int us = a.up >> 1;
   int hy[GH], hx[GH], hpix[GH], hoff[GH], dpix[GD], doff[GD];
   const int xc0 = (inA ? ch * 64 : ch * 64 - a.CAs) * 2;
 #pragma unroll
@@ -473,7 +477,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     const int idx = i * NTH + tid, hr = idx >> 3, pos = idx & 7;
     hy[i] = hr / HW - 1;
     hx[i] = hr % HW - 1;
-    hpix[i] = hy[i] * a.Ws + hx[i];
+    hpix[i] = (hy[i] >> us) * a.Ws + (hx[i] >> us);
     hoff[i] = xc0 + 16 * (pos ^ gsw<RB>(hr));
   }
 #pragma unroll
@@ -491,7 +495,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     const int img = r / ty_n;
     P.y0 = (r % ty_n) * PH;
     P.x0 = px * PW;
-    P.pbx = (img * a.Hs + P.y0) * a.Ws + P.x0;
+    P.pbx = (img * a.Hs + (P.y0 >> us)) * a.Ws + (P.x0 >> us);
     P.pbd = (img * a.Ho + P.y0) * a.Wo + P.x0;
     return P;
   };
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     const int idx = i * NTH + tid;
     if (i < GH - 1 || idx < HCH) {
       const int gy = P.y0 + hy[i], gx = P.x0 + hx[i];
-      const bool ok = (unsigned)gy < (unsigned)a.Hs && (unsigned)gx < (unsigned)a.Ws;
+      const bool ok = (unsigned)gy < (unsigned)(a.Hs << us) && (unsigned)gx < (unsigned)(a.Ws << us);
       const unsigned off = ok ? (unsigned)((P.pbx + hpix[i]) * xcs * 2 + hoff[i]) : WG_OOB;
       wg_buf_lds16(rsX, smem + buf * STAGE + (size_t)(i * NTH + wave * 64) * 16, off);
     }
@@ -948,7 +952,8 @@ namespace adp {
 static bool halop_ok(const WgradArgs& a) {
   const int cin = a.CAs + a.CBs;
   return option("wgrad_halop", 1) && !a.scA && !a.scB && a.CAs % 64 == 0 && a.CBs % 64 == 0 && a.kh == 3 &&
-         a.kw == 3 && a.dil == 1 && a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws &&
+         a.kw == 3 && a.dil == 1 && a.pad == 1 && a.stride == 1 && (a.up == 1 || a.up == 2) && a.Ho == a.Hs * a.up &&
+         a.Wo == a.Ws * a.up &&
          a.Ho % 8 == 0 && a.Wo % 32 == 0 && a.Nout % 64 == 0 && a.dy_mode == 0 && a.K == 9 * cin &&
          a.Kpad == a.K && a.dy_stride % 8 == 0 && a.dy_stride >= a.Nout &&
          // buffer-resource offsets: every operand below 2 GiB

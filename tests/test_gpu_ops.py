@@ -668,6 +668,38 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
 
+@pytest.mark.parametrize("N,Hs,Ws,parts,cout", [(2, 8, 16, [64], 64), (1, 16, 32, [128], 128), (2, 8, 32, [192], 192)])
+def test_wgrad_persistent_halo_upsample(N, Hs, Ws, parts, cout):
+    """Halo weight gradient with the nearest-x2 upsample folded into its input gather (adipose_v3's
+    UpSampling2D + conv, train_adipose_unet_v3.py:691-692) vs autograd of the oracle conv on the upsampled
+    input, and vs the tap64 / glds kernels (option wgrad_halop=0)."""
+    from adipose_amd import _lib
+    cin = sum(parts)
+    _, kern, bias, l = make_case(N, 2 * Hs, parts, cout, 1, False, seed=23)
+    g = torch.Generator().manual_seed(24)
+    dt = torch.bfloat16
+    x = rb(torch.randn(N, Hs, Ws, cin, generator=g), dt)
+    xu = x.repeat_interleave(2, 1).repeat_interleave(2, 2)
+    dZ = rb(torch.randn(N, 2 * Hs, 2 * Ws, cout, generator=g), dt)
+    kr = rb(kern, dt).clone().requires_grad_(True)
+    (R.conv2d_same(xu, kr, None, relu=False) * dZ).sum().backward()
+    xd = x.to(DEV, dt).contiguous()
+    dzd = nhwc_pad(dZ, l.cout_s, dt)
+    dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
+    ref = torch.zeros_like(dW)
+    try:
+        ops.conv_wgrad(xd, dzd, dW, l.Nout, up=True)
+        kname = _lib.lib().adp_last_kernel().decode()
+        ops.set_option("wgrad_halop", 0)
+        ops.conv_wgrad(xd, dzd, ref, l.Nout, up=True)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("wgrad_halop", None)
+    assert kname.startswith("igemm_wgrad_halop_kernel"), kname
+    assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
+    assert relerr(dW.cpu(), ref.cpu()) < 1e-4
+
+
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("S", [8, 64])
 def test_conv_transpose(dt, S):
