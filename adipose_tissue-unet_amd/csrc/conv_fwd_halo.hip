@@ -254,11 +254,14 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 #define HALOP_VALU_PER_MFMA 8
 #endif
 // EPI (non-BNR launches): 0 plain store, 1 + BatchNorm statistics, 2 + ReLU, 3 + ReLU + statistics of the
-// stored values -- compile-time, so the
-// epilogue carries no per-element selects for the launch-uniform flags
+// stored values, 4 + addend and / or ReLU-backward mask (the data gradients of the adipose_v3 convs:
+// out = (acc + addend) * (mask > 0 ? mask_scale : 0), mask2 / mask2_scale on a split store's second part,
+// the arithmetic of epi_rows) -- compile-time, so the epilogue carries no per-element selects for the
+// launch-uniform flags
 template <bool BNR, int NCH, int BN, bool PIPE, int EPI>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   static_assert(!BNR || EPI == 0, "the BN-backward reduction launch stores the plain product");
+  static_assert(EPI != 4 || !PIPE, "mask / addend quads and two accumulator sets do not fit the registers");
   // NCH 64-channel input chunks (1: Cin_s 64; 2: Cin_s 128 from one or two sources), BN output channels
   // per block (64, or 32 for two chunks: 2 x 340 halo rows + 9 x 2 x 32 weight rows = 157 KiB of LDS)
   constexpr int NTH = 512, NF = BN / 16;
@@ -372,28 +375,46 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       __builtin_amdgcn_make_buffer_rsrc((void*)obase, 0, a.M * ostride * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsZ = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(BNR ? a.bnr_z : a.out), 0, BNR ? a.M * a.bnr_zs * 2 : 0, 0x00020000);
-  // BNR: the z quads of one accumulator tile
-  auto load_z = [&](int mrow_, uint2 (&zr)[2][NF]) {
+  // EPI 4: the mask (mask2 on a split store's second part) and the addend (first part only) of the block
+  const void* mptr = second ? a.mask2 : a.mask;
+  const int mstr = second ? a.mask2_stride : a.mask_stride;
+  const float mscale = second ? a.mask2_scale : a.mask_scale;
+  const bool has_mask = EPI == 4 && mptr != nullptr, has_add = EPI == 4 && !second && a.addend != nullptr;
+  const __amdgpu_buffer_rsrc_t rsM =
+      __builtin_amdgcn_make_buffer_rsrc((void*)mptr, 0, has_mask ? a.M * mstr * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsD =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.addend, 0, has_add ? a.M * a.addend_stride * 2 : 0, 0x00020000);
+  // BNR: the z quads of one accumulator tile; EPI 4: its mask and addend quads (at the store's column)
+  auto load_q = [&](__amdgpu_buffer_rsrc_t rs, int str, int col0, int mrow_, uint2 (&zr)[2][NF]) {
 #pragma unroll
     for (int mf = 0; mf < 2; ++mf)
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf) {
         const int c0 = nf * 16 + 4 * h4;
-        const unsigned off = n0 + c0 < a.Nout ? (unsigned)(((mrow_ + mf * 16 + r16) * a.bnr_zs + n0 + c0) * 2) : 0x80000000u;
-        zr[mf][nf] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rsZ, off, 0, 0));
+        const unsigned off = n0 + c0 < nlim ? (unsigned)(((mrow_ + mf * 16 + r16) * str + col0 + c0) * 2) : 0x80000000u;
+        zr[mf][nf] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
       }
   };
+  auto load_z = [&](int mrow_, uint2 (&zr)[2][NF]) { load_q(rsZ, a.bnr_zs, n0, mrow_, zr); };
   // epilogue of accumulator tile (mf, nf): lane = pixel mrow_ + mf*16 + r16, channels nf*16 + 4*h4 .. +3
-  auto epi_unit = [&](int mf, int nf, const f32x4& av, uint2 zv, int mrow_) {
+  auto epi_unit = [&](int mf, int nf, const f32x4& av, uint2 zv, int mrow_, uint2 dv = uint2{0u, 0u}) {
     const int c0 = nf * 16 + 4 * h4;
     const bool cv = n0 + c0 < nlim;
     const float4 cb = *reinterpret_cast<const float4*>(cst + c0);
     const int m = mrow_ + mf * 16 + r16;
     float v[4] = {av[0] + cb.x, av[1] + cb.y, av[2] + cb.z, av[3] + cb.w};
+    if constexpr (EPI == 4) {   // epi_rows: + addend, then the mask
+      const bf16x4 dd = __builtin_bit_cast(bf16x4, dv), mm = __builtin_bit_cast(bf16x4, zv);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (has_add) v[i] += (float)dd[i];
+        if (has_mask) v[i] = (float)mm[i] > 0.f ? v[i] * mscale : 0.f;
+      }
+    }
     bf16x4 o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if constexpr (EPI >= 2) v[i] = fmaxf(v[i], 0.f);
+      if constexpr (EPI == 2 || EPI == 3) v[i] = fmaxf(v[i], 0.f);
       o[i] = (bf16)v[i];
     }
     const unsigned off = cv ? (unsigned)((m * ostride + ocol0 + c0) * 2) : 0x80000000u;
@@ -424,7 +445,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   };
 
   f32x4 acc[2][NF], accp[2][NF];   // this tile's / the previous tile's accumulators (PIPE)
-  uint2 zreg[2][NF];
+  uint2 zreg[2][NF], dreg[EPI == 4 ? 2 : 1][NF];
   int mrowp = 0;
   // one tile: prefetch the next tile's halo into registers, nine taps, then (PIPE) nothing -- the
   // previous tile's epilogue units run between this tile's taps -- or (!PIPE) this tile's epilogue
@@ -435,6 +456,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     tile_origin(k, img, y0, x0);
     const int mrow = (img * a.Ho + y0 + wave) * a.Wo + x0;   // first output pixel of this wave's row
     if constexpr (BNR) load_z(EPI_PREV ? mrowp : mrow, zreg);
+    if constexpr (EPI == 4) {
+      if (has_mask) load_q(rsM, mstr, ocol0, mrow, zreg);
+      if (has_add) load_q(rsD, a.addend_stride, ocol0, mrow, dreg);
+    }
     uint4 hreg[GH];
     if (more) {
       int img1, y01, x01;
@@ -505,7 +530,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
-        for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, acc[mf][nf], zreg[mf][nf], mrow);
+        for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, acc[mf][nf], zreg[mf][nf], mrow, dreg[EPI == 4 ? mf : 0][nf]);
     }
     if (more) {
       LDS_BAR();   // every wave is done with this tile's halo
@@ -567,19 +592,28 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     return 0;
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const bool one_chunk = Cin_s == 64;
-  const bool plain = !a.addend && !a.mask && !a.accum && a.drop_rate == 0.f && a.out_stride % 8 == 0;
+  const bool plain = !a.addend && !a.mask && !a.mask2 && !a.accum && a.drop_rate == 0.f && a.out_stride % 8 == 0;
+  // EPI 4 (option halop_mask): an addend and / or ReLU-backward masks, no bias / ReLU / statistics (the
+  // adipose_v3 data gradients); operands read as 8-B quads
+  const bool maskepi = (a.addend || a.mask || a.mask2) && !a.accum && a.drop_rate == 0.f && !a.bnr_z && !a.bn_sum && !a.relu && !a.bias &&
+                       a.out_stride % 8 == 0 && (!a.mask || a.mask_stride % 4 == 0) &&
+                       (!a.mask2 || a.mask2_stride % 4 == 0) && (!a.addend || a.addend_stride % 4 == 0) &&
+                       (size_t)a.M * std::max(std::max(a.mask ? a.mask_stride : 0, a.mask2 ? a.mask2_stride : 0),
+                                              a.addend ? a.addend_stride : 0) * 2 < ((size_t)1 << 31) &&
+                       option("halop_mask", 1);
   // persistent forms: one chunk with <= 64 outputs (one block) or 128 (two 64-wide blocks); two chunks
   // with 64 / 128 outputs in 32-wide blocks
   int bn = 0;
   if (one_chunk && (a.Nout <= 64 || a.Nout == 128)) bn = 64;
   else if (Cin_s == 128 && (a.Nout == 64 || a.Nout == 128) && option("halo_persist2", 1)) bn = 32;
   const int nt_n = bn ? (a.Nout + bn - 1) / bn : 1;
-  const bool split_ok = a.out_mode == 2 && bn && a.split_c > 0 && a.split_c % bn == 0 && a.split_c < a.Nout && !a.mask2 &&
-                        a.out2_stride % 8 == 0 && (a.Nout - a.split_c) % bn == 0;
+  const bool split_ok = a.out_mode == 2 && bn && a.split_c > 0 && a.split_c % bn == 0 && a.split_c < a.Nout &&
+                        (!a.mask2 || maskepi) && a.out2_stride % 8 == 0 && (a.Nout - a.split_c) % bn == 0;
   const size_t lim = (size_t)1 << 31;   // the persistent form stores / reads z through buffer resources
   const bool fits = (size_t)a.M * a.out_stride * 2 < lim && (!a.out2 || (size_t)a.M * a.out2_stride * 2 < lim) &&
                     (!a.bnr_z || (size_t)a.M * a.bnr_zs * 2 < lim);
-  if (bn && plain && fits && (a.out_mode == 0 || split_ok) && option("halo_persist", 1) && (a.up == 1 || !a.bnr_z)) {
+  if (bn && (plain || maskepi) && fits && (a.out_mode == 0 || split_ok) && option("halo_persist", 1) &&
+      (a.up == 1 || !a.bnr_z)) {
     const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * nt_n;
     a.ntile_n = nt_n;
     a.nblocks = tiles;   // the persistent kernel reads the tile count from nblocks
@@ -593,13 +627,14 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     // (one-chunk launches only by default: +8 % on the 64 -> 64 forward; the two-chunk form has twice the
     // MFMA work per epilogue and lost 2-5 % to the extra registers -- profiles/r02_halop_pipe_ab.txt)
     const int pm = option("halop_pipe", 1);
-    const bool pipe = !bnr && (pm == 2 || (pm == 1 && one_chunk));
-    const int epi = bnr ? 0 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
+    const bool pipe = !bnr && !maskepi && (pm == 2 || (pm == 1 && one_chunk));
+    const int epi = bnr ? 0 : maskepi ? 4 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
     adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
                     pipe ? "true" : "false", epi);
 #define HALOP_LAUNCH(NCH_, BN_)                                                                             \
   do {                                                                                                      \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4>), dim3(grid), dim3(512), 0, s, a); \
     else if (pipe) {                                                                                        \
       if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1>), dim3(grid), dim3(512), 0, s, a); \
       else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2>), dim3(grid), dim3(512), 0, s, a); \

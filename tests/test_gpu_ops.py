@@ -228,6 +228,66 @@ def test_tap64p_halo_matches(mode, grid, tile):
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
 
 
+@pytest.mark.parametrize("mode", ["mask", "addend_mask", "split_masks", "split_mask2", "two_chunks", "addend_only"])
+def test_halop_mask_addend_epilogue(mode):
+    """Persistent halo kernel with the addend / ReLU-backward-mask epilogue (EPI 4: the adipose_v3 data
+    gradients, out = (acc + addend) * (mask > 0 ? scale : 0), mask2 on a split store's second part) vs a
+    float64 reference and vs the non-persistent halo kernel (option halo_persist=0)."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(41)
+    N, H, W_ = 2, 16, 64
+    cin = 128 if mode == "two_chunks" else 64
+    nout = 128 if mode.startswith("split") else 64
+    x = torch.randn(N, H, W_, cin, generator=g).to(DEV, dt)
+    Wt = (torch.randn(nout, 9 * cin, generator=g) * 0.05).to(DEV, dt)
+    mk = torch.randn(N, H, W_, nout, generator=g).to(DEV, dt)
+    ad = torch.randn(N, H, W_, nout, generator=g).to(DEV, dt) if "addend" in mode else None
+    xd = x.double().permute(0, 3, 1, 2)
+    wk = Wt.double().view(nout, 3, 3, cin).permute(0, 3, 1, 2)
+    ref = F.conv2d(xd, wk, padding=1).permute(0, 2, 3, 1)
+    if ad is not None:
+        ref = ref + ad.double()
+    sc1, sc2 = 1.25, 0.5
+    if mode != "addend_only":
+        scale = torch.full((nout,), sc1, dtype=torch.float64, device=DEV)
+        if mode.startswith("split"):
+            scale[64:] = sc2
+        keep = mk.double() > 0
+        if mode == "split_mask2":   # no mask on the first part
+            scale[:64] = 1.0
+            keep[..., :64] = True
+        ref = torch.where(keep, ref * scale, torch.zeros_like(ref))
+    res = []
+    for persist in (1, 0):
+        kw = dict(addend=ad)
+        if mode.startswith("split"):
+            o1 = torch.zeros(N, H, W_, 64, dtype=dt, device=DEV)
+            o2 = torch.zeros(N, H, W_, 64, dtype=dt, device=DEV)
+            kw.update(out_mode=2, out2=o2, split_c=64, mask=mk[..., :64].contiguous(), mask_scale=sc1,
+                      mask2=mk[..., 64:].contiguous(), mask2_scale=sc2, addend=None)
+            if mode == "split_mask2":
+                kw.update(mask=None)
+            outs = [o1, o2]
+        else:
+            outs = [torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)]
+            if mode != "addend_only":
+                kw.update(mask=mk, mask_scale=sc1)
+        ops.set_option("halo_persist", persist)
+        try:
+            ops.conv_fwd(x, Wt, nout, out=outs[0], **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("halo_persist", None)
+        assert kname.startswith("igemm_fwd_halop_kernel") == bool(persist), kname
+        if persist:
+            assert kname.endswith(", false, 4>"), kname
+        res.append(torch.cat(outs, -1).double())
+    tol = 2 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
+    assert ((res[0] - ref).abs() - tol).max().item() < 0, (res[0] - ref).abs().max().item()
+    assert ((res[0] - res[1]).abs() - tol).max().item() < 0
+
+
 @pytest.mark.parametrize("form", ["halop_1ch", "halop_2ch", "tap64p_256", "tap64p_128"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
 def test_upsample_gather_halo_forms(form, grid):
