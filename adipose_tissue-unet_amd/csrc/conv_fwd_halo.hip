@@ -256,12 +256,13 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 // EPI (non-BNR launches): 0 plain store, 1 + BatchNorm statistics, 2 + ReLU, 3 + ReLU + statistics of the
 // stored values, 4 + addend and / or ReLU-backward mask (the data gradients of the adipose_v3 convs:
 // out = (acc + addend) * (mask > 0 ? mask_scale : 0), mask2 / mask2_scale on a split store's second part,
-// the arithmetic of epi_rows) -- compile-time, so the epilogue carries no per-element selects for the
-// launch-uniform flags
+// the arithmetic of epi_rows), 5 + ReLU + inverted dropout (adipose_v3's Dropout after up*_conv3: the
+// stateless hash of epi_rows, so the mask matches every other kernel's) -- compile-time, so the epilogue
+// carries no per-element selects for the launch-uniform flags
 template <bool BNR, int NCH, int BN, bool PIPE, int EPI>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   static_assert(!BNR || EPI == 0, "the BN-backward reduction launch stores the plain product");
-  static_assert(EPI != 4 || !PIPE, "mask / addend quads and two accumulator sets do not fit the registers");
+  static_assert(EPI < 4 || !PIPE, "mask / addend quads, the dropout hash and two accumulator sets: registers");
   // NCH 64-channel input chunks (1: Cin_s 64; 2: Cin_s 128 from one or two sources), BN output channels
   // per block (64, or 32 for two chunks: 2 x 340 halo rows + 9 x 2 x 32 weight rows = 157 KiB of LDS)
   constexpr int NTH = 512, NF = BN / 16;
@@ -409,6 +410,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       for (int i = 0; i < 4; ++i) {
         if (has_add) v[i] += (float)dd[i];
         if (has_mask) v[i] = (float)mm[i] > 0.f ? v[i] * mscale : 0.f;
+      }
+    }
+    if constexpr (EPI == 5) {   // epi_rows: ReLU, then the dropout of element (m, channel)
+      const float ks = 1.f / (1.f - a.drop_rate);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float u = adp_uniform(a.drop_seed, (uint64_t)m * (uint64_t)a.Nout + (n0 + c0 + i));
+        v[i] = u >= a.drop_rate ? fmaxf(v[i], 0.f) * ks : 0.f;
       }
     }
     bf16x4 o;
@@ -593,6 +602,9 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const bool one_chunk = Cin_s == 64;
   const bool plain = !a.addend && !a.mask && !a.mask2 && !a.accum && a.drop_rate == 0.f && a.out_stride % 8 == 0;
+  // EPI 5 (option halop_dropout): ReLU + dropout on a plain store (adipose_v3 up*_conv3 in training)
+  const bool dropepi = a.drop_rate > 0.f && a.relu && !a.addend && !a.mask && !a.mask2 && !a.accum && !a.bn_sum &&
+                       !a.bnr_z && a.out_mode == 0 && a.out_stride % 8 == 0 && option("halop_dropout", 1);
   // EPI 4 (option halop_mask): an addend and / or ReLU-backward masks, no bias / ReLU / statistics (the
   // adipose_v3 data gradients); operands read as 8-B quads
   const bool maskepi = (a.addend || a.mask || a.mask2) && !a.accum && a.drop_rate == 0.f && !a.bnr_z && !a.bn_sum && !a.relu && !a.bias &&
@@ -612,7 +624,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   const size_t lim = (size_t)1 << 31;   // the persistent form stores / reads z through buffer resources
   const bool fits = (size_t)a.M * a.out_stride * 2 < lim && (!a.out2 || (size_t)a.M * a.out2_stride * 2 < lim) &&
                     (!a.bnr_z || (size_t)a.M * a.bnr_zs * 2 < lim);
-  if (bn && (plain || maskepi) && fits && (a.out_mode == 0 || split_ok) && option("halo_persist", 1) &&
+  if (bn && (plain || maskepi || dropepi) && fits && (a.out_mode == 0 || split_ok) && option("halo_persist", 1) &&
       (a.up == 1 || !a.bnr_z)) {
     const int tiles = a.Nimg * (a.Ho / PH) * (a.Wo / PW) * nt_n;
     a.ntile_n = nt_n;
@@ -627,14 +639,15 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     // (one-chunk launches only by default: +8 % on the 64 -> 64 forward; the two-chunk form has twice the
     // MFMA work per epilogue and lost 2-5 % to the extra registers -- profiles/r02_halop_pipe_ab.txt)
     const int pm = option("halop_pipe", 1);
-    const bool pipe = !bnr && !maskepi && (pm == 2 || (pm == 1 && one_chunk));
-    const int epi = bnr ? 0 : maskepi ? 4 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
+    const bool pipe = !bnr && !maskepi && !dropepi && (pm == 2 || (pm == 1 && one_chunk));
+    const int epi = bnr ? 0 : dropepi ? 5 : maskepi ? 4 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
     adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
                     pipe ? "true" : "false", epi);
 #define HALOP_LAUNCH(NCH_, BN_)                                                                             \
   do {                                                                                                      \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0>), dim3(grid), dim3(512), 0, s, a); \
     else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 5) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 5>), dim3(grid), dim3(512), 0, s, a); \
     else if (pipe) {                                                                                        \
       if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1>), dim3(grid), dim3(512), 0, s, a); \
       else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2>), dim3(grid), dim3(512), 0, s, a); \

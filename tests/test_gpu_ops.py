@@ -228,6 +228,43 @@ def test_tap64p_halo_matches(mode, grid, tile):
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
 
 
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 128), (128, 64)])
+def test_halop_relu_dropout_epilogue(cin, cout):
+    """Persistent halo kernel with the ReLU + dropout epilogue (EPI 5, adipose_v3 up*_conv3 in training):
+    the same stateless dropout mask as the non-persistent halo kernel (option halo_persist=0), kept values
+    = relu(conv + b) / (1 - rate) within bf16 rounding of the no-dropout launch."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(43)
+    N, H, W_, rate = 2, 16, 64, 0.3
+    x = torch.randn(N, H, W_, cin, generator=g).to(DEV, dt)
+    Wt = (torch.randn(cout, 9 * cin, generator=g) * 0.05).to(DEV, dt)
+    b = torch.randn(cout, generator=g).to(DEV) * 0.1
+    res = {}
+    for persist in (1, 0):
+        for drop in (rate, 0.0):
+            out = torch.zeros(N, H, W_, cout, dtype=dt, device=DEV)
+            ops.set_option("halo_persist", persist)
+            try:
+                ops.conv_fwd(x, Wt, cout, out=out, bias=b, relu=True, dropout_rate=drop, dropout_seed=1234)
+                torch.cuda.synchronize()
+                kname = _lib.lib().adp_last_kernel().decode()
+            finally:
+                ops.set_option("halo_persist", None)
+            assert kname.startswith("igemm_fwd_halop_kernel") == bool(persist), kname
+            if persist and drop:
+                assert kname.endswith(", false, 5>"), kname
+            res[(persist, drop)] = out.double()
+    yp, yn, y0 = res[(1, rate)], res[(0, rate)], res[(1, 0.0)]
+    pos = y0 > 1e-2 * y0.abs().max()        # clearly positive before dropout: kept or dropped, never ReLU-zeroed
+    kept_p, kept_n = (yp != 0) & pos, (yn != 0) & pos
+    assert torch.equal(kept_p, kept_n)      # the same dropout mask
+    frac = kept_p.sum().item() / pos.sum().item()
+    assert abs(frac - (1 - rate)) < 0.02, frac
+    ks = 1.0 / (1.0 - rate)
+    assert ((yp - y0 * ks).abs() - 2 ** -6 * (y0 * ks).abs())[kept_p].max().item() < 1e-3
+    assert ((yp - yn).abs() - 2 ** -7 * yn.abs()).max().item() < 1e-2
+
+
 @pytest.mark.parametrize("mode", ["mask", "addend_mask", "split_masks", "split_mask2", "two_chunks", "addend_only"])
 def test_halop_mask_addend_epilogue(mode):
     """Persistent halo kernel with the addend / ReLU-backward-mask epilogue (EPI 4: the adipose_v3 data
