@@ -47,7 +47,8 @@ def main():
             flags = ",".join(n for n in ("addend", "mask", "mask2", "accum", "bn_stats", "bn_reduce", "bn_apply", "out2")
                              if k.get(n) is not None) + (f",dil={k['dil']}" if k.get("dil", 1) != 1 else "") + \
                 (",up" if k.get("up") else "") + (f",drop={k['dropout_rate']}" if k.get("dropout_rate") else "")
-            log.append((_fn, tuple(a[0].shape), a[2] if len(a) > 2 else a[1].shape[0], flags,
+            nout = a[3] if _fn == "conv_wgrad" else a[2]   # (conv_fwd: srcA, W, nout; conv_wgrad: srcA, dY, dW, nout)
+            log.append((_fn, tuple(a[0].shape), nout, flags,
                         _lib.lib().adp_last_kernel().decode()))
             return r
         setattr(ops, fn, wrap)
