@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class AdpError(RuntimeError):
@@ -62,6 +62,8 @@ _S = C.c_size_t
 _SIGS = {
     "adp_abi_version": [],
     "adp_set_option": [C.c_char_p, _I],
+    "adp_timing": [_I],
+    "adp_timing_read": [_I, C.c_char_p, _I, C.POINTER(C.c_float), C.POINTER(C.c_int)],
     "adp_conv_fwd": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P],
     "adp_conv_wgrad": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P, _I, _P, _P, _P],
     "adp_conv_wgrad_bn": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), C.POINTER(BnBwdArgs), _P, _I, _P, _P, _P],
@@ -110,6 +112,11 @@ _SIGS = {
     "adp_forward": [_P, _P, _I, C.c_longlong, _F, _F, _I, _P, _P],
     "adp_train_step": [_P, _P, _P, _I, _P, _F, _P, _P],
     "adp_auc_metrics": [_S, _P, _P, _P, _P],
+    "adp_border_weight": [_I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "adp_weighted_loss_stats": [_S, _P, _P, _P, _P, _P, _P],
+    "adp_weighted_loss_grad": [_S, _P, _P, _P, _P, _P, _F, _F, _P, _P],
+    "adp_value_stats": [_S, _P, _P, _P, _P],
+    "adp_onehot_counts": [_I, _I, _P, _P, _P, _P],
     "adp_pack_weights_batch": [_I, _I, _P, _P],
     "adp_bn_apply_maxpool2": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "adp_head_sigmoid_bwd_bnr": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],

@@ -7,16 +7,56 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
+#include <vector>
 #include "../../include/adipose_hip.h"
 
 namespace adp {
 static thread_local std::string g_err;
 static thread_local char g_kernel[160] = "";
+static thread_local hipStream_t g_launch_stream = nullptr;
+
+// Per-launch timing of the conv kernels (adp_timing_*): set_kernel, which every conv launcher calls right
+// before its main kernel, records a start event on the launch stream; kernel_end, called right after that
+// kernel (before any fold / split reduce / bias-sum launch that follows it), records the end event. So the
+// pair brackets exactly the kernel rocprofv3 lists under the recorded name.
+struct TimedLaunch {
+  char name[160];
+  hipEvent_t e0, e1;
+};
+static std::mutex g_time_mu;
+static bool g_timing = false;
+static std::vector<TimedLaunch> g_timed;
+static std::vector<hipEvent_t> g_event_pool;
+static hipEvent_t pool_event() {
+  hipEvent_t e = nullptr;
+  if (!g_event_pool.empty()) {
+    e = g_event_pool.back();
+    g_event_pool.pop_back();
+  } else if (hipEventCreate(&e) != hipSuccess) {
+    e = nullptr;
+  }
+  return e;
+}
+void set_launch_stream(hipStream_t s) { g_launch_stream = s; }
 void set_kernel(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(g_kernel, sizeof(g_kernel), fmt, ap);
   va_end(ap);
+  std::lock_guard<std::mutex> lk(g_time_mu);
+  if (!g_timing) return;
+  TimedLaunch t{};
+  std::snprintf(t.name, sizeof(t.name), "%s", g_kernel);
+  t.e0 = pool_event();
+  t.e1 = nullptr;
+  if (t.e0 && hipEventRecord(t.e0, g_launch_stream) == hipSuccess) g_timed.push_back(t);
+}
+void kernel_end() {
+  std::lock_guard<std::mutex> lk(g_time_mu);
+  if (!g_timing || g_timed.empty() || g_timed.back().e1) return;
+  hipEvent_t e = pool_event();
+  if (e && hipEventRecord(e, g_launch_stream) == hipSuccess) g_timed.back().e1 = e;
 }
 void set_error(const std::string& msg) { g_err = msg; }
 int check_launch(const char* what) {
@@ -39,11 +79,12 @@ int option(const char* name, int dflt) {
 }
 int resident_grid(const void* kernel, int threads, size_t smem) {
   static std::mutex mu;
-  static std::map<std::pair<const void*, int>, int> cache;
+  // the occupancy depends on the block size and the dynamic LDS as well as the kernel and device
+  static std::map<std::tuple<const void*, int, int, size_t>, int> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_pair(kernel, dev);
+  auto key = std::make_tuple(kernel, dev, threads, smem);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   int per = 0, cus = 0;
@@ -66,3 +107,37 @@ extern "C" int adp_set_option(const char* name, int value) {
 extern "C" const char* adp_last_error(void) { return adp::g_err.c_str(); }
 extern "C" const char* adp_last_kernel(void) { return adp::g_kernel; }
 extern "C" int adp_abi_version(void) { return ADP_ABI_VERSION; }
+
+extern "C" int adp_timing(int mode) {
+  if (mode < 0 || mode > 2) { adp::set_error("adp_timing: mode 0 (stop), 1 (clear + record) or 2 (stop + clear)"); return -1; }
+  std::lock_guard<std::mutex> lk(adp::g_time_mu);
+  if (mode != 0) {
+    for (auto& t : adp::g_timed) {
+      adp::g_event_pool.push_back(t.e0);
+      if (t.e1) adp::g_event_pool.push_back(t.e1);
+    }
+    adp::g_timed.clear();
+  }
+  adp::g_timing = mode == 1;
+  return 0;
+}
+
+extern "C" int adp_timing_read(int max, char* names, int name_len, float* ms, int* n) {
+  if (!n || (max > 0 && (!names || !ms || name_len < 2))) { adp::set_error("adp_timing_read: bad arguments"); return -1; }
+  std::lock_guard<std::mutex> lk(adp::g_time_mu);
+  const int cnt = (int)adp::g_timed.size();
+  *n = cnt;
+  for (int i = 0; i < cnt && i < max; ++i) {
+    const auto& t = adp::g_timed[i];
+    float v = -1.f;   // -1: no end event (a launcher without kernel_end)
+    if (t.e1) {
+      if (hipEventSynchronize(t.e1) != hipSuccess || hipEventElapsedTime(&v, t.e0, t.e1) != hipSuccess) {
+        adp::set_error("adp_timing_read: event query failed");
+        return -2;
+      }
+    }
+    std::snprintf(names + (size_t)i * name_len, name_len, "%s", t.name);
+    ms[i] = v;
+  }
+  return 0;
+}

@@ -113,6 +113,10 @@ int option(const char* name, int dflt);  // runtime switches set through adp_set
 int resident_grid(const void* kernel, int threads, size_t smem = 0);
 // name of the kernel the last conv launch of this thread used (adp_last_kernel), printf-style
 void set_kernel(const char* fmt, ...);
+// per-launch timing (adp_timing): the stream of the conv launch in progress (set at the ABI entry), and the
+// end mark of its main kernel (call right after launching it; set_kernel marks the start)
+void set_launch_stream(hipStream_t s);
+void kernel_end();
 // Replicated per-channel accumulators for the BatchNorm sums (statistics of a conv output, or the
 // BN-backward dbeta/dgamma reductions). f32 atomics execute at the memory side and serialise per
 // address, so thousands of blocks adding into the same C floats queue behind each other (measured:
@@ -120,7 +124,12 @@ void set_kernel(const char* fmt, ...);
 // instead and stat_fold() sums the replicas into the caller's accumulators and re-zeroes them.
 // Per device, lazily allocated and zeroed; launches that use it must be ordered on one stream.
 constexpr int STAT_REPL = 64, STAT_CMAX = 2048;
-float* stat_scratch();   // [STAT_REPL][2][STAT_CMAX] f32, or nullptr (error set) if allocation failed
+float* stat_scratch();   // [STAT_REPL][2][STAT_CMAX] f32, or nullptr (error set) if allocation failed or a
+                         // deferred fold is pending
+// bn_defer_fold bookkeeping: a launch that leaves its sums in the replicas records (C, sum, stream); only the
+// adp_bn_finalize_fold with the same three may take the replicas next (stat_scratch_fold clears the record)
+int defer_fold_begin(int C, const float* sum, hipStream_t s);
+float* stat_scratch_fold(int C, const float* sum, hipStream_t s);
 // per-device growable scratch (slot 0: weight-gradient split partials); growing synchronises the device
 void* scratch(int slot, size_t bytes);
 int stat_fold(int C, float* dst0, float* dst1, hipStream_t s);   // elementwise.hip

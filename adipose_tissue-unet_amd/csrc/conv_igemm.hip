@@ -1041,7 +1041,9 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
 // after a launch whose epilogue added BatchNorm sums into the replicas: fold them into the caller's
 // accumulators (statistics: bn_sum / bn_sq; BN-backward reduction: bnr_dbeta / bnr_dgamma)
 int fold_stats(const FwdArgs& a, hipStream_t s) {
-  if (!a.stat || a.defer_fold) return 0;   // (deferred: adp_bn_finalize_fold folds them)
+  if (!a.stat) return 0;
+  if (a.defer_fold)   // (deferred: adp_bn_finalize_fold folds them)
+    return adp::defer_fold_begin(a.out_mode == 1 ? a.Cps : a.Nout, a.bn_sum, s);
   const int C = a.out_mode == 1 ? a.Cps : a.Nout;
   if (a.bnr_z) return adp::stat_fold(C, a.bnr_dbeta, a.bnr_dgamma, s);
   return adp::stat_fold(C, a.bn_sum, a.bn_sq, s);
@@ -1065,6 +1067,7 @@ int launch_fwd_f8(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) 
     adp::set_error("adp_conv_fwd(fp8): no fp8 kernel for this geometry (needs K == taps * Cin_s, K % 128 == 0)");
     return -1;
   }
+  adp::kernel_end();
   return adp::check_launch("adp_conv_fwd");
 }
 
@@ -1080,12 +1083,14 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
                            a.bnr_dgamma && a.bnr_dbeta && a.bnr_zs == a.out_stride && a.bnr_zs % 8 == 0 &&
                            a.Nout % 8 == 0),
               "adp_conv_fwd: fused BN-backward reduction needs out_mode 0, all bnr_* pointers, z stride == out stride");
-  ADP_REQUIRE(!(a.bn_sum || a.bnr_z) || a.stat, "adp_conv_fwd: BatchNorm accumulator replicas unavailable");
+  ADP_REQUIRE(!(a.bn_sum || a.bnr_z) || a.stat,
+              std::string("adp_conv_fwd: BatchNorm accumulator replicas unavailable: ") + adp_last_error());
   ADP_REQUIRE(!a.stat || (d->out_mode == 1 ? d->shuffle_c : d->Nout) <= adp::STAT_CMAX,
               "adp_conv_fwd: BatchNorm sums need <= 2048 channels");
   const int fast = adp::option("conv_fast", 2);
   if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB &&
       (adp::launch_fwd_cin8(a, s) || adp::launch_fwd_halo(a, s) || adp::launch_fwd_tap64(a, s))) {
+    adp::kernel_end();
     if (adp::check_launch("adp_conv_fwd")) return -2;
     return fold_stats(a, s);
   }
@@ -1119,6 +1124,7 @@ int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
       adp::set_kernel("igemm_fwd_glds_kernel<256, 64>");
       hipLaunchKernelGGL((igemm_fwd_glds_kernel<256, 64>), dim3(a.nblocks), dim3(NT), 0, s, a);
     }
+    adp::kernel_end();
     return adp::check_launch("adp_conv_fwd");
   }
   if (std::is_same<T, bf16>::value && fast >= 1) {
@@ -1135,6 +1141,7 @@ int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
       adp::set_kernel("igemm_fwd_bf16_kernel<256, 64>");
       hipLaunchKernelGGL((igemm_fwd_bf16_kernel<256, 64>), dim3(a.nblocks), dim3(NT), 0, s, a);
     }
+    adp::kernel_end();
     return adp::check_launch("adp_conv_fwd");
   }
   a.ntile_n = (a.Nout + BN - 1) / BN;
@@ -1142,6 +1149,7 @@ int launch_fwd_plain(FwdArgs& a, hipStream_t s, int fast) {
   a.nblocks = ntm * a.ntile_n;
   adp::set_kernel(std::is_same<T, bf16>::value ? "igemm_fwd_kernel<bf16>" : "igemm_fwd_kernel<float>");
   hipLaunchKernelGGL(igemm_fwd_kernel<T>, dim3(a.nblocks), dim3(NT), 0, s, a);
+  adp::kernel_end();
   return adp::check_launch("adp_conv_fwd");
 }
 
@@ -1176,6 +1184,12 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
   }
   if (std::is_same<T, bf16>::value && adp::option("conv_fast", 2) == 2 && !a.scA && !a.scB) {
     if (!adp::launch_wgrad_tap64(a, s)) {
+      if (a.bna_dA) {   // no kernel took the fused form: dY = bn_bwd_apply(dA, z) first, then the fallback
+        a.bna_dA = nullptr;
+        if (adp_bn_bwd_apply(ADP_BF16, (size_t)a.M, dy_stride, bn->dA, bn->z, bn->scale, bn->shift, bn->mean,
+                             bn->invstd, bn->gamma, bn->dgamma, bn->dbeta, bn->count, const_cast<void*>(dY), s))
+          return -2;
+      }
       const int TN = (a.Nout <= 64 && adp::option("wgrad_glds_tn64", 1)) ? 64 : 128, TK = TN == 64 ? 256 : 128;
       a.ntile_k = (a.K + TK - 1) / TK;
       a.ntile_n = (a.Nout + TN - 1) / TN;
@@ -1192,6 +1206,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
         { adp::set_kernel("igemm_wgrad_glds_kernel<128, 128>");
           hipLaunchKernelGGL((igemm_wgrad_glds_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a); }
     }
+    adp::kernel_end();   // (no-op when launch_wgrad_tap64 marked it before its split reduce)
     if (a.dB) {
       const int G = a.Nout / 8, lanes = NT / G;
       const int blocks = (int)std::min<long long>((a.M + lanes - 1) / lanes, 1024);
@@ -1226,6 +1241,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
     else
       { adp::set_kernel("igemm_wgrad_bf16_kernel<128, 128>");
         hipLaunchKernelGGL((igemm_wgrad_bf16_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a); }
+    adp::kernel_end();
     return adp::check_launch("adp_conv_wgrad");
   }
   a.ntile_k = (a.K + 63) / 64;
@@ -1239,6 +1255,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
   splits = (a.M + a.mchunk - 1) / a.mchunk;
   adp::set_kernel(std::is_same<T, bf16>::value ? "igemm_wgrad_kernel<bf16>" : "igemm_wgrad_kernel<float>");
   hipLaunchKernelGGL(igemm_wgrad_kernel<T>, dim3(tiles, splits), dim3(NT), 0, s, a);
+  adp::kernel_end();
   return adp::check_launch("adp_conv_wgrad");
 }
 }  // namespace
@@ -1246,6 +1263,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
 extern "C" int adp_conv_fwd(int dtype, const adp_conv_desc* d, const adp_conv_io* io, adp_stream_t st) {
   hipStream_t s = (hipStream_t)st;
   ADP_REQUIRE(d && io, "adp_conv_fwd: null descriptor");
+  adp::set_launch_stream(s);
   if (dtype == ADP_F32) return launch_fwd<float>(d, io, s);
   if (dtype == ADP_BF16) return launch_fwd<bf16>(d, io, s);
   if (dtype == ADP_FP8) return launch_fwd_f8(d, io, s);
@@ -1257,6 +1275,7 @@ extern "C" int adp_conv_wgrad_bn(int dtype, const adp_conv_desc* d, const adp_co
                                  void* dY, int dy_stride, float* dW, float* dB, adp_stream_t st) {
   hipStream_t s = (hipStream_t)st;
   ADP_REQUIRE(d && io && bn && bn->dA && bn->z && dY && dW, "adp_conv_wgrad_bn: null argument");
+  adp::set_launch_stream(s);
   ADP_REQUIRE(bn->scale && bn->shift && bn->mean && bn->invstd && bn->gamma && bn->dgamma && bn->dbeta && bn->count > 0,
               "adp_conv_wgrad_bn: BatchNorm vectors and count");
   ADP_REQUIRE(d->out_mode == 0 && dy_stride == d->Nout && dy_stride % 8 == 0,
@@ -1271,6 +1290,7 @@ extern "C" int adp_conv_wgrad(int dtype, const adp_conv_desc* d, const adp_conv_
                               int dy_stride, float* dW, float* dB, adp_stream_t st) {
   hipStream_t s = (hipStream_t)st;
   ADP_REQUIRE(d && io && dY && dW, "adp_conv_wgrad: null argument");
+  adp::set_launch_stream(s);
   if (dtype == ADP_F32) return launch_wgrad<float>(d, io, dY, dy_stride, dW, dB, s);
   if (dtype == ADP_BF16) return launch_wgrad<bf16>(d, io, dY, dy_stride, dW, dB, s);
   adp::set_error("adp_conv_wgrad: unknown dtype");

@@ -936,6 +936,7 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   else if (ra) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, true>), grid, block, 0, s, a);
   else if (!two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, false>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, false>), grid, block, 0, s, a);
+  adp::kernel_end();   // (the split reduce below is a kernel of its own in rocprofv3's list)
   if (a.part) {
     const size_t n4 = slab / 4;
     const int groups = (splits + WG_SG - 1) / WG_SG;
@@ -965,8 +966,10 @@ static bool halop_ok(const WgradArgs& a) {
 // its output block's dY tile, so only layers with at most wgrad_bna_maxch (default 2) 64-channel input
 // chunks take it (levels 0-1 of unet_bn; deeper layers re-read dA/z once per chunk)
 bool wgrad_bna_fusable(const WgradArgs& a) {
-  return a.bna_dA && a.bna_z && option("wgrad_bna", 1) && option("wgrad_halop_waves", 8) == 8 && halop_ok(a) &&
-         (a.CAs + a.CBs) / 64 <= option("wgrad_bna_maxch", 2);
+  // (launch_wgrad_tap64 takes the halo kernel only with wgrad_tap64 != 0: with it off, the fused form would
+  //  fall through to a kernel that reads a dY nothing has computed)
+  return a.bna_dA && a.bna_z && option("wgrad_tap64", 1) != 0 && option("wgrad_bna", 1) &&
+         option("wgrad_halop_waves", 8) == 8 && halop_ok(a) && (a.CAs + a.CBs) / 64 <= option("wgrad_bna_maxch", 2);
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 128x256 (8 waves, 64x64),
@@ -974,7 +977,7 @@ bool wgrad_bna_fusable(const WgradArgs& a) {
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   const int mode = option("wgrad_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
-  if (option("wgrad_cin8", 1) && !a.scA && a.CAs == 8 && a.CBs == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
+  if (option("wgrad_cin8", 1) && !a.bna_dA && !a.scA && a.CAs == 8 && a.CBs == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
       a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
       a.Nout == 64 && a.dy_mode == 0 && a.K == 72 && a.Kpad >= 72 && a.dy_stride % 8 == 0 && a.dy_stride >= 64) {
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
@@ -1015,6 +1018,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     }
     return 1;
   }
+  if (a.bna_dA) return 0;   // only the halo kernel computes dY itself (the caller runs the apply, then a fallback)
   const int Cin_s = a.CAs + a.CBs;
   if (a.scA || a.scB || a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 ||
       a.Kpad != a.K)

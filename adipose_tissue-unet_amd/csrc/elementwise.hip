@@ -831,11 +831,43 @@ __global__ void ema_kernel(size_t n, float* ema, const float* p, float d) {
 }  // namespace
 
 namespace adp {
-float* stat_scratch() {
+// a conv launch with bn_defer_fold leaves its BatchNorm sums in the replicas; until the matching
+// adp_bn_finalize_fold (same channel count, sum vector and stream) runs, no other launch may use them
+struct PendingFold { bool on = false; int C = 0; const float* sum = nullptr; hipStream_t s = nullptr; };
+static std::mutex g_fold_mu;
+static std::map<int, PendingFold>& pending_folds() {
+  static std::map<int, PendingFold> m;
+  return m;
+}
+int defer_fold_begin(int C, const float* sum, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { set_error("defer_fold: hipGetDevice failed"); return -2; }
+  std::lock_guard<std::mutex> lk(g_fold_mu);
+  pending_folds()[dev] = PendingFold{true, C, sum, s};
+  return 0;
+}
+static float* stat_scratch_impl(bool fold, int C, const float* sum, hipStream_t s) {
   static std::mutex mu;
   static std::map<int, float*> per_dev;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("stat_scratch: hipGetDevice failed"); return nullptr; }
+  {
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    PendingFold& pf = pending_folds()[dev];
+    if (fold) {
+      if (!pf.on || pf.C != C || pf.sum != sum || pf.s != s) {
+        set_error(pf.on ? "adp_bn_finalize_fold: does not match the pending deferred fold (channel count, sum "
+                          "vector or stream differ)"
+                        : "adp_bn_finalize_fold: no conv launch with bn_defer_fold is pending");
+        return nullptr;
+      }
+      pf.on = false;
+    } else if (pf.on) {
+      set_error("BatchNorm accumulator replicas hold the sums of a bn_defer_fold launch: adp_bn_finalize_fold "
+                "must run first");
+      return nullptr;
+    }
+  }
   std::lock_guard<std::mutex> lk(mu);
   auto it = per_dev.find(dev);
   if (it != per_dev.end()) return it->second;
@@ -849,6 +881,8 @@ float* stat_scratch() {
   per_dev[dev] = p;
   return p;
 }
+float* stat_scratch() { return stat_scratch_impl(false, 0, nullptr, nullptr); }
+float* stat_scratch_fold(int C, const float* sum, hipStream_t s) { return stat_scratch_impl(true, C, sum, s); }
 void* scratch(int slot, size_t bytes) {
   static std::mutex mu;
   static std::map<std::pair<int, int>, std::pair<void*, size_t>> bufs;
@@ -966,7 +1000,7 @@ extern "C" int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C, const
   const int blocks = (int)std::max<size_t>(1, std::min<size_t>((P + lanes - 1) / lanes,
                                                                (size_t)adp::option("pool_bnr_blocks", 2048)));
   float* stat = adp::stat_scratch();
-  ADP_REQUIRE(stat, adp_last_error());
+  if (!stat) return -1;
   DTYPE_SWITCH(dtype, T,
                if (src) hipLaunchKernelGGL((maxpool_bwd_bnr_kernel<T, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st,
                                            N, H, W, C, (const T*)src, (const T*)dpool, (const T*)addend, (T*)dsrc,
@@ -1048,8 +1082,8 @@ extern "C" int adp_bn_finalize_fold(int C, float count, float* sum, float* sq, c
   ADP_REQUIRE(C > 0 && C <= adp::STAT_CMAX && count > 0 && sum && sq && gamma && beta && scale && shift && mean &&
                   invstd,
               "adp_bn_finalize_fold: bad arguments (training statistics, C <= 2048)");
-  float* sc = adp::stat_scratch();
-  ADP_REQUIRE(sc, adp_last_error());
+  float* sc = adp::stat_scratch_fold(C, sum, (hipStream_t)st);
+  if (!sc) return -1;
   hipLaunchKernelGGL(bn_fold_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)st, C, sc, sum, sq,
                      count, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean, rvar);
   return adp::check_launch("adp_bn_finalize_fold");
@@ -1062,7 +1096,7 @@ extern "C" int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, con
   int lanes = TPB / (C / 8);
   int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 2048);
   float* stat = adp::stat_scratch();
-  ADP_REQUIRE(stat, adp_last_error());
+  if (!stat) return -1;
   DTYPE_SWITCH(dtype, T,
                hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, C,
                                   (const T*)dA, (const T*)z, sc, sh, mean, invstd, dgamma, dbeta, stat));

@@ -1,23 +1,29 @@
-// Handle-level C ABI: a native adipose_v3 inference engine for non-Python callers.
+// Handle-level C ABI: native engines for non-Python callers, one per topology preset.
 //
-//   adp_create(cfg, device, &h)          topology of AdiposeUNetV3.build_model (train_adipose_unet_v3.py:660-758,
-//                                         segmentation_inference.py:88-146) at tile S, activation buffers for
-//                                         cfg->max_batch images x TTA views, allocated once
-//   adp_set_param / adp_get_param         Keras layer names and layouts (kernel HWIO, bias), so a
-//                                         .weights.h5 maps 1:1 (slot 0 kernel, 1 bias)
+//   adp_create(cfg, device, &h)          ADP_PRESET_ADIPOSE_V3: AdiposeUNetV3.build_model (train_adipose_unet_v3.py:
+//                                         660-758, segmentation_inference.py:88-146) at tile S;
+//                                         ADP_PRESET_UNET_BN: the north-star L-level base-64 BatchNorm U-Net of
+//                                         BASELINE.json configs 2/3/5 (nets.UNetBN); buffers for cfg->max_batch
+//                                         images x TTA views, allocated once
+//   adp_set_param / adp_get_param         Keras layer names and layouts, so a .weights.h5 maps 1:1 (adipose_v3:
+//                                         slot 0 kernel, 1 bias; unet_bn: conv 0 kernel, 1 gamma, 2 beta,
+//                                         3 moving mean, 4 moving variance; ConvTranspose / head 0 kernel, 1 bias)
 //   adp_forward(h, images, n, ...)        predict_single (segmentation_inference.py:153-158) with optional
 //                                         TTA (:181-229): z-score + view transform on load, all views of a
 //                                         tile batched in one forward, inverse views averaged
 //   adp_train_step(h, x, y, n, cfg, lr)   one model.net.fit step (train_adipose_unet_v3.py:1316-1324): forward
-//                                         with dropout, OHEM / BCE+Dice / deep-supervision losses
-//                                         (:217-363, :780-879), backward, [RCCL SUM all-reduce], Adam/AdamW
+//                                         (adipose_v3 with dropout; unet_bn with batch statistics), OHEM /
+//                                         BCE+Dice / deep-supervision losses (:217-363, :780-879), backward with
+//                                         the bucketed RCCL SUM all-reduce of the gradients on a communication
+//                                         stream (each bucket launched as soon as the backward has finished its
+//                                         layers, overlapping the remaining backward convs), Adam / AdamW
 //   adp_set_comm / adp_comm_*             data parallel over an RCCL communicator (loaded at run time)
 //   adp_destroy(h)
 //
-// The engine is host code over the library's own launchers (adp_conv_fwd, adp_maxpool2_fwd,
-// adp_head_*_fwd, adp_prep_input, adp_tta_merge): the same kernels and schedule as nets.AdiposeV3Net.
-// One handle per device and thread; calls are stream-ordered on the caller's stream (weights are
-// uploaded synchronously by the first adp_forward after an adp_set_param).
+// The engines are host code over the library's own launchers (adp_conv_fwd, adp_conv_wgrad(_bn), adp_bn_*,
+// adp_maxpool2_*, adp_head_*, adp_loss_*, adp_adam, adp_prep_input, adp_tta_merge): the same kernels and
+// schedules as nets.AdiposeV3Net / nets.UNetBN with trainer.Trainer / GradBuckets. One handle per device and
+// thread; calls are stream-ordered on the caller's stream.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>   // types and enums only: RCCL itself is loaded with dlopen
@@ -26,6 +32,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -58,6 +65,19 @@ struct HeadL {
   float* W = nullptr;   // [nout][cin]
   float* b = nullptr;
   size_t offW = 0, offB = 0;
+};
+
+// unet_bn layers (nets.UNetBN.build_layers): kind 0 = 3x3 conv + BatchNorm (no bias), 1 = ConvTranspose 2x2/s2
+// (1x1 GEMM over 4*C outputs + pixel-shuffle store, bias), 2 = 1x1 sigmoid head
+struct BnLayer {
+  std::string name;
+  int kind = 0, level = 0;
+  std::vector<int> cin, cin_s;   // logical / stored input channels per concat part
+  int Cin_s = 0, cout = 0, cout_s = 0, taps = 9, Nout = 0, K = 0, Kpad = 0, Npad = 0, dNpad = 0, dKpad = 0;
+  size_t offW = 0, offB = 0, offG = 0, offBeta = 0;   // flat-buffer offsets (nets.ParamStore layout)
+  float* st = nullptr;                                // [6][cout_s]: sum, sq, scale, shift, mean, invstd
+  float *rmean = nullptr, *rvar = nullptr;            // running statistics (PyTorch semantics)
+  void* Wd = nullptr;                                 // data-gradient weights [dNpad][dKpad]
 };
 
 #define CK(x)                                              \
@@ -133,7 +153,44 @@ struct adp_handle {
   int step = 0;
   void* comm = nullptr;
 
+  // ---- unet_bn preset (nets.UNetBN): layers, the flat parameter buffers P/G/Mo/Vo (allocated at create),
+  // a compute-dtype mirror of P (the forward weights: one cast per step), the per-step statistic arena
+  std::vector<BnLayer> bl;
+  std::map<std::string, int> bl_idx;
+  int levels = 0, base = 64, in_ch = 3;
+  void* Pc = nullptr;                 // bf16 mirror of P (forward weights of every layer)
+  float *stat_fwd = nullptr, *stat_bwd = nullptr;
+  size_t n_stat_fwd = 0, n_stat_bwd = 0;
+  std::vector<float*> dtsum;          // per decoder level: [2][Cin_s] channel sums of the concat data gradient
+  static constexpr float bn_eps = 1e-5f, bn_momentum = 0.1f;
+
+  // ---- data-parallel gradient buckets (trainer.GradBuckets): reverse flat-buffer order, ~16 MB each; a bucket
+  // is SUM-all-reduced on the communication stream as soon as the backward has finished all its layers
+  struct Bucket {
+    size_t lo = 0, hi = 0;
+    std::set<int> layers;
+    int pending = 0;
+    bool launched = false;
+  };
+  std::vector<Bucket> buckets;
+  std::map<int, int> bucket_of;       // layer id -> bucket
+  std::vector<std::pair<size_t, size_t>> layer_span;   // layer id -> [lo, hi) in the flat buffer
+  hipStream_t cstream = nullptr;      // RCCL stream
+  std::vector<hipEvent_t> bev;        // one "layers done" event per bucket
+  hipEvent_t comm_done = nullptr;
+  bool dp_active = false;
+  std::string comm_err;
+
   ~adp_handle() {
+    for (auto& l : bl) (void)hipFree(l.Wd);
+    if (!bl.empty()) {
+      for (auto& l : bl) { (void)hipFree(l.rmean); (void)hipFree(l.rvar); }
+      (void)hipFree(Pc);
+      (void)hipFree(stat_fwd);
+    }
+    for (auto e : bev) (void)hipEventDestroy(e);
+    if (comm_done) (void)hipEventDestroy(comm_done);
+    if (cstream) (void)hipStreamDestroy(cstream);
     for (auto& l : dense) {
       if (!train_on || cfg.dtype != ADP_DTYPE_F32) (void)hipFree(l.W);
       if (!train_on) (void)hipFree(l.b);
@@ -295,6 +352,11 @@ struct adp_handle {
       off += rup64(h.nout);
     }
     nflat = off;
+    // layer ids for the gradient buckets: dense layers, then heads; each owns [offW, end of its bias)
+    layer_span.clear();
+    for (auto& l : dense) layer_span.push_back({l.offW, l.offB + rup64(l.cout_s)});
+    for (auto& h : heads) layer_span.push_back({h.offW, h.offB + rup64(h.nout)});
+    build_buckets();
     for (float** p : {&P, &G, &Mo, &Vo}) {
       CK(hipMalloc(reinterpret_cast<void**>(p), sizeof(float) * nflat));
       CK(hipMemset(*p, 0, sizeof(float) * nflat));
@@ -395,7 +457,8 @@ struct adp_handle {
     d.mask_scale = d.mask2_scale = 1.f;
     io.srcA = srcA;
     io.srcB = srcB;
-    return adp_conv_wgrad(cfg.dtype, &d, &io, dZ, l.cout_s, G + l.offW, G + l.offB, s);
+    CL(adp_conv_wgrad(cfg.dtype, &d, &io, dZ, l.cout_s, G + l.offW, G + l.offB, s));
+    return ready(dense_id(name), s);
   }
 
   // data gradient (nets.UNetEngine.dgrad): a forward-shaped launch over dZ with the flipped weights;
@@ -518,6 +581,7 @@ struct adp_handle {
     const HeadL& h = heads[head_idx.at("output_softmax")];
     CL(adp_head_softmax2_bwd(dt, (size_t)N * S * S, ch[0], h.cin, b("u1"), h.W, nullptr, nullptr, b<float>("p_main"),
                              b<float>("dp_main"), nullptr, b("u1"), keep, b("g_u1"), G + h.offW, G + h.offB, s));
+    CL(ready(head_id("output_softmax"), s));
     const void* aux_add[3] = {nullptr, nullptr, nullptr};   // by level: [1] u2, [2] u3
     if (cfg.deep_supervision) {
       const char* src[2] = {"u3", "u2"};
@@ -534,6 +598,7 @@ struct adp_handle {
         CL(adp_head_sigmoid_bwd(dt, (size_t)N * z * z, ch[lv[k]], a.cin, b(src[k]), a.W, nullptr, nullptr,
                                 b<float>(sb[k]), b<float>(dsb[k]), nullptr, nullptr, 1.f, b(dx[k]), G + a.offW,
                                 G + a.offB, s));
+        CL(ready(head_id(hn[k]), s));
         aux_add[lv[k]] = b(dx[k]);
       }
     }
@@ -597,16 +662,676 @@ struct adp_handle {
     }
     return 0;
   }
+
+  // ================================================================ data-parallel gradient buckets
+  // trainer.GradBuckets: layers in reverse flat-buffer order (the order the backward finishes them), cut into
+  // buckets of ~bucket_bytes; a bucket's SUM all-reduce is issued on the communication stream, after an event
+  // on the compute stream, as soon as every non-frozen layer of it has reported (ready), so it overlaps the
+  // backward launches that follow; dp_finish issues the rest and makes the compute stream wait for all of them
+  void build_buckets(size_t bucket_bytes = (size_t)16 << 20) {
+    buckets.clear();
+    bucket_of.clear();
+    std::vector<int> order(layer_span.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return layer_span[a].first > layer_span[b].first; });
+    Bucket cur;
+    bool open = false;
+    for (int id : order) {
+      const size_t lo = layer_span[id].first, hi = layer_span[id].second;
+      if (open && (cur.hi - lo) * sizeof(float) > bucket_bytes) {
+        buckets.push_back(cur);
+        open = false;
+      }
+      if (!open) {
+        cur = Bucket();
+        cur.hi = hi;
+        open = true;
+      }
+      cur.lo = lo;
+      cur.layers.insert(id);
+    }
+    if (open) buckets.push_back(cur);
+    for (size_t b = 0; b < buckets.size(); ++b)
+      for (int id : buckets[b].layers) bucket_of[id] = (int)b;
+  }
+  std::vector<std::set<int>> pend;
+  int dp_begin(const std::set<int>& frozen) {
+    dp_active = false;
+    if (!comm) return 0;
+    if (!cstream) {
+      CK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+      CK(hipEventCreateWithFlags(&comm_done, hipEventDisableTiming));
+    }
+    while (bev.size() < buckets.size()) {
+      hipEvent_t e = nullptr;
+      CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      bev.push_back(e);
+    }
+    pend.assign(buckets.size(), {});
+    for (size_t b = 0; b < buckets.size(); ++b) {
+      buckets[b].launched = false;
+      for (int id : buckets[b].layers)
+        if (!frozen.count(id)) pend[b].insert(id);
+    }
+    dp_active = true;
+    return 0;
+  }
+  int dp_launch(int bi, hipStream_t s) {
+    Bucket& bk = buckets[bi];
+    bk.launched = true;
+    CK(hipEventRecord(bev[bi], s));
+    CK(hipStreamWaitEvent(cstream, bev[bi], 0));
+    NC(rccl().allreduce(G + bk.lo, G + bk.lo, bk.hi - bk.lo, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm),
+                        cstream));
+    return 0;
+  }
+  // the layer's parameter gradients are final in stream order on s
+  int ready(int id, hipStream_t s) {
+    if (!dp_active) return 0;
+    auto it = bucket_of.find(id);
+    if (it == bucket_of.end()) return 0;
+    const int bi = it->second;
+    pend[bi].erase(id);
+    if (pend[bi].empty() && !buckets[bi].launched) return dp_launch(bi, s);
+    return 0;
+  }
+  int dp_finish(hipStream_t s) {
+    if (!dp_active) return 0;
+    for (size_t b = 0; b < buckets.size(); ++b)   // buckets whose layers never reported (frozen only)
+      if (!buckets[b].launched) CL(dp_launch((int)b, s));
+    CK(hipEventRecord(comm_done, cstream));
+    CK(hipStreamWaitEvent(s, comm_done, 0));
+    dp_active = false;
+    return 0;
+  }
+  int dense_id(const char* name) const { return dense_idx.at(name); }
+  int head_id(const char* name) const { return (int)dense.size() + head_idx.at(name); }
+
+  // ================================================================ unet_bn (nets.UNetBN)
+  int ch_of(int lvl) const { return base << lvl; }
+  int side(int lvl) const { return S >> lvl; }
+  BnLayer& L(const std::string& n) { return bl[bl_idx.at(n)]; }
+  void* wfwd(const BnLayer& l) {   // forward-layout weights in the compute dtype
+    return cfg.dtype == ADP_DTYPE_F32 ? static_cast<void*>(P + l.offW)
+                                      : static_cast<void*>(static_cast<char*>(Pc) + l.offW * es);
+  }
+  void add_bl(const std::string& name, int kind, int level, std::vector<int> cin, int cout) {
+    BnLayer l;
+    l.name = name;
+    l.kind = kind;
+    l.level = level;
+    l.cin = cin;
+    for (int c : cin) l.cin_s.push_back(round_up(c, 8));
+    for (int c : l.cin_s) l.Cin_s += c;
+    l.cout = cout;
+    l.cout_s = round_up(cout, 8);
+    if (kind == 0) {
+      l.taps = 9;
+      l.Nout = l.cout_s;
+    } else if (kind == 1) {
+      l.taps = 1;
+      l.Nout = 4 * l.cout_s;
+    } else {
+      l.taps = 1;
+      l.Nout = 1;
+    }
+    l.K = l.taps * l.Cin_s;
+    l.Kpad = round_up(l.K, 32);
+    l.Npad = round_up(l.Nout, 64);
+    l.dNpad = round_up(l.Cin_s, 64) + (l.cin.size() > 1 ? 64 : 0);
+    l.dKpad = round_up((kind == 1 ? 4 : l.taps) * l.cout_s, 32);
+    bl_idx[name] = (int)bl.size();
+    bl.push_back(std::move(l));
+  }
+
+  int create_unet_bn() {
+    const int Lv = levels;
+    int cin = in_ch;
+    for (int i = 0; i < Lv; ++i) {
+      add_bl("enc" + std::to_string(i) + "_conv1", 0, i, {cin}, ch_of(i));
+      add_bl("enc" + std::to_string(i) + "_conv2", 0, i, {ch_of(i)}, ch_of(i));
+      cin = ch_of(i);
+    }
+    for (int i = Lv - 2; i >= 0; --i) {
+      const std::string n = "dec" + std::to_string(i);
+      add_bl(n + "_up", 1, i, {ch_of(i + 1)}, ch_of(i));
+      add_bl(n + "_conv1", 0, i, {ch_of(i), ch_of(i)}, ch_of(i));
+      add_bl(n + "_conv2", 0, i, {ch_of(i)}, ch_of(i));
+    }
+    add_bl("head", 2, 0, {ch_of(0)}, 1);
+    // flat layout of nets.ParamStore (W, [b], [gamma, beta] per layer, 64-float aligned slices)
+    size_t off = 0;
+    for (auto& l : bl) {
+      const size_t lo = off;
+      l.offW = off;
+      off += rup64(l.kind == 2 ? (size_t)l.cin[0] : (size_t)l.Npad * l.Kpad);
+      if (l.kind == 0) {
+        l.offG = off;
+        off += rup64(l.cout_s);
+        l.offBeta = off;
+        off += rup64(l.cout_s);
+      } else {
+        l.offB = off;
+        off += rup64(l.kind == 2 ? 1 : l.cout_s);
+      }
+      layer_span.push_back({lo, off});
+    }
+    nflat = off;
+    for (float** p : {&P, &G, &Mo, &Vo}) {
+      CK(hipMalloc(reinterpret_cast<void**>(p), sizeof(float) * nflat));
+      CK(hipMemset(*p, 0, sizeof(float) * nflat));
+    }
+    if (cfg.dtype != ADP_DTYPE_F32) {
+      CK(hipMalloc(&Pc, (size_t)es * nflat));
+      CK(hipMemset(Pc, 0, (size_t)es * nflat));
+    }
+    n_stat_fwd = 0;
+    n_stat_bwd = 0;
+    for (auto& l : bl) {
+      if (l.kind == 0) n_stat_fwd += 6 * (size_t)l.cout_s;
+      if (l.kind == 0 && l.cin.size() > 1) n_stat_bwd += 2 * (size_t)l.Cin_s;
+    }
+    CK(hipMalloc(reinterpret_cast<void**>(&stat_fwd), sizeof(float) * (n_stat_fwd + n_stat_bwd)));
+    CK(hipMemset(stat_fwd, 0, sizeof(float) * (n_stat_fwd + n_stat_bwd)));
+    stat_bwd = stat_fwd + n_stat_fwd;
+    size_t so = 0, sb = 0;
+    dtsum.assign(Lv > 1 ? Lv - 1 : 0, nullptr);
+    for (auto& l : bl) {
+      if (l.kind == 0) {
+        l.st = stat_fwd + so;
+        so += 6 * (size_t)l.cout_s;
+        CK(hipMalloc(reinterpret_cast<void**>(&l.rmean), sizeof(float) * l.cout_s));
+        CK(hipMalloc(reinterpret_cast<void**>(&l.rvar), sizeof(float) * l.cout_s));
+        CK(hipMemset(l.rmean, 0, sizeof(float) * l.cout_s));
+        CL(adp_fill_f32(l.cout_s, 1.f, l.rvar, nullptr));
+        CL(adp_fill_f32(l.cout_s, 1.f, P + l.offG, nullptr));   // Keras / torch BatchNorm init: gamma 1
+        if (l.cin.size() > 1) {
+          dtsum[l.level] = stat_bwd + sb;
+          sb += 2 * (size_t)l.Cin_s;
+        }
+      }
+      if (l.name != "enc0_conv1" && l.kind != 2) {
+        CK(hipMalloc(&l.Wd, (size_t)l.dNpad * l.dKpad * es));
+        CK(hipMemset(l.Wd, 0, (size_t)l.dNpad * l.dKpad * es));
+      }
+    }
+    CK(hipDeviceSynchronize());
+    // activations (nets.UNetBN.alloc) and the gradient buffers of its backward, for max_batch images
+    const size_t B_ = B;
+    auto act = [&](const std::string& n, int lvl) {
+      return alloc(n.c_str(), B_ * side(lvl) * side(lvl) * ch_of(lvl) * es);
+    };
+    int rc = alloc("x", B_ * S * S * 8 * es);
+    for (int i = 0; i < Lv && !rc; ++i) {
+      const std::string k = std::to_string(i);
+      rc = act("z" + k + "_1", i) || act("z" + k + "_2", i) || act("az" + k + "_1", i) || act("az" + k + "_2", i) ||
+           act("dA_z" + k + "_2", i) || act("dz_z" + k + "_2", i) || act("dA_z" + k + "_1", i) ||
+           act("dz_z" + k + "_1", i);
+      if (!rc && i < Lv - 1)
+        rc = act("y" + k + "_1", i) || act("y" + k + "_2", i) || act("ay" + k + "_1", i) || act("ay" + k + "_2", i) ||
+             act("t" + k, i) || act("dz_y" + k + "_2", i) || act("dA_y" + k + "_1", i) ||
+             act("dz_y" + k + "_1", i) || act("skip" + k, i) || act("dt" + k, i) || act("dA_up" + k, i + 1) ||
+             alloc(("pool" + k).c_str(), B_ * side(i + 1) * side(i + 1) * ch_of(i) * es) ||
+             alloc(("dpool" + k).c_str(), B_ * side(i + 1) * side(i + 1) * ch_of(i) * es);
+    }
+    if (rc) return rc;
+    rc = alloc("p", B_ * S * S * 4) || alloc("dp_main", B_ * S * S * 4) || alloc("probs", B_ * S * S * 4) ||
+         alloc("rows", B_ * S * 3 * 4) || alloc("coef", B_ * S * 3 * 4) || alloc("stats", 3 * 8 * 8) ||
+         alloc("lossbuf", 4 * 8);
+    if (rc) return rc;
+    build_buckets();
+    train_on = true;
+    dirty = false;
+    return 0;
+  }
+
+  // -- launch helpers (the descriptors ops.conv_fwd / ops.conv_wgrad build for nets.UNetBN)
+  static adp_conv_desc desc3(int N, int H, const BnLayer& l) {
+    adp_conv_desc d{};
+    d.N = N;
+    d.Hs = d.Ws = H;
+    d.CA_stride = l.cin_s[0];
+    d.CB_stride = l.cin_s.size() > 1 ? l.cin_s[1] : 0;
+    d.Ho = d.Wo = H;
+    d.stride = 1;
+    d.kh = d.kw = 3;
+    d.dil = 1;
+    d.pad = 1;
+    d.Nout = l.cout_s;
+    d.out_stride = l.cout_s;
+    d.mask_scale = d.mask2_scale = 1.f;
+    return d;
+  }
+  float* stv(const BnLayer& l, int k) const { return l.st + (size_t)k * l.cout_s; }
+  // conv -> BatchNorm statistics (epilogue, folded by the finalize) -> scale / shift -> relu(bn) materialised
+  // (with its 2x2 max-pool when pool != nullptr; act == nullptr: the consumer applies it on load)
+  int bn_conv(const std::string& name, int N, const void* srcA, const void* srcB, void* out, void* act, void* pool,
+              bool train, hipStream_t s) {
+    BnLayer& l = L(name);
+    const int H = side(l.level), C = l.cout_s;
+    adp_conv_desc d = desc3(N, H, l);
+    adp_conv_io io{};
+    io.srcA = srcA;
+    io.srcB = srcB;
+    io.W = wfwd(l);
+    io.out = out;
+    if (train) {
+      io.bn_sum = stv(l, 0);
+      io.bn_sqsum = stv(l, 1);
+      d.bn_defer_fold = 1;
+    }
+    CL(adp_conv_fwd(cfg.dtype, &d, &io, s));
+    if (train)
+      CL(adp_bn_finalize_fold(C, (float)((double)N * H * H), stv(l, 0), stv(l, 1), P + l.offG, P + l.offBeta, bn_eps,
+                              bn_momentum, stv(l, 2), stv(l, 3), stv(l, 4), stv(l, 5), l.rmean, l.rvar, s));
+    else   // eval: (count < 0) the running statistics stand in for the batch sums
+      CL(adp_bn_finalize(C, -1.f, l.rmean, l.rvar, P + l.offG, P + l.offBeta, bn_eps, 0.f, stv(l, 2), stv(l, 3),
+                         stv(l, 4), stv(l, 5), nullptr, nullptr, s));
+    if (pool) CL(adp_bn_apply_maxpool2(cfg.dtype, N, H, H, C, out, stv(l, 2), stv(l, 3), act, pool, s));
+    else if (act) CL(adp_bn_apply(cfg.dtype, (size_t)N * H * H, C, out, stv(l, 2), stv(l, 3), act, s));
+    return 0;
+  }
+  int convt_fwd(const std::string& name, int N, const void* src, void* out, hipStream_t s) {
+    BnLayer& l = L(name);
+    adp_conv_desc d{};
+    d.N = N;
+    d.Hs = d.Ws = d.Ho = d.Wo = side(l.level + 1);
+    d.CA_stride = l.cin_s[0];
+    d.stride = 1;
+    d.kh = d.kw = 1;
+    d.dil = 1;
+    d.pad = 0;
+    d.Nout = l.Nout;
+    d.out_stride = l.cout_s;
+    d.out_mode = 1;
+    d.shuffle_c = l.cout_s;
+    d.mask_scale = d.mask2_scale = 1.f;
+    adp_conv_io io{};
+    io.srcA = src;
+    io.W = wfwd(l);
+    io.bias = P + l.offB;
+    io.out = out;
+    return adp_conv_fwd(cfg.dtype, &d, &io, s);
+  }
+  int bn_forward(int N, bool train, hipStream_t s) {
+    if (cfg.dtype != ADP_DTYPE_F32) CL(adp_cast(ADP_DTYPE_F32, cfg.dtype, nflat, P, Pc, s));
+    if (train) CL(adp_fill_f32(n_stat_fwd, 0.f, stat_fwd, s));
+    const int Lv = levels;
+    const void* src = b("x");
+    for (int i = 0; i < Lv; ++i) {
+      const std::string k = std::to_string(i);
+      CL(bn_conv("enc" + k + "_conv1", N, src, nullptr, b(("z" + k + "_1").c_str()), b(("az" + k + "_1").c_str()),
+                 nullptr, train, s));
+      CL(bn_conv("enc" + k + "_conv2", N, b(("az" + k + "_1").c_str()), nullptr, b(("z" + k + "_2").c_str()),
+                 b(("az" + k + "_2").c_str()), i < Lv - 1 ? b(("pool" + k).c_str()) : nullptr, train, s));
+      if (i < Lv - 1) src = b(("pool" + k).c_str());
+    }
+    const void* prev = b(("az" + std::to_string(Lv - 1) + "_2").c_str());
+    for (int i = Lv - 2; i >= 0; --i) {
+      const std::string k = std::to_string(i);
+      CL(convt_fwd("dec" + k + "_up", N, prev, b(("t" + k).c_str()), s));
+      CL(bn_conv("dec" + k + "_conv1", N, b(("az" + k + "_2").c_str()), b(("t" + k).c_str()),
+                 b(("y" + k + "_1").c_str()), b(("ay" + k + "_1").c_str()), nullptr, train, s));
+      // level 0: relu(bn(y0_2)) is only read by the head, which applies it on load
+      CL(bn_conv("dec" + k + "_conv2", N, b(("ay" + k + "_1").c_str()), nullptr, b(("y" + k + "_2").c_str()),
+                 i == 0 ? nullptr : b(("ay" + k + "_2").c_str()), nullptr, train, s));
+      prev = b(("ay" + k + "_2").c_str());
+    }
+    const BnLayer& h = L("head");
+    const BnLayer& l0 = L("dec0_conv2");
+    CL(adp_head_sigmoid_fwd(cfg.dtype, (size_t)N * S * S, l0.cout_s, h.cin[0], b("y0_2"), P + h.offW, P + h.offB,
+                            stv(l0, 2), stv(l0, 3), b<float>("p"), s));
+    return 0;
+  }
+
+  // -- backward launches
+  int bn_dgrad(const std::string& name, int N, const void* dZ, void* out, const std::string& red, const void* redz,
+               hipStream_t s) {
+    BnLayer& l = L(name);
+    const int H = side(l.level);
+    adp_conv_desc d = desc3(N, H, l);
+    d.CA_stride = l.cout_s;
+    d.CB_stride = 0;
+    d.Nout = l.Cin_s;
+    d.out_stride = l.Cin_s;
+    adp_conv_io io{};
+    io.srcA = dZ;
+    io.W = l.Wd;
+    io.out = out;
+    if (!red.empty()) {   // the BatchNorm-backward reduction of the layer `out` is the gradient of
+      BnLayer& r = L(red);
+      d.bnr_stride = r.cout_s;
+      io.bnr_z = redz;
+      io.bnr_scale = stv(r, 2);
+      io.bnr_shift = stv(r, 3);
+      io.bnr_mean = stv(r, 4);
+      io.bnr_invstd = stv(r, 5);
+      io.bnr_dgamma = G + r.offG;
+      io.bnr_dbeta = G + r.offBeta;
+    }
+    return adp_conv_fwd(cfg.dtype, &d, &io, s);
+  }
+  int convt_dgrad(const std::string& name, int N, const void* dZ, void* out, const std::string& red, const void* redz,
+                  hipStream_t s) {
+    BnLayer& l = L(name);
+    const int H = side(l.level + 1);
+    adp_conv_desc d{};
+    d.N = N;
+    d.Hs = d.Ws = 2 * H;
+    d.CA_stride = l.cout_s;
+    d.Ho = d.Wo = H;
+    d.stride = 2;
+    d.kh = d.kw = 2;
+    d.dil = 1;
+    d.pad = 0;
+    d.Nout = l.Cin_s;
+    d.out_stride = l.Cin_s;
+    d.mask_scale = d.mask2_scale = 1.f;
+    adp_conv_io io{};
+    io.srcA = dZ;
+    io.W = l.Wd;
+    io.out = out;
+    BnLayer& r = L(red);
+    d.bnr_stride = r.cout_s;
+    io.bnr_z = redz;
+    io.bnr_scale = stv(r, 2);
+    io.bnr_shift = stv(r, 3);
+    io.bnr_mean = stv(r, 4);
+    io.bnr_invstd = stv(r, 5);
+    io.bnr_dgamma = G + r.offG;
+    io.bnr_dbeta = G + r.offBeta;
+    return adp_conv_fwd(cfg.dtype, &d, &io, s);
+  }
+  // weight gradient of a BatchNorm conv over dz = bn_bwd_apply(dA, z) (computed inside the launch where the halo
+  // kernel takes the shape, adp_conv_wgrad_bn); dA == nullptr: dz is already stored
+  int bn_wgrad(const std::string& name, int N, const void* srcA, const void* srcB, const void* dA, const void* z,
+               void* dz, hipStream_t s) {
+    BnLayer& l = L(name);
+    const int H = side(l.level);
+    adp_conv_desc d = desc3(N, H, l);
+    adp_conv_io io{};
+    io.srcA = srcA;
+    io.srcB = srcB;
+    if (dA) {
+      adp_bn_bwd_args a{};
+      a.dA = dA;
+      a.z = z;
+      a.scale = stv(l, 2);
+      a.shift = stv(l, 3);
+      a.mean = stv(l, 4);
+      a.invstd = stv(l, 5);
+      a.gamma = P + l.offG;
+      a.dgamma = G + l.offG;
+      a.dbeta = G + l.offBeta;
+      a.count = (float)((double)N * H * H);
+      CL(adp_conv_wgrad_bn(cfg.dtype, &d, &io, &a, dz, l.cout_s, G + l.offW, nullptr, s));
+    } else {
+      CL(adp_conv_wgrad(cfg.dtype, &d, &io, dz, l.cout_s, G + l.offW, nullptr, s));
+    }
+    return ready(bl_idx.at(name), s);
+  }
+  int bn_backward(int N, hipStream_t s) {
+    const int dt = cfg.dtype, Lv = levels;
+    // data-gradient weights of every layer but the input conv and the head, batched
+    std::vector<adp_pack_job> jobs;
+    for (auto& l : bl) {
+      if (!l.Wd) continue;
+      adp_pack_job j{};
+      j.src = P + l.offW;
+      j.dst = l.Wd;
+      j.taps = l.kind == 1 ? 1 : l.taps;
+      j.Cin_s = l.Cin_s;
+      j.Nout = l.kind == 1 ? l.Nout : l.cout_s;
+      j.src_kpad = l.Kpad;
+      j.dst_rows = l.dNpad;
+      j.dst_kpad = l.dKpad;
+      jobs.push_back(j);
+    }
+    for (size_t i = 0; i < jobs.size(); i += ADP_PACK_MAX_JOBS)
+      CL(adp_pack_weights_batch(dt, (int)std::min<size_t>(ADP_PACK_MAX_JOBS, jobs.size() - i), jobs.data() + i, s));
+    const size_t M0 = (size_t)N * S * S;
+    BnLayer& h = L("head");
+    BnLayer& l0 = L("dec0_conv2");
+    // head backward with dec0_conv2's BatchNorm-backward reduction fused; dA is not stored (recomputed below)
+    CL(adp_head_sigmoid_bwd_bnr(dt, M0, l0.cout_s, h.cin[0], b("y0_2"), P + h.offW, stv(l0, 2), stv(l0, 3),
+                                stv(l0, 4), stv(l0, 5), b<float>("p"), b<float>("dp_main"), nullptr, G + h.offW,
+                                G + h.offB, G + l0.offG, G + l0.offBeta, s));
+    CL(ready(bl_idx.at("head"), s));
+    CL(adp_fill_f32(n_stat_bwd, 0.f, stat_bwd, s));
+    const void* cur_dA = nullptr;
+    const void* bott_dA = nullptr;
+    std::vector<void*> skip(Lv, nullptr);
+    for (int i = 0; i < Lv - 1; ++i) {
+      const std::string k = std::to_string(i), dn = "dec" + k;
+      void* dz = b(("dz_y" + k + "_2").c_str());
+      if (!cur_dA) {   // level 0: dA = dL/d relu(bn(y0_2)) recomputed from the head (bit-identical dz)
+        CL(adp_bn_bwd_apply_head(dt, M0, l0.cout_s, h.cin[0], P + h.offW, b<float>("p"), b<float>("dp_main"),
+                                 b("y0_2"), stv(l0, 2), stv(l0, 3), stv(l0, 4), stv(l0, 5), P + l0.offG, G + l0.offG,
+                                 G + l0.offBeta, (float)M0, dz, s));
+        CL(bn_wgrad(dn + "_conv2", N, b(("ay" + k + "_1").c_str()), nullptr, nullptr, nullptr, dz, s));
+      } else {
+        CL(bn_wgrad(dn + "_conv2", N, b(("ay" + k + "_1").c_str()), nullptr, cur_dA, b(("y" + k + "_2").c_str()), dz,
+                    s));
+      }
+      void* dA1 = b(("dA_y" + k + "_1").c_str());
+      CL(bn_dgrad(dn + "_conv2", N, dz, dA1, dn + "_conv1", b(("y" + k + "_1").c_str()), s));
+      void* dz1 = b(("dz_y" + k + "_1").c_str());
+      CL(bn_wgrad(dn + "_conv1", N, b(("az" + k + "_2").c_str()), b(("t" + k).c_str()), dA1, b(("y" + k + "_1").c_str()),
+                  dz1, s));
+      // concat data gradient split into the skip part and the ConvTranspose output part; the ConvTranspose
+      // bias gradient is the epilogue channel sum of the second part
+      BnLayer& l1 = L(dn + "_conv1");
+      BnLayer& lu = L(dn + "_up");
+      void* sk = b(("skip" + k).c_str());
+      void* dtb = b(("dt" + k).c_str());
+      {
+        const int H = side(i);
+        adp_conv_desc d = desc3(N, H, l1);
+        d.CA_stride = l1.cout_s;
+        d.CB_stride = 0;
+        d.Nout = l1.Cin_s;
+        d.out_mode = 2;
+        d.out_stride = l1.cin_s[0];
+        d.out2_stride = l1.cin_s[1];
+        d.split_c = l1.cin_s[0];
+        adp_conv_io io{};
+        io.srcA = dz1;
+        io.W = l1.Wd;
+        io.out = sk;
+        io.out2 = dtb;
+        io.bn_sum = dtsum[i];
+        io.bn_sqsum = dtsum[i] + l1.Cin_s;
+        CL(adp_conv_fwd(dt, &d, &io, s));
+      }
+      CL(adp_ew_add_mask(ADP_DTYPE_F32, lu.cout_s, G + lu.offB, dtsum[i] + l1.cin_s[0], nullptr, 1.f, G + lu.offB, s));
+      skip[i] = sk;
+      const std::string pk = std::to_string(i + 1);
+      const void* pact = i + 1 < Lv - 1 ? b(("ay" + pk + "_2").c_str()) : b(("az" + std::to_string(Lv - 1) + "_2").c_str());
+      {
+        adp_conv_desc d{};
+        d.N = N;
+        d.Hs = d.Ws = d.Ho = d.Wo = side(i + 1);
+        d.CA_stride = lu.cin_s[0];
+        d.stride = 1;
+        d.kh = d.kw = 1;
+        d.dil = 1;
+        d.pad = 0;
+        d.Nout = lu.Nout;
+        d.out_mode = 1;
+        d.shuffle_c = lu.cout_s;
+        d.mask_scale = d.mask2_scale = 1.f;
+        adp_conv_io io{};
+        io.srcA = pact;
+        CL(adp_conv_wgrad(dt, &d, &io, dtb, lu.cout_s, G + lu.offW, nullptr, s));
+        CL(ready(bl_idx.at(lu.name), s));
+      }
+      void* dAp = b(("dA_up" + k).c_str());
+      if (i + 1 < Lv - 1) {
+        CL(convt_dgrad(lu.name, N, dtb, dAp, "dec" + pk + "_conv2", b(("y" + pk + "_2").c_str()), s));
+        cur_dA = dAp;
+      } else {
+        CL(convt_dgrad(lu.name, N, dtb, dAp, "enc" + pk + "_conv2", b(("z" + pk + "_2").c_str()), s));
+        bott_dA = dAp;
+      }
+    }
+    // bottleneck + encoder, deepest level first
+    const void* dpool = nullptr;
+    for (int i = Lv - 1; i >= 0; --i) {
+      const std::string k = std::to_string(i), en = "enc" + k;
+      void* z2 = b(("z" + k + "_2").c_str());
+      void* z1 = b(("z" + k + "_1").c_str());
+      const void* dA2 = nullptr;
+      if (i < Lv - 1) {   // pool backward (argmax recomputed from z) + skip gradient + fused BN-backward reduction
+        BnLayer& r = L(en + "_conv2");
+        void* d2 = b(("dA_z" + k + "_2").c_str());
+        CL(adp_maxpool2_bwd_bnr(dt, N, side(i), side(i), r.cout_s, nullptr, dpool, skip[i], d2, z2, stv(r, 2), stv(r, 3),
+                                stv(r, 4), stv(r, 5), G + r.offG, G + r.offBeta, s));
+        dA2 = d2;
+      } else {
+        dA2 = Lv > 1 ? bott_dA : nullptr;
+        if (!dA2) { adp::set_error("unet_bn handle: needs levels >= 2"); return -1; }
+      }
+      void* dz2 = b(("dz_z" + k + "_2").c_str());
+      CL(bn_wgrad(en + "_conv2", N, b(("az" + k + "_1").c_str()), nullptr, dA2, z2, dz2, s));
+      void* dA1 = b(("dA_z" + k + "_1").c_str());
+      CL(bn_dgrad(en + "_conv2", N, dz2, dA1, en + "_conv1", z1, s));
+      void* dz1 = b(("dz_z" + k + "_1").c_str());
+      const void* src = i == 0 ? b("x") : b(("pool" + std::to_string(i - 1)).c_str());
+      CL(bn_wgrad(en + "_conv1", N, src, nullptr, dA1, z1, dz1, s));
+      if (i > 0) {
+        void* dp = b(("dpool" + std::to_string(i - 1)).c_str());
+        CL(bn_dgrad(en + "_conv1", N, dz1, dp, "", nullptr, s));
+        dpool = dp;
+      }
+    }
+    return 0;
+  }
+
+  // -- Keras-layout parameter I/O of unet_bn (slot 0 kernel, conv+BN: 1 gamma, 2 beta, 3 moving mean,
+  // 4 moving variance; ConvTranspose / head: 1 bias); synchronous
+  size_t bn_param_size(const BnLayer& l, int slot) const {
+    const size_t cin = l.kind == 2 ? l.cin[0] : (size_t)(l.cin.size() > 1 ? l.cin[0] + l.cin[1] : l.cin[0]);
+    if (slot == 0) return l.kind == 0 ? 9 * cin * l.cout : (l.kind == 1 ? 4 * cin * l.cout : cin);
+    if (l.kind == 0) return slot <= 4 ? (size_t)l.cout : 0;
+    return slot == 1 ? (size_t)(l.kind == 2 ? 1 : l.cout) : 0;
+  }
+  std::vector<int> cmap(const BnLayer& l) const {
+    std::vector<int> cm;
+    int base_c = 0;
+    for (size_t p = 0; p < l.cin.size(); ++p) {
+      for (int c = 0; c < l.cin[p]; ++c) cm.push_back(base_c + c);
+      base_c += l.cin_s[p];
+    }
+    return cm;
+  }
+  float* bn_slot_ptr(BnLayer& l, int slot) {
+    if (l.kind == 0) {
+      switch (slot) {
+        case 1: return P + l.offG;
+        case 2: return P + l.offBeta;
+        case 3: return l.rmean;
+        case 4: return l.rvar;
+      }
+      return nullptr;
+    }
+    return slot == 1 ? P + l.offB : nullptr;
+  }
+  int bn_set_param(BnLayer& l, int slot, const float* host) {
+    CK(hipDeviceSynchronize());
+    if (slot != 0) {
+      CK(hipMemcpy(bn_slot_ptr(l, slot), host, sizeof(float) * bn_param_size(l, slot), hipMemcpyHostToDevice));
+      return 0;
+    }
+    const std::vector<int> cm = cmap(l);
+    const int cin = (int)cm.size();
+    if (l.kind == 2) {
+      std::vector<float> w(rup64(cin), 0.f);
+      for (int c = 0; c < cin; ++c) w[c] = host[c];
+      CK(hipMemcpy(P + l.offW, w.data(), sizeof(float) * cin, hipMemcpyHostToDevice));
+      return 0;
+    }
+    std::vector<float> wp((size_t)l.Npad * l.Kpad, 0.f);
+    if (l.kind == 0) {   // HWIO (3, 3, cin, cout) -> [co][t * Cin_s + cm[ci]]
+      for (int t = 0; t < 9; ++t)
+        for (int ci = 0; ci < cin; ++ci)
+          for (int co = 0; co < l.cout; ++co)
+            wp[(size_t)co * l.Kpad + t * l.Cin_s + cm[ci]] = host[((size_t)t * cin + ci) * l.cout + co];
+    } else {             // torch ConvTranspose (cin, cout, 2, 2) -> [sub * cout_s + co][cm[ci]]
+      for (int ci = 0; ci < cin; ++ci)
+        for (int co = 0; co < l.cout; ++co)
+          for (int sub = 0; sub < 4; ++sub)
+            wp[(size_t)(sub * l.cout_s + co) * l.Kpad + cm[ci]] = host[((size_t)ci * l.cout + co) * 4 + sub];
+    }
+    CK(hipMemcpy(P + l.offW, wp.data(), sizeof(float) * wp.size(), hipMemcpyHostToDevice));
+    return 0;
+  }
+  int bn_get_param(BnLayer& l, int slot, float* host) {
+    CK(hipDeviceSynchronize());
+    if (slot != 0) {
+      CK(hipMemcpy(host, bn_slot_ptr(l, slot), sizeof(float) * bn_param_size(l, slot), hipMemcpyDeviceToHost));
+      return 0;
+    }
+    const std::vector<int> cm = cmap(l);
+    const int cin = (int)cm.size();
+    if (l.kind == 2) {
+      CK(hipMemcpy(host, P + l.offW, sizeof(float) * cin, hipMemcpyDeviceToHost));
+      return 0;
+    }
+    std::vector<float> wp((size_t)l.Npad * l.Kpad);
+    CK(hipMemcpy(wp.data(), P + l.offW, sizeof(float) * wp.size(), hipMemcpyDeviceToHost));
+    if (l.kind == 0) {
+      for (int t = 0; t < 9; ++t)
+        for (int ci = 0; ci < cin; ++ci)
+          for (int co = 0; co < l.cout; ++co)
+            host[((size_t)t * cin + ci) * l.cout + co] = wp[(size_t)co * l.Kpad + t * l.Cin_s + cm[ci]];
+    } else {
+      for (int ci = 0; ci < cin; ++ci)
+        for (int co = 0; co < l.cout; ++co)
+          for (int sub = 0; sub < 4; ++sub)
+            host[((size_t)ci * l.cout + co) * 4 + sub] = wp[(size_t)(sub * l.cout_s + co) * l.Kpad + cm[ci]];
+    }
+    return 0;
+  }
 };
 
 extern "C" int adp_create(const adp_config* cfg, int device, adp_handle** out) {
   if (!cfg || !out) { adp::set_error("adp_create: null argument"); return -1; }
   *out = nullptr;
-  if (cfg->preset != ADP_PRESET_ADIPOSE_V3) { adp::set_error("adp_create: only ADP_PRESET_ADIPOSE_V3"); return -1; }
+  if (cfg->preset != ADP_PRESET_ADIPOSE_V3 && cfg->preset != ADP_PRESET_UNET_BN) {
+    adp::set_error("adp_create: preset ADP_PRESET_ADIPOSE_V3 or ADP_PRESET_UNET_BN");
+    return -1;
+  }
   if (cfg->tile <= 0 || cfg->tile % 8 || cfg->max_batch <= 0 ||
       (cfg->dtype != ADP_DTYPE_F32 && cfg->dtype != ADP_DTYPE_BF16)) {
     adp::set_error("adp_create: tile % 8 == 0, max_batch > 0, dtype f32 or bf16");
     return -1;
+  }
+  if (cfg->dropout_rate < 0.f || cfg->dropout_rate >= 1.f) {
+    adp::set_error("adp_create: dropout_rate in [0, 1)");
+    return -1;
+  }
+  if (cfg->preset == ADP_PRESET_UNET_BN) {
+    const int lv = cfg->levels > 0 ? cfg->levels : 5, bs = cfg->base > 0 ? cfg->base : 64;
+    const int ic = cfg->in_ch > 0 ? cfg->in_ch : 3;
+    if (lv < 2 || lv > 8 || cfg->tile % (1 << (lv - 1)) || bs % 8 || ic > 8 || (bs << (lv - 1)) > 2048) {
+      adp::set_error("adp_create(unet_bn): 2 <= levels <= 8, tile divisible by 2^(levels-1), base % 8 == 0, "
+                     "in_ch <= 8, base << (levels-1) <= 2048");
+      return -1;
+    }
+    if (hipSetDevice(device) != hipSuccess) { adp::set_error("adp_create: hipSetDevice failed"); return -2; }
+    auto* h = new adp_handle();
+    h->cfg = *cfg;
+    h->device = device;
+    h->S = cfg->tile;
+    h->B = cfg->max_batch;
+    h->es = cfg->dtype == ADP_DTYPE_F32 ? 4 : 2;
+    h->levels = lv;
+    h->base = bs;
+    h->in_ch = ic;
+    const int rc = h->create_unet_bn();
+    if (rc) { delete h; return rc; }
+    *out = h;
+    return 0;
   }
   if (hipSetDevice(device) != hipSuccess) { adp::set_error("adp_create: hipSetDevice failed"); return -2; }
   auto* h = new adp_handle();
@@ -702,6 +1427,7 @@ extern "C" int adp_destroy(adp_handle* h) {
 
 extern "C" const char* adp_param_name(const adp_handle* h, int i) {
   if (!h || i < 0) return nullptr;
+  if (!h->bl.empty()) return i < (int)h->bl.size() ? h->bl[i].name.c_str() : nullptr;
   if (i < (int)h->dense.size()) return h->dense[i].name.c_str();
   i -= (int)h->dense.size();
   return i < (int)h->heads.size() ? h->heads[i].name.c_str() : nullptr;
@@ -716,7 +1442,25 @@ static std::vector<float>* param_ref(adp_handle* h, const char* layer, int slot)
   return nullptr;
 }
 
+// unet_bn handles: the layer, or nullptr (error set) for an unknown name / slot
+static BnLayer* bn_param(adp_handle* h, const char* layer, int slot, const char* who) {
+  auto it = h->bl_idx.find(layer ? layer : "");
+  if (it == h->bl_idx.end() || slot < 0 || h->bn_param_size(h->bl[it->second], slot) == 0) {
+    adp::set_error(std::string(who) + ": unknown unet_bn parameter " + (layer ? layer : "(null)") + " slot " +
+                   std::to_string(slot) + " (conv: 0 kernel, 1 gamma, 2 beta, 3 moving mean, 4 moving variance; "
+                   "ConvTranspose / head: 0 kernel, 1 bias)");
+    return nullptr;
+  }
+  return &h->bl[it->second];
+}
+
 extern "C" int adp_param_size(adp_handle* h, const char* layer, int slot, size_t* n) {
+  if (h && !h->bl.empty()) {
+    BnLayer* l = bn_param(h, layer, slot, "adp_param_size");
+    if (!l || !n) return -1;
+    *n = h->bn_param_size(*l, slot);
+    return 0;
+  }
   std::vector<float>* v = param_ref(h, layer, slot);
   if (!v || !n) { adp::set_error(std::string("adp_param_size: unknown parameter ") + (layer ? layer : "(null)")); return -1; }
   *n = v->size();
@@ -724,6 +1468,17 @@ extern "C" int adp_param_size(adp_handle* h, const char* layer, int slot, size_t
 }
 
 extern "C" int adp_set_param(adp_handle* h, const char* layer, int slot, const float* host, size_t n) {
+  if (h && !h->bl.empty()) {
+    BnLayer* l = bn_param(h, layer, slot, "adp_set_param");
+    if (!l) return -1;
+    if (!host || n != h->bn_param_size(*l, slot)) {
+      adp::set_error("adp_set_param: " + std::string(layer) + " slot " + std::to_string(slot) + " expects " +
+                     std::to_string(h->bn_param_size(*l, slot)) + " floats");
+      return -1;
+    }
+    if (hipSetDevice(h->device) != hipSuccess) { adp::set_error("adp_set_param: hipSetDevice failed"); return -2; }
+    return h->bn_set_param(*l, slot, host);
+  }
   std::vector<float>* v = param_ref(h, layer, slot);
   if (!v) { adp::set_error(std::string("adp_set_param: unknown parameter ") + (layer ? layer : "(null)")); return -1; }
   if (!host || n != v->size()) {
@@ -737,6 +1492,13 @@ extern "C" int adp_set_param(adp_handle* h, const char* layer, int slot, const f
 }
 
 extern "C" int adp_get_param(adp_handle* h, const char* layer, int slot, float* host, size_t n) {
+  if (h && !h->bl.empty()) {
+    BnLayer* l = bn_param(h, layer, slot, "adp_get_param");
+    if (!l) return -1;
+    if (!host || n != h->bn_param_size(*l, slot)) { adp::set_error("adp_get_param: size mismatch"); return -1; }
+    if (hipSetDevice(h->device) != hipSuccess) { adp::set_error("adp_get_param: hipSetDevice failed"); return -2; }
+    return h->bn_get_param(*l, slot, host);
+  }
   std::vector<float>* v = param_ref(h, layer, slot);
   if (!v || !host || n != v->size()) { adp::set_error("adp_get_param: unknown parameter or size mismatch"); return -1; }
   if (h->host_stale) {
@@ -755,27 +1517,30 @@ extern "C" int adp_forward(adp_handle* h, const float* images, int n, long long 
   }
   hipStream_t s = (hipStream_t)st;
   if (hipSetDevice(h->device) != hipSuccess) { adp::set_error("adp_forward: hipSetDevice failed"); return -2; }
-  if (h->dirty) CL(h->upload(s));
-  if (h->wpack_stale) CL(h->pack_forward(s));
+  const bool bn = !h->bl.empty();
+  if (!bn && h->dirty) CL(h->upload(s));
+  if (!bn && h->wpack_stale) CL(h->pack_forward(s));
+  const int cin = bn ? h->in_ch : 1;   // unet_bn tiles: (S, S, in_ch) interleaved
   static const int views_tab[4][8] = {{0}, {0, 4}, {0, 4, 5, 1}, {0, 1, 2, 3, 4, 5, 6, 7}};
   static const int nviews[4] = {1, 2, 4, 8};
   const int nv = nviews[tta_mode];
   const int* views = views_tab[tta_mode];
   const int S = h->S;
   const size_t plane = (size_t)S * S;
-  const long long istride = img_stride > 0 ? img_stride : (long long)plane;
+  const long long istride = img_stride > 0 ? img_stride : (long long)plane * cin;
   const int per = std::max(1, h->B / nv);
   for (int i0 = 0; i0 < n; i0 += per) {
     const int cnt = std::min(per, n - i0), N = cnt * nv;
     if (N > h->B) { adp::set_error("adp_forward: TTA views exceed max_batch"); return -1; }
     for (int t = 0; t < cnt; ++t)
       for (int k = 0; k < nv; ++k)
-        CL(adp_prep_input(h->cfg.dtype, 1, S, S, 1, images + (size_t)(i0 + t) * istride, S, (long long)plane, mean,
-                          std_, views[k], 8, static_cast<char*>(h->b("x")) + (size_t)(t * nv + k) * plane * 8 * h->es,
-                          s));
-    CL(h->forward(N, s));
+        CL(adp_prep_input(h->cfg.dtype, 1, S, S, cin, images + (size_t)(i0 + t) * istride, S, (long long)plane * cin,
+                          mean, std_, views[k], 8,
+                          static_cast<char*>(h->b("x")) + (size_t)(t * nv + k) * plane * 8 * h->es, s));
+    if (bn) CL(h->bn_forward(N, false, s));
+    else CL(h->forward(N, s));
     for (int t = 0; t < cnt; ++t) {
-      const float* p = h->b<float>("p_main") + (size_t)t * nv * plane;
+      const float* p = h->b<float>(bn ? "p" : "p_main") + (size_t)t * nv * plane;
       if (nv == 1) CL(adp_cast(ADP_DTYPE_F32, ADP_DTYPE_F32, plane, p, prob + (size_t)(i0 + t) * plane, s));
       else CL(adp_tta_merge(S, S, nv, views, p, prob + (size_t)(i0 + t) * plane, s));
     }
@@ -822,32 +1587,45 @@ extern "C" int adp_train_step(adp_handle* h, const float* x, const float* y, int
                               float* metrics, adp_stream_t st) {
   if (!h || !x || !y || !cfg || n <= 0) { adp::set_error("adp_train_step: bad arguments"); return -1; }
   if (n > h->B) { adp::set_error("adp_train_step: n exceeds max_batch"); return -1; }
-  if (cfg->dropout_rate < 0.f || cfg->dropout_rate >= 1.f || cfg->hard_example_ratio <= 0.f ||
-      cfg->hard_example_ratio > 1.f) {
-    adp::set_error("adp_train_step: dropout_rate in [0, 1), hard_example_ratio in (0, 1]");
+  if (cfg->dropout_rate >= 1.f || cfg->hard_example_ratio <= 0.f || cfg->hard_example_ratio > 1.f) {
+    adp::set_error("adp_train_step: dropout_rate < 1 (< 0: the model's build_model rate), hard_example_ratio in (0, 1]");
+    return -1;
+  }
+  const bool bn = !h->bl.empty();
+  if (bn && cfg->freeze_encoder) {
+    adp::set_error("adp_train_step: the unet_bn preset has no frozen-encoder phase");
     return -1;
   }
   hipStream_t s = (hipStream_t)st;
   if (hipSetDevice(h->device) != hipSuccess) { adp::set_error("adp_train_step: hipSetDevice failed"); return -2; }
-  CL(h->ensure_train());
-  if (h->dirty) CL(h->upload(s));
-  CL(h->pack_forward(s));
+  if (!bn) {
+    CL(h->ensure_train());
+    if (h->dirty) CL(h->upload(s));
+    CL(h->pack_forward(s));
+  }
   const int S = h->S, N = n;
   const size_t plane = (size_t)S * S;
   int world = 1;
   ncclComm_t comm = static_cast<ncclComm_t>(h->comm);
   if (comm) NC(rccl().count(comm, &world));
   // forward (Trainer.train_step: prep_input(x, mean 0, std 1), iterations += 1, forward(train, seed))
-  CL(adp_prep_input(h->cfg.dtype, N, S, S, 1, x, S, (long long)plane, 0.f, 1.f, 0, 8, h->b("x"), s));
+  const int cin = bn ? h->in_ch : 1;
+  CL(adp_prep_input(h->cfg.dtype, N, S, S, cin, x, S, (long long)plane * cin, 0.f, 1.f, 0, 8, h->b("x"), s));
   h->step += 1;
-  const float r = cfg->dropout_rate;
-  const float keep = r > 0.f ? (float)(1.0 / (1.0 - (double)r)) : 1.f;
-  const unsigned sd = (unsigned)((unsigned long long)((long long)h->step * 7919 + 17) & 0xFFFFFFFFull);
-  CL(h->forward(N, s, true, r, sd));
+  float keep = 1.f;
+  if (bn) {
+    CL(h->bn_forward(N, true, s));
+  } else {
+    const float r = cfg->dropout_rate >= 0.f ? cfg->dropout_rate : h->cfg.dropout_rate;
+    keep = r > 0.f ? (float)(1.0 / (1.0 - (double)r)) : 1.f;
+    const unsigned sd =
+        (unsigned)((unsigned long long)((long long)(h->cfg.seed + (unsigned)h->step) * 7919 + 17) & 0xFFFFFFFFull);
+    CL(h->forward(N, s, true, r, sd));
+  }
   // losses and dL/dp (Trainer.loss_and_grads)
-  const bool ds = h->cfg.deep_supervision != 0;
+  const bool ds = !bn && h->cfg.deep_supervision != 0;
   struct Spec { const char* p; const char* dp; float w; int ohem; };
-  std::vector<Spec> specs = {{"p_main", "dp_main", ds ? cfg->w_main : 1.f, cfg->use_hard_mining}};
+  std::vector<Spec> specs = {{bn ? "p" : "p_main", "dp_main", ds ? cfg->w_main : 1.f, cfg->use_hard_mining}};
   if (ds) {
     specs.push_back({"p_aux1", "dp_aux1", cfg->w_aux1, 0});
     specs.push_back({"p_aux2", "dp_aux2", cfg->w_aux2, 0});
@@ -861,6 +1639,7 @@ extern "C" int adp_train_step(adp_handle* h, const float* x, const float* y, int
   for (size_t i = 0; i < specs.size(); ++i)
     CL(adp_loss_rows(N, S, S, h->b<float>(specs[i].p), y, cfg->use_label_smoothing, cfg->epsilon_pos,
                      cfg->epsilon_neg, rows + i * (size_t)N * S, stats + 8 * i, s));
+  // batch-global Dice sums (train_adipose_unet_v3.py:217-225) before the gradient
   if (comm) NC(rccl().allreduce(stats, stats, 24, ncclFloat64, ncclSum, comm, s));
   for (size_t i = 0; i < specs.size(); ++i) {
     const int k = specs[i].ohem ? (int)((float)S * cfg->hard_example_ratio) : S;
@@ -870,16 +1649,27 @@ extern "C" int adp_train_step(adp_handle* h, const float* x, const float* y, int
                      cfg->epsilon_neg, coef + i * (size_t)N * S, stats + 8 * i, specs[i].w, 0,
                      h->b<float>(specs[i].dp), s));
   }
-  // backward, gradient all-reduce, Adam / AdamW over the trainable part of the flat buffer
+  // backward with the bucketed gradient all-reduce overlapped, then Adam / AdamW over the trainable range
   CL(adp_fill_f32(h->nflat, 0.f, h->G, s));
   const bool full = !cfg->freeze_encoder;
-  CL(h->backward(N, keep, full, s));
-  if (comm) NC(rccl().allreduce(h->G, h->G, h->nflat, ncclFloat32, ncclSum, comm, s));
+  std::set<int> frozen;
+  if (!full)
+    for (const char* e : {"down1_conv1", "down1_conv2", "down2_conv1", "down2_conv2", "down3_conv1", "down3_conv2"})
+      frozen.insert(h->dense_id(e));
+  CL(h->dp_begin(frozen));
+  const int brc = bn ? h->bn_backward(N, s) : h->backward(N, keep, full, s);
+  if (brc) {
+    h->dp_active = false;
+    return brc;
+  }
+  CL(h->dp_finish(s));
   const size_t lo = full ? 0 : h->enc_end;
   CL(adp_adam(h->nflat - lo, h->P + lo, h->G + lo, h->Mo + lo, h->Vo + lo, lr, cfg->beta1, cfg->beta2, cfg->eps, h->step,
               cfg->optimizer == 1 ? cfg->weight_decay : 0.f, 1.f, s));
-  h->host_stale = true;
-  h->wpack_stale = h->cfg.dtype != ADP_DTYPE_F32;
+  if (!bn) {
+    h->host_stale = true;
+    h->wpack_stale = h->cfg.dtype != ADP_DTYPE_F32;
+  }
   if (!metrics) return 0;
   // Trainer.read_metrics (host read-back, synchronises)
   if (comm) NC(rccl().allreduce(lossbuf, lossbuf, 4, ncclFloat64, ncclSum, comm, s));

@@ -15,12 +15,15 @@ import torch
 from ._lib import AdpError, call, lib, ptr, stream_ptr
 
 ADP_PRESET_ADIPOSE_V3 = 0
+ADP_PRESET_UNET_BN = 1
 DTYPES = {"f32": 0, "bf16": 1}
 TTA_MODES = {None: 0, "none": 0, "minimal": 1, "basic": 2, "full": 3}
 
 
 class AdpConfig(C.Structure):
-    _fields_ = [(n, C.c_int) for n in ("preset", "tile", "max_batch", "dtype", "deep_supervision", "init_nb")]
+    _fields_ = [(n, C.c_int) for n in ("preset", "tile", "max_batch", "dtype", "deep_supervision", "init_nb",
+                                       "levels", "base", "in_ch")] + [("dropout_rate", C.c_float),
+                                                                      ("seed", C.c_uint)]
 
 
 class AdpTrainCfg(C.Structure):
@@ -65,9 +68,17 @@ def comm_destroy(comm):
 class NativeAdiposeV3:
     """One adp_handle: build (topology + buffers) at construction, Keras-layout weights, batched TTA."""
 
-    def __init__(self, tile=1024, max_batch=8, dtype="f32", deep_supervision=True, init_nb=44, device=0):
+    in_ch = 1
+    nslots = 2
+
+    def __init__(self, tile=1024, max_batch=8, dtype="f32", deep_supervision=True, init_nb=44, device=0,
+                 dropout_rate=0.3, seed=0):
         self.tile, self.max_batch, self.device = tile, max_batch, torch.device("cuda", device)
-        cfg = AdpConfig(ADP_PRESET_ADIPOSE_V3, tile, max_batch, DTYPES[dtype], int(deep_supervision), init_nb)
+        cfg = AdpConfig(ADP_PRESET_ADIPOSE_V3, tile, max_batch, DTYPES[dtype], int(deep_supervision), init_nb,
+                        0, 0, 0, float(dropout_rate), int(seed))
+        self._create(cfg, device)
+
+    def _create(self, cfg, device):
         h = C.c_void_p()
         call("adp_create", C.byref(cfg), device, C.byref(h))
         self._h = h
@@ -99,15 +110,18 @@ class NativeAdiposeV3:
         for layer, arrs in weights.items():
             if layer not in names:
                 continue
-            for slot, a in enumerate(arrs[:2]):
+            for slot, a in enumerate(arrs[:self.nslots]):
                 a = np.ascontiguousarray(np.asarray(a, np.float32))
                 call("adp_set_param", self._h, layer.encode(), slot, a.ctypes.data, a.size)
+
+    def _slots(self, layer):
+        return (0, 1)
 
     def get_weights(self):
         out = {}
         for layer in self.layer_names():
             arrs = []
-            for slot in (0, 1):
+            for slot in self._slots(layer):
                 n = C.c_size_t()
                 call("adp_param_size", self._h, layer.encode(), slot, C.byref(n))
                 a = np.empty(n.value, np.float32)
@@ -116,16 +130,22 @@ class NativeAdiposeV3:
             out[layer] = arrs
         return out
 
-    def predict_batch(self, images, mean, std, tta_mode=None):
-        """images: (n, S, S) f32 (host or device) raw gray -> (n, S, S) device f32 probabilities."""
+    def _tiles(self, images):
         x = images if isinstance(images, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(images, np.float32))
         x = x.to(self.device, torch.float32).contiguous()
-        if x.dim() == 2:
+        shape = (self.tile, self.tile) if self.in_ch == 1 else (self.tile, self.tile, self.in_ch)
+        if x.dim() == len(shape):
             x = x[None]
-        if tuple(x.shape[1:]) != (self.tile, self.tile):
-            raise AdpError(f"engine built for {self.tile}x{self.tile} tiles, got {tuple(x.shape[1:])}")
-        out = torch.empty_like(x)
-        call("adp_forward", self._h, ptr(x), x.shape[0], x.shape[1] * x.shape[2], float(mean), float(std),
+        if tuple(x.shape[1:]) != shape:
+            raise AdpError(f"engine built for {shape} tiles, got {tuple(x.shape[1:])}")
+        return x
+
+    def predict_batch(self, images, mean, std, tta_mode=None):
+        """images: (n, S, S) f32 raw gray (unet_bn: (n, S, S, in_ch)), host or device -> (n, S, S) device f32
+        probabilities."""
+        x = self._tiles(images)
+        out = torch.empty((x.shape[0], self.tile, self.tile), dtype=torch.float32, device=self.device)
+        call("adp_forward", self._h, ptr(x), x.shape[0], x[0].numel(), float(mean), float(std),
              TTA_MODES[tta_mode], ptr(out), stream_ptr())
         return out
 
@@ -142,11 +162,42 @@ class NativeAdiposeV3:
         """One native training step: x (n, S, S) normalised images, y (n, S, S) labels (host or device).
         Returns the Keras per-batch metrics (METRIC_NAMES)."""
         cfg = cfg or train_cfg()
-        xs = [t if isinstance(t, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(t, np.float32))
-              for t in (x, y)]
-        xd, yd = (t.to(self.device, torch.float32).contiguous() for t in xs)
-        if xd.dim() == 2:
-            xd, yd = xd[None], yd[None]
+        xd = self._tiles(x)
+        yt = y if isinstance(y, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(y, np.float32))
+        yd = yt.to(self.device, torch.float32).contiguous()
+        if yd.dim() == 2:
+            yd = yd[None]
+        if tuple(yd.shape) != (xd.shape[0], self.tile, self.tile):
+            raise AdpError(f"labels {tuple(yd.shape)} do not match {xd.shape[0]} tiles of {self.tile}^2")
         m = (C.c_float * 6)()
         call("adp_train_step", self._h, ptr(xd), ptr(yd), xd.shape[0], C.byref(cfg), float(lr), m, stream_ptr())
         return dict(zip(METRIC_NAMES, (float(v) for v in m)))
+
+
+class NativeUNetBN(NativeAdiposeV3):
+    """The unet_bn preset behind the same handle ABI (BASELINE.json configs 2/3/5; nets.UNetBN is the Python
+    schedule of the same network): Keras-style weights per layer ([kernel, gamma, beta] for the conv + BatchNorm
+    layers, as nets.UNetBN.get_weights returns them, plus slots 3 / 4 = moving mean / variance; [kernel, bias]
+    for the ConvTranspose layers (torch (Cin, Cout, 2, 2) layout) and the head)."""
+
+    nslots = 3
+
+    def __init__(self, tile=1024, max_batch=4, dtype="bf16", levels=5, base=64, in_ch=3, device=0, seed=0):
+        self.tile, self.max_batch, self.device = tile, max_batch, torch.device("cuda", device)
+        self.in_ch = in_ch
+        cfg = AdpConfig(ADP_PRESET_UNET_BN, tile, max_batch, DTYPES[dtype], 0, 0, levels, base, in_ch, 0.0, int(seed))
+        self._create(cfg, device)
+
+    def _slots(self, layer):
+        return (0, 1, 2) if ("_conv" in layer) else (0, 1)
+
+    def running_stats(self, layer):
+        """(moving mean, moving variance) of a conv + BatchNorm layer (slots 3, 4)."""
+        out = []
+        for slot in (3, 4):
+            n = C.c_size_t()
+            call("adp_param_size", self._h, layer.encode(), slot, C.byref(n))
+            a = np.empty(n.value, np.float32)
+            call("adp_get_param", self._h, layer.encode(), slot, a.ctypes.data, a.size)
+            out.append(a)
+        return out

@@ -23,30 +23,43 @@ def round_up(x, m):
 
 
 class LaunchTimer:
-    """Optional per-launch HIP-event timing of the GEMM kernels (bench.py roofline leg).
-    Events are recorded on the launch stream (torch's current stream), so they bracket exactly the
-    kernel they surround; each launch is keyed by the kernel instantiation the library reports for
-    it (adp_last_kernel, the name rocprofv3 prints) and the launch dtype."""
+    """Optional per-launch timing of the conv kernels (bench.py roofline leg).
+
+    The library brackets the MAIN kernel of every adp_conv_fwd / adp_conv_wgrad(_bn) call with a HIP
+    event pair on the launch stream (adp_timing): the statistic folds, split reduces, bias sums and
+    BatchNorm applies a call may launch around it are outside the pair, so each timing is exactly one
+    kernel of rocprofv3's list, under the name the library reports for it (adp_last_kernel). The wrapper
+    records, per call and in the same order, the launch dtype and its algorithmic FLOPs and bytes."""
+
+    NAME_LEN = 160
 
     def __init__(self):
         self.recs = []
 
-    def wrap(self, dcode, flops, fn):
-        s = torch.cuda.current_stream()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(s)
+    def wrap(self, dcode, flops, fn, nbytes=0.0):
         fn()
-        e1.record(s)
-        self.recs.append(((lib().adp_last_kernel().decode(), dcode), flops, e0, e1))
+        self.recs.append((dcode, flops, nbytes))
 
     def summary(self):
-        """(kernel name, dtype code) -> (launches, total flops, total ms) (synchronises)."""
+        """(kernel name, dtype code) -> (launches, total flops, total ms, total algorithmic bytes)
+        (synchronises; ends the library's recording)."""
         torch.cuda.synchronize()
+        n = C.c_int(0)
+        call("adp_timing_read", 0, None, 0, None, C.byref(n))
+        cnt = n.value
+        names = C.create_string_buffer(max(1, cnt) * self.NAME_LEN)
+        ms = (C.c_float * max(1, cnt))()
+        call("adp_timing_read", cnt, names, self.NAME_LEN, ms, C.byref(n))
+        call("adp_timing", 2)
+        _check(cnt == len(self.recs), f"LaunchTimer: {cnt} timed kernels for {len(self.recs)} conv calls")
         out = {}
-        for k, f, e0, e1 in self.recs:
-            n, fl, ms = out.get(k, (0, 0.0, 0.0))
-            out[k] = (n + 1, fl + f, ms + e0.elapsed_time(e1))
+        raw = names.raw
+        for i, (dcode, f, nb) in enumerate(self.recs):
+            name = raw[i * self.NAME_LEN:(i + 1) * self.NAME_LEN].split(b"\0", 1)[0].decode()
+            _check(ms[i] >= 0, f"LaunchTimer: {name} has no end mark")
+            k = (name, dcode)
+            c, fl, t, b = out.get(k, (0, 0.0, 0.0, 0.0))
+            out[k] = (c + 1, fl + f, t + ms[i], b + nb)
         return out
 
 
@@ -54,15 +67,17 @@ _timer = None
 
 
 def set_launch_timer(t):
+    """Start (t = a LaunchTimer) or stop (None) recording; the record is read by t.summary()."""
     global _timer
     _timer = t
+    call("adp_timing", 1 if t is not None else 0)
 
 
-def _timed(dcode, flops, fn):
+def _timed(dcode, flops, fn, nbytes=0.0):
     if _timer is None:
         fn()
     else:
-        _timer.wrap(dcode, flops, fn)
+        _timer.wrap(dcode, flops, fn, nbytes)
 
 
 def set_option(name, value):
@@ -215,9 +230,16 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
         io.bnr_invstd, io.bnr_dgamma, io.bnr_dbeta = ptr(ist), ptr(dg), ptr(dbt)
     dc = dtype_code(srcA)
     flops = 2.0 * N * Ho * Wo * nout * kh * kw * (d.CA_stride + d.CB_stride)
+    # algorithmic bytes: every operand read once, every output written once
+    nbytes = _nbytes(srcA) + _nbytes(srcB) + _nbytes(W) + _nbytes(out) + _nbytes(out2) + _nbytes(addend) + \
+        _nbytes(mask) + _nbytes(mask2) + 2 * _nbytes(accum) + (_nbytes(bn_reduce[0]) if bn_reduce else 0)
     _timed(dc, flops,
-           lambda: call("adp_conv_fwd", dc, C.byref(d), C.byref(io), stream_ptr()))
+           lambda: call("adp_conv_fwd", dc, C.byref(d), C.byref(io), stream_ptr()), nbytes)
     return out
+
+
+def _nbytes(t):
+    return 0 if t is None else t.numel() * t.element_size()
 
 
 def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up=False, stride=1, kh=3, kw=3,
@@ -260,6 +282,8 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     del Wdummy
     dc = dtype_code(srcA)
     flops = 2.0 * N * Ho * Wo * nout * K
+    # algorithmic bytes: sources and dY read once, dW (f32) accumulated once
+    nbytes = _nbytes(srcA) + _nbytes(srcB) + _nbytes(dY) + 4.0 * nout * Kpad
     if bn_apply is not None:
         dA, z, sc, sh, mu, ist, gam, dg, dbt, count = bn_apply
         _check(not shuffle_c and dA.shape == z.shape == dY.shape and dY.shape[3] == nout and
@@ -268,11 +292,11 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
                        float(count))
         _timed(dc, flops,
                lambda: call("adp_conv_wgrad_bn", dc, C.byref(d), C.byref(io), C.byref(bn), ptr(dY),
-                            int(dY.shape[3]), ptr(dW), ptr(dB), stream_ptr()))
+                            int(dY.shape[3]), ptr(dW), ptr(dB), stream_ptr()), nbytes + 2 * _nbytes(dA))
         return
     _timed(dc, flops,
            lambda: call("adp_conv_wgrad", dc, C.byref(d), C.byref(io), ptr(dY), int(dY.shape[3]), ptr(dW),
-                        ptr(dB), stream_ptr()))
+                        ptr(dB), stream_ptr()), nbytes)
 
 
 def pack_weights(src, dst, mode, *, taps=1, cin_s=0, nout=0):

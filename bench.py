@@ -35,47 +35,86 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-size", type=int, default=1024, help="tile size of the CPU baseline sample")
     p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
     return p.parse_args()
 
 
-def cpu_baseline(args):
-    """Oracle (torch CPU fp32 restatement, oracle/torch_ref.py) on a bounded sample: ONE training step
-    (forward + loss + backward + Adam) on 1 tile of the same workload, on the host cores."""
-    import numpy as np
+def host_threads():
+    """Host threads for the CPU baseline: the CPUs this process may run on (sched_getaffinity), capped by
+    the cgroup CPU quota when one is set (a GPU box shows the whole machine's CPUs but grants a share);
+    returns (threads, description)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, f"{aff} CPUs in the affinity mask" + (f", cgroup quota {quota} CPUs" if quota else ", no cgroup quota")
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, min_seconds=10.0, max_steps=30):
+    """The reference's path on the host cores (BASELINE.md:30-44): the oracle's CPU fp32 restatement of
+    AdiposeUNetV3 (oracle/torch_ref.py, train_adipose_unet_v3.py:660-758) training at BASELINE configs[0]
+    (256x256 gray tiles, batch 2, fp32): forward, OHEM main + 0.4/0.3 deep-supervision BCE+Dice losses
+    (compile_model :780-879), backward, Keras Adam. One untimed warm-up step, then steps until >= min_seconds
+    and >= 3 steps. Reported in 1024^2-tile equivalents (16 256^2 tiles = one 1024^2 tile: the same FLOPs)."""
     import torch
 
     from oracle import torch_ref as R
 
-    threads = torch.get_num_threads()
-    S = args.cpu_size
+    threads, tdesc = host_threads()
+    torch.set_num_threads(threads)
+    S, B = 256, 2
     g = torch.Generator().manual_seed(865)
-    if args.preset == "unet_bn":
-        w = R.unet_bn_keras_weights(levels=args.levels, base=64, in_ch=3, seed=865)
-        W = {k: [torch.tensor(v, requires_grad=True) for v in vs] for k, vs in w.items()}
-        x = torch.randn(1, S, S, 3, generator=g)
-        fwd = lambda: R.unet_bn_forward(x, W, levels=args.levels)  # noqa: E731
-        lossf = R.combined_loss_standard
-    else:
-        w = R.adipose_v3_keras_weights(seed=865)
-        W = {k: [torch.tensor(v, requires_grad=True) for v in vs] for k, vs in w.items()}
-        x = torch.randn(1, S, S, generator=g)
-        fwd = lambda: R.adipose_v3_forward(x, W)  # noqa: E731
-        lossf = None
-    y = (torch.rand(1, S, S, generator=g) > 0.7).float()
+    w = R.adipose_v3_keras_weights(seed=865)
+    W = {k: [torch.tensor(v, requires_grad=True) for v in vs] for k, vs in w.items()}
+    x = torch.randn(B, S, S, generator=g)
+    y = (torch.rand(B, S, S, generator=g) > 0.7).float()
     params = [p for vs in W.values() for p in vs]
     opt = R.KerasAdam(params, lr=1e-4)
-    t0 = time.perf_counter()
-    out = fwd()
-    loss = lossf(y, out) if lossf else R.ds_total_loss(y, out)
-    loss.backward()
-    opt.step([p.grad for p in params])
+
+    def step():
+        for p in params:
+            p.grad = None
+        R.ds_total_loss(y, R.adipose_v3_forward(x, W)).backward()
+        opt.step([p.grad for p in params])
+
+    step()   # warm-up (first-call allocations, thread pool start)
+    n, t0 = 0, time.perf_counter()
+    while n < 3 or (time.perf_counter() - t0 < min_seconds and n < max_steps):
+        step()
+        n += 1
     dt = time.perf_counter() - t0
-    tiles = (S / 1024.0) ** 2
-    return {"value": round(tiles / dt, 6), "unit": "1024^2 tiles/s", "cores": threads, "kind": "port",
-            "sample": f"1 train step (fwd+BCE/Dice+bwd+Adam) on 1 {S}x{S} tile, torch CPU fp32, "
-                      f"{threads} threads ({os.cpu_count()} host CPUs visible), {dt:.2f} s"}
+    tiles = n * B * (S / 1024.0) ** 2
+    return {"value": round(tiles / dt, 6), "unit": "1024^2 tiles/s (train, 1024^2-equivalent)", "cores": threads,
+            "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"oracle adipose_v3 (reference topology) fp32 train steps at BASELINE configs[0]: {S}x{S} gray, "
+                      f"B={B}, OHEM + deep-supervision losses, Keras Adam; 1 warm-up + {n} timed steps in {dt:.2f} s "
+                      f"({n * B / dt:.3f} {S}^2 tiles/s); torch CPU, {threads} threads ({tdesc})"}
+
+
+def workload_label(args):
+    """What this run trains, and which BASELINE.json config it is (if any)."""
+    if args.preset == "unet_bn":
+        wl = f"unet_bn L{args.levels} base64 {args.size}x{args.size}x3 {args.dtype} B={args.batch}/GPU"
+        cfg = {(5, 1024, 4, "bf16"): 2, (4, 512, 8, "bf16"): 1}.get((args.levels, args.size, args.batch, args.dtype))
+    else:
+        wl = f"adipose_v3 (reference topology) {args.size}x{args.size}x1 {args.dtype} B={args.batch}/GPU"
+        cfg = 0 if (args.size, args.batch, args.dtype) == (256, 2, "f32") else None
+    return wl + (f" (BASELINE configs[{cfg}])" if cfg is not None else " (not a BASELINE config)")
 
 
 def committed_traffic(kernel):
@@ -183,17 +222,22 @@ def main():
     # roofline of the dominant kernel: the GEMM kernel instantiation with the largest total time
     # (names as rocprofv3 prints them; profiles/ holds the matching --kernel-trace --stats summary)
     dom = max(summ.items(), key=lambda kv: kv[1][2])
-    (kname, dcode), (n, flops, ms) = dom
+    (kname, dcode), (n, flops, ms, abytes) = dom
     dname = {0: "f32", 1: "bf16", 2: "fp8"}[dcode]
     achieved = flops / (ms * 1e-3) / 1e12
     step_ms = elapsed * 1e3
     per_kernel = {k[0]: {"launches": v[0], "avg_ms": round(v[2] / v[0], 4),
-                         "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2), "share_of_step": round(v[2] / step_ms, 4)}
+                         "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
+                         "alg_gbs": round(v[3] / (v[2] * 1e-3) / 1e9, 1),
+                         "share_of_step": round(v[2] / step_ms, 4)}
                   for k, v in sorted(summ.items(), key=lambda kv: -kv[1][2])}
     traffic, tsrc = committed_traffic(kname)
+    alg_bytes = abytes / n
     roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2),
             "peak": MI355X_PEAK[dname], "unit": "TFLOP/s", "frac": round(achieved / MI355X_PEAK[dname], 4),
             "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc,
+            "algorithmic_bytes": round(alg_bytes),
+            "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
             "avg_launch_ms": round(ms / n, 4), "launches": n,
             "flops_per_launch": round(flops / n / 1e9, 3),
             "gemm_share_of_step": round(sum(v[2] for v in summ.values()) / step_ms, 4),
@@ -205,8 +249,7 @@ def main():
             cpu = cpu_baseline(args)
         except Exception as e:  # report, never fake
             cpu = {"value": None, "error": repr(e)}
-    wl = ("unet_bn L5 base64 1024x1024x3 bf16 B=4/GPU DP (BASELINE configs[2])" if args.preset == "unet_bn"
-          else "adipose_v3 (reference topology) train step")
+    wl = workload_label(args)
     line = {
         "metric": "1024^2 tiles/sec (train)", "value": round(value, 4), "unit": "tiles/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),

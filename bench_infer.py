@@ -109,7 +109,7 @@ def fp8_main(args):
              for b in range(B)]
     f8 = {k: v for k, v in summ.items() if k[1] == 2}
     dom = max(f8.items(), key=lambda kv: kv[1][2])
-    (kname, dcode), (n, flops, ms) = dom
+    (kname, dcode), (n, flops, ms, _nb) = dom
     achieved = flops / (ms * 1e-3) / 1e12
     line = {
         "metric": "1024^2 tiles/s (fp8 forward) + Dice vs bf16", "value": round(steps * B / el8, 3), "unit": "tiles/s",
@@ -220,7 +220,7 @@ def main():
     summ = timer.summary()
     if rank == 0:
         dom = max(summ.items(), key=lambda kv: kv[1][2])
-        (kname, dcode), (n, flops, ms) = dom
+        (kname, dcode), (n, flops, ms, _nb) = dom
         dname = DNAME[dcode]
         achieved = flops / (ms * 1e-3) / 1e12
         tot_ms = sum(v[2] for v in summ.values())

@@ -29,13 +29,13 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 11 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 12 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
                               v9: adp_conv_desc.bn_defer_fold + adp_bn_finalize_fold;
                               v10: adp_bn_bwd_apply_head, adp_head_sigmoid_bwd_bnr with dx = NULL, adp_conv_wgrad_bn;
-                              v11: adp_sum_bf16 */
+                              v11: adp_sum_bf16; v12: adp_timing / adp_timing_read, unet_bn handle preset */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -109,6 +109,15 @@ int adp_abi_version(void);
  * "tap64_bal", "tap64_korder", "wgrad_ra", "wgrad_blocks", "wgrad_min_chunk", "wgrad_glds_tn64";
  * "wgrad_debug" is a timing-only ablation (bit 0 skips the dW atomics: results invalid). */
 int adp_set_option(const char* name, int value);
+/* Per-launch timing of the conv kernels (bench roofline; no reference counterpart). mode 1: clear the record
+ * and start recording a HIP event pair around the MAIN kernel of every adp_conv_fwd / adp_conv_wgrad(_bn)
+ * launch (the kernel adp_last_kernel names; statistic folds, split reduces, bias sums and BatchNorm applies
+ * around it are excluded, so each pair times exactly one kernel of rocprofv3's list); 0: stop recording (the
+ * record is kept); 2: stop and clear. */
+int adp_timing(int mode);
+/* Reads the record (synchronises on its events): *n = number of timed launches; for i < max: names[i *
+ * name_len] = kernel name, ms[i] = its duration (-1 if its end was not marked). max = 0 only counts. */
+int adp_timing_read(int max, char* names, int name_len, float* ms, int* n);
 
 /* ---- dense layers (replace Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter / BiasAdd /
  *      Relu / ResizeNearestNeighbor / ConcatV2 / AddN / Dropout of
@@ -278,6 +287,31 @@ int adp_pixel_counts(size_t n, const float* pred, const float* truth, float thr,
 int adp_threshold_hist(size_t n, const float* pred, const float* truth, int nthr, const double* thr,
                        unsigned long long* hist, adp_stream_t s);
 
+/* ---- the rest of the src/utils/model.py loss / metric surface (not on the v3 training step) ---------- */
+/* weighted_dice_loss / weighted_bce_dice_loss weight map (model.py:104-116, 140-151): y (B,H,W) f32 is expanded
+ * to (1,B,H,W) channels_last, so K.pool2d(ksize x ksize, stride 1, 'same', 'avg') averages over (B, H) per W
+ * (TF 'SAME' average: padding excluded from the count); weight = 1 + 2 * (0.005 < avg < 0.995); wsum[0] +=
+ * sum(weight) (f64, caller zeroes). tmp: B*H*W f32 scratch. ksize odd (21 in the reference). */
+int adp_border_weight(int B, int H, int W, int ksize, const float* y, float* tmp, float* weight, double* wsum,
+                      adp_stream_t s);
+/* With w = weight * (n / wsum[0]) (f32, the w0/w1 renormalisation): stats[0..4] += {sum w^2 y p, sum w^2 y,
+ * sum w^2 p, sum bce_w, sum w}, bce_w = (1-y) l + (1 + (w-1) y)(log(1 + exp(-|l|)) + max(-l, 0)),
+ * l = log(p'/(1-p')), p' = clip(p, 1e-7, 1-1e-7) (weighted_dice_coeff :120-125, weighted_bce_loss :127-136). */
+int adp_weighted_loss_stats(size_t n, const float* y, const float* p, const float* weight, const double* wsum,
+                            double* stats, adp_stream_t s);
+/* dp = wbce * d(stats[3]/stats[4])/dp + wdice * d(1 - (2 stats[0] + 1)/(stats[1] + stats[2] + 1))/dp (TF's
+ * subgradients of clip / abs / maximum), from the final stats. */
+int adp_weighted_loss_grad(size_t n, const float* y, const float* p, const float* weight, const double* wsum,
+                           const double* stats, float wbce, float wdice, float* dp, adp_stream_t s);
+/* K.mean / K.min / K.max / K.std (population) of n floats (act_mean, act_min, act_max, act_std, mean_diff
+ * model.py:21-34): out (device f64[4]) = {mean, min, max, std}; work >= 1024 * 40 bytes. */
+int adp_value_stats(size_t n, const float* x, void* work, double* out, adp_stream_t s);
+/* argmax / argmin over the last axis (first occurrence) of y and p, rows x W (model.py:36-91): out (int64[7],
+ * caller zeroes) += {tru_pos = sum at*ap, fls_pos = sum clip(ap-at,0,1), tru_neg = sum it*ip,
+ * fls_neg = sum clip(ip-it,0,1), #(at*ap >= 1), #(ap >= 1), #(at >= 1)} (the last three: precision_onehot /
+ * recall_onehot's rounded counts). */
+int adp_onehot_counts(int rows, int W, const float* y, const float* p, unsigned long long* out, adp_stream_t s);
+
 /* ---- training-time augmentation + normalisation of gray (H, W) f32 planes (src/utils/data.py:13-264,
  * 398-429); random parameters are drawn by the host in the reference's RandomState order ---------- */
 /* np.rot90(k) then fliplr then flipud (random_rotation_90 / random_flip, data.py:13-29); out of place */
@@ -339,21 +373,35 @@ int adp_boundary_metrics(int H, int W, const float* pred, const float* truth, fl
                          double* out, adp_stream_t s);
 
 /* ---- handle-level engine: native adipose_v3 inference for non-Python callers ---- */
-#define ADP_PRESET_ADIPOSE_V3 0
+#define ADP_PRESET_ADIPOSE_V3 0 /* AdiposeUNetV3.build_model (train_adipose_unet_v3.py:660-758) */
+#define ADP_PRESET_UNET_BN 1    /* BASELINE.json configs 2/3/5: L levels, base width, [conv3x3 -> BatchNorm -> ReLU] x 2,
+                                   MaxPool 2x2, ConvTranspose 2x2/s2 + skip concat, 1x1 sigmoid head (no reference
+                                   code; the Python schedule is nets.UNetBN) */
 typedef struct adp_handle adp_handle; /* opaque: topology, packed weights, activation buffers */
 typedef struct adp_config {
-  int preset;            /* ADP_PRESET_ADIPOSE_V3 (train_adipose_unet_v3.py:660-758) */
-  int tile;              /* S (the reference hard-codes 1024), multiple of 8 */
+  int preset;            /* ADP_PRESET_ADIPOSE_V3 or ADP_PRESET_UNET_BN */
+  int tile;              /* S (the reference hard-codes 1024), multiple of 8 (unet_bn: of 2^(levels-1)) */
   int max_batch;         /* images x TTA views per forward (activation buffers are sized for it) */
   int dtype;             /* ADP_DTYPE_F32 (the reference's fp32 numerics) or ADP_DTYPE_BF16 */
-  int deep_supervision;  /* 1: the aux_out1 / aux_out2 heads exist (checkpoint layout); inference = main_out */
-  int init_nb;           /* base width, 44 (build_model(init_nb=44)) */
+  int deep_supervision;  /* adipose_v3: 1 = the aux_out1 / aux_out2 heads exist (checkpoint layout); inference = main_out */
+  int init_nb;           /* adipose_v3 base width, 44 (build_model(init_nb=44)) */
+  /* v12 */
+  int levels;            /* unet_bn: resolution levels (0 -> 5; configs[2] = 5, configs[1] = 4) */
+  int base;              /* unet_bn: level-0 width (0 -> 64) */
+  int in_ch;             /* unet_bn: input channels (0 -> 3), tiles (S, S, in_ch) interleaved f32 */
+  float dropout_rate;    /* adipose_v3: build_model(dropout_rate) (0.3), used by adp_train_step when its cfg's
+                            dropout_rate < 0; unet_bn has no dropout layers (ignored) */
+  unsigned seed;         /* dropout mask stream: step k uses hash seed (seed + k) * 7919 + 17 (0 = the Python
+                            Trainer's stream) */
 } adp_config;
 int adp_create(const adp_config* cfg, int device, adp_handle** out);
 int adp_destroy(adp_handle* h);
 /* i-th parameterised layer name (Keras layer names), NULL past the end */
 const char* adp_param_name(const adp_handle* h, int i);
-/* slot 0 = kernel (Keras HWIO for convs, (1,1,Cin,Nout) for heads), 1 = bias; n = element count */
+/* adipose_v3: slot 0 = kernel (Keras HWIO for convs, (1,1,Cin,Nout) for heads), 1 = bias. unet_bn: conv layers
+ * (enc*_conv*, dec*_conv*) 0 = kernel HWIO, 1 = gamma, 2 = beta, 3 = moving mean, 4 = moving variance;
+ * ConvTranspose dec*_up 0 = kernel (Cin, Cout, 2, 2), 1 = bias; head 0 = kernel (1,1,Cin,1), 1 = bias.
+ * n = element count. unet_bn parameter I/O is synchronous (the device is synchronised first). */
 int adp_param_size(adp_handle* h, const char* layer, int slot, size_t* n);
 int adp_set_param(adp_handle* h, const char* layer, int slot, const float* host, size_t n);
 int adp_get_param(adp_handle* h, const char* layer, int slot, float* host, size_t n);
@@ -365,6 +413,8 @@ int adp_get_param(adp_handle* h, const char* layer, int slot, float* host, size_
 int adp_forward(adp_handle* h, const float* images, int n, long long img_stride, float mean, float std,
                 int tta_mode, float* prob, adp_stream_t s);
 
+/* unet_bn: images are n device f32 (S, S, in_ch) interleaved tiles (img_stride floats apart, <= 0: dense);
+ * BatchNorm uses the running statistics (eval). */
 /* One training step of AdiposeUNetV3 (model.net.fit, train_adipose_unet_v3.py:1316-1324) on the handle:
  * forward with dropout -> main / deep-supervision losses and their gradients (compile_model :780-879:
  * OHEM or BCE+Dice main head, BCE+Dice aux heads, label smoothing :244-279, weights 1.0 / 0.4 / 0.3) ->
@@ -373,7 +423,12 @@ int adp_forward(adp_handle* h, const float* images, int n, long long img_stride,
  * gradients or updates. x: n device f32 (S,S) normalised images, y: n device f32 (S,S) labels in {0,1};
  * n <= max_batch. metrics (host, 6 floats, the call synchronises the stream): loss, main_out_loss,
  * aux_out1_loss, aux_out2_loss, main_out_dice_coef, main_out_binary_accuracy (Keras' per-batch values;
- * with a communicator: of the global batch). The first call allocates the optimizer state (m, v = 0). */
+ * with a communicator: of the global batch). The first call allocates the optimizer state (m, v = 0).
+ * With a communicator the gradients are SUM-all-reduced in ~16 MB buckets on a communication stream, each as
+ * soon as the backward has produced all of its layers (overlapping the remaining backward launches).
+ * unet_bn: x is n (S, S, in_ch) f32 normalised tiles; the loss is the main head's (OHEM or BCE + Dice per
+ * use_hard_mining, label smoothing), BatchNorm uses batch statistics and updates the running ones
+ * (momentum 0.1, eps 1e-5); freeze_encoder must be 0. */
 typedef struct adp_train_cfg {
   int use_hard_mining;       /* OHEM main loss (--use-hard-mining, default on) */
   float hard_example_ratio;  /* 0.7 */

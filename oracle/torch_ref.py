@@ -277,6 +277,90 @@ def binary_accuracy(y, p, threshold=0.5):
     return (y == (p > threshold).to(p.dtype)).to(torch.float32).mean()
 
 
+# ------------------------------------------------------- rest of the model.py loss / metric surface
+def jaccard_coef(y, p):
+    """src/utils/model.py:8-12 (axis=[0,-1,-2] of a (B,H,W) tensor: one scalar)."""
+    inter = (y * p).sum()
+    return (inter + KEPS) / ((y + p).sum() - inter + KEPS)
+
+
+def jaccard_coef_int(y, p):
+    """model.py:14-19: round(clip(p, 0, 1)) in the intersection, raw p in the sum (quirk kept)."""
+    inter = (y * torch.round(torch.clamp(p, 0.0, 1.0))).sum()
+    return (inter + KEPS) / ((y + p).sum() - inter + KEPS)
+
+
+def avg_pool_same(x4, k):
+    """K.pool2d(x4, (k, k), strides=(1, 1), padding='same', pool_mode='avg') on a channels_last (N, D1, D2, C)
+    tensor: TF's SAME average pooling divides by the number of VALID elements in each window."""
+    xc = x4.permute(0, 3, 1, 2)
+    r = k // 2
+    s = F.avg_pool2d(xc, k, stride=1, padding=r, count_include_pad=False)
+    return s.permute(0, 2, 3, 1)
+
+
+def border_weight(y, k=21):
+    """The weight map of weighted_dice_loss / weighted_bce_dice_loss (model.py:104-116, 140-151):
+    y (B,H,W) -> expand_dims(0) = (1,B,H,W), pooled over (B,H) with W as channels (the reference's quirk);
+    border = (avg > 0.005) * (avg < 0.995); weight = 1 + 2 * border renormalised by sum(ones)/sum(weight).
+    Returns the (1,B,H,W) weight."""
+    y4 = y[None]
+    avg = avg_pool_same(y4, k)
+    border = (avg > 0.005).to(y.dtype) * (avg < 0.995).to(y.dtype)
+    weight = torch.ones_like(avg)
+    w0 = weight.sum()
+    weight = weight + border * 2
+    w1 = weight.sum()
+    return weight * (w0 / w1)
+
+
+def weighted_dice_coeff(y, p, weight):
+    """model.py:120-125 (y and p broadcast against weight's (1,B,H,W))."""
+    w = weight * weight
+    return (2.0 * (w * (y * p)).sum() + 1.0) / ((w * y).sum() + (w * p).sum() + 1.0)
+
+
+def weighted_bce_loss(y, p, weight):
+    """model.py:127-136; max(-l, 0) written as where(-l >= 0, -l, 0) so its subgradient at l = 0 is TF's
+    (tf.maximum routes the gradient to its first argument on ties; torch.maximum would split it)."""
+    pc = torch.clamp(p, KEPS, 1.0 - KEPS)
+    lg = torch.log(pc / (1.0 - pc))
+    relu_neg = torch.where(-lg >= 0, -lg, torch.zeros_like(lg))
+    loss = (1.0 - y) * lg + (1.0 + (weight - 1.0) * y) * (torch.log(1.0 + torch.exp(-torch.abs(lg))) + relu_neg)
+    return loss.sum() / weight.sum()
+
+
+def weighted_dice_loss(y, p):
+    """model.py:103-118 (y expanded to (1,B,H,W) before the pool and the coefficient)."""
+    wt = border_weight(y)
+    return 1.0 - weighted_dice_coeff(y[None], p, wt)
+
+
+def weighted_bce_dice_loss(y, p):
+    """model.py:139-153"""
+    wt = border_weight(y)
+    y4 = y[None]
+    return weighted_bce_loss(y4, p, wt) + (1.0 - weighted_dice_coeff(y4, p, wt))
+
+
+def metric_helpers(y, p):
+    """model.py:21-91 on (B,H,W) tensors: argmax / argmin over the last axis (first occurrence)."""
+    at, ap = torch.argmax(y, -1), torch.argmax(p, -1)
+    it, ip = torch.argmin(y, -1), torch.argmin(p, -1)
+    ytf, ypf = at.double(), ap.double()
+    tp = torch.round(torch.clamp(ytf * ypf, 0, 1)).sum()
+    pp = torch.round(torch.clamp(ypf, 0, 1)).sum()
+    pos = torch.round(torch.clamp(ytf, 0, 1)).sum()
+    prec = tp / (pp + KEPS)
+    rec = tp / (pos + KEPS)
+    return {"mean_diff": (p.double().mean() - y.double().mean()).item(), "act_mean": p.double().mean().item(),
+            "act_min": p.min().item(), "act_max": p.max().item(), "act_std": p.double().std(unbiased=False).item(),
+            "tru_pos": int((at * ap).sum()), "fls_pos": int(torch.clamp(ap - at, 0, 1).sum()),
+            "tru_neg": int((it * ip).sum()), "fls_neg": int(torch.clamp(ip - it, 0, 1).sum()),
+            "precision_onehot": prec.item(), "recall_onehot": rec.item(),
+            "fmeasure_onehot": (2 * (prec * rec) / (prec + rec + KEPS)).item()}
+
+
 # --------------------------------------------------------------------------------- optimizer
 class KerasAdam:
     """Keras 2.13 Adam / AdamW update_step (optimizer_experimental), for parity tests."""

@@ -183,3 +183,92 @@ def test_native_train_step_bf16_and_comm(weights):
     comm_destroy(comm)
     for e in (eng, a, b):
         e.close()
+
+
+# ------------------------------------------------------------------------------ unet_bn behind the handle
+def _bn_case(L=3, S_=64, B=2, seed=5):
+    w = R.unet_bn_keras_weights(levels=L, base=64, in_ch=3, seed=seed)
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((B, S_, S_, 3)).astype(np.float32)
+    yy, xx = np.mgrid[0:S_, 0:S_]
+    y = np.stack([((yy - 20 - 8 * b) ** 2 + (xx - 30) ** 2 < 300).astype(np.float32) for b in range(B)])
+    return w, x, y
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_native_unet_bn_train_step_matches_python(dtype):
+    """unet_bn through adp_create -> adp_train_step -> adp_get_param (csrc/engine.cpp) vs the Python schedule
+    (nets.UNetBN + trainer.Trainer) on the same weights and tiles: per-step Keras metrics, weights after two
+    Adam steps, BatchNorm running statistics, and the eval forward (adp_forward) after training."""
+    from adipose_amd.engine import NativeUNetBN, train_cfg
+    from adipose_amd.nets import UNetBN
+    from adipose_amd.trainer import LossConfig, Trainer
+    L, S_, B, lr = 3, 64, 2, 1e-3
+    w, x, y = _bn_case(L, S_, B)
+    net = UNetBN(B, S_, levels=L, base=64, in_ch=3, dtype=dtype, device="cuda")
+    net.set_weights(w)
+    tr = Trainer(net, LossConfig(use_hard_mining=False), lr=lr)
+    eng = NativeUNetBN(tile=S_, max_batch=B, dtype=dtype, levels=L)
+    assert eng.layer_names() == list(net.layers)
+    eng.set_weights(w)
+    got0 = eng.get_weights()
+    for k in w:
+        for a, b in zip(w[k], got0[k]):
+            np.testing.assert_array_equal(np.asarray(a, np.float32).ravel(), b)
+    cfg = train_cfg(use_hard_mining=False)
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    tol = 2e-5 if dtype == "f32" else 1e-3
+    for step in range(2):
+        tr.train_step(xd, yd)
+        ref = tr.read_metrics()
+        got = eng.train_step(x, y, lr, cfg)
+        for k in ("loss", "main_out_loss", "main_out_dice_coef", "main_out_binary_accuracy"):
+            assert abs(got[k] - ref[k]) <= tol * max(1.0, abs(ref[k])), (step, k, got[k], ref[k])
+    w_eng = eng.get_weights()
+    w_py = {n: net.get_layer_weights(n) for n in net.layers}
+    _compare_weights(w_eng, w_py, lr, 2)
+    for n, l in net.layers.items():
+        if getattr(l, "bn", False):
+            rm, rv = eng.running_stats(n)
+            np.testing.assert_allclose(rm, net.running[n][0][:l.cout].cpu().numpy(), rtol=1e-3, atol=1e-5, err_msg=n)
+            np.testing.assert_allclose(rv, net.running[n][1][:l.cout].cpu().numpy(), rtol=1e-3, atol=1e-5, err_msg=n)
+    # eval forward (running statistics) of the trained handle vs the Python network
+    p_eng = eng.predict_batch(x, 0.0, 1.0).cpu().numpy()
+    ops_x = net.acts(B)["x"]
+    from adipose_amd import ops
+    ops.prep_input(xd, ops_x, mean=0.0, std=1.0)
+    p_py = net.forward(B, train=False)["main_out"].cpu().numpy()
+    assert np.abs(p_eng - p_py).max() <= (1e-4 if dtype == "f32" else 2e-2), np.abs(p_eng - p_py).max()
+    eng.close()
+
+
+def test_native_unet_bn_bucketed_comm_and_errors():
+    """The bucketed, stream-overlapped gradient all-reduce (one-rank RCCL communicator) leaves the unet_bn step
+    unchanged; bad parameter names / slots and a frozen-encoder request are rejected."""
+    from adipose_amd._lib import AdpError
+    from adipose_amd.engine import NativeUNetBN, comm_destroy, comm_init, comm_unique_id, train_cfg
+    L, S_, B, lr = 3, 64, 2, 1e-3
+    w, x, y = _bn_case(L, S_, B, seed=6)
+    a = NativeUNetBN(tile=S_, max_batch=B, dtype="f32", levels=L)
+    b = NativeUNetBN(tile=S_, max_batch=B, dtype="f32", levels=L)
+    a.set_weights(w)
+    b.set_weights(w)
+    comm = comm_init(1, comm_unique_id(), 0)
+    b.set_comm(comm)
+    cfg = train_cfg(use_hard_mining=False)
+    for _ in range(2):
+        ma, mb = a.train_step(x, y, lr, cfg), b.train_step(x, y, lr, cfg)
+        for k in ma:
+            assert abs(ma[k] - mb[k]) <= 2e-5 * max(1.0, abs(ma[k])), k
+    _compare_weights(a.get_weights(), b.get_weights(), lr, 2)
+    b.set_comm(None)
+    comm_destroy(comm)
+    with pytest.raises(AdpError):
+        a.train_step(x, y, lr, train_cfg(use_hard_mining=False, freeze_encoder=True))
+    with pytest.raises(AdpError):
+        a.set_weights({"enc0_conv1": [np.zeros(7, np.float32)]})
+    from adipose_amd._lib import call
+    with pytest.raises(AdpError):
+        call("adp_set_param", a._h, b"head", 2, np.zeros(1, np.float32).ctypes.data, 1)
+    a.close()
+    b.close()
