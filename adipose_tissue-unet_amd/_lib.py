@@ -117,6 +117,7 @@ _SIGS = {
     "adp_weighted_loss_grad": [_S, _P, _P, _P, _P, _P, _F, _F, _P, _P],
     "adp_value_stats": [_S, _P, _P, _P, _P],
     "adp_onehot_counts": [_I, _I, _P, _P, _P, _P],
+    "adp_boundary_refine": [_I, _I, _P, _I, C.POINTER(C.c_int), C.POINTER(C.c_int), _I, _F, _F, _P, _P, _P],
     "adp_pack_weights_batch": [_I, _I, _P, _P],
     "adp_bn_apply_maxpool2": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "adp_head_sigmoid_bwd_bnr": [_I, _S, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],

@@ -666,6 +666,9 @@ class UNetBN(UNetEngine):
     # (adp_conv_wgrad_bn: computed inside the halo weight-gradient kernel on levels 0-1, which also stores
     # dz for the data gradient); False: adp_bn_bwd_apply, then the weight gradient re-reads dz
     fuse_bn_wgrad = True
+    # the encoder pool backward recomputes its argmax from z (relu(z*scale+shift), rounded as stored) instead of
+    # reading the stored activation
+    pool_argmax_from_z = True
 
     def __init__(self, batch, size, *, levels=5, base=64, in_ch=3, dtype="bf16", device="cuda", seed=865,
                  bn_eps=1e-5, bn_momentum=0.1):
@@ -988,7 +991,7 @@ class UNetBN(UNetEngine):
                 dA2 = gb(f"dA_z{i}_2", z2)
                 # pool backward + skip gradient, with enc{i}_conv2's BN-backward reduction fused in
                 ops.maxpool2_bwd(a[f"az{i}_2"], dpool, dA2, addend=skip_grad[i],
-                                 bn_reduce=self._bn_red(f"enc{i}_conv2", z2))
+                                 bn_reduce=self._bn_red(f"enc{i}_conv2", z2), argmax_from_z=self.pool_argmax_from_z)
             else:
                 dA2 = bott_dA
             dz2 = gb(f"dz_z{i}_2", z2)

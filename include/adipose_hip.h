@@ -372,6 +372,14 @@ int adp_distance_transform(int H, int W, const float* src, float thr, double sy,
 int adp_boundary_metrics(int H, int W, const float* pred, const float* truth, float thr, double sy, double sx,
                          double* out, adp_stream_t s);
 
+/* BoundaryRefiner.refine (full_evaluation_enhanced.py:357-393) of one (H, W) f32 probability map: m = u8(mask*255),
+ * ellipse (ksize; row_lo / row_hi = HOST arrays of ksize column extents, getStructuringElement(MORPH_ELLIPSE))
+ * erode / dilate -> band = dilated>0 xor eroded>0, bilateral filter (d, sigma_color, sigma_space;
+ * cv2.bilateralFilter semantics, BORDER_REFLECT_101) inside the band, MORPH_OPEN then MORPH_CLOSE, out = f32(x / 255).
+ * work: >= 4*H*W bytes. ksize <= 31, d / 2 <= 15. */
+int adp_boundary_refine(int H, int W, const float* mask, int ksize, const int* row_lo, const int* row_hi, int d,
+                        float sigma_color, float sigma_space, void* work, float* out, adp_stream_t s);
+
 /* ---- handle-level engine: native adipose_v3 inference for non-Python callers ---- */
 #define ADP_PRESET_ADIPOSE_V3 0 /* AdiposeUNetV3.build_model (train_adipose_unet_v3.py:660-758) */
 #define ADP_PRESET_UNET_BN 1    /* BASELINE.json configs 2/3/5: L levels, base width, [conv3x3 -> BatchNorm -> ReLU] x 2,

@@ -139,16 +139,40 @@ def test_auc_metrics_vs_sklearn(shape, levels):
     assert abs(m["pr_auc"] - average_precision_score(yt, pf)) <= 1e-9
 
 
-def test_boundary_refiner_shapes_and_fixed_points():
-    r = E.BoundaryRefiner(kernel_size=5)
+def test_oracle_boundary_refiner_fixed_points_and_ellipse():
+    """The cv2 restatement the GPU refiner is checked against: getStructuringElement(MORPH_ELLIPSE) rows for
+    5 x 5 and 7 x 7 (OpenCV's published masks), constant maps are fixed points, output in [0, 1]."""
+    lo, hi = NR.cv_ellipse_rows(5)
+    assert list(zip(lo, hi)) == [(2, 3), (0, 5), (0, 5), (0, 5), (2, 3)]
+    lo, hi = NR.cv_ellipse_rows(7)
+    assert list(zip(lo, hi)) == [(3, 4), (1, 6), (0, 7), (0, 7), (0, 7), (1, 6), (3, 4)]
+    assert E.ellipse_rows(9) == NR.cv_ellipse_rows(9)
     z = np.zeros((24, 24), np.float32)
-    assert np.array_equal(r.refine(z), z)
+    assert np.array_equal(NR.boundary_refine(z), z)
     o = np.ones((24, 24), np.float32)
-    assert np.array_equal(r.refine(o), o)
+    assert np.array_equal(NR.boundary_refine(o), o)
     m = np.zeros((24, 24), np.float32)
     m[6:18, 6:18] = 1
-    out = r.refine(m)
+    out = NR.boundary_refine(m)
     assert out.dtype == np.float32 and out.shape == m.shape and out.min() >= 0 and out.max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,k,d,seed", [(64, 64, 5, 5, 0), (100, 37, 7, 9, 1), (256, 256, 5, 5, 2), (33, 65, 3, 3, 3)])
+def test_gpu_boundary_refiner_vs_oracle(H, W, k, d, seed):
+    """adp_boundary_refine (csrc/refine.hip) bit for bit against the numpy restatement of the cv2 calls on
+    smoothed random probability maps (soft edges, so the bilateral filter acts inside the band)."""
+    from scipy import ndimage
+    rng = np.random.default_rng(seed)
+    m = ndimage.gaussian_filter(rng.random((H, W)), 3)
+    m = np.clip((m - m.mean()) * 8 + 0.5, 0, 1).astype(np.float32)
+    r = E.BoundaryRefiner(kernel_size=k, bilateral_d=d)
+    got = r.refine(m)
+    ref = NR.boundary_refine(m, kernel_size=k, d=d)
+    assert got.dtype == np.float32
+    np.testing.assert_array_equal(got, ref)
+    for c in (np.zeros((H, W), np.float32), np.ones((H, W), np.float32)):
+        np.testing.assert_array_equal(r.refine(c), c)
 
 
 def test_eval_cli_flags():

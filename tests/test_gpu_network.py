@@ -224,6 +224,34 @@ def test_unet_bn_forward_and_grads(dtype, base, S):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("flag", ["fuse_head_bn", "head_recompute_dA", "fuse_bn_fold", "fuse_bn_wgrad",
+                                  "pool_argmax_from_z"])
+def test_unet_bn_fallback_paths_match_default(flag):
+    """The alternate schedules nets.UNetBN keeps for A/B runs (each fusion flag off, and the pool backward's
+    argmax read from the stored activation instead of recomputed from z) give the default path's outputs and
+    gradients (bf16, base 64, so every fused kernel form is the one the bench runs). The BatchNorm sums are
+    atomics in a run-dependent order, so two runs of one path already differ by bf16 rounding flips: outputs
+    within 5e-3, gradient cosines above 0.999 (a dropped or doubled term is far outside both)."""
+    B, L, S = 2, 3, 64
+    w = R.unet_bn_keras_weights(levels=L, base=64, in_ch=3, seed=5)
+    x, y = synth_batch(B, S, C=3, seed=9)
+    res = []
+    for off in (False, True):
+        net = UNetBN(B, S, levels=L, base=64, in_ch=3, dtype="bf16", device=DEV)
+        net.set_weights(w)
+        if off:
+            setattr(net, flag, False)
+        tr = Trainer(net, LossConfig(use_hard_mining=False))
+        outs, _ = _unet_bn_step(net, tr, x, y, B)
+        res.append((outs["main_out"].cpu().clone(), {n: net.get_layer_grads(n) for n in w}))
+    (p0, g0), (p1, g1) = res
+    assert (p0 - p1).abs().max().item() <= 5e-3
+    for n in w:
+        for a, b in zip(g0[n], g1[n]):
+            c = cos(torch.as_tensor(a), torch.as_tensor(b))
+            assert c > 0.999, (flag, n, c)
+
+
 def test_unet_bn_repeated_steps_and_double_backward():
     """The per-step statistic arena (BatchNorm sums zeroed once per training forward, the ConvTranspose
     bias-gradient sums once per backward) must not carry anything over: a second training forward +

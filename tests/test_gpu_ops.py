@@ -721,6 +721,36 @@ def test_wgrad_bn_apply_fused(N, H, W, parts, cout, dtn, fused):
     assert relerr(dW2.cpu(), dW1.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("opt", ["wgrad_tap64", "wgrad_halop", "wgrad_bna"])
+def test_wgrad_bn_apply_with_kernel_options_off(opt):
+    """adp_conv_wgrad_bn with the halo weight-gradient kernel switched off (wgrad_tap64 = 0 is a documented
+    'off' value): the library must run the BatchNorm-backward apply itself before the fallback kernel, so dz
+    and dW equal the two-launch form (the fused form used to fall through to a kernel reading an
+    uncomputed dY)."""
+    N, H, W, cout = 2, 32, 64, 64
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(N, H, W, 64, generator=g).to(DEV, torch.bfloat16)
+    z = (torch.randn(N, H, W, cout, generator=g) * 2).to(DEV, torch.bfloat16)
+    dA = torch.randn(N, H, W, cout, generator=g).to(DEV, torch.bfloat16)
+    vec = lambda: (torch.rand(cout, generator=g) + 0.5).to(DEV)   # noqa: E731
+    sc, sh, mu, ist, gam = vec(), vec() - 1.0, vec() - 1.0, vec(), vec()
+    dg, db = torch.randn(cout, generator=g).to(DEV), torch.randn(cout, generator=g).to(DEV)
+    count = N * H * W
+    dz1, dz2 = torch.full_like(z, 7.0), torch.full_like(z, 7.0)
+    dW1 = torch.zeros((cout, 9 * 64), device=DEV)
+    dW2 = torch.zeros_like(dW1)
+    ops.bn_bwd_apply(dA, z, sc, sh, mu, ist, gam, dg, db, count, dz1)
+    ops.conv_wgrad(x, dz1, dW1, cout)
+    ops.set_option(opt, 0)
+    try:
+        ops.conv_wgrad(x, dz2, dW2, cout, bn_apply=(dA, z, sc, sh, mu, ist, gam, dg, db, count))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option(opt, None)
+    assert torch.equal(dz1, dz2)
+    assert relerr(dW2.cpu(), dW1.cpu()) < 1e-5
+
+
 @pytest.mark.parametrize("N,H,W,parts,cout", [(2, 64, 64, [64], 64), (1, 32, 96, [64], 64), (3, 16, 32, [64], 64),
                                                (2, 32, 64, [64, 64], 64), (1, 32, 32, [128], 128),
                                                (2, 16, 64, [128, 64], 128)])
