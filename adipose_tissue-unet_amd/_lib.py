@@ -136,10 +136,30 @@ _SIGS = {
 }
 
 _lib = None
+CSRC = os.path.join(PKG_DIR, "csrc")
 
 
 def exported_symbols():
-    return ["adp_last_error", "adp_last_kernel", "adp_param_name"] + list(_SIGS)
+    return ["adp_last_error", "adp_last_kernel", "adp_param_name", "adp_source_hash"] + list(_SIGS)
+
+
+def source_hash():
+    """sha256 of the sources the Makefile hashes into the library's build record (same files, same order),
+    or None when the sources are not beside the package."""
+    import hashlib
+    import re
+    mk = os.path.join(CSRC, "Makefile")
+    if not os.path.exists(mk):
+        return None
+    text = open(mk).read()
+    srcs = re.search(r"^SRCS = (.*)$", text, re.M).group(1).split()
+    hashed = re.search(r"^HASHED = (.*)$", text, re.M).group(1).split()
+    files = [f for h in hashed for f in (srcs if h == "$(SRCS)" else [h])]
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def lib():
@@ -157,12 +177,20 @@ def lib():
         L.adp_last_kernel.argtypes = []
         L.adp_param_name.restype = C.c_char_p
         L.adp_param_name.argtypes = [C.c_void_p, C.c_int]
+        L.adp_source_hash.restype = C.c_char_p
+        L.adp_source_hash.argtypes = []
         for name, args in _SIGS.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
         if L.adp_abi_version() != ABI_VERSION:
             raise AdpError(f"{LIB_PATH}: ABI version {L.adp_abi_version()} != {ABI_VERSION}; rebuild the library")
+        # the build record ties the binary to the sources beside it (a stale library is refused)
+        want = source_hash()
+        got = L.adp_source_hash().decode()
+        if want is not None and got != want and not os.environ.get("ADP_LIB_PATH"):
+            raise AdpError(f"{LIB_PATH} was built from other sources (record {got[:16]}, tree {want[:16]}); "
+                           "rebuild it: make -C adipose_tissue-unet_amd/csrc")
         _lib = L
     return _lib
 

@@ -103,6 +103,9 @@ const char* adp_last_error(void);
    (as rocprofv3 prints it), for per-kernel timing and roofline accounting. */
 const char* adp_last_kernel(void);
 int adp_abi_version(void);
+/* Build record: sha256 (hex) of the library's sources, in the Makefile's HASHED order (a caller can check that
+ * a prebuilt binary matches the sources it ships with). */
+const char* adp_source_hash(void);
 /* Runtime switches, process-global (A/B of kernel variants in one process). value == INT_MIN restores
  * the built-in default. Kernel selection: "conv_fast" (2 = LDS-DMA kernels, default; 1 = register-staged;
  * 0 = generic), "fwd_tap64" / "wgrad_tap64" (0 off, 1 auto, 2+c force tile configuration c),
