@@ -40,6 +40,7 @@ struct FwdArgs {
   int debug_flags;       // timing-only ablations (option "fwd_debug"): bit1 skips the BN-statistics atomics
   float* stat;           // BatchNorm accumulator replicas (adp::stat_scratch) for bn_sum / bnr_* launches
   int defer_fold;        // bn_sum launch whose replica sums adp_bn_finalize_fold adds in (adp_conv_desc)
+  int f32;               // f32 launch on the LDS-DMA tap kernel (32-channel K steps, f32 MFMA)
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
@@ -144,7 +145,7 @@ ADP_DEV bf16x8 tr_frag_sw(const unsigned char* base, int row0, int col0, int lan
 // stored values, or with bnr_z the BatchNorm-backward sums (db, db*xhat) of the stored gradient.
 // F8: fp8 launch — acc * wscale[n] before the bias, fp8 or bf16 store (compiled only into the fp8
 // kernels, so the bf16 kernels keep their register budget)
-template <int NTH, int BN, bool F8 = false>
+template <int NTH, int BN, bool F8 = false, typename TO = bf16>
 ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int n0, int tid,
                       float (&bs)[8], float (&bq)[8]) {
   constexpr int LT = BN + 4;
@@ -183,7 +184,7 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
         v[j] = (u >= a.drop_rate) ? v[j] * ks : 0.f;
       }
     }
-    Grp<bf16> gr;
+    Grp<TO> gr;
     if (a.out_mode == 1) {
       int sub = n / a.Cps, c = n - sub * a.Cps;
       int nimg = m / HWo, rem = m - nimg * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
@@ -195,18 +196,18 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
         }
       }
       grp_from_f(gr, v);
-      grp_store(gr, reinterpret_cast<bf16*>(a.out) + pix * a.out_stride + c);
+      grp_store(gr, reinterpret_cast<TO*>(a.out) + pix * a.out_stride + c);
     } else if (a.out_mode == 2 && n >= a.split_c) {
       const int c = n - a.split_c;
       if (a.mask2) {
         float mk[8];
-        grp_load(gr, reinterpret_cast<const bf16*>(a.mask2) + (size_t)m * a.mask2_stride + c);
+        grp_load(gr, reinterpret_cast<const TO*>(a.mask2) + (size_t)m * a.mask2_stride + c);
         grp_to_f(gr, mk);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = mk[j] > 0.f ? v[j] * a.mask2_scale : 0.f;
       }
       grp_from_f(gr, v);
-      grp_store(gr, reinterpret_cast<bf16*>(a.out2) + (size_t)m * a.out2_stride + c);
+      grp_store(gr, reinterpret_cast<TO*>(a.out2) + (size_t)m * a.out2_stride + c);
       if (a.bn_sum) {   // channel sums of the out2 part too (e.g. a ConvTranspose bias gradient)
 #pragma unroll
         for (int j = 0; j < 8; ++j) { bs[j] += v[j]; bq[j] += v[j] * v[j]; }
@@ -223,19 +224,19 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
       }
       float f[8];
       if (a.addend) {
-        grp_load(gr, reinterpret_cast<const bf16*>(a.addend) + (size_t)m * a.addend_stride + n);
+        grp_load(gr, reinterpret_cast<const TO*>(a.addend) + (size_t)m * a.addend_stride + n);
         grp_to_f(gr, f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += f[j];
       }
       if (a.mask) {
-        grp_load(gr, reinterpret_cast<const bf16*>(a.mask) + (size_t)m * a.mask_stride + n);
+        grp_load(gr, reinterpret_cast<const TO*>(a.mask) + (size_t)m * a.mask_stride + n);
         grp_to_f(gr, f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = f[j] > 0.f ? v[j] * a.mask_scale : 0.f;
       }
       grp_from_f(gr, v);
-      grp_store(gr, reinterpret_cast<bf16*>(a.out) + (size_t)m * a.out_stride + n);
+      grp_store(gr, reinterpret_cast<TO*>(a.out) + (size_t)m * a.out_stride + n);
       if (a.accum) {
         float* ap = a.accum + (size_t)m * a.accum_stride + n;
         float r[8];
@@ -256,7 +257,7 @@ ADP_DEV void epi_rows(const FwdArgs& a, const float* tile, int rows, int m0, int
 // stored (bf16-rounded) dA, exactly what adp_bn_bwd_reduce would read. Kept separate from epi_rows so
 // that the per-channel parameters cost registers only in the kernels that use them (they are read
 // per row from L1 rather than held across the row loop).
-template <int NTH, int BN>
+template <int NTH, int BN, typename TO = bf16>
 ADP_DEV void epi_rows_bnr(const FwdArgs& a, const float* tile, int rows, int m0, int n0, int tid,
                           float (&bs)[8], float (&bq)[8]) {
   constexpr int LT = BN + 4;
@@ -272,23 +273,23 @@ ADP_DEV void epi_rows_bnr(const FwdArgs& a, const float* tile, int rows, int m0,
     const float4* tp = reinterpret_cast<const float4*>(tile + row * LT + cg * 8);
     float4 t0 = tp[0], t1 = tp[1];
     v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w; v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
-    Grp<bf16> gr;
+    Grp<TO> gr;
     if (a.addend) {
-      grp_load(gr, reinterpret_cast<const bf16*>(a.addend) + (size_t)m * a.addend_stride + n);
+      grp_load(gr, reinterpret_cast<const TO*>(a.addend) + (size_t)m * a.addend_stride + n);
       grp_to_f(gr, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += f[j];
     }
     if (a.mask) {
-      grp_load(gr, reinterpret_cast<const bf16*>(a.mask) + (size_t)m * a.mask_stride + n);
+      grp_load(gr, reinterpret_cast<const TO*>(a.mask) + (size_t)m * a.mask_stride + n);
       grp_to_f(gr, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = f[j] > 0.f ? v[j] * a.mask_scale : 0.f;
     }
     grp_from_f(gr, v);
-    grp_store(gr, reinterpret_cast<bf16*>(a.out) + (size_t)m * a.out_stride + n);
+    grp_store(gr, reinterpret_cast<TO*>(a.out) + (size_t)m * a.out_stride + n);
     grp_to_f(gr, v);   // the stored (rounded) gradient
-    grp_load(gr, reinterpret_cast<const bf16*>(a.bnr_z) + (size_t)m * a.bnr_zs + n);
+    grp_load(gr, reinterpret_cast<const TO*>(a.bnr_z) + (size_t)m * a.bnr_zs + n);
     grp_to_f(gr, f);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {

@@ -22,6 +22,8 @@
 // h4 and h4+4 of the row: the bf16 read pattern, conflict-free under the swizzle), so the k order inside
 // the instruction cancels out of the dot product.
 // The per-output-channel weight scale is applied in the epilogue (FwdArgs::wscale).
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace {
@@ -60,12 +62,18 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, u
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
 }
 
-template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8>
+// F32 (the f32 parity path, adipose_v3 / unet_bn at the reference's precision): 32-channel K steps (a 128-B row
+// holds 32 floats: staging, swizzle and barriers unchanged); each 16-B fragment is 4 k values of one row, fed to
+// four exact v_mfma_f32_16x16x4_f32 (lane group g supplies k = 4g + j to the j-th one: A and B share the
+// permutation, so every k of the step enters the dot product once); f32 epilogue stores.
+template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8, bool F32 = false>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
+  static_assert(!(F8 && F32), "one operand dtype");
+  using TO = typename std::conditional<F32, float, bf16>::type;   // output dtype
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
-  constexpr int ROWB = 128;                        // one K step of one row: 64 bf16 / 128 fp8
-  constexpr int ES = F8 ? 1 : 2;                   // bytes per element
+  constexpr int ROWB = 128;                        // one K step of one row: 64 bf16 / 128 fp8 / 32 f32
+  constexpr int ES = F8 ? 1 : (F32 ? 4 : 2);       // bytes per element
   constexpr int KSTEP = ROWB / ES;                 // K elements per step
   constexpr int QA = BM / 2, QB = BN / 2;          // rows per quarter-tile
   constexpr int GA = QA * 8 / NTH, GB = QB * 8 / NTH;  // glds per thread per quarter
@@ -216,6 +224,19 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
           acc[ha * MIQ + mi][hb * 2 + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
               __builtin_bit_cast(v8i32, fa[mi]), __builtin_bit_cast(v8i32, fb[ni]), acc[ha * MIQ + mi][hb * 2 + ni],
               0, 0, 0, 127, 0, 127);
+    } else if constexpr (F32) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            const f32x4 av = __builtin_bit_cast(f32x4, fa[mi][s]), bv = __builtin_bit_cast(f32x4, fb[ni][s]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[ha * MIQ + mi][hb * 2 + ni] =
+                  __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j], acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
+          }
     } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -290,8 +311,8 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
             tile[((mt / MIQ) * HM + (mt % MIQ) * 16 + rq + r) * LT + wc * 64 + nt * 16 + col] = acc[mt][nt][r];
     }
     ADP_LDS_BARRIER();
-    if constexpr (BNR) epi_rows_bnr<NTH, BN>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
-    else epi_rows<NTH, BN, F8>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
+    if constexpr (BNR) epi_rows_bnr<NTH, BN, TO>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
+    else epi_rows<NTH, BN, F8, TO>(a, tile, TM, m0 + p * TM, n0, tid, bs, bq);
     ADP_LDS_BARRIER();
   }
   if (a.bn_sum || a.bnr_z) epi_bn_flush<NTH, BN>(a, tile, n0, tid, bs, bq);
@@ -306,7 +327,7 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
   const dim3 g(a.nblocks), b(WM * WN * 64);
   // buffer-resource loads need every operand below 2 GiB (32-bit offsets, T64_OOB reserved)
-  const int es = a.f8 ? 1 : 2;
+  const int es = a.f8 ? 1 : (a.f32 ? 4 : 2);
   const size_t pix = (size_t)a.Nimg * a.Hs * a.Ws, lim = (size_t)1 << 31;
   const bool buf = adp::option("tap64_buf", 1) && pix * a.CAs * es < lim && pix * a.CBs * es < lim &&
                    (size_t)((a.Nout + 63) / 64 * 64) * a.Kpad * es < lim;
@@ -316,6 +337,22 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
                     BNRV ? "true" : "false", F8V ? "true" : "false");                                  \
     hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, F8V>), g, b, 0, s, a);           \
   } while (0)
+#define T64_LAUNCH32(BUFV, BNRV)                                                                        \
+  do {                                                                                                 \
+    adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, true>", WM, WN, TM,              \
+                    BUFV ? "true" : "false", BNRV ? "true" : "false");                                 \
+    hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, true>), g, b, 0, s, a);   \
+  } while (0)
+  if (a.f32) {
+    if (a.bnr_z) {
+      if (buf) T64_LAUNCH32(true, true);
+      else T64_LAUNCH32(false, true);
+    } else {
+      if (buf) T64_LAUNCH32(true, false);
+      else T64_LAUNCH32(false, false);
+    }
+    return;
+  }
   if constexpr (TM == 64) {   // fp8: the 64-row-per-wave tiles only (the 128-row ones spill in the K loop)
     if (a.f8) {               // inference launches: no BN-backward epilogue
       if (buf) T64_LAUNCH(true, false, true);
@@ -331,6 +368,7 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
     else T64_LAUNCH(false, false, false);
   }
 #undef T64_LAUNCH
+#undef T64_LAUNCH32
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 256x128 (8 waves, 64x64),
@@ -352,12 +390,13 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   // the fused BN-backward epilogue handles plain stores only (what the data-gradient launches use)
   if (a.bnr_z && (a.out_mode != 0 || a.bias || a.relu || a.drop_rate > 0.f || a.accum || a.bn_sum)) return 0;
   const int Cin_s = a.CAs + a.CBs;
-  const int ks = a.f8 ? 128 : 64;   // channels per K step
+  const int ks = a.f8 ? 128 : (a.f32 ? 32 : 64);   // channels per K step (one 128-B LDS row)
   if (a.scA || a.scB || a.CAs % ks != 0 || a.CBs % ks != 0 || a.K != a.kh * a.kw * Cin_s || a.K % ks != 0 ||
       a.Kpad != a.K)
     return 0;
   int cfg = mode - 2;
   // fp8: the persistent halo forms first (256x256 when a 256-wide N tile is at least 3/4 used, else 256x128)
+  if (a.f32 && !option("f32_tap", 1)) return 0;
   if (a.f8 && (mode == 1 || cfg == 0 || cfg == 1)) {
     const int t = mode == 1 ? ((a.Nout % 256 == 0 || (a.Nout > 256 && a.Nout % 256 >= 192)) ? 0 : 1) : cfg;
     if (launch_fwd_tap64p(a, s, t)) return 1;
@@ -369,6 +408,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
     double best = 0.0;
     for (int c = 0; c < 4; ++c) {
       if (a.f8 && CFG_BM[c] * CFG_BN[c] > 256 * 128) continue;   // fp8: 256x128 / 256x64 tiles
+      if (a.f32 && c == 0) continue;   // f32: the 256x256 tile spills in its f32 epilogue; 256x128 keeps 156 VGPRs
       const long long tn = (a.Nout + CFG_BN[c] - 1) / CFG_BN[c], tmm = (a.M + CFG_BM[c] - 1) / CFG_BM[c];
       const long long blocks = tn * tmm, waves = (blocks + 255) / 256;
       const double colu = (double)a.Nout / (tn * CFG_BN[c]);
@@ -379,8 +419,9 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
     if (best <= 0.0) return 0;
   }
   // the persistent kernel for the 256x256 and 256x128 tiles (BNR launches: option tap64p_bnr)
-  if ((cfg == 0 || cfg == 1) && !a.f8 && (!a.bnr_z || option("tap64p_bnr", 1)) && launch_fwd_tap64p(a, s, cfg))
+  if ((cfg == 0 || cfg == 1) && !a.f8 && !a.f32 && (!a.bnr_z || option("tap64p_bnr", 1)) && launch_fwd_tap64p(a, s, cfg))
     return 1;
+  if (a.f32 && cfg == 0) cfg = 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);
   else if (cfg == 2) launch_cfg<4, 1, 128>(a, s);

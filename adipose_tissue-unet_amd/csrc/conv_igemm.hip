@@ -1035,6 +1035,7 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
   a.bnr_dgamma = io->bnr_dgamma; a.bnr_dbeta = io->bnr_dbeta;
   a.M = d->N * d->Ho * d->Wo;
   a.debug_flags = adp::option("fwd_debug", 0);
+  a.f32 = 0;
   a.stat = (a.bn_sum || a.bnr_z) ? adp::stat_scratch() : nullptr;
 }
 
@@ -1093,6 +1094,16 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
     adp::kernel_end();
     if (adp::check_launch("adp_conv_fwd")) return -2;
     return fold_stats(a, s);
+  }
+  // f32: the LDS-DMA tap kernel with 32-channel K steps where every K step lies in one tap and one source
+  if (std::is_same<T, float>::value && fast == 2 && !a.scA && !a.scB) {
+    a.f32 = 1;
+    if (adp::launch_fwd_tap64(a, s)) {
+      adp::kernel_end();
+      if (adp::check_launch("adp_conv_fwd")) return -2;
+      return fold_stats(a, s);
+    }
+    a.f32 = 0;
   }
   // every other kernel: plain launch, then the standalone BN-backward reduction on the stored output
   const FwdArgs bnr = a;

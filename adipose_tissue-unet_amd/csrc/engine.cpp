@@ -1341,10 +1341,8 @@ extern "C" int adp_create(const adp_config* cfg, int device, adp_handle** out) {
   h->B = cfg->max_batch;
   h->nb = cfg->init_nb > 0 ? cfg->init_nb : 44;
   h->es = cfg->dtype == ADP_DTYPE_F32 ? 4 : 2;
-  if (cfg->dtype == ADP_DTYPE_BF16) {   // channel layout of predictor.INFER_CPAD: 64/128/192/384
-    const int cp[4] = {64, 64, 64, 64};
-    for (int i = 0; i < 4; ++i) h->cpad[i] = cp[i];
-  }
+  // channel layout of nets.AdiposeV3Net: bf16 64/128/192/384 (predictor.INFER_CPAD), f32 64/96/192/352
+  for (int i = 0; i < 4; ++i) h->cpad[i] = cfg->dtype == ADP_DTYPE_BF16 ? 64 : 32;
   const int nb = h->nb;
   for (int i = 0; i < 4; ++i) {
     h->ch[i] = round_up((1 << i) * nb, h->cpad[i]);

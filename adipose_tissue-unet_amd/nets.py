@@ -417,9 +417,10 @@ class AdiposeV3Net(UNetEngine):
         # channel-stride granule per resolution level (int = all levels): a 64 granule stores 44/88/176/352
         # as 64/128/192/384 so those levels run on the tap64 / halo MFMA kernels (the pad channels are exact
         # zeros: zero weights and biases in, ReLU(0) = 0 out, zero gradients back); 8 keeps 48/88/176/352 on
-        # the generic LDS-DMA kernels. f32 (parity) uses 8 everywhere.
+        # the generic LDS-DMA kernels. f32 uses 32 (64/96/192/352): every 32-channel K step then lies in one
+        # tap, which puts the forward and data-gradient launches on the LDS-DMA tap kernel's f32 form.
         if cpad is None:
-            cpad = 64 if dtype == "bf16" else 8
+            cpad = 64 if dtype == "bf16" else 32
         cpad = tuple(cpad) if isinstance(cpad, (tuple, list)) else (int(cpad),)
         self.cpad = cpad * 4 if len(cpad) == 1 else cpad   # one granule: every level
         assert size % 8 == 0, "adipose_v3 needs S % 8 == 0 (3 poolings)"

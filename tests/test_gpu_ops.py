@@ -1183,3 +1183,111 @@ def test_bn_bwd_apply_head_recompute(dt):
     torch.testing.assert_close(gb2, gb1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dg2, dg1, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db2, db1, rtol=1e-4, atol=1e-3)
+
+
+def test_deferred_bn_fold_is_guarded():
+    """A conv launch with bn_defer_fold leaves its BatchNorm sums in the library's accumulator replicas: until
+    the matching adp_bn_finalize_fold (same channel count, sum vector, stream) runs, every other launch that
+    uses the replicas must fail loudly instead of mixing its sums in, and the matching finalize
+    then gives the statistics of the non-deferred form."""
+    g = torch.Generator().manual_seed(5)
+    N, H, C = 2, 16, 64
+    x = torch.randn(N, H, 32, 64, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(64, 9 * 64, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    out = torch.zeros(N, H, 32, C, device=DEV, dtype=torch.bfloat16)
+    gamma, beta = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    vec = lambda: torch.zeros(C, device=DEV)   # noqa: E731
+    sc, sh, mu, ist = vec(), vec(), vec(), vec()
+    # reference: statistics folded by the conv launch itself
+    s_ref, q_ref = vec(), vec()
+    ops.conv_fwd(x, W, C, out=out, bn_stats=(s_ref, q_ref))
+    s0, q0 = vec(), vec()
+    ops.conv_fwd(x, W, C, out=out, bn_stats=(s0, q0), defer_fold=True)
+    z = out.clone()
+    with pytest.raises(ops.AdpError):   # another statistics launch while the fold is pending
+        ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()))
+    with pytest.raises(ops.AdpError):   # a BN-backward reduction while the fold is pending
+        ops.bn_bwd_reduce(z, z, sc, sh, mu, ist, vec(), vec())
+    with pytest.raises(ops.AdpError):   # a finalize for another sum vector
+        ops.bn_finalize(N * H * 32, vec(), q0, gamma, beta, 1e-5, 0.1, sc, sh, mu, ist, fold=True)
+    ops.bn_finalize(N * H * 32, s0, q0, gamma, beta, 1e-5, 0.1, sc, sh, mu, ist, fold=True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(s0, s_ref, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(q0, q_ref, rtol=1e-5, atol=1e-3)
+    with pytest.raises(ops.AdpError):   # nothing pending any more
+        ops.bn_finalize(N * H * 32, s0, q0, gamma, beta, 1e-5, 0.1, sc, sh, mu, ist, fold=True)
+    ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()))   # the replicas are usable again
+    torch.cuda.synchronize()
+
+
+F32_TAP_CASES = [
+    # name, N, S, cin_parts, cout, dil, up, mode
+    ("plain_relu_bias", 2, 24, [64], 96, 1, False, "plain"),
+    ("dil4_concat", 1, 20, [32, 64], 64, 4, False, "plain"),
+    ("up_stats", 2, 8, [96], 64, 1, True, "stats"),
+    ("addend_mask", 2, 16, [64], 64, 2, False, "addmask"),
+    ("split_mask2", 1, 16, [64], 96, 1, False, "split"),
+    ("bnr", 2, 16, [192], 64, 1, False, "bnr"),
+    ("convt", 2, 8, [128], 64, 1, False, "convt"),
+]
+
+
+@pytest.mark.parametrize("case", F32_TAP_CASES, ids=[c[0] for c in F32_TAP_CASES])
+def test_f32_tap_kernel_matches_generic(case):
+    """The f32 form of the LDS-DMA tap kernel (32-channel K steps, exact v_mfma_f32_16x16x4_f32; every 32-channel
+    K step inside one tap) against the register-staged f32 kernel (option f32_tap=0) on the same operands, for
+    each epilogue mode it takes: bias + ReLU, BatchNorm statistics, addend + mask, channel-split store with mask2,
+    the fused BatchNorm-backward reduction, and the ConvTranspose pixel-shuffle store."""
+    name, N, S, parts, cout, dil, up, mode = case
+    g = torch.Generator().manual_seed(len(name))
+    dt = torch.float32
+    l = Dense("t", parts, cout, dil=dil, up=up, transpose=mode == "convt", cpad=32)
+    srcs = [torch.randn(N, S, S, cs, generator=g).to(DEV) for cs in l.cin_s]
+    W = (torch.randn(l.Npad, l.Kpad, generator=g) * (1.0 / np.sqrt(l.K))).to(DEV)
+    So = 2 * S if up else S
+    res = []
+    for tap in (1, 0):
+        ops.set_option("f32_tap", tap)
+        try:
+            kw = {}
+            if mode == "convt":
+                out = torch.zeros(N, 2 * S, 2 * S, l.cout_s, device=DEV)
+                bias = torch.randn(l.cout_s, generator=g).to(DEV)
+                ops.conv_fwd(srcs[0], W, l.Nout, out=out, bias=bias, kh=1, kw=1, pad=0, out_mode=1, shuffle_c=l.cout_s)
+                extra = ()
+            else:
+                out = torch.zeros(N, So, So, l.cout_s, device=DEV)
+                if mode == "plain":
+                    kw = dict(bias=torch.linspace(-0.5, 0.5, l.cout_s, device=DEV), relu=True)
+                if mode == "stats":
+                    s1, s2 = torch.zeros(l.cout_s, device=DEV), torch.zeros(l.cout_s, device=DEV)
+                    kw = dict(bn_stats=(s1, s2))
+                if mode == "addmask":
+                    ga = torch.Generator().manual_seed(3)
+                    kw = dict(addend=torch.randn(out.shape, generator=ga).to(DEV),
+                              mask=torch.randn(out.shape, generator=ga).to(DEV), mask_scale=1.4)
+                if mode == "bnr":
+                    gz = torch.Generator().manual_seed(4)
+                    z = torch.randn(out.shape, generator=gz).to(DEV)
+                    vec = lambda: (torch.rand(l.cout_s, generator=gz) + 0.5).to(DEV)   # noqa: E731
+                    dg, db = torch.zeros(l.cout_s, device=DEV), torch.zeros(l.cout_s, device=DEV)
+                    kw = dict(bn_reduce=(z, vec(), vec() - 1.0, vec() - 1.0, vec(), dg, db))
+                if mode == "split":
+                    c0 = 64
+                    out = torch.zeros(N, So, So, c0, device=DEV)
+                    out2 = torch.zeros(N, So, So, l.cout_s - c0, device=DEV)
+                    m2 = torch.randn(out2.shape, generator=torch.Generator().manual_seed(6)).to(DEV)
+                    kw = dict(out_mode=2, out2=out2, split_c=c0, mask2=m2, mask2_scale=0.7)
+                ops.conv_fwd(srcs[0], W, l.Nout, out=out, srcB=srcs[1] if len(srcs) > 1 else None, up=up, dil=dil,
+                             **kw)
+                extra = tuple(v for k, v in kw.items() if k in ("out2",)) + \
+                    (kw["bn_stats"] if "bn_stats" in kw else ()) + ((kw["bn_reduce"][5], kw["bn_reduce"][6])
+                                                                  if "bn_reduce" in kw else ())
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("f32_tap", None)
+        assert kname.startswith("igemm_fwd_tap64_kernel") == bool(tap) and kname.endswith("true>") == bool(tap), kname
+        res.append([out.clone()] + [e.clone() for e in extra])
+    for a, b in zip(*res):
+        assert relerr(a, b) < 1e-5, (name, relerr(a, b))

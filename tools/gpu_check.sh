@@ -31,6 +31,14 @@ for s in $STEPS; do
     infer) timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 > gpurun_out/infer_tiles.log 2>&1 &&
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8 > gpurun_out/infer_tiles_cpad8.log 2>&1 &&
            timeout -k 10 400 python bench_infer.py --mode wsi > gpurun_out/infer_wsi.log 2>&1 ;;
+    f32bench) timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 256 --batch 2 --steps 10 \
+                --no-cpu-baseline > gpurun_out/f32_cfg1_bench.log 2>&1 &&
+              timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 5 \
+                --warmup 2 --no-cpu-baseline > gpurun_out/f32_1024_bench.log 2>&1 ;;
+    cfg2bench) timeout -k 10 300 python bench.py --levels 4 --size 512 --batch 8 --no-cpu-baseline \
+                > gpurun_out/cfg2_bench.log 2>&1 ;;
+    bnaab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "wgrad_bna_maxch=2;wgrad_bna_maxch=1" \
+             > gpurun_out/bna_maxch_ab.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   rc=$?
