@@ -109,6 +109,7 @@ _SIGS = {
     "adp_param_size": [_P, C.c_char_p, _I, C.POINTER(C.c_size_t)],
     "adp_set_param": [_P, C.c_char_p, _I, _P, _S],
     "adp_get_param": [_P, C.c_char_p, _I, _P, _S],
+    "adp_get_grad": [_P, C.c_char_p, _I, _P, _S],
     "adp_forward": [_P, _P, _I, C.c_longlong, _F, _F, _I, _P, _P],
     "adp_train_step": [_P, _P, _P, _I, _P, _F, _P, _P],
     "adp_auc_metrics": [_S, _P, _P, _P, _P],

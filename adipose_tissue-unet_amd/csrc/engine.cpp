@@ -320,6 +320,43 @@ struct adp_handle {
     return 0;
   }
 
+  // the last step's gradient of one layer in the Keras layout (slot 0 kernel, 1 bias), from G
+  int v3_get_grad(const std::string& name, int slot, float* host) {
+    CK(hipDeviceSynchronize());
+    auto d = dense_idx.find(name);
+    if (d != dense_idx.end()) {
+      const DenseL& l = dense[d->second];
+      if (slot == 1) {
+        CK(hipMemcpy(host, G + l.offB, sizeof(float) * l.cout, hipMemcpyDeviceToHost));
+        return 0;
+      }
+      std::vector<float> wp((size_t)l.Npad * l.Kpad);
+      CK(hipMemcpy(wp.data(), G + l.offW, sizeof(float) * wp.size(), hipMemcpyDeviceToHost));
+      std::vector<int> cm;
+      int base_c = 0;
+      for (size_t p = 0; p < l.cin.size(); ++p) {
+        for (int c = 0; c < l.cin[p]; ++c) cm.push_back(base_c + c);
+        base_c += l.cin_s[p];
+      }
+      const int cin = (int)cm.size();
+      for (int t = 0; t < 9; ++t)
+        for (int ci = 0; ci < cin; ++ci)
+          for (int co = 0; co < l.cout; ++co)
+            host[((size_t)t * cin + ci) * l.cout + co] = wp[(size_t)co * l.Kpad + t * l.Cin_s + cm[ci]];
+      return 0;
+    }
+    const HeadL& h = heads[head_idx.at(name)];
+    if (slot == 1) {
+      CK(hipMemcpy(host, G + h.offB, sizeof(float) * h.nout, hipMemcpyDeviceToHost));
+      return 0;
+    }
+    std::vector<float> wt((size_t)h.nout * h.cin);
+    CK(hipMemcpy(wt.data(), G + h.offW, sizeof(float) * wt.size(), hipMemcpyDeviceToHost));
+    for (int ci = 0; ci < h.cin; ++ci)
+      for (int o = 0; o < h.nout; ++o) host[(size_t)ci * h.nout + o] = wt[(size_t)o * h.cin + ci];
+    return 0;
+  }
+
   // bf16: compute-dtype forward weights from the master copy (every training step, and before an
   // inference forward that follows a step)
   int pack_forward(hipStream_t s) {
@@ -1265,20 +1302,28 @@ struct adp_handle {
     CK(hipMemcpy(P + l.offW, wp.data(), sizeof(float) * wp.size(), hipMemcpyHostToDevice));
     return 0;
   }
-  int bn_get_param(BnLayer& l, int slot, float* host) {
+  // src = P (parameters) or G (the last step's gradients; slots 3 / 4 have none)
+  int bn_get_param(BnLayer& l, int slot, float* host, const float* src = nullptr) {
     CK(hipDeviceSynchronize());
+    const bool grad = src == G;
+    if (!src) src = P;
     if (slot != 0) {
-      CK(hipMemcpy(host, bn_slot_ptr(l, slot), sizeof(float) * bn_param_size(l, slot), hipMemcpyDeviceToHost));
+      const float* p = bn_slot_ptr(l, slot);
+      if (grad) {
+        if (l.kind == 0 && slot >= 3) { adp::set_error("adp_get_grad: running statistics have no gradient"); return -1; }
+        p = G + (p - P);
+      }
+      CK(hipMemcpy(host, p, sizeof(float) * bn_param_size(l, slot), hipMemcpyDeviceToHost));
       return 0;
     }
     const std::vector<int> cm = cmap(l);
     const int cin = (int)cm.size();
     if (l.kind == 2) {
-      CK(hipMemcpy(host, P + l.offW, sizeof(float) * cin, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(host, src + l.offW, sizeof(float) * cin, hipMemcpyDeviceToHost));
       return 0;
     }
     std::vector<float> wp((size_t)l.Npad * l.Kpad);
-    CK(hipMemcpy(wp.data(), P + l.offW, sizeof(float) * wp.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(wp.data(), src + l.offW, sizeof(float) * wp.size(), hipMemcpyDeviceToHost));
     if (l.kind == 0) {
       for (int t = 0; t < 9; ++t)
         for (int ci = 0; ci < cin; ++ci)
@@ -1505,6 +1550,21 @@ extern "C" int adp_get_param(adp_handle* h, const char* layer, int slot, float* 
   }
   std::memcpy(host, v->data(), n * sizeof(float));
   return 0;
+}
+
+extern "C" int adp_get_grad(adp_handle* h, const char* layer, int slot, float* host, size_t n) {
+  if (!h || !host) { adp::set_error("adp_get_grad: null argument"); return -1; }
+  if (!h->train_on || !h->G || h->step == 0) { adp::set_error("adp_get_grad: no training step has run"); return -1; }
+  if (hipSetDevice(h->device) != hipSuccess) { adp::set_error("adp_get_grad: hipSetDevice failed"); return -2; }
+  if (!h->bl.empty()) {
+    BnLayer* l = bn_param(h, layer, slot, "adp_get_grad");
+    if (!l) return -1;
+    if (n != h->bn_param_size(*l, slot)) { adp::set_error("adp_get_grad: size mismatch"); return -1; }
+    return h->bn_get_param(*l, slot, host, h->G);
+  }
+  std::vector<float>* v = param_ref(h, layer, slot);
+  if (!v || n != v->size()) { adp::set_error("adp_get_grad: unknown parameter or size mismatch"); return -1; }
+  return h->v3_get_grad(layer, slot, host);
 }
 
 extern "C" int adp_forward(adp_handle* h, const float* images, int n, long long img_stride, float mean, float std_,

@@ -140,6 +140,20 @@ class NativeAdiposeV3:
             raise AdpError(f"engine built for {shape} tiles, got {tuple(x.shape[1:])}")
         return x
 
+    def get_grads(self):
+        """The last train_step's gradients, {layer: [kernel grad, bias / gamma / beta grads ...]} (Keras layout)."""
+        out = {}
+        for layer in self.layer_names():
+            arrs = []
+            for slot in self._slots(layer):
+                n = C.c_size_t()
+                call("adp_param_size", self._h, layer.encode(), slot, C.byref(n))
+                a = np.empty(n.value, np.float32)
+                call("adp_get_grad", self._h, layer.encode(), slot, a.ctypes.data, a.size)
+                arrs.append(a)
+            out[layer] = arrs
+        return out
+
     def predict_batch(self, images, mean, std, tta_mode=None):
         """images: (n, S, S) f32 raw gray (unet_bn: (n, S, S, in_ch)), host or device -> (n, S, S) device f32
         probabilities."""

