@@ -1245,6 +1245,7 @@ def test_f32_tap_kernel_matches_generic(case):
     srcs = [torch.randn(N, S, S, cs, generator=g).to(DEV) for cs in l.cin_s]
     W = (torch.randn(l.Npad, l.Kpad, generator=g) * (1.0 / np.sqrt(l.K))).to(DEV)
     So = 2 * S if up else S
+    bias = torch.randn(l.cout_s, generator=g).to(DEV)
     res = []
     for tap in (1, 0):
         ops.set_option("f32_tap", tap)
@@ -1252,7 +1253,6 @@ def test_f32_tap_kernel_matches_generic(case):
             kw = {}
             if mode == "convt":
                 out = torch.zeros(N, 2 * S, 2 * S, l.cout_s, device=DEV)
-                bias = torch.randn(l.cout_s, generator=g).to(DEV)
                 ops.conv_fwd(srcs[0], W, l.Nout, out=out, bias=bias, kh=1, kw=1, pad=0, out_mode=1, shuffle_c=l.cout_s)
                 extra = ()
             else:
