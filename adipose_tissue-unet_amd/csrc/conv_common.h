@@ -349,6 +349,9 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s);
 int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile);   // tile: tap64 config 0 (256x256) / 1 (256x128)
 // conv_fwd_halo.hip: halo-reuse 3x3 kernel for narrow (<= 128 output channels) stride-1 layers.
 int launch_fwd_halo(FwdArgs& a, hipStream_t s);
+// conv_fwd_w4.hip: four-wave persistent halo forward (weights straight to registers) for 3x3 'same'
+// layers with Nout % 256 == 0; called by launch_fwd_tap64p for its 256x256 halo shapes.
+int launch_fwd_w4(FwdArgs& a, hipStream_t s);
 int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);

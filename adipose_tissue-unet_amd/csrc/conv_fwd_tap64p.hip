@@ -698,6 +698,8 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     }
     return 1;
   }
+  // the four-wave direct-weight form (conv_fwd_w4.hip) for the layers it covers
+  if (halo_shape && cfg == 1 && launch_fwd_w4(a, s)) return 1;
   if (halo_shape && cfg == 1) {
     adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);

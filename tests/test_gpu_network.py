@@ -231,7 +231,9 @@ def test_unet_bn_fallback_paths_match_default(flag):
     argmax read from the stored activation instead of recomputed from z) give the default path's outputs and
     gradients (bf16, base 64, so every fused kernel form is the one the bench runs). The BatchNorm sums are
     atomics in a run-dependent order, so two runs of one path already differ by bf16 rounding flips: outputs
-    within 1.5e-2 (a few bf16 ulps of the logit) and 1e-3 on average, gradient cosines above 0.999 (a dropped or doubled term is far outside both)."""
+    within 1.5e-2 (a few bf16 ulps of the logit) and 2.5e-3 on average (two runs of the default path alone differ
+    by 1.1e-3 on average: tools/diag_bn_layers.py traces it to the f32 atomic order of the first 128-channel
+    layer's sums, amplified by bf16 rounding flips through the deeper layers), gradient cosines above 0.999 (a dropped or doubled term is far outside both)."""
     B, L, S = 2, 3, 64
     w = R.unet_bn_keras_weights(levels=L, base=64, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
@@ -246,7 +248,7 @@ def test_unet_bn_fallback_paths_match_default(flag):
         res.append((outs["main_out"].cpu().clone(), {n: net.get_layer_grads(n) for n in w}))
     (p0, g0), (p1, g1) = res
     d = (p0 - p1).abs()
-    assert d.max().item() <= 1.5e-2 and d.mean().item() <= 1e-3, (d.max().item(), d.mean().item())
+    assert d.max().item() <= 1.5e-2 and d.mean().item() <= 2.5e-3, (d.max().item(), d.mean().item())
     for n in w:
         for a, b in zip(g0[n], g1[n]):
             c = cos(torch.as_tensor(a), torch.as_tensor(b))

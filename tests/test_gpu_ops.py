@@ -208,6 +208,7 @@ def test_tap64p_halo_matches(mode, grid, tile):
         ops.set_option("fwd_tap64", 2 if tile == 256 else 3)   # the 256x256 / 256x128 configuration
         ops.set_option("fwd_halo", 0)   # (the <= 128-output halo kernels would take the narrow shapes)
         ops.set_option("tap64p_halo", halo)
+        ops.set_option("fwd_w4", 0)   # (the four-wave form takes the Nout % 256 == 0 shapes: its own test)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
@@ -215,7 +216,7 @@ def test_tap64p_halo_matches(mode, grid, tile):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid"):
+            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4"):
                 ops.set_option(o_, None)
         assert kname == "igemm_fwd_tap64p_kernel<256, %d, %d, false, %s, false>" % (
             tile, 2 if tile == 256 else 3, "true" if halo else "false"), kname
@@ -226,6 +227,72 @@ def test_tap64p_halo_matches(mode, grid, tile):
     torch.testing.assert_close(sh_, sg, rtol=1e-4, atol=1e-2)
     rf = ref.reshape(-1, nout)
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
+
+
+W4_CASES = [
+    # name, source channels, Nout, up, relu + bias, BatchNorm sums
+    ("one_chunk_stats", [64], 256, 1, False, True),
+    ("concat_relu", [64, 128], 256, 1, True, False),
+    ("wide_stats", [256], 512, 1, False, True),
+    ("up2_concat_stats", [128, 128], 256, 2, False, True),
+    ("n1024_relu_stats", [128], 1024, 1, True, True),
+]
+
+
+@pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
+@pytest.mark.parametrize("case", W4_CASES, ids=[c[0] for c in W4_CASES])
+def test_fwd_w4_matches(case, grid):
+    """Four-wave direct-weight forward (conv_fwd_w4.hip: one wave per SIMD, 128x128 per wave, weights loaded
+    straight into registers, halo through registers into LDS once per chunk) vs a float64 reference convolution
+    of the same bf16 operands, and vs the 8-wave LDS-DMA halo kernel (fwd_w4=0): the same chunk / tap / 32-deep
+    MFMA order, so the stored outputs are identical; the BatchNorm sums (a different order of f32 additions)
+    to 1e-5. Upsample x2 folded into the gather, two sources, 1-4 N tiles, 3 / 7-block grids."""
+    name, parts, nout, up, relu, stats = case
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(21)
+    N, H, W_ = 2, 32, 64
+    cin = sum(parts)
+    srcs = [torch.randn(N, H // up, W_ // up, c, generator=g).to(DEV, dt) for c in parts]
+    Wt = (torch.randn(nout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV) if relu else None
+    x = torch.cat([t.double() for t in srcs], -1).permute(0, 3, 1, 2)
+    if up == 2:
+        x = x.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    wk = Wt.double().view(nout, 3, 3, cin).permute(0, 3, 1, 2)
+    ref = F.conv2d(x, wk, padding=1).permute(0, 2, 3, 1)
+    if relu:
+        ref = (ref + bias.double()).clamp_min(0.0)
+    res = []
+    for w4 in (1, 0):
+        out = torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)
+        st = torch.zeros(2, nout, device=DEV)
+        kw = dict(srcB=srcs[1] if len(srcs) > 1 else None, bias=bias, relu=relu, up=up == 2)
+        if stats:
+            kw["bn_stats"] = (st[0], st[1])
+        ops.set_option("fwd_tap64", 2)   # the 256x256 configuration
+        ops.set_option("fwd_halo", 0)
+        ops.set_option("fwd_w4", w4)
+        if grid:
+            ops.set_option("tap64_persist_grid", grid)
+            ops.set_option("fwd_w4_grid", grid)
+        try:
+            ops.conv_fwd(srcs[0], Wt, nout, out=out, **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for o_ in ("fwd_tap64", "fwd_halo", "fwd_w4", "tap64_persist_grid", "fwd_w4_grid"):
+                ops.set_option(o_, None)
+        want = ("igemm_fwd_w4_kernel<%s>" % ("true" if stats else "false") if w4 else
+                "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>")
+        assert kname == want, kname
+        res.append((out.double(), st.double()))
+    (y4, s4), (y8, s8) = res
+    assert (y4 - ref).abs().max().item() < 0.02 * ref.abs().max().item()
+    assert torch.equal(y4, y8), (y4 - y8).abs().max().item()
+    if stats:
+        torch.testing.assert_close(s4, s8, rtol=1e-5, atol=1e-3)
+        rf = ref.reshape(-1, nout)
+        torch.testing.assert_close(s4[0], rf.sum(0), rtol=2e-3, atol=1.0)
 
 
 @pytest.mark.parametrize("cin,cout", [(64, 64), (128, 128), (128, 64)])
@@ -325,7 +392,7 @@ def test_halop_mask_addend_epilogue(mode):
     assert ((res[0] - res[1]).abs() - tol).max().item() < 0
 
 
-@pytest.mark.parametrize("form", ["halop_1ch", "halop_2ch", "tap64p_256", "tap64p_128"])
+@pytest.mark.parametrize("form", ["halop_1ch", "halop_2ch", "tap64p_256", "tap64p_128", "w4_256"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
 def test_upsample_gather_halo_forms(form, grid):
     """Nearest-x2 upsample folded into the halo gathers of the persistent forward kernels (adipose_v3's
@@ -339,7 +406,8 @@ def test_upsample_gather_halo_forms(form, grid):
     cin, nout, kern = {"halop_1ch": (64, 64, "igemm_fwd_halop_kernel<false, 1, 64"),
                        "halop_2ch": (128, 64, "igemm_fwd_halop_kernel<false, 2, 32"),
                        "tap64p_256": (128, 256, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>"),
-                       "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false>")}[form]
+                       "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false>"),
+                       "w4_256": (128, 256, "igemm_fwd_w4_kernel<true>")}[form]
     x = torch.randn(N, Hs, Ws, cin, generator=g).to(DEV, dt)
     Wt = (torch.randn(nout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
     bias = torch.randn(nout, generator=g).to(DEV)
@@ -352,9 +420,11 @@ def test_upsample_gather_halo_forms(form, grid):
         st = torch.zeros(2, nout, device=DEV)
         opts = {"halo_persist": persist, "tap64_persist": persist}
         if form.startswith("tap64p"):   # the 256x256 / 256x128 configuration (small M picks narrow tiles)
-            opts.update(fwd_halo=0, fwd_tap64=2 if form == "tap64p_256" else 3)
+            opts.update(fwd_halo=0, fwd_tap64=2 if form == "tap64p_256" else 3, fwd_w4=0)
+        if form == "w4_256":
+            opts.update(fwd_halo=0, fwd_tap64=2)
         if grid:
-            opts.update(tap64_persist_grid=grid, halo_persist_grid=grid)
+            opts.update(tap64_persist_grid=grid, halo_persist_grid=grid, fwd_w4_grid=grid)
         for k_, v_ in opts.items():
             ops.set_option(k_, v_)
         try:
@@ -367,7 +437,7 @@ def test_upsample_gather_halo_forms(form, grid):
         res.append((out.double(), st.double(), kname))
     (yp, sp, kp), (yn, sn, kn) = res
     assert kp.startswith(kern), kp
-    assert not kn.startswith("igemm_fwd_halop") and not kn.startswith("igemm_fwd_tap64p"), kn
+    assert not kn.startswith("igemm_fwd_halop") and not kn.startswith("igemm_fwd_tap64p") and "w4" not in kn, kn
     assert (yp - ref).abs().max().item() < 0.02 * ref.abs().max().item()
     assert (yp - yn).abs().max().item() <= 0.01 * ref.abs().max().item()
     torch.testing.assert_close(sp, sn, rtol=1e-4, atol=1e-2)

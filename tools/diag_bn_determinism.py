@@ -4,6 +4,7 @@ import sys
 import torch
 sys.path.insert(0, ".")
 sys.path.insert(0, "tests")
+import _adipose_pkg  # noqa: E402,F401
 import test_gpu_network as T  # noqa: E402
 from oracle import torch_ref as R  # noqa: E402
 from adipose_amd.nets import UNetBN  # noqa: E402

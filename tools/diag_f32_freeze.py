@@ -5,6 +5,7 @@ import numpy as np
 import torch
 sys.path.insert(0, ".")
 sys.path.insert(0, "tests")
+import _adipose_pkg  # noqa: E402,F401
 import test_engine as T  # noqa: E402
 from oracle import torch_ref as R  # noqa: E402
 from adipose_amd import ops  # noqa: E402
