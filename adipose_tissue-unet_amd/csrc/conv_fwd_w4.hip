@@ -27,7 +27,6 @@ constexpr unsigned W4_OOB = 0x80000000u;
 constexpr int W4_RSRC3 = 0x00020000;
 constexpr int W4_HROWS = 340, W4_HBUF = W4_HROWS * 128;   // halo pixels of an 8 x 32 patch, bytes per slot
 constexpr int W4_GH = (W4_HROWS * 8 + 255) / 256;          // 16-B halo groups per thread per chunk (11)
-constexpr int W4_DUMMY = 2 * W4_HBUF + 3 * 256 * 4;          // LDS scratch row for the halo stores not needed
 typedef unsigned int v2u32_4 __attribute__((ext_vector_type(2)));
 typedef unsigned int v4u32_4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4_4 __attribute__((ext_vector_type(4)));
@@ -38,12 +37,19 @@ __device__ __forceinline__ v4u32_4 w4_ld16(__amdgpu_buffer_rsrc_t r, unsigned of
 
 // DBG (timing-only ablations, option fwd_w4_dbg; results invalid): bit 0 no weight reloads in the K loop,
 // bit 1 no halo refills, bit 2 no epilogue stores
-template <bool STATS, int DBG = 0>
+// LB: the weight tile of a K step goes global -> registers (8 x 16 B per thread, whole 128-B rows) -> LDS
+// (two-stage ring, written once per step, one barrier per step), and every wave reads its fragments from
+// there: half the L2 / TA traffic of the direct form (the two waves of a channel half no longer fetch the
+// same fragments) at 32 KiB of LDS writes and 64 KiB of reads per step.
+template <bool STATS, int DBG = 0, bool LB = false>
 __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
   constexpr int NTH = 256, ROWB = 128;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * W4_HBUF + 3 * 256 * 4 + 256 * 16];
-  float* cst = reinterpret_cast<float*>(smem + 2 * W4_HBUF);   // bias [256]
-  float* sacc = cst + 256;                                      // block's BN sums [2][256]
+  constexpr int OBS = 2 * W4_HBUF, BSTAGE = 256 * ROWB;            // weight stages (LB)
+  constexpr int OCST = OBS + (LB ? 2 * BSTAGE : 0);
+  constexpr int ODUM = OCST + 3 * 256 * 4;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[ODUM + 256 * 16];
+  float* cst = reinterpret_cast<float*>(smem + OCST);   // bias [256]
+  float* sacc = cst + 256;                              // block's BN sums [2][256]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
     const int idx = g * NTH + tid;
     const int hr = idx >> 3, hp = idx & 7;
     const unsigned off = ok && idx < W4_HROWS * 8 ? (unsigned)(slot * W4_HBUF + hr * ROWB + ((hp ^ (hr & 7)) << 4))
-                                                  : (unsigned)(W4_DUMMY + tid * 16);
+                                                  : (unsigned)(ODUM + tid * 16);
     *reinterpret_cast<v4u32_4*>(smem + off) = v;
   };
 
@@ -121,6 +127,34 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
     const unsigned kb = (unsigned)(tp * nch + c) * ROWB + 64 * s;
 #pragma unroll
     for (int ni = 0; ni < 8; ++ni) B[ni][s] = __builtin_bit_cast(bf16x8, w4_ld16(rsW, bo[ni] + kb));
+  };
+
+  // LB: thread t stages rows (t >> 3) + 32 i (i < 8), 16-B chunk t & 7, of the step's 256 x 64 weight tile;
+  // the LDS image uses the MFMA-fragment swizzle of conv_common.h (chunk c of row r at c ^ swz(r))
+  unsigned wo[LB ? 8 : 1];
+  if constexpr (LB) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wo[i] = (unsigned)((n0 + (tid >> 3) + 32 * i) * a.Kpad * 2 + 16 * (tid & 7));
+  }
+  auto stage_load = [&](int g, v4u32_4 (&st)[8]) {
+    const int t = g % nk, c = t / 9, tp = t - 9 * c;
+    const unsigned kb = (unsigned)(tp * nch + c) * ROWB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = w4_ld16(rsW, wo[LB ? i : 0] + kb);
+  };
+  auto stage_store = [&](int buf, const v4u32_4 (&st)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = (tid >> 3) + 32 * i, cp = tid & 7;
+      *reinterpret_cast<v4u32_4*>(smem + OBS + buf * BSTAGE + r * ROWB + ((cp ^ swz(r)) << 4)) = st[i];
+    }
+  };
+  auto frag_B = [&](int buf, int s_, bf16x8 (&Bf)[8]) {
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) {
+      const int r = wc * 128 + ni * 16 + r16, cc = 4 * s_ + h4;
+      Bf[ni] = *reinterpret_cast<const bf16x8*>(smem + OBS + buf * BSTAGE + r * ROWB + ((cc ^ swz(r)) << 4));
+    }
   };
 
   f32x4 acc[8][8];
@@ -182,11 +216,76 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
   const int hbase = (4 * wr) * 34 + r16;   // halo row of fragment mi = 0 at tap 0: patch row 4 wr, column r16
 #pragma unroll
   for (int g = 0; g < W4_GH; ++g) halo_store(g, 0, halo_load(0, 0, g, true), true);
+  v4u32_4 hs[2];
+  hs[0] = hs[1] = v4u32_4{0u, 0u, 0u, 0u};
+  if constexpr (LB) {
+    v4u32_4 st[8];
+    bf16x8 Bf0[8], Bf1[8];
+    stage_load(0, st);
+    stage_store(0, st);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    frag_B(0, 0, Bf0);
+    int g = 0;
+    for (int k = 0; k < mine; ++k) {
+#pragma unroll 1
+      for (int c = 0; c < nch; ++c) {
+        const int slot = (k * nch + c) & 1;
+        const bool has_next = c + 1 < nch || k + 1 < mine;
+        const int k2 = c + 1 < nch ? k : k + 1, c2 = c + 1 < nch ? c + 1 : 0;
+        const unsigned char* hb = smem + slot * W4_HBUF;
+#pragma unroll 1
+        for (int tp = 0; tp < 9; ++tp, ++g) {
+          // (the step barrier below orders the halo slots: a chunk's halo is stored at its predecessor's taps
+          // 1-6, and the slot it overwrites was last read at tap 8 of the chunk before, behind two barriers)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int gs_ = 2 * (tp - 1) + j;
+            halo_store(gs_ < 0 ? 0 : gs_, slot ^ 1, hs[j], has_next && tp >= 1 && gs_ < W4_GH);
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int gl = 2 * tp + j;
+            hs[j] = halo_load(k2, c2, gl, has_next && gl < W4_GH);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          stage_load(g + 1 < total ? g + 1 : g, st);   // next step's weight tile, stored mid-step
+          __builtin_amdgcn_sched_barrier(0);
+          frag_B(g & 1, 1, Bf1);                          // this step's second half
+          const int dy = tp / 3, dx = tp - 3 * dy;
+          auto readA = [&](int q) {
+            const int s_ = q >> 3, mi = q & 7;
+            const int hr = hbase + ((mi >> 1) + dy) * 34 + (mi & 1) * 16 + dx, cc = 4 * s_ + h4;
+            return *reinterpret_cast<const bf16x8*>(hb + hr * ROWB + ((cc ^ (hr & 7)) << 4));
+          };
+          bf16x8 Ar[3];
+          Ar[0] = readA(0);
+          Ar[1] = readA(1);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            if (q + 2 < 16) Ar[(q + 2) % 3] = readA(q + 2);
+            const int mi = q & 7;
+#pragma unroll
+            for (int ni = 0; ni < 8; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(q < 8 ? Bf0[ni] : Bf1[ni], Ar[q % 3], acc[mi][ni],
+                                                                    0, 0, 0);
+            if (q == 11) {   // next step's tile into the other stage; barrier; its first-half fragments
+              __builtin_amdgcn_sched_barrier(0);
+              stage_store((g + 1) & 1, st);
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              __builtin_amdgcn_s_barrier();
+              frag_B((g + 1) & 1, 0, Bf0);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+      }
+      epilogue(k);
+    }
+  } else {
   // one register set of weight fragments: the half s is refilled with the next step's fragments as soon as
   // its 64 MFMAs are issued (half a K step of load cover)
   bf16x8 B[8][2];
-  v4u32_4 hs[2];
-  hs[0] = hs[1] = v4u32_4{0u, 0u, 0u, 0u};
   load_B(0, 0, B);
   load_B(0, 1, B);
   int g = 0;   // stream step
@@ -245,6 +344,7 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
     }
     epilogue(k);
   }
+  }
 
   // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
   if constexpr (STATS) {
@@ -267,7 +367,7 @@ namespace adp {
 // sources of 64-channel multiples) with Nout % 256 == 0 and a plain / bias / ReLU / BatchNorm-statistics
 // epilogue. 0 = not eligible (the caller falls back).
 int launch_fwd_w4(FwdArgs& a, hipStream_t s) {
-  if (!option("fwd_w4", 1)) return 0;
+  if (!option("fwd_w4", 0)) return 0;   // opt-in: slower than the 8-wave kernel (profiles/r03_w4_ab.txt)
   if (a.f8 || a.f32 || a.bnr_z || a.out_mode != 0 || a.addend || a.mask || a.mask2 || a.accum ||
       a.drop_rate > 0.f || a.scA || a.scB || !a.out)
     return 0;
@@ -287,6 +387,16 @@ int launch_fwd_w4(FwdArgs& a, hipStream_t s) {
   grid -= grid % a.ntile_n;
   if (grid <= 0) grid = a.ntile_n;
   const int dbg = option("fwd_w4_dbg", 0);
+  if (option("fwd_w4_lb", 1)) {
+    if (a.bn_sum) {
+      adp::set_kernel("igemm_fwd_w4_kernel<true, 0, true>");
+      hipLaunchKernelGGL((igemm_fwd_w4_kernel<true, 0, true>), dim3(grid), dim3(256), 0, s, a);
+    } else {
+      adp::set_kernel("igemm_fwd_w4_kernel<false, 0, true>");
+      hipLaunchKernelGGL((igemm_fwd_w4_kernel<false, 0, true>), dim3(grid), dim3(256), 0, s, a);
+    }
+    return 1;
+  }
   if (a.bn_sum && dbg > 0 && dbg < 8) {
     adp::set_kernel("igemm_fwd_w4_kernel<true, %d>", dbg);
 #define W4_DBG(D) if (dbg == D) hipLaunchKernelGGL((igemm_fwd_w4_kernel<true, D>), dim3(grid), dim3(256), 0, s, a)

@@ -42,7 +42,7 @@ for s in $STEPS; do
     w4) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
           -k "w4 or upsample_gather or tap64p_halo" > gpurun_out/w4_tests.log 2>&1 &&
         timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L2,L3,L4" \
-          --variants "fwd_w4=0;fwd_w4=1" > gpurun_out/w4_kernels.log 2>&1 &&
+          --variants "fwd_w4=0;fwd_w4=1,fwd_w4_lb=0;fwd_w4=1" > gpurun_out/w4_kernels.log 2>&1 &&
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "fwd_w4=0;fwd_w4=1" > gpurun_out/w4_ab.log 2>&1 ;;
     w4dbg) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats --layers "L2,L3,L4 1024->1024" \
              --variants "fwd_w4=0;fwd_w4=1;fwd_w4_dbg=1;fwd_w4_dbg=2;fwd_w4_dbg=4;fwd_w4_dbg=7" > gpurun_out/w4_dbg.log 2>&1 ;;
