@@ -23,6 +23,7 @@ constexpr int P_RSRC3 = 0x00020000;       // raw buffer descriptor word 3 (gfx9:
 typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef int v8i32 __attribute__((ext_vector_type(8)));
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void p_lds16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
@@ -81,9 +82,14 @@ __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_ha
 // (a 128-B row is 128 fp8 channels); the two 16-B fragments a lane reads per row are one 32-B operand of
 // v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales; A and B share the permutation of K), and the
 // epilogue multiplies by the per-column weight scale; bf16 output, plain store, no BatchNorm sums.
-template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false>
+// WREG (halo form, 2 stages, bf16): the weight rows of a K step are not moved by LDS-DMA but loaded into
+// registers one step ahead (4 x 16-B buffer loads per thread) and written into the free stage with ds_write
+// when the step is issued: the LDS-DMA issue (60-185 cycles per 1-KiB wave piece, what the K loop waited on:
+// profiles/r02_tap64p_halo_ablation.txt) is left to the <= 1 halo group per step.
+template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   static_assert(!F8 || !BNR, "fp8: no BN-backward reduction");
+  static_assert(!WREG || (HALO && NST == 2 && !F8), "register-staged weights: the bf16 2-stage halo form");
   constexpr int NTH = 512, ROWB = 128, ES = F8 ? 1 : 2, KSTEP = F8 ? 128 : 64;
   constexpr int OES = 2;   // output / z element bytes (bf16)
   constexpr int WN = BN / 64, WM = 8 / WN, TM = BM / WM;
@@ -263,7 +269,54 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     }
     return true;
   };
+  // WREG: the halo group g of chunk c of tile k through a register (ok = false: an out-of-range load, 0)
+  auto load_halo_reg = [&](int k, int c, int g, bool ok) -> v4u32_t {
+    const int idx = g * NTH + tid;
+    const PatchO P = patch_of(k);
+    const int hr = idx >> 3, hp = idx & 7;
+    const int yi = P.y0 - 1 + hr / 34, xi = P.x0 - 1 + hr % 34;
+    const int ci = c * KSTEP;
+    const bool srcb = ci >= a.CAs;
+    const int cs = (srcb ? a.CBs : a.CAs) * ES, cb = (srcb ? ci - a.CAs : ci) * ES;
+    const int sy = yi >> (a.up >> 1), sx = xi >> (a.up >> 1);
+    const bool v = ok && idx < P_HROWS * 8 && (unsigned)sy < (unsigned)a.Hs && (unsigned)sx < (unsigned)a.Ws;
+    const unsigned off = v ? (unsigned)(((P.img * a.Hs + sy) * a.Ws + sx) * cs + cb + 16 * (hp ^ p_hswz(hr))) : P_OOB;
+    return __builtin_amdgcn_raw_buffer_load_b128(srcb ? rsB : rsA, off, 0, 0);
+  };
+  // ... and its LDS store; a store not wanted goes to `spare` (a slot the caller overwrites right after)
+  auto store_halo_reg = [&](int g, int slot, v4u32_t v, bool ok, unsigned spare) {
+    const int idx = g * NTH + tid;
+    const unsigned off = ok && idx < P_HROWS * 8 ? (unsigned)(OH + slot * HBUF + idx * 16) : spare;
+    *reinterpret_cast<v4u32_t*>(smem + off) = v;
+  };
+  v4u32_t hreg = {0u, 0u, 0u, 0u};   // WREG: halo group loaded at the previous step, stored at this one
+  int hpend_g = 0, hpend_slot = 0;
+  bool hpend = false;
   bool hg_last = false;   // HALO: the latest load_next issued a halo group after its weights (wave-uniform)
+  // WREG: the weights of the next step to be issued, in registers (same per-lane source offsets and LDS
+  // positions as the LDS-DMA pieces)
+  v4u32_t wst[WREG ? 2 : 1][WREG ? GB : 1];
+  auto load_w = [&](int lt_) {
+    if constexpr (WREG) {
+      const int c_ = lt_ / 9, tp_ = lt_ - 9 * c_;
+      const unsigned kt = (unsigned)(tp_ * nch + c_);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < GB; ++i)
+          wst[h][i] = __builtin_amdgcn_raw_buffer_load_b128(rsW, bo[h][i] == P_OOB ? P_OOB : bo[h][i] + kt * ROWB, 0, 0);
+    }
+  };
+  auto store_w = [&](int buf) {
+    if constexpr (WREG) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < GB; ++i)
+          *reinterpret_cast<v4u32_t*>(smem + buf * STAGE + (h ? OB1 : OB0) + wave * 8 * ROWB + i * (NTH / 8) * ROWB +
+                                      lane * 16) = wst[h][i];
+    }
+  };
   auto load_next_halo = [&]() {
     hg_last = false;
     if (lk >= mine) return;
@@ -274,6 +327,25 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     }
     ++nissued;
     const int c = lt / 9, tp = lt - 9 * c;
+    if constexpr (WREG) {
+      // the halo group loaded at the previous step into its slot (or, if none, into this thread's first
+      // weight slot of stage ls, which store_w overwrites next), this step's staged weights into stage ls,
+      // then the next halo group (taps NST-1 .. NST-1+GH-1 of a chunk) and the next step's weights into
+      // registers. No LDS-DMA: every wait is the compiler's, on registers.
+      store_halo_reg(hpend_g, hpend_slot, hreg, hpend, (unsigned)(ls * STAGE + OB0 + wave * 8 * ROWB + lane * 16));
+      store_w(ls);
+      const int e = lk * nch + c;
+      const int nk2 = c + 1 < nch ? lk : lk + 1, nc2 = c + 1 < nch ? c + 1 : 0;
+      hpend = tp >= NST - 1 && tp < NST - 1 + GH && nk2 < mine;
+      hpend_g = hpend ? tp - (NST - 1) : 0;
+      hpend_slot = (e + 1) & 1;
+      hreg = load_halo_reg(nk2 < mine ? nk2 : lk, nc2, hpend_g, hpend);
+      const int lt2 = lt + 1 < nk ? lt + 1 : 0, lk2 = lt + 1 < nk ? lk : lk + 1;
+      load_w(lk2 < mine ? lt2 : lt);
+      ls = ls == NST - 1 ? 0 : ls + 1;
+      if (++lt == nk) { lt = 0; ++lk; }
+      return;
+    }
     {   // weights of (tap tp, chunk c): GEMM K rows kt = tp * nch + c
       const unsigned kt = (unsigned)(tp * nch + c);
 #pragma unroll
@@ -546,10 +618,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // The wait counts what was issued after the stage: the NST - 2 younger stages and, when a tile ended
   // inside that window, its EPI_OPS epilogue ops; near the end of the stream (fewer younger stages) it
   // drains everything.
-  if constexpr (HALO) {   // the first chunk's whole halo ahead of the stream
+  if constexpr (WREG) {   // the first chunk's whole halo ahead of the stream (registers -> LDS)
+#pragma unroll
+    for (int g = 0; g < GH; ++g) store_halo_reg(g, 0, load_halo_reg(0, 0, g, true), true, (unsigned)(OB0 + tid * 16));
+  } else if constexpr (HALO) {   // the first chunk's whole halo ahead of the stream
 #pragma unroll
     for (int g = 0; g < GH; ++g) issue_halo(0, 0, g, 0);
   }
+  if constexpr (WREG) load_w(0);   // (the first load_next stores them into stage 0)
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i) load_next();
   const int total = mine * nk;
@@ -571,7 +647,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       if constexpr (HALO) {
         // NST = 3: the younger stage's weights are counted, its halo groups not (a smaller count only
         // waits longer)
-        if (a.debug_flags & 64) {   // timing-only ablation (fwd_debug bit 6): LDS-DMA issued, never waited for
+        if constexpr (WREG) {
+          // the stage and the halo groups were written by every wave's ds_write at earlier steps
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else if (a.debug_flags & 64) {   // timing-only ablation (fwd_debug bit 6): LDS-DMA issued, never waited for
         } else if (gs + NST - 2 >= total) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (last_epi > gs - NST) {
@@ -700,6 +779,11 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   }
   // the four-wave direct-weight form (conv_fwd_w4.hip) for the layers it covers
   if (halo_shape && cfg == 1 && launch_fwd_w4(a, s)) return 1;
+  if (halo_shape && cfg == 1 && option("tap64p_wreg", 0)) {   // opt-in: 5-9 % slower (profiles/r03_wreg_ab.txt)
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true>");
+    hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true>), dim3(grid), dim3(512), 0, s, a);
+    return 1;
+  }
   if (halo_shape && cfg == 1) {
     adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);

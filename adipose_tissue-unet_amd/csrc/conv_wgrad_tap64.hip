@@ -963,13 +963,13 @@ static bool halop_ok(const WgradArgs& a) {
 }
 
 // BatchNorm-backward apply fused into the halo weight gradient: every block of input chunk c recomputes
-// its output block's dY tile, so only layers with at most wgrad_bna_maxch (default 2) 64-channel input
+// its output block's dY tile, so only layers with at most wgrad_bna_maxch (default 1) 64-channel input
 // chunks take it (levels 0-1 of unet_bn; deeper layers re-read dA/z once per chunk)
 bool wgrad_bna_fusable(const WgradArgs& a) {
   // (launch_wgrad_tap64 takes the halo kernel only with wgrad_tap64 != 0: with it off, the fused form would
   //  fall through to a kernel that reads a dY nothing has computed)
   return a.bna_dA && a.bna_z && option("wgrad_tap64", 1) != 0 && option("wgrad_bna", 1) &&
-         option("wgrad_halop_waves", 8) == 8 && halop_ok(a) && (a.CAs + a.CBs) / 64 <= option("wgrad_bna_maxch", 2);
+         option("wgrad_halop_waves", 8) == 8 && halop_ok(a) && (a.CAs + a.CBs) / 64 <= option("wgrad_bna_maxch", 1);
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 128x256 (8 waves, 64x64),

@@ -65,7 +65,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args, min_seconds=10.0, max_steps=30):
+def cpu_baseline(args, min_seconds=10.0, max_steps=60):
     """The reference's path on the host cores (BASELINE.md:30-44): the oracle's CPU fp32 restatement of
     AdiposeUNetV3 (oracle/torch_ref.py, train_adipose_unet_v3.py:660-758) training at BASELINE configs[0]
     (256x256 gray tiles, batch 2, fp32): forward, OHEM main + 0.4/0.3 deep-supervision BCE+Dice losses
@@ -118,21 +118,20 @@ def workload_label(args):
 
 
 def committed_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary that holds it
     (profiles/<round>_traffic.json, written by tools/profile_round.sh from rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes of this same bench command); (None, None) if absent."""
+    WRITE_SIZE passes of the bench command of that workload); (None, None) if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")))
-    if not files:
-        return None, None
-    try:
-        d = json.load(open(files[-1]))
-    except (OSError, ValueError):
-        return None, None
-    e = d.get(kernel)
-    if not e or e.get("traffic_bytes") is None:
-        return None, os.path.basename(files[-1])
-    return int(e["traffic_bytes"]), os.path.basename(files[-1])
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        e = d.get(kernel)
+        if e and e.get("traffic_bytes") is not None:
+            return int(e["traffic_bytes"]), os.path.basename(f)
+    return None, None
 
 
 def main():

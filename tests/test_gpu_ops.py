@@ -218,8 +218,8 @@ def test_tap64p_halo_matches(mode, grid, tile):
         finally:
             for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4"):
                 ops.set_option(o_, None)
-        assert kname == "igemm_fwd_tap64p_kernel<256, %d, %d, false, %s, false>" % (
-            tile, 2 if tile == 256 else 3, "true" if halo else "false"), kname
+        assert kname.startswith("igemm_fwd_tap64p_kernel<256, %d, %d, false, %s, false" % (
+            tile, 2 if tile == 256 else 3, "true" if halo else "false")), kname
         res.append((torch.cat(outs, -1).double(), st.double()))
     (yh, sh_), (yg, sg) = res
     assert (yh - ref).abs().max().item() < 0.02 * ref.abs().max().item()
@@ -227,6 +227,49 @@ def test_tap64p_halo_matches(mode, grid, tile):
     torch.testing.assert_close(sh_, sg, rtol=1e-4, atol=1e-2)
     rf = ref.reshape(-1, nout)
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
+
+
+@pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
+@pytest.mark.parametrize("mode", ["one_chunk", "concat", "ragged_n", "split", "up2"])
+def test_tap64p_wreg_matches_dma(mode, grid):
+    """The 256x256 halo kernel with its weights and halo groups staged through registers (ds_write into the
+    free stage, option tap64p_wreg=1) against the LDS-DMA form (tap64p_wreg=0, the default): the same K
+    order and fragments, so the stored outputs are identical and the BatchNorm sums agree to f32 order."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(17)
+    N, H, W_ = 2, 32, 64
+    parts = {"one_chunk": [64], "concat": [64, 128], "ragged_n": [128], "split": [128, 64], "up2": [192]}[mode]
+    nout = {"ragged_n": 320}.get(mode, 256)
+    up = mode == "up2"
+    cin = sum(parts)
+    srcs = [torch.randn(N, H // (2 if up else 1), W_ // (2 if up else 1), c, generator=g).to(DEV, dt) for c in parts]
+    Wt = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV)
+    res = []
+    for wreg in (1, 0):
+        outs = [torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)]
+        kw = dict(srcB=srcs[1] if len(srcs) > 1 else None, bias=bias, relu=mode != "split", up=up)
+        if mode == "split":
+            outs = [torch.zeros(N, H, W_, 128, dtype=dt, device=DEV), torch.zeros(N, H, W_, nout - 128, dtype=dt, device=DEV)]
+            kw.update(out_mode=2, out2=outs[1], split_c=128)
+        st = torch.zeros(2, nout, device=DEV)
+        opts = dict(fwd_tap64=2, fwd_halo=0, fwd_w4=0, tap64p_wreg=wreg)
+        if grid:
+            opts["tap64_persist_grid"] = grid
+        for k_, v_ in opts.items():
+            ops.set_option(k_, v_)
+        try:
+            ops.conv_fwd(srcs[0], Wt, nout, out=outs[0], bn_stats=(st[0], st[1]), **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for k_ in opts:
+                ops.set_option(k_, None)
+        assert kname == "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false%s>" % (", true" if wreg else ""), kname
+        res.append((torch.cat(outs, -1), st.double()))
+    (y1, s1), (y0, s0) = res
+    assert torch.equal(y1, y0), (y1.double() - y0.double()).abs().max().item()
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-3)
 
 
 W4_CASES = [
@@ -283,7 +326,7 @@ def test_fwd_w4_matches(case, grid):
             for o_ in ("fwd_tap64", "fwd_halo", "fwd_w4", "tap64_persist_grid", "fwd_w4_grid"):
                 ops.set_option(o_, None)
         want = ("igemm_fwd_w4_kernel<%s" % ("true" if stats else "false") if w4 else
-                "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>")
+                "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false")
         assert kname.startswith(want), kname
         res.append((out.double(), st.double()))
     (y4, s4), (y8, s8) = res
@@ -405,7 +448,7 @@ def test_upsample_gather_halo_forms(form, grid):
     N, Hs, Ws = 2, 16, 32
     cin, nout, kern = {"halop_1ch": (64, 64, "igemm_fwd_halop_kernel<false, 1, 64"),
                        "halop_2ch": (128, 64, "igemm_fwd_halop_kernel<false, 2, 32"),
-                       "tap64p_256": (128, 256, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>"),
+                       "tap64p_256": (128, 256, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false"),
                        "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false>"),
                        "w4_256": (128, 256, "igemm_fwd_w4_kernel<true")}[form]
     x = torch.randn(N, Hs, Ws, cin, generator=g).to(DEV, dt)

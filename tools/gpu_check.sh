@@ -15,6 +15,8 @@ for s in $STEPS; do
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 ;;
     prof) bash tools/profile_round.sh "$TAG" > gpurun_out/prof.log 2>&1 ;;
+    proff32) bash tools/profile_round.sh "${TAG}_f32" --preset adipose_v3 --dtype f32 --size 1024 --batch 2 \
+               --steps 5 --warmup 2 > gpurun_out/prof_f32.log 2>&1 ;;
     nettests) timeout -k 10 600 python -u -m pytest tests/test_gpu_network.py -x -v --timeout 120 \
              --timeout-method thread > gpurun_out/gpu_nettests.log 2>&1 ;;
     v3bench) timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --no-cpu-baseline \
@@ -44,6 +46,11 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L2,L3,L4" \
           --variants "fwd_w4=0;fwd_w4=1,fwd_w4_lb=0;fwd_w4=1" > gpurun_out/w4_kernels.log 2>&1 &&
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "fwd_w4=0;fwd_w4=1" > gpurun_out/w4_ab.log 2>&1 ;;
+    wreg) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
+          -k "wreg or w4 or upsample_gather or tap64p_halo" > gpurun_out/wreg_tests.log 2>&1 &&
+        timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L2,L3,L4" \
+          --variants "tap64p_wreg=0;tap64p_wreg=1" > gpurun_out/wreg_kernels.log 2>&1 &&
+        timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_wreg=0;tap64p_wreg=1" > gpurun_out/wreg_ab.log 2>&1 ;;
     w4dbg) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats --layers "L2,L3,L4 1024->1024" \
              --variants "fwd_w4=0;fwd_w4=1;fwd_w4_dbg=1;fwd_w4_dbg=2;fwd_w4_dbg=4;fwd_w4_dbg=7" > gpurun_out/w4_dbg.log 2>&1 ;;
     diag) timeout -k 10 300 python -u tools/diag_bn_determinism.py > gpurun_out/diag_bn.log 2>&1 &&
