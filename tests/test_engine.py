@@ -261,8 +261,9 @@ def test_native_unet_bn_train_step_matches_python(dtype):
         if getattr(l, "bn", False):
             rm, rv = eng.running_stats(n)
             # (the second step's batch statistics come from weights that differ by <= 2 lr in a few elements)
-            np.testing.assert_allclose(rm, net.running[n][0][:l.cout].cpu().numpy(), rtol=1e-2, atol=2e-3, err_msg=n)
-            np.testing.assert_allclose(rv, net.running[n][1][:l.cout].cpu().numpy(), rtol=1e-2, atol=2e-3, err_msg=n)
+            at = 2e-3 if dtype == "f32" else 2e-2
+            np.testing.assert_allclose(rm, net.running[n][0][:l.cout].cpu().numpy(), rtol=1e-2, atol=at, err_msg=n)
+            np.testing.assert_allclose(rv, net.running[n][1][:l.cout].cpu().numpy(), rtol=1e-2, atol=at, err_msg=n)
     # eval forward (running statistics) of the trained handle vs the Python network
     p_eng = eng.predict_batch(x, 0.0, 1.0).cpu().numpy()
     ops.prep_input(xd, net.acts(B)["x"], mean=0.0, std=1.0)
@@ -290,8 +291,8 @@ def test_native_unet_bn_bucketed_comm_and_errors():
     cfg = train_cfg(use_hard_mining=False)
     for step in range(2):
         ma, mb = a.train_step(x, y, lr, cfg), b.train_step(x, y, lr, cfg)
-        for k in ma:
-            assert abs(ma[k] - mb[k]) <= 2e-5 * max(1.0, abs(ma[k])), k
+        for k in ma:   # (step 2: weights differ where Adam took a rounding-level gradient's sign)
+            assert abs(ma[k] - mb[k]) <= (2e-5 if step == 0 else 1e-4) * max(1.0, abs(ma[k])), (step, k)
         _compare_grads(b.get_grads(), a.get_grads(), "f32", f"step {step} grads")
     b.set_comm(None)
     comm_destroy(comm)

@@ -805,10 +805,13 @@ def test_wgrad_input_layer_cin8(N, H, W, cin):
     (2, 32, 64, [64, 64], 64, "bf16", True), (1, 32, 32, [128], 128, "bf16", True),
     (1, 16, 64, [64], 128, "bf16", True), (2, 16, 64, [128, 64], 128, "bf16", False),
     (1, 16, 32, [64], 64, "f32", False)])
-def test_wgrad_bn_apply_fused(N, H, W, parts, cout, dtn, fused):
+@pytest.mark.parametrize("maxch", [None, 2], ids=["default", "maxch2"])
+def test_wgrad_bn_apply_fused(N, H, W, parts, cout, dtn, fused, maxch):
     """adp_conv_wgrad_bn (BatchNorm-backward apply computed inside the halo weight-gradient kernel, dz
     stored for the data gradient) == adp_bn_bwd_apply + adp_conv_wgrad: dz bit for bit, dW to f32
-    summation order; shapes the fused kernel does not take run the two launches."""
+    summation order; shapes the fused kernel does not take run the two launches. By default only
+    single-chunk layers take the fused kernel (wgrad_bna_maxch=1, step A/B in profiles/r03_bna_maxch_ab.txt);
+    option wgrad_bna_maxch=2 keeps the two-chunk form reachable."""
     from adipose_amd import _lib
     dt = torch.bfloat16 if dtn == "bf16" else torch.float32
     g = torch.Generator().manual_seed(31)
@@ -826,9 +829,14 @@ def test_wgrad_bn_apply_fused(N, H, W, parts, cout, dtn, fused):
     dW2 = torch.zeros_like(dW1)
     ops.bn_bwd_apply(dA, z, sc, sh, mu, ist, gam, dg, db, count, dz1)
     ops.conv_wgrad(xs[0], dz1, dW1, cout, srcB=srcB)
-    ops.conv_wgrad(xs[0], dz2, dW2, cout, srcB=srcB, bn_apply=(dA, z, sc, sh, mu, ist, gam, dg, db, count))
-    kname = _lib.lib().adp_last_kernel().decode()
-    torch.cuda.synchronize()
+    ops.set_option("wgrad_bna_maxch", maxch)
+    try:
+        ops.conv_wgrad(xs[0], dz2, dW2, cout, srcB=srcB, bn_apply=(dA, z, sc, sh, mu, ist, gam, dg, db, count))
+        kname = _lib.lib().adp_last_kernel().decode()
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("wgrad_bna_maxch", None)
+    fused = fused and (maxch == 2 or sum(parts) == 64)
     assert kname.startswith("igemm_wgrad_halop_kernel<8, true") == fused, kname
     assert torch.equal(dz1, dz2)
     assert relerr(dW2.cpu(), dW1.cpu()) < 1e-5
