@@ -291,8 +291,10 @@ def test_native_unet_bn_bucketed_comm_and_errors():
     cfg = train_cfg(use_hard_mining=False)
     for step in range(2):
         ma, mb = a.train_step(x, y, lr, cfg), b.train_step(x, y, lr, cfg)
-        for k in ma:   # (step 2: weights differ where Adam took a rounding-level gradient's sign)
-            assert abs(ma[k] - mb[k]) <= (2e-5 if step == 0 else 1e-4) * max(1.0, abs(ma[k])), (step, k)
+        for k in ma:   # (step 2: weights differ where Adam took a rounding-level gradient's sign: a few pixels
+            # of 8192 may cross 0.5, so binary accuracy to 1e-3 there)
+            tol = 2e-5 if step == 0 else (1e-3 if "accuracy" in k else 1e-4)
+            assert abs(ma[k] - mb[k]) <= tol * max(1.0, abs(ma[k])), (step, k)
         _compare_grads(b.get_grads(), a.get_grads(), "f32", f"step {step} grads")
     b.set_comm(None)
     comm_destroy(comm)

@@ -233,8 +233,9 @@ def test_unet_bn_fallback_paths_match_default(flag):
     atomics in a run-dependent order, so two runs of one path already differ by bf16 rounding flips: outputs
     within 1.5e-2 (a few bf16 ulps of the logit) and 2.5e-3 on average (two runs of the default path alone differ
     by 1.1e-3 on average: tools/diag_bn_layers.py traces it to the f32 atomic order of the first 128-channel
-    layer's sums, amplified by bf16 rounding flips through the deeper layers), gradient cosines above 0.99
-    (the input layer's gradient, at the end of the bf16 BatchNorm-backward chain, measured down to 0.993) (a dropped or doubled term is far outside both)."""
+    layer's sums, amplified by bf16 rounding flips through the deeper layers), gradient cosines above 0.98
+    (five identical passes of ONE path already differ down to cosine 0.9895 on a BatchNorm gamma/beta gradient:
+    tools/diag_bn_grads.py, the same with every weight-gradient routing) (a dropped or doubled term is far outside both)."""
     B, L, S = 2, 3, 64
     w = R.unet_bn_keras_weights(levels=L, base=64, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
@@ -253,7 +254,7 @@ def test_unet_bn_fallback_paths_match_default(flag):
     for n in w:
         for a, b in zip(g0[n], g1[n]):
             c = cos(torch.as_tensor(a), torch.as_tensor(b))
-            assert c > 0.99, (flag, n, c)
+            assert c > 0.98, (flag, n, c)
 
 
 def test_unet_bn_repeated_steps_and_double_backward():
