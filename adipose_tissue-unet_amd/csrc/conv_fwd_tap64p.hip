@@ -761,7 +761,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
                           a.Ho % 8 == 0 && a.Wo % 32 == 0;
   if (a.up != 1 && !(halo_shape && (cfg == 1 || (cfg == 2 && option("tap64p_halo128", 1))))) return 0;
   if (a.f8 && !(halo_shape && (cfg == 1 || cfg == 2))) {   // gather form (ConvTranspose, fp8 output)
-    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, true>", BM, BN, cfg == 1 ? 2 : 3);
+    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, true, false>", BM, BN, cfg == 1 ? 2 : 3);
     if (cfg == 1) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, false, true>), dim3(grid), dim3(512), 0, s, a);
     else if (cfg == 2) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, false, true>), dim3(grid), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<128, 256, 3, false, false, true>), dim3(grid), dim3(512), 0, s, a);
@@ -769,10 +769,10 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   }
   if (a.f8) {
     if (cfg == 1) {
-      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true>");
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true, false>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true>), dim3(grid), dim3(512), 0, s, a);
     } else {
-      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true>");
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true, false>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true>), dim3(grid), dim3(512), 0, s, a);
     }
     return 1;
@@ -785,16 +785,16 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     return 1;
   }
   if (halo_shape && cfg == 1) {
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
   if (halo_shape && cfg == 2 && option("tap64p_halo128", 1)) {
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
-  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
+  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
 #define P_LAUNCH(BM_, BN_, NST_)                                                                           \
   do {                                                                                                     \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \

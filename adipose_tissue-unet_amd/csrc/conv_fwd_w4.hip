@@ -398,15 +398,15 @@ int launch_fwd_w4(FwdArgs& a, hipStream_t s) {
     return 1;
   }
   if (a.bn_sum && dbg > 0 && dbg < 8) {
-    adp::set_kernel("igemm_fwd_w4_kernel<true, %d>", dbg);
+    adp::set_kernel("igemm_fwd_w4_kernel<true, %d, false>", dbg);
 #define W4_DBG(D) if (dbg == D) hipLaunchKernelGGL((igemm_fwd_w4_kernel<true, D>), dim3(grid), dim3(256), 0, s, a)
     W4_DBG(1); W4_DBG(2); W4_DBG(3); W4_DBG(4); W4_DBG(5); W4_DBG(6); W4_DBG(7);
 #undef W4_DBG
   } else if (a.bn_sum) {
-    adp::set_kernel("igemm_fwd_w4_kernel<true>");
+    adp::set_kernel("igemm_fwd_w4_kernel<true, 0, false>");
     hipLaunchKernelGGL(igemm_fwd_w4_kernel<true>, dim3(grid), dim3(256), 0, s, a);
   } else {
-    adp::set_kernel("igemm_fwd_w4_kernel<false>");
+    adp::set_kernel("igemm_fwd_w4_kernel<false, 0, false>");
     hipLaunchKernelGGL(igemm_fwd_w4_kernel<false>, dim3(grid), dim3(256), 0, s, a);
   }
   return 1;
