@@ -355,6 +355,8 @@ int launch_fwd_w4(FwdArgs& a, hipStream_t s);
 int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
+// conv_wgrad_f32.hip: f32 weight gradient on LDS-DMA staging (32-pixel stages, exact f32 MFMA)
+int launch_wgrad_f32(WgradArgs& a, hipStream_t s);
 // the persistent halo weight-gradient kernel takes this launch with the BatchNorm-backward apply fused
 bool wgrad_bna_fusable(const WgradArgs& a);
 }

@@ -1255,6 +1255,24 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
     adp::kernel_end();
     return adp::check_launch("adp_conv_wgrad");
   }
+  // f32: the LDS-DMA weight-gradient kernel (conv_wgrad_f32.hip), bias gradient as a channel-sum launch
+  if (std::is_same<T, float>::value && adp::launch_wgrad_f32(a, s)) {
+    if (a.dB) {
+      const int G = a.Nout / 8, lanes = NT / G;
+      const int blocks = (int)std::min<long long>((a.M + lanes - 1) / lanes, 1024);
+      if (a.dy_mode == 0) {
+        hipLaunchKernelGGL(channel_sum_kernel<float>, dim3(blocks), dim3(NT), 0, s, (size_t)a.M, a.Nout,
+                           a.dy_stride, reinterpret_cast<const float*>(a.dY), a.dB, 0);
+      } else {
+        const int Gc = a.Cps / 8, lc = NT / Gc;
+        const size_t Mo = (size_t)a.M * 4;
+        const int bl = (int)std::min<size_t>((Mo + lc - 1) / lc, 1024);
+        hipLaunchKernelGGL(channel_sum_kernel<float>, dim3(bl), dim3(NT), 0, s, Mo, a.Cps, a.dy_stride,
+                           reinterpret_cast<const float*>(a.dY), a.dB, 0);
+      }
+    }
+    return adp::check_launch("adp_conv_wgrad");
+  }
   a.ntile_k = (a.K + 63) / 64;
   a.ntile_n = (a.Nout + 63) / 64;
   const int tiles = a.ntile_k * a.ntile_n;

@@ -36,6 +36,9 @@ def parse():
     p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="collective backend for N > 1 (nccl = RCCL; gloo only to rehearse the multi-rank plumbing with "
+                        "several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -149,9 +152,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.dist_backend == "gloo":   # rehearsal: ranks share the visible GPUs
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

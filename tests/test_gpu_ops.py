@@ -770,6 +770,66 @@ def test_wgrad_tap64_configs(cfg, cout, S):
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
 
 
+WF32_CASES = [
+    # name, N, H, W, CA, CB, Nout, k, dil, up, shuffle_c (ConvT 1x1 with pixel-shuffled dY)
+    ("plain_n96", 2, 24, 40, 64, 0, 96, 3, 1, False, 0),
+    ("concat_n64", 1, 20, 36, 32, 64, 64, 3, 1, False, 0),
+    ("dil4_n48", 2, 16, 16, 96, 0, 48, 3, 4, False, 0),
+    ("up2_n128", 2, 12, 20, 64, 0, 128, 3, 1, True, 0),
+    ("wide_n256", 1, 16, 32, 128, 0, 256, 3, 1, False, 0),
+    ("ragged_n44", 1, 13, 23, 32, 0, 44, 3, 1, False, 0),
+    ("convt_c32", 2, 8, 16, 64, 0, 128, 1, 1, False, 32),
+]
+
+
+@pytest.mark.parametrize("case", WF32_CASES, ids=[c[0] for c in WF32_CASES])
+def test_wgrad_f32_lds_kernel(case):
+    """f32 weight gradient on the LDS-DMA kernel (conv_wgrad_f32.hip: 32-pixel stages, exact
+    v_mfma_f32_16x16x4_f32, per-split slabs / atomics) vs the register-staged f32 kernel (option
+    wgrad_f32=0) on the same operands to 1e-5, and vs a float64 autograd of the convolution; the bias
+    gradient (channel-sum launch) to 1e-5. Plain / concat / dilated / upsample-gather / 1-4 N tiles / ragged
+    pixel count and N / ConvT pixel-shuffle dY."""
+    name, N, H, W_, CA, CB, nout, k, dil, up, shuf = case
+    g = torch.Generator().manual_seed(41)
+    Hs, Ws = (H // 2, W_ // 2) if up else (H, W_)
+    xa = torch.randn(N, Hs, Ws, CA, generator=g)
+    xb = torch.randn(N, Hs, Ws, CB, generator=g) if CB else None
+    if shuf:
+        dY = torch.randn(N, 2 * H, 2 * W_, shuf, generator=g)
+    else:
+        dY = torch.randn(N, H, W_, nout, generator=g)
+    kw = dict(srcB=xb.to(DEV) if CB else None, up=up, dil=dil, kh=k, kw=k)
+    if shuf:
+        kw.update(pad=0, shuffle_c=shuf)
+    res = []
+    for f32k in (1, 0):
+        K = k * k * (CA + CB)
+        dW = torch.zeros(nout, (K + 31) // 32 * 32, device=DEV)
+        dB = torch.zeros(shuf if shuf else nout, device=DEV)
+        ops.set_option("wgrad_f32", f32k)
+        try:
+            ops.conv_wgrad(xa.to(DEV), dY.to(DEV), dW, nout, dB=dB, **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("wgrad_f32", None)
+        assert kname.startswith("igemm_wgrad_f32_kernel") == bool(f32k), kname
+        res.append((dW.cpu().double(), dB.cpu().double()))
+    (w1, b1), (w0, b0) = res
+    assert relerr(w1, w0) < 1e-5, relerr(w1, w0)
+    assert relerr(b1, b0) < 1e-5
+    if not shuf:   # float64 autograd: dW[n][tap * Cin + c]
+        x = torch.cat([xa, xb], -1) if CB else xa
+        x = x.double().permute(0, 3, 1, 2)
+        if up:
+            x = x.repeat_interleave(2, 2).repeat_interleave(2, 3)
+        wt = torch.zeros(nout, CA + CB, k, k, dtype=torch.float64, requires_grad=True)
+        y = F.conv2d(x, wt, padding=dil * (k // 2), dilation=dil)
+        (y * dY.double().permute(0, 3, 1, 2)).sum().backward()
+        ref = wt.grad.permute(0, 2, 3, 1).reshape(nout, -1)
+        assert relerr(w1[:, :ref.shape[1]], ref) < 1e-5, relerr(w1[:, :ref.shape[1]], ref)
+
+
 @pytest.mark.parametrize("N,H,W,cin", [(2, 32, 64, 3), (1, 16, 96, 1), (3, 8, 32, 8)])
 def test_wgrad_input_layer_cin8(N, H, W, cin):
     """Input-layer weight gradient (one 8-channel source, 64 outputs): the persistent cin8 kernel vs

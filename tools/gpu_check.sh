@@ -53,6 +53,16 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_wreg=0;tap64p_wreg=1" > gpurun_out/wreg_ab.log 2>&1 ;;
     w4dbg) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats --layers "L2,L3,L4 1024->1024" \
              --variants "fwd_w4=0;fwd_w4=1;fwd_w4_dbg=1;fwd_w4_dbg=2;fwd_w4_dbg=4;fwd_w4_dbg=7" > gpurun_out/w4_dbg.log 2>&1 ;;
+    wf32) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_network.py tests/test_engine.py \
+            tests/test_gpu_configs.py -v --timeout 200 --timeout-method thread -k "f32 or wgrad or cfg1" \
+            > gpurun_out/wf32_tests.log 2>&1 &&
+          timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 5 \
+            --warmup 2 --no-cpu-baseline > gpurun_out/f32_1024_bench.log 2>&1 &&
+          timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 256 --batch 2 --steps 10 \
+            --no-cpu-baseline > gpurun_out/f32_cfg1_bench.log 2>&1 ;;
+    dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+           --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
+           > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
     diag) timeout -k 10 300 python -u tools/diag_bn_determinism.py > gpurun_out/diag_bn.log 2>&1 &&
           timeout -k 10 300 python -u tools/diag_f32_freeze.py > gpurun_out/diag_freeze.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
