@@ -263,7 +263,10 @@ namespace adp {
 // f32 weight gradient on the LDS-DMA kernel: any stride / dilation / padding / nearest-x2 gather, one or two
 // sources, plain or pixel-shuffle dY, no BN-apply on load; 0 = not eligible (the caller falls back)
 int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
-  if (!option("wgrad_f32", 1) || a.scA || a.scB || a.bna_dA) return 0;
+  // opt-in: on adipose_v3's f32 layers (44 * 2^l channels, K = 9 Cin_s) its 64-granular N tiles and 128-512-wide
+  // K tiles run 39-66 % full, and it measured 62-64 TF against the register-staged kernel's 84 TF
+  // (profiles/r03_wgrad_f32_ab.txt)
+  if (!option("wgrad_f32", 0) || a.scA || a.scB || a.bna_dA) return 0;
   const int Cin_s = a.CAs + a.CBs;
   if (a.CAs % 4 != 0 || a.CBs % 4 != 0 || a.K != a.kh * a.kw * Cin_s || a.Kpad % 4 != 0 || a.Kpad < a.K ||
       a.dy_stride % 4 != 0 || a.Nout % 4 != 0 || (a.dy_mode == 1 && a.Cps % 4 != 0))

@@ -784,7 +784,7 @@ WF32_CASES = [
 
 @pytest.mark.parametrize("case", WF32_CASES, ids=[c[0] for c in WF32_CASES])
 def test_wgrad_f32_lds_kernel(case):
-    """f32 weight gradient on the LDS-DMA kernel (conv_wgrad_f32.hip: 32-pixel stages, exact
+    """f32 weight gradient on the LDS-DMA kernel (opt-in, conv_wgrad_f32.hip: 32-pixel stages, exact
     v_mfma_f32_16x16x4_f32, per-split slabs / atomics) vs the register-staged f32 kernel (option
     wgrad_f32=0) on the same operands to 1e-5, and vs a float64 autograd of the convolution; the bias
     gradient (channel-sum launch) to 1e-5. Plain / concat / dilated / upsample-gather / 1-4 N tiles / ragged
