@@ -1,5 +1,6 @@
 // f32 weight gradient on the LDS-DMA staging of the bf16 kernels (the reference-precision path every drop-in
-// CLI defaults to; replaces the register-staged igemm_wgrad_kernel<float> of conv_igemm.hip):
+// CLI defaults to; an opt-in alternative to the register-staged igemm_wgrad_kernel<float> of conv_igemm.hip,
+// option wgrad_f32=1: slower on adipose_v3's channel widths, see launch_wgrad_f32):
 //   dW[n][k] += sum_m dY[m][n] * X(k)[m]      (k = tap * Cin_s + ci, m = output pixel)
 // Block = WN x WK waves, dW tile (WN*64) x (WK*64), each wave a 64 x 64 tile of exact v_mfma_f32_16x16x4_f32
 // accumulators. A stage is 32 output pixels: the dY rows (TN f32 channels) and the gathered X rows (TK f32
