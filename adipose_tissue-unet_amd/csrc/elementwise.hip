@@ -1163,6 +1163,19 @@ extern "C" int adp_pack_weights_fp8(int rows, const float* src, int src_kpad, vo
   return adp::check_launch("adp_pack_weights_fp8");
 }
 
+namespace {
+__global__ void vec_mul_kernel(size_t n, const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ o) {
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) o[i] = a[i] * b[i];
+}
+}  // namespace
+
+extern "C" int adp_vec_mul(size_t n, const float* a, const float* b, float* out, adp_stream_t st) {
+  ADP_REQUIRE(a && b && out, "adp_vec_mul: null vector");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(vec_mul_kernel, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, n, a, b, out);
+  return adp::check_launch("adp_vec_mul");
+}
+
 extern "C" int adp_bn_apply_fp8(int dtype, size_t M, int C, const void* z, const float* sc, const float* sh,
                                 void* out, adp_stream_t st) {
   ADP_REQUIRE(C % 8 == 0 && sc && sh, "adp_bn_apply_fp8: bad arguments");

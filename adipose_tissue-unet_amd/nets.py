@@ -660,6 +660,7 @@ class UNetBN(UNetEngine):
     # the training conv leaves its BatchNorm sums in the replica scratch and the finalize folds them (one
     # launch); False: the conv's own fold launch, then the finalize
     fuse_bn_fold = True
+    fuse_eval_bn = True   # forward_fp8: eval BatchNorm + ReLU in the fp8 conv epilogues (False: z + apply pass)
     # with fuse_head_bn: the head backward stores no dA for dec0_conv2; that layer's BatchNorm-backward
     # apply recomputes it from p, dL/dp and the head weights (adp_bn_bwd_apply_head, bit-identical dz)
     head_recompute_dA = True
@@ -841,10 +842,19 @@ class UNetBN(UNetEngine):
     def _bn_conv_eval(self, name, srcA, z, act, *, srcB=None):
         l = self.layers[name]
         s = self.st[name]
-        self._conv_any(l, srcA, z, srcB=srcB)
         rm, rv = self.running[name]
         ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                         self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
+        if srcA.dtype == ops.FP8_DTYPE and self.fuse_eval_bn:
+            # eval BatchNorm folded into the fp8 conv: dequantisation scale x BN scale, BN shift as the bias,
+            # ReLU in the epilogue, the next conv's fp8 (or bf16) operand stored directly (no z, no apply pass)
+            W8, ws = self._packed8[name]
+            wsb = self.buf("w8sb/" + name, tuple(ws.shape), torch.float32)
+            ops.vec_mul(ws[:l.Nout], s[2], wsb)
+            ops.conv_fwd(srcA, W8, l.Nout, out=act, srcB=srcB, bias=s[3], kh=l.k, kw=l.k, dil=l.dil, relu=True,
+                         w_scale=wsb)
+            return
+        self._conv_any(l, srcA, z, srcB=srcB)
         if act.dtype == ops.FP8_DTYPE:
             ops.bn_apply_fp8(z, s[2], s[3], act)
         else:

@@ -348,6 +348,14 @@ def pack_weights_fp8(src, dst, scale):
          ptr(scale), stream_ptr())
 
 
+def vec_mul(a, b, out):
+    """out = a * b on f32 vectors (adp_vec_mul)."""
+    _check(a.dtype == b.dtype == out.dtype == torch.float32 and a.numel() <= b.numel() and a.numel() <= out.numel(),
+           "vec_mul: f32 vectors, b and out at least as long as a")
+    call("adp_vec_mul", a.numel(), ptr(a), ptr(b), ptr(out), stream_ptr())
+    return out
+
+
 def bn_apply_fp8(z, scale, shift, out):
     _check(out.shape == z.shape and out.dtype == FP8_DTYPE, "bn_apply_fp8 shapes")
     Cs = z.shape[-1]

@@ -29,13 +29,14 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 12 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 13 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
                               v9: adp_conv_desc.bn_defer_fold + adp_bn_finalize_fold;
                               v10: adp_bn_bwd_apply_head, adp_head_sigmoid_bwd_bnr with dx = NULL, adp_conv_wgrad_bn;
-                              v11: adp_sum_bf16; v12: adp_timing / adp_timing_read, unet_bn handle preset */
+                              v11: adp_sum_bf16; v12: adp_timing / adp_timing_read, unet_bn handle preset;
+                              v13: adp_vec_mul (eval BatchNorm folded into the fp8 dequantisation scale) */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -218,6 +219,9 @@ int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* scale, 
 /* the same activation stored as fp8 e4m3 (z of dtype dtype_in): the operand of an fp8 conv launch */
 int adp_bn_apply_fp8(int dtype_in, size_t M, int C, const void* z, const float* scale, const float* shift,
                      void* out_fp8, adp_stream_t s);
+/* out[i] = a[i] * b[i] (f32 vectors): e.g. an fp8 layer's per-column dequantisation scale times its eval
+   BatchNorm scale, so that the conv epilogue writes relu(bn(z)) directly (UNetBN.forward_fp8) */
+int adp_vec_mul(size_t n, const float* a, const float* b, float* out, adp_stream_t s);
 /* dBN = dA * (relu(z*scale+shift) > 0); dgamma += sum dBN*xhat; dbeta += sum dBN */
 int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, const void* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, float* dgamma,

@@ -220,3 +220,35 @@ def test_unet_bn_fp8_forward_vs_bf16(S):
     # the bf16 path is unchanged by an fp8 pass on the same buffers
     p16b = net.forward(B, train=False)["main_out"]
     assert torch.equal(p16b, p16)
+
+
+@pytest.mark.parametrize("S", [64, 128])
+def test_unet_bn_fp8_eval_bn_folded(S):
+    """forward_fp8 with the eval BatchNorm folded into the fp8 convs (dequantisation scale x BN scale via
+    adp_vec_mul, BN shift as bias, ReLU and the fp8 / bf16 operand store in the epilogue) against the
+    unfolded schedule (bf16 z, then the apply pass): the folded form skips the bf16 rounding of z, so the
+    two agree to fp8 rounding (mean 5e-3), and both stay within the fp8-vs-bf16 gate."""
+    B, L = 2, 3
+    net = UNetBN(B, S, levels=L, base=64, in_ch=3, dtype="bf16", device=DEV, seed=12)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, S, S, 3, generator=g)
+    ops.prep_input(x.to(DEV), net.acts(B)["x"], mean=0.0, std=1.0)
+    p16 = net.forward(B, train=False)["main_out"].clone()
+    net.fuse_eval_bn = False
+    p_apply = net.forward_fp8(B)["main_out"].clone()
+    net.fuse_eval_bn = True
+    p_fold = net.forward_fp8(B)["main_out"].clone()
+    torch.cuda.synchronize()
+    d = (p_fold - p_apply).abs()
+    assert d.mean().item() < 5e-3 and d.max().item() < 0.1, (d.mean().item(), d.max().item())
+    d16 = (p_fold - p16).abs()
+    assert d16.mean().item() < 1e-2 and d16.max().item() < 0.1, (d16.mean().item(), d16.max().item())
+
+
+def test_vec_mul_exact():
+    g = torch.Generator().manual_seed(6)
+    a, b = torch.randn(1000, generator=g).to(DEV), torch.randn(1000, generator=g).to(DEV)
+    out = torch.empty(1000, device=DEV)
+    ops.vec_mul(a, b, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, a * b)
