@@ -36,3 +36,19 @@ def test_conv_desc_layout_matches_header():
     assert ctypes.sizeof(_lib.ConvDesc) == 30 * 4
     # 16 operand pointers + 7 fused BatchNorm-backward reduction pointers + fp8 weight scales
     assert ctypes.sizeof(_lib.ConvIO) == 24 * 8
+
+
+CLIENT = os.path.join(ROOT, "adipose_tissue-unet_amd", "abi_client")
+
+
+def test_c_client_links_and_reports_errors():
+    """tests/c_abi/abi_client.c, a plain C11 caller of the handle ABI built by the library's Makefile (gcc against
+    libadipose_hip.so and the HIP runtime): it links, sees the header's ABI version, and gets a status code and a
+    message from adp_create for an unknown preset -- no device needed."""
+    import subprocess
+    if not os.path.exists(CLIENT):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "adipose_tissue-unet_amd", "csrc")], check=True,
+                       capture_output=True)
+    r = subprocess.run([CLIENT, "nogpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "nogpu: 0 failed" in r.stdout

@@ -311,3 +311,18 @@ def test_native_unet_bn_bucketed_comm_and_errors():
         call("adp_get_grad", a._h, b"enc0_conv1", 3, np.zeros(64, np.float32).ctypes.data, 64)
     a.close()
     b.close()
+
+
+def test_c_client_trains_both_presets():
+    """The plain C caller (tests/c_abi/abi_client.c, built next to the library) drives both presets on device 0
+    with its own HIP device buffers: adp_create -> adp_set_param (every layer / slot) -> four adp_train_step
+    (finite metrics, falling loss) -> adp_get_grad -> adp_forward (probabilities in [0, 1]) -> a rejected
+    oversized forward -> adp_destroy."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    client = os.path.join(root, "adipose_tissue-unet_amd", "abi_client")
+    assert os.path.exists(client), "abi_client is built with the library (make -C adipose_tissue-unet_amd/csrc)"
+    r = subprocess.run([client, "gpu"], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gpu: 0 failed" in r.stdout, r.stdout
