@@ -150,8 +150,9 @@ static void run_preset(int preset, int dtype, int S, int B) {
   CHECK(in01, "preset %d: adp_forward probabilities in [0, 1] (pixel agreement with the labels %.3f) %s", preset,
         agree / (double)npx, rc ? adp_last_error() : "");
 
-  rc = adp_forward(h, dx_, B + 1, 0, 0.f, 1.f, 0, dp, NULL);
-  CHECK(rc != 0 && strlen(adp_last_error()) > 0, "preset %d: n > max_batch rejected: %s", preset, adp_last_error());
+  rc = adp_forward(h, dx_, B, 0, 0.f, 1.f, 7, dp, NULL);   /* (n > max_batch is valid: processed in chunks) */
+  CHECK(rc != 0 && strstr(adp_last_error(), "tta_mode"), "preset %d: an unknown TTA mode is rejected: %s", preset,
+        adp_last_error());
   CHECK(adp_destroy(h) == 0, "preset %d: adp_destroy", preset);
   hipFree(dx_);
   hipFree(dy_);

@@ -317,7 +317,7 @@ def test_c_client_trains_both_presets():
     """The plain C caller (tests/c_abi/abi_client.c, built next to the library) drives both presets on device 0
     with its own HIP device buffers: adp_create -> adp_set_param (every layer / slot) -> four adp_train_step
     (finite metrics, falling loss) -> adp_get_grad -> adp_forward (probabilities in [0, 1]) -> a rejected
-    oversized forward -> adp_destroy."""
+    TTA mode -> adp_destroy."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
