@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 class AdpError(RuntimeError):
@@ -73,6 +73,7 @@ _SIGS = {
     "adp_pack_weights_fp8": [_I, _P, _I, _P, _I, _P, _P],
     "adp_bn_apply_fp8": [_I, _S, _I, _P, _P, _P, _P, _P],
     "adp_vec_mul": [_S, _P, _P, _P, _P],
+    "adp_scale_rows": [_I, _I, _I, _P, _I, _P, _I, _P, _I, _P],
     "adp_maxpool2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _P, _P],
     "adp_maxpool2_bwd_bnr": [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "adp_upsample2_bwd": [_I, _I, _I, _I, _I, _P, _P, _P, _F, _P, _P],

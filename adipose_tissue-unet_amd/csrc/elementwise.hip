@@ -1169,6 +1169,30 @@ __global__ void vec_mul_kernel(size_t n, const float* __restrict__ a, const floa
 }
 }  // namespace
 
+namespace {
+template <typename T>
+__global__ void scale_rows_kernel(int rows, int cols, const float* __restrict__ src, int src_ld,
+                                  const float* __restrict__ scale, int nscale, T* __restrict__ dst, int dst_ld) {
+  const size_t n = (size_t)rows * cols;
+  for (size_t i = blockIdx.x * (size_t)TPB + threadIdx.x; i < n; i += (size_t)gridDim.x * TPB) {
+    const int r = (int)(i / cols), c = (int)(i - (size_t)r * cols);
+    const float sc = r < nscale ? scale[r] : 0.f;
+    dst[(size_t)r * dst_ld + c] = from_f<T>(src[(size_t)r * src_ld + c] * sc);
+  }
+}
+}  // namespace
+
+extern "C" int adp_scale_rows(int dtype_out, int rows, int cols, const float* src, int src_ld, const float* scale,
+                              int nscale, void* dst, int dst_ld, adp_stream_t st) {
+  ADP_REQUIRE(src && scale && dst && rows > 0 && cols > 0 && src_ld >= cols && dst_ld >= cols && nscale >= 0,
+              "adp_scale_rows: bad arguments");
+  const size_t n = (size_t)rows * cols;
+  DTYPE_SWITCH(dtype_out, T,
+               hipLaunchKernelGGL(scale_rows_kernel<T>, dim3(nblk(n)), dim3(TPB), 0, (hipStream_t)st, rows, cols, src,
+                                  src_ld, scale, nscale, (T*)dst, dst_ld));
+  return adp::check_launch("adp_scale_rows");
+}
+
 extern "C" int adp_vec_mul(size_t n, const float* a, const float* b, float* out, adp_stream_t st) {
   ADP_REQUIRE(a && b && out, "adp_vec_mul: null vector");
   if (n == 0) return 0;

@@ -660,7 +660,7 @@ class UNetBN(UNetEngine):
     # the training conv leaves its BatchNorm sums in the replica scratch and the finalize folds them (one
     # launch); False: the conv's own fold launch, then the finalize
     fuse_bn_fold = True
-    fuse_eval_bn = True   # forward_fp8: eval BatchNorm + ReLU in the fp8 conv epilogues (False: z + apply pass)
+    fuse_eval_bn = True   # eval forwards: BatchNorm + ReLU folded into the conv epilogues (False: z + apply pass)
     # with fuse_head_bn: the head backward stores no dA for dec0_conv2; that layer's BatchNorm-backward
     # apply recomputes it from p, dL/dp and the head weights (adp_bn_bwd_apply_head, bit-identical dz)
     head_recompute_dA = True
@@ -761,15 +761,31 @@ class UNetBN(UNetEngine):
             ops.bn_finalize(count, s[0], s[1], self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                             self.bn_eps, self.bn_momentum, s[2], s[3], s[4], s[5], rm, rv, fold=fold)
         else:
-            self.conv(l, srcA, out, srcB=srcB)
             rm, rv = self.running[name]
             # eval: count < 0 -> (sum, sqsum) are read as (running mean, running var)
             ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                             self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
+            if self.fuse_eval_bn and act is not None:
+                self._conv_eval_folded(l, srcA, act, srcB=srcB)
+                if pool is not None:
+                    ops.maxpool2_fwd(act, pool)
+                return
+            self.conv(l, srcA, out, srcB=srcB)
         if pool is not None:
             ops.bn_apply_maxpool2(out, s[2], s[3], act, pool)
         elif act is not None:
             ops.bn_apply(out, s[2], s[3], act)
+
+    def _conv_eval_folded(self, l, srcA, act, *, srcB=None):
+        """Eval conv with its BatchNorm folded in: forward weights scaled per output channel by the BN scale
+        (adp_scale_rows, in the compute dtype), BN shift as the bias, ReLU in the epilogue: act = relu(bn(z))
+        in one launch, no z and no apply pass (the BN vectors of the layer are final: bn_finalize ran)."""
+        s = self.st[l.name]
+        Wm = self.ps.view(l.name + "/W")
+        We = self.buf("we/" + l.name, tuple(Wm.shape), self.dt)
+        ops.scale_rows(Wm, s[2], We)
+        ops.conv_fwd(srcA, We, l.Nout, out=act, srcB=srcB, bias=s[3], up=l.up, kh=l.k, kw=l.k, dil=l.dil,
+                     relu=True)
 
     def forward(self, batch=None, *, train=False, seed=0, pack=True):
         a = self.acts(batch or self.B)
@@ -789,12 +805,14 @@ class UNetBN(UNetEngine):
         for i in range(Lv - 2, -1, -1):
             self.conv(self.layers[f"dec{i}_up"], prev, a[f"t{i}"])
             self._bn_conv(f"dec{i}_conv1", a[f"az{i}_2"], a[f"y{i}_1"], a[f"ay{i}_1"], srcB=a[f"t{i}"], train=train)
-            # level 0: relu(bn(y0_2)) is only read by the head, which applies it on load (same rounding)
-            fuse = i == 0 and self.fuse_head_bn
+            # level 0: relu(bn(y0_2)) is only read by the head, which applies it on load (same rounding); eval
+            # with the BatchNorm folded into the convs materialises it in the conv epilogue instead
+            head_bn = self.fuse_head_bn and (train or not self.fuse_eval_bn)
+            fuse = i == 0 and head_bn
             self._bn_conv(f"dec{i}_conv2", a[f"ay{i}_1"], a[f"y{i}_2"], None if fuse else a[f"ay{i}_2"],
                           train=train)
             prev = a[f"ay{i}_2"]
-        if self.fuse_head_bn:
+        if self.fuse_head_bn and (train or not self.fuse_eval_bn):
             ops.head_fwd(a["y0_2"], self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0),
                          softmax2=False, bn=self.bnvec("dec0_conv2"))
         else:
@@ -845,6 +863,9 @@ class UNetBN(UNetEngine):
         rm, rv = self.running[name]
         ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                         self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
+        if srcA.dtype != ops.FP8_DTYPE and act.dtype != ops.FP8_DTYPE and self.fuse_eval_bn:
+            self._conv_eval_folded(l, srcA, act, srcB=srcB)
+            return
         if srcA.dtype == ops.FP8_DTYPE and self.fuse_eval_bn:
             # eval BatchNorm folded into the fp8 conv: dequantisation scale x BN scale, BN shift as the bias,
             # ReLU in the epilogue, the next conv's fp8 (or bf16) operand stored directly (no z, no apply pass)

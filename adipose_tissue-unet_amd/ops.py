@@ -356,6 +356,15 @@ def vec_mul(a, b, out):
     return out
 
 
+def scale_rows(src, scale, dst):
+    """dst = src * scale[:, None] (rows past scale's length: 0) cast to dst's dtype (adp_scale_rows)."""
+    _check(src.dtype == torch.float32 and src.dim() == 2 and dst.dim() == 2 and dst.shape == src.shape and
+           scale.dtype == torch.float32 and dst.is_contiguous() and src.stride(1) == 1, "scale_rows: bad tensors")
+    call("adp_scale_rows", dtype_code(dst), int(src.shape[0]), int(src.shape[1]), ptr(src), int(src.stride(0)),
+         ptr(scale), int(scale.numel()), ptr(dst), int(dst.shape[1]), stream_ptr())
+    return dst
+
+
 def bn_apply_fp8(z, scale, shift, out):
     _check(out.shape == z.shape and out.dtype == FP8_DTYPE, "bn_apply_fp8 shapes")
     Cs = z.shape[-1]

@@ -29,14 +29,15 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 13 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 14 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
                               v9: adp_conv_desc.bn_defer_fold + adp_bn_finalize_fold;
                               v10: adp_bn_bwd_apply_head, adp_head_sigmoid_bwd_bnr with dx = NULL, adp_conv_wgrad_bn;
                               v11: adp_sum_bf16; v12: adp_timing / adp_timing_read, unet_bn handle preset;
-                              v13: adp_vec_mul (eval BatchNorm folded into the fp8 dequantisation scale) */
+                              v13: adp_vec_mul (eval BatchNorm folded into the fp8 dequantisation scale);
+                              v14: adp_scale_rows (eval BatchNorm folded into bf16 / f32 forward weights) */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -222,6 +223,11 @@ int adp_bn_apply_fp8(int dtype_in, size_t M, int C, const void* z, const float* 
 /* out[i] = a[i] * b[i] (f32 vectors): e.g. an fp8 layer's per-column dequantisation scale times its eval
    BatchNorm scale, so that the conv epilogue writes relu(bn(z)) directly (UNetBN.forward_fp8) */
 int adp_vec_mul(size_t n, const float* a, const float* b, float* out, adp_stream_t s);
+/* dst[r][c] = src[r][c] * scale[r] (0 for r >= nscale), c < cols, stored as dtype_out (ADP_DTYPE_F32 / BF16): a
+   layer's forward weights ([Npad][Kpad] master layout) with its eval BatchNorm scale folded in, so that the conv
+   epilogue (bias = BN shift, ReLU) writes relu(bn(z)) directly (UNetBN.forward(train=False)) */
+int adp_scale_rows(int dtype_out, int rows, int cols, const float* src, int src_ld, const float* scale, int nscale,
+                   void* dst, int dst_ld, adp_stream_t s);
 /* dBN = dA * (relu(z*scale+shift) > 0); dgamma += sum dBN*xhat; dbeta += sum dBN */
 int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, const void* z, const float* scale,
                       const float* shift, const float* mean, const float* invstd, float* dgamma,

@@ -295,3 +295,31 @@ def test_unet_bn_repeated_steps_and_double_backward():
             ev = (1 - mom) * ev + mom * r["var_unbiased"]
         np.testing.assert_allclose(rm[:c].cpu().numpy(), em.numpy(), rtol=1e-4, atol=1e-5, err_msg=n)
         np.testing.assert_allclose(rv[:c].cpu().numpy(), ev.numpy(), rtol=1e-4, atol=1e-5, err_msg=n)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_unet_bn_eval_bn_folded(dtype):
+    """Eval forward with each conv's BatchNorm folded in (forward weights scaled per output channel by the BN
+    scale with adp_scale_rows, BN shift as the bias, ReLU and the activation store in the conv epilogue; no z, no
+    apply pass, the encoder pools from the stored activation) against the unfolded schedule (z, then the BN
+    apply), after a few training steps so the running statistics are not the initial ones: f32 to 1e-5, bf16 to
+    the storage rounding of z the folded form skips."""
+    B, L, S = 2, 3, 64
+    w = R.unet_bn_keras_weights(levels=L, base=32, in_ch=3, seed=7)
+    x, y = synth_batch(B, S, C=3, seed=13)
+    net = UNetBN(B, S, levels=L, base=32, in_ch=3, dtype=dtype, device=DEV)
+    net.set_weights(w)
+    tr = Trainer(net, LossConfig(use_hard_mining=False))
+    for _ in range(3):
+        tr.train_step(x.to(DEV), y.to(DEV))
+    outs = {}
+    for fold in (False, True):
+        net.fuse_eval_bn = fold
+        ops.prep_input(x.to(DEV), net.acts(B)["x"], mean=0.0, std=1.0)
+        outs[fold] = net.forward(B, train=False)["main_out"].cpu().clone()
+    net.fuse_eval_bn = True
+    d = (outs[True] - outs[False]).abs()
+    if dtype == "f32":
+        assert d.max().item() < 1e-5, d.max().item()
+    else:
+        assert d.max().item() < 2e-2 and d.mean().item() < 2e-3, (d.max().item(), d.mean().item())
