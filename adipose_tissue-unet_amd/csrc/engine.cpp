@@ -912,6 +912,11 @@ struct adp_handle {
              alloc(("dpool" + k).c_str(), B_ * side(i + 1) * side(i + 1) * ch_of(i) * es);
     }
     if (rc) return rc;
+    size_t wmax = 0;   // eval: one layer's forward weights with its BatchNorm scale folded in (bn_conv)
+    for (auto& l : bl)
+      if (l.kind == 0) wmax = std::max(wmax, (size_t)l.Npad * l.Kpad);
+    rc = alloc("wfold", wmax * es);
+    if (rc) return rc;
     rc = alloc("p", B_ * S * S * 4) || alloc("dp_main", B_ * S * S * 4) || alloc("probs", B_ * S * S * 4) ||
          alloc("rows", B_ * S * 3 * 4) || alloc("coef", B_ * S * 3 * 4) || alloc("stats", 3 * 8 * 8) ||
          alloc("lossbuf", 4 * 8);
@@ -952,6 +957,22 @@ struct adp_handle {
     io.srcB = srcB;
     io.W = wfwd(l);
     io.out = out;
+    if (!train && act) {
+      // eval (nets.UNetBN._conv_eval_folded): the running-statistics BatchNorm is affine, so its scale goes into
+      // the weights (f32 master rows x scale -> compute dtype) and its shift + ReLU into the conv epilogue, which
+      // writes relu(bn(z)) straight into act: no z round trip, no separate apply pass
+      CL(adp_bn_finalize(C, -1.f, l.rmean, l.rvar, P + l.offG, P + l.offBeta, bn_eps, 0.f, stv(l, 2), stv(l, 3),
+                         stv(l, 4), stv(l, 5), nullptr, nullptr, s));
+      void* wf = b("wfold");
+      CL(adp_scale_rows(cfg.dtype, l.Npad, l.Kpad, P + l.offW, l.Kpad, stv(l, 2), C, wf, l.Kpad, s));
+      io.W = wf;
+      io.bias = stv(l, 3);
+      io.out = act;
+      d.relu = 1;
+      CL(adp_conv_fwd(cfg.dtype, &d, &io, s));
+      if (pool) CL(adp_maxpool2_fwd(cfg.dtype, N, H, H, C, act, nullptr, nullptr, pool, s));
+      return 0;
+    }
     if (train) {
       io.bn_sum = stv(l, 0);
       io.bn_sqsum = stv(l, 1);
