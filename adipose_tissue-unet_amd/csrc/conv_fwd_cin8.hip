@@ -13,6 +13,7 @@
 #include "conv_common.h"
 
 namespace {
+typedef unsigned C8v2u32 __attribute__((ext_vector_type(2)));
 
 template <int KS, int UNR>
 __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
@@ -117,12 +118,148 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
     }
 }
 
+// Pipelined form (option cin8_pf, default on when source and output are < 2 GiB): the same product and
+// store layout, with every access a buffer load / store whose out-of-range offset stands for "padding"
+// or "past the end" (reads 0, writes dropped) and the ReLU / validity tests as selects, so the loop has
+// no branch. Passes alternate between two register sets: the gathers of pass k + 1 are issued before
+// pass k's MFMAs and stores, and the wait before pass k's MFMAs counts exactly the later pass's loads
+// and this pass's stores (vmcnt retires in order), so gather latency hides behind the previous pass.
+template <int KS, int UNR>
+__global__ __launch_bounds__(256) void igemm_fwd_cin8p_kernel(FwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r16 = lane & 15, h4 = lane >> 4;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+  const bf16* W = reinterpret_cast<const bf16*>(a.W);
+  const int HWo = a.Ho * a.Wo;
+  const int nimg = (a.M + HWo - 1) / HWo;
+  const __amdgpu_buffer_rsrc_t rsX =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.srcA, 0, nimg * a.Hs * a.Ws * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsO =
+      __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.M * a.out_stride * 2, 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+
+  bf16x8 wf[4][KS];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[mb][ks] = *reinterpret_cast<const bf16x8*>(W + (size_t)(16 * mb + r16) * a.Kpad + 32 * ks + 8 * h4);
+  const int ntaps = a.kh * a.kw;
+  int toy[KS], tox[KS];
+  bool tval[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int t = 4 * ks + h4;
+    tval[ks] = t < ntaps;
+    const int ty = t / a.kw, tx = t - ty * a.kw;
+    toy[ks] = ty * a.dil - a.pad;
+    tox[ks] = tx * a.dil - a.pad;
+  }
+  const float lo = a.relu ? 0.f : -INFINITY;
+  float bias[4][4], s1[4][4], s2[4][4];
+  bool cval[4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    cval[mb] = 16 * mb + 4 * h4 < a.Nout;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = 16 * mb + 4 * h4 + i;
+      bias[mb][i] = (a.bias && co < a.Nout) ? a.bias[co] : 0.f;
+      s1[mb][i] = 0.f;
+      s2[mb][i] = 0.f;
+    }
+  }
+  const int groups = (a.M + 15) / 16;
+  const int step = nwaves * UNR;
+
+  auto gather = [&](int g, bf16x8 (&xv)[UNR][KS]) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int m = (g + u) * 16 + r16;
+      const bool mv = m < a.M;
+      const int mc = mv ? m : 0;
+      const int n = mc / HWo, rem = mc - n * HWo, y = rem / a.Wo, x = rem - y * a.Wo;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int yi = y + toy[ks], xi = x + tox[ks];
+        const bool ok = mv && tval[ks] && (unsigned)yi < (unsigned)a.Hs && (unsigned)xi < (unsigned)a.Ws;
+        const unsigned off = ok ? (unsigned)(((n * a.Hs + yi) * a.Ws + xi) * 16) : OOB;
+        xv[u][ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsX, off, 0, 0));
+      }
+    }
+  };
+  auto pass = [&](int g, const bf16x8 (&xv)[UNR][KS]) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+          acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mb][ks], xv[u][ks], acc[mb], 0, 0, 0);
+      const int m = (g + u) * 16 + r16;
+      const bool mv = m < a.M;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int co0 = 16 * mb + 4 * h4;
+        const bool ok = mv && cval[mb];
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = fmaxf(acc[mb][i] + bias[mb][i], lo);
+          const float vs = ok ? v[i] : 0.f;
+          s1[mb][i] += vs;
+          s2[mb][i] += vs * vs;
+        }
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)v[i];
+        const unsigned off = ok ? (unsigned)(((size_t)m * a.out_stride + co0) * 2) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(C8v2u32, o), rsO, off, 0, 0);
+      }
+    }
+  };
+  bf16x8 xa[UNR][KS], xb[UNR][KS];
+  int g0 = wave * UNR;
+  if (g0 < groups) gather(g0, xa);
+  for (; g0 < groups; g0 += 2 * step) {
+    gather(g0 + step, xb);   // (a pass past the end gathers zeros from out-of-range offsets)
+    pass(g0, xa);
+    if (g0 + step >= groups) break;
+    gather(g0 + 2 * step, xa);
+    pass(g0 + step, xb);
+  }
+  if (!a.bn_sum || (a.debug_flags & 2)) return;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = row16_sum(s1[mb][i]), y = row16_sum(s2[mb][i]);
+      const int co = 16 * mb + 4 * h4 + i;
+      if (r16 == 0 && co < a.Nout) {
+        float* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+        atomicAdd(rep + co, x);
+        atomicAdd(rep + adp::STAT_CMAX + co, y);
+      }
+    }
+}
+
 template <int KS, int UNR>
 void launch_cin8_u(FwdArgs& a, hipStream_t s) {
   const int groups = (a.M + 15) / 16;
   // (4 groups per pass on 2048 waves: 0.255 -> 0.239 ms at unet_bn's 1024^2 x 4 input layer,
   //  profiles/r02_cin8_ab.txt)
   const int waves = std::max(1, std::min((groups + UNR - 1) / UNR, adp::option("cin8_waves", 2048)));
+  const size_t HWo = (size_t)a.Ho * a.Wo;
+  const size_t src_bytes = ((size_t)a.M + HWo - 1) / HWo * a.Hs * a.Ws * 16, out_bytes = (size_t)a.M * a.out_stride * 2;
+  if (adp::option("cin8_pf", 1) && src_bytes < (1ull << 31) && out_bytes < (1ull << 31)) {
+    adp::set_kernel("igemm_fwd_cin8p_kernel<%d, %d>", KS, UNR);
+    hipLaunchKernelGGL((igemm_fwd_cin8p_kernel<KS, UNR>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+    return;
+  }
   adp::set_kernel("igemm_fwd_cin8_kernel<%d, %d>", KS, UNR);
   hipLaunchKernelGGL((igemm_fwd_cin8_kernel<KS, UNR>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
 }

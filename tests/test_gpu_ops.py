@@ -1106,7 +1106,7 @@ def test_cin8_input_layer_bn_stats(S, cout):
     s2 = torch.zeros(l.cout_s, device=DEV)
     ops.conv_fwd(src, W, l.Nout, out=out, bias=b, relu=False, bn_stats=(s1, s2))
     torch.cuda.synchronize()
-    assert lib().adp_last_kernel().decode().startswith("igemm_fwd_cin8_kernel")
+    assert lib().adp_last_kernel().decode().startswith("igemm_fwd_cin8p_kernel")
     ref = oracle_fwd([rb(xs[0], torch.bfloat16)], rb(kern, torch.bfloat16), bias, 1, False, relu=False)
     assert relerr(out[..., :cout], ref) < TOL[torch.bfloat16]
     if l.cout_s > cout:
@@ -1114,6 +1114,41 @@ def test_cin8_input_layer_bn_stats(S, cout):
     r = ref.reshape(-1, cout).double()
     assert bool(((s1[:cout].cpu().double() - r.sum(0)).abs() <= 1e-2 * r.abs().sum(0) + 1e-3).all())
     assert bool(((s2[:cout].cpu().double() - (r * r).sum(0)).abs() <= 1e-2 * (r * r).sum(0) + 1e-3).all())
+
+
+@pytest.mark.parametrize("N,S,cin,cout,dil,relu", [(2, 32, 3, 64, 1, True), (3, 13, 1, 44, 2, False),
+                                                     (1, 10, 3, 24, 1, True), (5, 8, 3, 64, 1, False)])
+def test_cin8_pipelined_matches_plain(N, S, cin, cout, dil, relu):
+    """The pipelined branch-free input-layer kernel (igemm_fwd_cin8p_kernel, buffer accesses with
+    out-of-range padding / tail offsets) against the plain one (option cin8_pf=0): same MFMA order, so the
+    stored outputs are bit-identical; BatchNorm sums equal up to the order of the per-wave atomics; pad
+    channels and rows past M untouched. Ragged images (13x13, 10x10, 8x8) leave partial 16-pixel groups."""
+    from adipose_amd._lib import lib
+    xs, kern, bias, l = make_case(N, S, [cin], cout, dil, False, seed=11)
+    W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).to(torch.bfloat16).contiguous()
+    b = torch.zeros(l.cout_s, device=DEV)
+    b[:cout] = bias.to(DEV)
+    src = nhwc_pad(xs[0], l.cin_s[0], torch.bfloat16)
+    res = {}
+    for pf in (1, 0):
+        ops.set_option("cin8_pf", pf)
+        try:
+            out = torch.full((N, S, S, l.cout_s), 7.0, dtype=torch.bfloat16, device=DEV)
+            s1 = torch.zeros(l.cout_s, device=DEV)
+            s2 = torch.zeros(l.cout_s, device=DEV)
+            ops.conv_fwd(src, W, l.Nout, out=out, bias=b, relu=relu, dil=dil, bn_stats=(s1, s2))
+            torch.cuda.synchronize()
+            res[pf] = (out.clone(), s1.clone(), s2.clone(), lib().adp_last_kernel().decode())
+        finally:
+            ops.set_option("cin8_pf", None)
+    assert res[1][3].startswith("igemm_fwd_cin8p_kernel") and res[0][3].startswith("igemm_fwd_cin8_kernel")
+    assert torch.equal(res[1][0], res[0][0])
+    if l.cout_s > cout:
+        assert bool((res[1][0][..., cout:] == 7.0).all())
+    ref = oracle_fwd([rb(xs[0], torch.bfloat16)], rb(kern, torch.bfloat16), bias, dil, False, relu=relu)
+    assert relerr(res[1][0][..., :cout], ref) < TOL[torch.bfloat16]
+    for k in (1, 2):
+        assert torch.allclose(res[1][k], res[0][k], rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.parametrize("dt", DTS)
