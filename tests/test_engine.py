@@ -293,12 +293,15 @@ def test_native_unet_bn_bucketed_comm_and_errors():
     b.set_comm(comm)
     cfg = train_cfg(use_hard_mining=False)
     for step in range(2):
+        if step:   # Adam's first step moves a weight by ~lr * sign(g), and a rounding-level gradient takes either
+            # sign in two runs (f32 atomic order), so the second step starts both handles from a's weights:
+            # the comparison is then of the step itself, not of Adam's amplified rounding (measured: per-layer
+            # gradient cosines down to 0.9908 otherwise)
+            b.set_weights(a.get_weights())
         ma, mb = a.train_step(x, y, lr, cfg), b.train_step(x, y, lr, cfg)
-        for k in ma:   # (step 2: weights differ where Adam took a rounding-level gradient's sign: a few pixels
-            # of 8192 may cross 0.5, so binary accuracy to 1e-3 there)
-            tol = 2e-5 if step == 0 else (1e-3 if "accuracy" in k else 1e-4)
-            assert abs(ma[k] - mb[k]) <= tol * max(1.0, abs(ma[k])), (step, k)
-        _compare_grads(b.get_grads(), a.get_grads(), "f32", f"step {step} grads", after_step=step > 0)
+        for k in ma:
+            assert abs(ma[k] - mb[k]) <= 2e-5 * max(1.0, abs(ma[k])), (step, k)
+        _compare_grads(b.get_grads(), a.get_grads(), "f32", f"step {step} grads")
     b.set_comm(None)
     comm_destroy(comm)
     with pytest.raises(AdpError):
