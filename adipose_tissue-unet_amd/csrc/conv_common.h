@@ -81,6 +81,23 @@ namespace {
 // permutes, then the half-row and row mirrors (after the quad steps the lanes of a quad hold equal values,
 // so a mirror adds exactly what xor 4 / xor 8 would) -- the butterfly of __shfl_xor(v, 1..8) term for term,
 // as four DPP-modified VALU adds instead of four ds_bpermute round trips through the LDS pipe
+// MFMA-cluster wave priority (build-time ADP_PRIO, A/B only): 0 = s_setprio 1 around each MFMA cluster of the
+// hot K loops (default); 1 = no priority changes; 2 = the second-dispatched half of a 512-thread block (waves 4-7)
+// at priority 1 for the whole kernel, no per-cluster flips
+#ifndef ADP_PRIO
+#define ADP_PRIO 0
+#endif
+__device__ __forceinline__ void prio_hi() {
+  if constexpr (ADP_PRIO == 0) __builtin_amdgcn_s_setprio(1);
+}
+__device__ __forceinline__ void prio_lo() {
+  if constexpr (ADP_PRIO == 0) __builtin_amdgcn_s_setprio(0);
+}
+__device__ __forceinline__ void prio_static(int wave) {
+  if constexpr (ADP_PRIO == 2) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+}
 __device__ __forceinline__ float row16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
