@@ -281,7 +281,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = patch row
-  prio_static(wave);
+  prio_static<ADP_PRIO_FWD>(wave);
   const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
   const int T = a.nblocks, G = gridDim.x;
   const int lin = xcd_remap(blockIdx.x, G);
@@ -513,13 +513,13 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
             const int u = t - 1, mf = u & 1, nf = u >> 1;
             epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
           }
-          if (!with_unit) prio_hi();   // (setprio would split the interleave region)
+          if (!with_unit) prio_hi<ADP_PRIO_FWD>();   // (setprio would split the interleave region)
 #pragma unroll
           for (int mf = 0; mf < 2; ++mf)
 #pragma unroll
             for (int nf = 0; nf < NF; ++nf)   // transposed: rows = output channels, columns = pixels
               acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nf], fa[mf], acc[mf][nf], 0, 0, 0);
-          if (!with_unit) prio_lo();
+          if (!with_unit) prio_lo<ADP_PRIO_FWD>();
           if (with_unit) {
 #pragma unroll
             for (int i = 0; i < 2 * NF; ++i) {

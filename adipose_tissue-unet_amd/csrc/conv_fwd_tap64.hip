@@ -87,6 +87,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (WM * WN == 8) prio_static<ADP_PRIO_T64>(wave);
   const int wr = wave / WN, wc = wave % WN;
   const int lin = xcd_remap(blockIdx.x, a.nblocks);
   const int tn = lin % a.ntile_n, tm = lin / a.ntile_n;
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
-    __builtin_amdgcn_s_setprio(1);
+    prio_hi<ADP_PRIO_T64>();
     if constexpr (F8) {
 #pragma unroll
       for (int mi = 0; mi < MIQ; ++mi)
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
             acc[ha * MIQ + mi][hb * 2 + ni] =
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][s], fb[ni][s], acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
     }
-    __builtin_amdgcn_s_setprio(0);
+    prio_lo<ADP_PRIO_T64>();
   };
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];

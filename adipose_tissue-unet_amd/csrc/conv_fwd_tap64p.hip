@@ -124,7 +124,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WN, wc = wave % WN;
   const int G = gridDim.x;
-  prio_static(wave);
+  prio_static<ADP_PRIO_FWD>(wave);
   const int lin = xcd_remap(blockIdx.x, G);
   const int ntiles = a.nblocks;
   const int mine = lin < ntiles ? (ntiles - lin + G - 1) / G : 0;
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // column = pixel m0 + wr*TM + ha*HM + mi*16 + r16
   f32x4 acc[2 * MIQ][4];
   auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
-    prio_hi();
+    prio_hi<ADP_PRIO_FWD>();
     if constexpr (F8) {
 #pragma unroll
       for (int mi = 0; mi < MIQ; ++mi)
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           acc[ha * MIQ + mi][hb * 2 + ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
               __builtin_bit_cast(v8i32, fb[ni]), __builtin_bit_cast(v8i32, fa[mi]), acc[ha * MIQ + mi][hb * 2 + ni],
               0, 0, 0, 127, 0, 127);
-      prio_lo();
+      prio_lo<ADP_PRIO_FWD>();
       return;
     }
 #pragma unroll
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         for (int ni = 0; ni < 2; ++ni)
           acc[ha * MIQ + mi][hb * 2 + ni] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[ni][s], fa[mi][s], acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
-    prio_lo();
+    prio_lo<ADP_PRIO_FWD>();
   };
 
   // ---- epilogue resources

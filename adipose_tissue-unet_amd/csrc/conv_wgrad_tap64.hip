@@ -443,7 +443,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap
-  prio_static(wave);
+  prio_static<ADP_PRIO_WGRAD>(wave);
   const int dy = wave / 3, dx = wave - 3 * (wave / 3);
   const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
   // work unit = (patch, 64-channel input chunk, 64-wide output block); a block keeps one
@@ -708,7 +708,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
         else if (cb == 1) lgkm_wait<4>();
         else if (cb == 2) lgkm_wait<2>();
         else lgkm_wait<0>();
-        prio_hi();
+        prio_hi<ADP_PRIO_WGRAD>();
         if (NW == 8 && cb == 0) {
           acc8[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd8, fx8[0], acc8[0], 0, 0, 0);
           acc8[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd8, fx8[1], acc8[1], 0, 0, 0);
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb)
           acc[nb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[nb], fx[cb], acc[nb][cb], 0, 0, 0);
-        prio_lo();
+        prio_lo<ADP_PRIO_WGRAD>();
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next patch landed
