@@ -107,6 +107,8 @@ template <int M>
 __device__ __forceinline__ void prio_static(int wave) {
   if constexpr (M == 2) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (M == 3) {   // (A/B only: the first-dispatched half instead)
+    if (wave < 4) __builtin_amdgcn_s_setprio(1);
   }
 }
 __device__ __forceinline__ float row16_sum(float v) {
