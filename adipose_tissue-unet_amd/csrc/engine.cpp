@@ -1030,15 +1030,20 @@ struct adp_handle {
       CL(convt_fwd("dec" + k + "_up", N, prev, b(("t" + k).c_str()), s));
       CL(bn_conv("dec" + k + "_conv1", N, b(("az" + k + "_2").c_str()), b(("t" + k).c_str()),
                  b(("y" + k + "_1").c_str()), b(("ay" + k + "_1").c_str()), nullptr, train, s));
-      // level 0: relu(bn(y0_2)) is only read by the head, which applies it on load
+      // level 0 in training: relu(bn(y0_2)) is only read by the head, which applies it on load; in eval the
+      // folded conv writes it (nets.UNetBN.forward: head_bn only when training)
       CL(bn_conv("dec" + k + "_conv2", N, b(("ay" + k + "_1").c_str()), nullptr, b(("y" + k + "_2").c_str()),
-                 i == 0 ? nullptr : b(("ay" + k + "_2").c_str()), nullptr, train, s));
+                 i == 0 && train ? nullptr : b(("ay" + k + "_2").c_str()), nullptr, train, s));
       prev = b(("ay" + k + "_2").c_str());
     }
     const BnLayer& h = L("head");
     const BnLayer& l0 = L("dec0_conv2");
-    CL(adp_head_sigmoid_fwd(cfg.dtype, (size_t)N * S * S, l0.cout_s, h.cin[0], b("y0_2"), P + h.offW, P + h.offB,
-                            stv(l0, 2), stv(l0, 3), b<float>("p"), s));
+    if (train)
+      CL(adp_head_sigmoid_fwd(cfg.dtype, (size_t)N * S * S, l0.cout_s, h.cin[0], b("y0_2"), P + h.offW, P + h.offB,
+                              stv(l0, 2), stv(l0, 3), b<float>("p"), s));
+    else
+      CL(adp_head_sigmoid_fwd(cfg.dtype, (size_t)N * S * S, l0.cout_s, h.cin[0], b("ay0_2"), P + h.offW, P + h.offB,
+                              nullptr, nullptr, b<float>("p"), s));
     return 0;
   }
 

@@ -275,6 +275,40 @@ def test_native_unet_bn_train_step_matches_python(dtype):
     eng.close()
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_native_unet_bn_eval_matches_python(dtype):
+    """adp_forward of the unet_bn handle vs nets.UNetBN.forward(train=False) on the same weights and running
+    statistics: both fold the eval BatchNorm into the conv weights (adp_scale_rows) and epilogues, the level-0
+    activation is materialised by its folded conv and the head reads it without BatchNorm-on-load; the eval
+    path has no atomics, so the two schedules give the same probabilities."""
+    from adipose_amd import ops
+    from adipose_amd.engine import NativeUNetBN
+    from adipose_amd.nets import UNetBN
+    L, S_, B = 3, 64, 2
+    w, x, _ = _bn_case(L, S_, B, seed=9)
+    rng = np.random.default_rng(9)
+    net = UNetBN(B, S_, levels=L, base=64, in_ch=3, dtype=dtype, device="cuda")
+    net.set_weights(w)
+    w5 = {}
+    for n, l in net.layers.items():
+        if getattr(l, "bn", False):
+            rm = rng.normal(0, 0.2, l.cout).astype(np.float32)
+            rv = rng.uniform(0.5, 1.5, l.cout).astype(np.float32)
+            net.running[n][0][:l.cout].copy_(torch.from_numpy(rm))
+            net.running[n][1][:l.cout].copy_(torch.from_numpy(rv))
+            w5[n] = list(w[n]) + [rm, rv]
+        else:
+            w5[n] = w[n]
+    eng = NativeUNetBN(tile=S_, max_batch=B, dtype=dtype, levels=L)
+    eng.set_weights(w5)
+    p_eng = eng.predict_batch(x, 0.0, 1.0).cpu().numpy()
+    xd = torch.from_numpy(x).cuda()
+    ops.prep_input(xd, net.acts(B)["x"], mean=0.0, std=1.0)
+    p_py = net.forward(B, train=False)["main_out"].cpu().numpy()
+    assert np.abs(p_eng - p_py).max() <= 1e-6, np.abs(p_eng - p_py).max()
+    eng.close()
+
+
 def test_native_unet_bn_bucketed_comm_and_errors():
     """The bucketed, stream-overlapped gradient all-reduce (one-rank RCCL communicator) leaves the unet_bn step
     unchanged (metrics, per-layer gradients); bad parameter names / slots, a gradient read of a running
