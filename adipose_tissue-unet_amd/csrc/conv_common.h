@@ -81,13 +81,13 @@ namespace {
 // permutes, then the half-row and row mirrors (after the quad steps the lanes of a quad hold equal values,
 // so a mirror adds exactly what xor 4 / xor 8 would) -- the butterfly of __shfl_xor(v, 1..8) term for term,
 // as four DPP-modified VALU adds instead of four ds_bpermute round trips through the LDS pipe
-// MFMA-cluster wave priority of the hot K loops, per kernel family: 0 = s_setprio 1 around each MFMA cluster;
-// 1 = no priority changes; 2 = the second-dispatched half of a 512-thread block (waves 4-7) at priority 1 for
-// the whole kernel, no per-cluster flips. Same-box A/B of library builds (profiles/r03_prio_ab.txt): mode 2
-// takes 1.5-3.6 % off the persistent and halo forwards, and costs the persistent weight gradient 4 %, so the
-// forwards (ADP_PRIO_FWD) default to 2 and the weight gradient (ADP_PRIO_WGRAD) to 0.
+// MFMA-cluster wave priority of the hot K loops, per kernel family (build-time, A/B only): 0 = s_setprio 1
+// around each MFMA cluster (default); 1 = no priority changes; 2 = the second-dispatched half of a 512-thread
+// block (waves 4-7) at priority 1 for the whole kernel, no per-cluster flips; 3 = the first half instead.
+// Same-box A/B of library builds (profiles/r03_prio_ab.txt): on the forwards every mode is within the 1-2 %
+// drift of consecutive runs on one box; on the persistent weight gradient modes 1-3 cost 3-4 %.
 #ifndef ADP_PRIO_FWD
-#define ADP_PRIO_FWD 2
+#define ADP_PRIO_FWD 0
 #endif
 #ifndef ADP_PRIO_WGRAD
 #define ADP_PRIO_WGRAD 0
