@@ -205,6 +205,12 @@ class NativeUNetBN(NativeAdiposeV3):
     def _slots(self, layer):
         return (0, 1, 2) if ("_conv" in layer) else (0, 1)
 
+    def set_running_stats(self, layer, mean, var):
+        """Set the moving mean / variance (slots 3, 4) of a conv + BatchNorm layer (e.g. from a checkpoint)."""
+        for slot, a in ((3, mean), (4, var)):
+            a = np.ascontiguousarray(np.asarray(a, np.float32))
+            call("adp_set_param", self._h, layer.encode(), slot, a.ctypes.data, a.size)
+
     def running_stats(self, layer):
         """(moving mean, moving variance) of a conv + BatchNorm layer (slots 3, 4)."""
         out = []

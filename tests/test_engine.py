@@ -289,18 +289,18 @@ def test_native_unet_bn_eval_matches_python(dtype):
     rng = np.random.default_rng(9)
     net = UNetBN(B, S_, levels=L, base=64, in_ch=3, dtype=dtype, device="cuda")
     net.set_weights(w)
-    w5 = {}
+    eng = NativeUNetBN(tile=S_, max_batch=B, dtype=dtype, levels=L)
+    eng.set_weights(w)
     for n, l in net.layers.items():
         if getattr(l, "bn", False):
             rm = rng.normal(0, 0.2, l.cout).astype(np.float32)
             rv = rng.uniform(0.5, 1.5, l.cout).astype(np.float32)
             net.running[n][0][:l.cout].copy_(torch.from_numpy(rm))
             net.running[n][1][:l.cout].copy_(torch.from_numpy(rv))
-            w5[n] = list(w[n]) + [rm, rv]
-        else:
-            w5[n] = w[n]
-    eng = NativeUNetBN(tile=S_, max_batch=B, dtype=dtype, levels=L)
-    eng.set_weights(w5)
+            eng.set_running_stats(n, rm, rv)
+            got = eng.running_stats(n)
+            np.testing.assert_array_equal(got[0], rm)
+            np.testing.assert_array_equal(got[1], rv)
     p_eng = eng.predict_batch(x, 0.0, 1.0).cpu().numpy()
     xd = torch.from_numpy(x).cuda()
     ops.prep_input(xd, net.acts(B)["x"], mean=0.0, std=1.0)
