@@ -109,8 +109,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   constexpr int LOPS = HALO ? 2 * GB : 2 * GA + 2 * GB;   // LDS-DMA pieces per thread per stage (HALO: + halo)
   constexpr bool ZALL = BNR && MIQ == 2;                     // (see load_zall)
   constexpr int EPI_OPS = 2 * MIQ * 4 * (BNR && !ZALL ? 2 : 1);   // vector-memory ops per thread per epilogue
+  constexpr int EPI_OPS_W = 2 * MIQ * 2;                          // ... with 16-B stores (wide_st)
   // (vmcnt holds 0..63: a larger count is clamped, which only waits for more)
   constexpr int VM_EPI = (NST - 2) * LOPS + EPI_OPS < 63 ? (NST - 2) * LOPS + EPI_OPS : 63;
+  constexpr int VM_EPI_W = (NST - 2) * LOPS + EPI_OPS_W < 63 ? (NST - 2) * LOPS + EPI_OPS_W : 63;
   constexpr int VM_Z = (NST - 2) * LOPS + 4 * 2 * MIQ < 63 ? (NST - 2) * LOPS + 4 * 2 * MIQ : 63;
   // ONE LDS object: with several, the compiler tags every LDS access with per-object alias scopes, and the
   // waitcnt pass then drains vmcnt(0) between the LDS-DMA prefetch of stage t+1 and the fragment reads of
@@ -588,6 +590,91 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       }
     }
   };
+  // wide_st (bf16, no BN-backward reduction): the channel quads of 16-channel groups nt and nt + 1 are
+  // joined into 8-channel runs before the store. Lane row h4 (16 lanes, one pixel each) holds channels
+  // 16 nt + 4 h4 .. + 3; v_permlane16_swap exchanges the odd rows of group nt with the even rows of group
+  // nt + 1, after which row h4 holds channels 16 (nt + (h4 & 1)) + 8 (h4 >> 1) .. + 7 of its pixel: one
+  // 16-B store per (pixel, pair of groups) instead of two 8-B ones, 64 contiguous bytes of a pixel per
+  // instruction instead of 32. Needs Nout % 16 == 0 and a split point on a 32-channel boundary (host).
+  auto epilogue_wide = [&](int m0) {
+    if constexpr (!BNR && !F8) {
+      int tidv = tid;
+      asm volatile("" : "+v"(tidv));
+      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+#pragma unroll
+      for (int np = 0; np < 4; np += 2) {
+        float bias[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4 b4 = p_lds_f4(&cst[0][wc * 64 + (np + j) * 16 + 4 * h4]);
+          bias[j][0] = b4.x; bias[j][1] = b4.y; bias[j][2] = b4.z; bias[j][3] = b4.w;
+        }
+        // this lane's 8-channel run after the exchange, and its store target
+        const int cw = n0 + wc * 64 + 16 * (np + (h4 & 1)) + 8 * (h4 >> 1);
+        const bool cv = cw < a.Nout;
+        int sub = 0, cq = cw;
+        if (shuffle) { sub = cw / a.Cps; cq = cw - sub * a.Cps; }
+        const bool second = split && __builtin_amdgcn_readfirstlane(n0 + wc * 64 + np * 16) >= a.split_c;
+        if (second) cq = cw - a.split_c;
+        const int ostr = second ? a.out2_stride : a.out_stride;
+        const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc(second ? a.out2 : a.out, 0,
+                                                                           second ? out2_bytes : (int)out_bytes, P_RSRC3);
+        float s1[2][4] = {}, s2[2][4] = {};
+#pragma unroll
+        for (int mt = 0; mt < 2 * MIQ; ++mt) {
+          const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
+          const bool mv = m < a.M;
+          v2u32 o2[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const bool qv = mv && n0 + wc * 64 + (np + j) * 16 + 4 * h4 < a.Nout;   // (statistics: own quad)
+            float x[4];
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              x[r] = acc[mt][np + j][r] + bias[j][r];
+              if (a.relu) x[r] = fmaxf(x[r], 0.f);
+              o[r] = (bf16)x[r];
+            }
+            o2[j] = __builtin_bit_cast(v2u32, o);
+            if (stats && qv) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) { s1[j][r] += x[r]; s2[j][r] += x[r] * x[r]; }
+            }
+          }
+          const auto e0 = __builtin_amdgcn_permlane16_swap(o2[0].x, o2[1].x, false, false);
+          const auto e1 = __builtin_amdgcn_permlane16_swap(o2[0].y, o2[1].y, false, false);
+          const v4u32_t st = {e0[0], e1[0], e0[1], e1[1]};
+          int pixo = m;
+          if (shuffle) {
+            const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+            pixo = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
+          }
+          const unsigned off = mv && cv && !(a.debug_flags & 128) ? (unsigned)((pixo * ostr + cq) * OES) : P_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(st, rsO, off, 0, 0);
+        }
+        if (stats) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              s1[j][r] = row16_sum(s1[j][r]);
+              s2[j][r] = row16_sum(s2[j][r]);
+            }
+            if (r16 == 0) {
+              const int cl = wc * 64 + (np + j) * 16 + 4 * h4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                p_lds_add(&sacc[0][cl + r], s1[j][r]);
+                p_lds_add(&sacc[1][cl + r], s2[j][r]);
+              }
+            }
+          }
+        }
+      }
+    }
+  };
+  const bool wide = !BNR && !F8 && a.wide_st;
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
@@ -655,8 +742,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         } else if (gs + NST - 2 >= total) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (last_epi > gs - NST) {
-          if (NST == 2 && hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI + 1 < 63 ? VM_EPI + 1 : 63) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
+          if (wide) {
+            if (NST == 2 && hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W + 1 < 63 ? VM_EPI_W + 1 : 63) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W) : "memory");
+          } else if (NST == 2 && hg_last) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI + 1 < 63 ? VM_EPI + 1 : 63) : "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
+          }
         } else if (NST == 2 && hg_last) {
           asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         } else {
@@ -667,6 +760,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         hdy = tp / 3;
         hdx = tp - 3 * hdy;
       } else if (gs + NST - 2 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (last_epi > gs - NST && wide) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W) : "memory");
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
       else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
@@ -691,7 +785,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       last_epi = -NST;   // (no epilogue ops were issued)
       continue;
     }
-    epilogue(m0c);
+    if (wide) epilogue_wide(m0c);
+    else epilogue(m0c);
   }
 
   // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
@@ -743,6 +838,10 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // reduction only on the 256x128 form (its z loads wait behind the prefetch stream, which costs the
   // 256x256 form 5-8 % against tap64's LDS-staged epilogue)
   a.stagger = option("tap64p_stagger", 1);
+  // 16-B epilogue stores (bf16, no BN-backward reduction; whole 16-channel groups, split on 32 channels):
+  // level 2 forward +6 %, level 3 +3 %, step -1.4 %, bit-identical (profiles/r03_wide_store_ab.txt)
+  a.wide_st = option("tap64p_wide", 1) && !a.f8 && !a.bnr_z && a.Nout % 16 == 0 &&
+              (a.out_mode != 2 || a.split_c % 32 == 0);
   int cfg = option("tap64p_cfg", 0);
   if (cfg < 1 || cfg > 3) {
     if (a.bnr_z && tile != 1 && option("tap64p_bnr", 1) < 2) return 0;

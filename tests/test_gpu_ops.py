@@ -171,10 +171,11 @@ def test_tap64_configs(cfg):
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("wide", [0, 1], ids=["st8", "st16"])
 @pytest.mark.parametrize("tile", [256, 128], ids=["256x256x2", "256x128x3"])
 @pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
 @pytest.mark.parametrize("mode", ["plain", "one_chunk", "concat", "split"])
-def test_tap64p_halo_matches(mode, grid, tile):
+def test_tap64p_halo_matches(mode, grid, tile, wide):
     """Halo form of the persistent 256x256 forward (A operand read from a 10x34 halo moved into LDS once per
     64-channel chunk, chunk-major K stream, next chunk's halo issued one group per step) vs a float64
     reference convolution of the same bf16 operands, and vs the gathered form (tap64p_halo=0) to within the
@@ -209,6 +210,7 @@ def test_tap64p_halo_matches(mode, grid, tile):
         ops.set_option("fwd_halo", 0)   # (the <= 128-output halo kernels would take the narrow shapes)
         ops.set_option("tap64p_halo", halo)
         ops.set_option("fwd_w4", 0)   # (the four-wave form takes the Nout % 256 == 0 shapes: its own test)
+        ops.set_option("tap64p_wide", wide)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
@@ -216,7 +218,7 @@ def test_tap64p_halo_matches(mode, grid, tile):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4"):
+            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4", "tap64p_wide"):
                 ops.set_option(o_, None)
         assert kname.startswith("igemm_fwd_tap64p_kernel<256, %d, %d, false, %s, false" % (
             tile, 2 if tile == 256 else 3, "true" if halo else "false")), kname
@@ -486,12 +488,14 @@ def test_upsample_gather_halo_forms(form, grid):
     torch.testing.assert_close(sp, sn, rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("wide", [0, 1], ids=["st8", "st16"])
 @pytest.mark.parametrize("cfg", [1, 2, 3], ids=["256x256x2", "256x128x3", "128x256x3"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
 @pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad", "bnr", "dilated"])
-def test_tap64_persistent_matches(mode, grid, cfg):
+def test_tap64_persistent_matches(mode, grid, cfg, wide):
     """Persistent tap64 kernel (conv_fwd_tap64p.hip: one K-step stream over the block's tiles through an
-    NST-stage LDS ring, register epilogue with 8-B buffer stores) in its three tile / ring forms vs the
+    NST-stage LDS ring, register epilogue with 8-B buffer stores, or with 16-B stores of channel pairs joined
+    by permlane16_swap: option tap64p_wide) in its three tile / ring forms vs the
     non-persistent kernel on the same launch: bit-identical outputs and equal BatchNorm sums (statistics,
     or the fused BatchNorm-backward reduction for bnr); a 3-block grid makes every block walk many tiles
     (ragged last M tile, partial N tile), so the cross-tile prefetch and the counted vmcnt waits are
@@ -547,6 +551,7 @@ def test_tap64_persistent_matches(mode, grid, cfg):
         ops.set_option("tap64_persist", persist)
         ops.set_option("fwd_tap64", 2)   # the 256x256 configuration (small problems would pick narrower tiles)
         ops.set_option("tap64p_cfg", cfg)
+        ops.set_option("tap64p_wide", wide)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
@@ -557,7 +562,7 @@ def test_tap64_persistent_matches(mode, grid, cfg):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("tap64_persist", "fwd_tap64", "tap64_persist_grid", "tap64p_cfg"):
+            for o_ in ("tap64_persist", "fwd_tap64", "tap64_persist_grid", "tap64p_cfg", "tap64p_wide"):
                 ops.set_option(o_, None)
         res.append(([o.clone() for o in outs], st.clone(), kname))
     assert res[0][2].startswith("igemm_fwd_tap64_kernel") and res[1][2].startswith("igemm_fwd_tap64p_kernel"), \
