@@ -259,7 +259,11 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 // the arithmetic of epi_rows), 5 + ReLU + inverted dropout (adipose_v3's Dropout after up*_conv3: the
 // stateless hash of epi_rows, so the mask matches every other kernel's) -- compile-time, so the epilogue
 // carries no per-element selects for the launch-uniform flags
-template <bool BNR, int NCH, int BN, bool PIPE, int EPI>
+// WIDE: the epilogue handles the channel quads of 16-channel groups nf and nf + 1 together and joins them
+// with v_permlane16_swap into 8-channel runs (lane row h4 then holds channels 16 (nf + (h4 & 1)) + 8 (h4 >> 1)
+// .. + 7 of its pixel): one 16-B store per pair of units instead of two 8-B ones (the persistent forward's
+// tap64p_wide); needs the store limit (Nout, or split_c for the first part) on an 8-channel boundary
+template <bool BNR, int NCH, int BN, bool PIPE, int EPI, bool WIDE = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   static_assert(!BNR || EPI == 0, "the BN-backward reduction launch stores the plain product");
   static_assert(EPI < 4 || !PIPE, "mask / addend quads, the dropout hash and two accumulator sets: registers");
@@ -398,10 +402,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       }
   };
   auto load_z = [&](int mrow_, uint2 (&zr)[2][NF]) { load_q(rsZ, a.bnr_zs, n0, mrow_, zr); };
-  // epilogue of accumulator tile (mf, nf): lane = pixel mrow_ + mf*16 + r16, channels nf*16 + 4*h4 .. +3
-  auto epi_unit = [&](int mf, int nf, const f32x4& av, uint2 zv, int mrow_, uint2 dv = uint2{0u, 0u}) {
+  // epilogue of accumulator tile (mf, nf): lane = pixel mrow_ + mf*16 + r16, channels nf*16 + 4*h4 .. +3;
+  // returns the stored quad (the BatchNorm sums are taken here), epi_unit / epi_pair store it
+  auto epi_vals = [&](int mf, int nf, const f32x4& av, uint2 zv, int mrow_, uint2 dv = uint2{0u, 0u}) -> bf16x4 {
     const int c0 = nf * 16 + 4 * h4;
-    const bool cv = n0 + c0 < nlim;
     const float4 cb = *reinterpret_cast<const float4*>(cst + c0);
     const int m = mrow_ + mf * 16 + r16;
     float v[4] = {av[0] + cb.x, av[1] + cb.y, av[2] + cb.z, av[3] + cb.w};
@@ -427,8 +431,6 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       if constexpr (EPI == 2 || EPI == 3) v[i] = fmaxf(v[i], 0.f);
       o[i] = (bf16)v[i];
     }
-    const unsigned off = cv ? (unsigned)((m * ostride + ocol0 + c0) * 2) : 0x80000000u;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_h, o), rsO, off, 0, 0);
     if constexpr (BNR) {
       const float4 sc = *reinterpret_cast<const float4*>(cst + BN + c0);
       const float4 sh = *reinterpret_cast<const float4*>(cst + 2 * BN + c0);
@@ -451,6 +453,42 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
         s1[nf][i] += v[i];
         s2[nf][i] = fmaf(v[i], v[i], s2[nf][i]);
       }
+    }
+    return o;
+  };
+  auto epi_unit = [&](int mf, int nf, const f32x4& av, uint2 zv, int mrow_, uint2 dv = uint2{0u, 0u}) {
+    const bf16x4 o = epi_vals(mf, nf, av, zv, mrow_, dv);
+    const int c0 = nf * 16 + 4 * h4, m = mrow_ + mf * 16 + r16;
+    const unsigned off = n0 + c0 < nlim ? (unsigned)((m * ostride + ocol0 + c0) * 2) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_h, o), rsO, off, 0, 0);
+  };
+  // WIDE: units (mf, nf) and (mf, nf + 1), nf even, as one 16-B store per lane
+  auto epi_pair = [&](int mf, int nf, const f32x4& av0, const f32x4& av1, uint2 zv0, uint2 zv1, int mrow_,
+                      uint2 dv0 = uint2{0u, 0u}, uint2 dv1 = uint2{0u, 0u}) {
+    const v2u32_h o0 = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf, av0, zv0, mrow_, dv0));
+    const v2u32_h o1 = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf + 1, av1, zv1, mrow_, dv1));
+    const auto e0 = __builtin_amdgcn_permlane16_swap(o0.x, o1.x, false, false);
+    const auto e1 = __builtin_amdgcn_permlane16_swap(o0.y, o1.y, false, false);
+    typedef unsigned int v4u32_h __attribute__((ext_vector_type(4)));
+    const v4u32_h st = {e0[0], e1[0], e0[1], e1[1]};
+    const int cw = 16 * (nf + (h4 & 1)) + 8 * (h4 >> 1), m = mrow_ + mf * 16 + r16;
+    const unsigned off = n0 + cw < nlim ? (unsigned)((m * ostride + ocol0 + cw) * 2) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b128(st, rsO, off, 0, 0);
+  };
+  // every unit of an accumulator set, in the store form of the launch
+  auto epi_all = [&](const f32x4 (&av)[2][NF], const uint2 (&zv)[2][NF], int mrow_, const uint2 (&dv)[EPI == 4 ? 2 : 1][NF]) {
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int nf = 0; nf < NF; nf += 2)
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf)
+          epi_pair(mf, nf, av[mf][nf], av[mf][nf + 1], zv[mf][nf], zv[mf][nf + 1], mrow_, dv[EPI == 4 ? mf : 0][nf],
+                   dv[EPI == 4 ? mf : 0][nf + 1]);
+    } else {
+#pragma unroll
+      for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, av[mf][nf], zv[mf][nf], mrow_, dv[EPI == 4 ? mf : 0][nf]);
     }
   };
 
@@ -508,10 +546,16 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
           // previous tile's epilogue unit u in tap u + 1 (the z loads had a tap's time to land), its VALU
           // spread between this step's MFMAs
           constexpr bool unit_here = EPI_PREV;
-          const bool with_unit = unit_here && cc == 0 && kq == 0 && t >= 1 && t - 1 < 2 * NF;
+          const bool with_unit = unit_here && cc == 0 && kq == 0 && t >= 1 && t - 1 < (WIDE ? NF : 2 * NF);
           if (with_unit) {
-            const int u = t - 1, mf = u & 1, nf = u >> 1;
-            epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
+            const int u = t - 1, mf = u & 1;
+            if constexpr (WIDE) {   // pair u: units (u & 1, 2 (u >> 1)) and (u & 1, 2 (u >> 1) + 1)
+              const int nf = 2 * (u >> 1);
+              epi_pair(mf, nf, accp[mf][nf], accp[mf][nf + 1], zreg[mf][nf], zreg[mf][nf + 1], mrowp);
+            } else {
+              const int nf = u >> 1;
+              epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
+            }
           }
           if (!with_unit) prio_hi<ADP_PRIO_FWD>();   // (setprio would split the interleave region)
 #pragma unroll
@@ -537,10 +581,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
         for (int j = 0; j < NF; ++j) accp[i][j] = acc[i][j];
       mrowp = mrow;
     } else {
-#pragma unroll
-      for (int nf = 0; nf < NF; ++nf)
-#pragma unroll
-        for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, acc[mf][nf], zreg[mf][nf], mrow, dreg[EPI == 4 ? mf : 0][nf]);
+      epi_all(acc, zreg, mrow, dreg);
     }
     if (more) {
       LDS_BAR();   // every wave is done with this tile's halo
@@ -554,10 +595,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   for (int k = 1; k < nt; ++k) run_tile(k, std::integral_constant<bool, PIPE>{});
   if constexpr (PIPE) {   // the last tile's epilogue
     if constexpr (BNR) load_z(mrowp, zreg);
-#pragma unroll
-    for (int nf = 0; nf < NF; ++nf)
-#pragma unroll
-      for (int mf = 0; mf < 2; ++mf) epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
+    epi_all(accp, zreg, mrowp, dreg);
   }
   if (!stats || (a.debug_flags & 2)) return;   // (uniform)
   float* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
@@ -642,27 +680,41 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     const int pm = option("halop_pipe", 1);
     const bool pipe = !bnr && !maskepi && !dropepi && (pm == 2 || (pm == 1 && one_chunk));
     const int epi = bnr ? 0 : dropepi ? 5 : maskepi ? 4 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
-    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
-                    pipe ? "true" : "false", epi);
-#define HALOP_LAUNCH(NCH_, BN_)                                                                             \
+    // WIDE (option halop_wide: 0 off, 1 the tile-serial forms, 2 every form): 16-B stores of channel-quad
+    // pairs when every 8-channel run of the store is wholly inside or outside its limit. Not the BN-backward
+    // reduction forms (two units' z quads and constants at once spill) and by default not the pipelined
+    // ones (a pair unit between two taps' MFMAs: level-0 64->64 forward with statistics -5 %); the two-chunk
+    // forward with statistics +4 % (profiles/r03_halop_wide_ab.txt)
+    const int wm = option("halop_wide", 1);
+    const bool wide = !bnr && (wm == 2 || (wm == 1 && !pipe)) && a.Nout % 8 == 0 &&
+                      (a.out_mode != 2 || a.split_c % 8 == 0);
+    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
+                    pipe ? "true" : "false", epi, wide ? "true" : "false");
+#define HALOP_LAUNCH_W(NCH_, BN_, W_)                                                                       \
   do {                                                                                                      \
-    if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0>), dim3(grid), dim3(512), 0, s, a); \
-    else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4>), dim3(grid), dim3(512), 0, s, a); \
-    else if (epi == 5) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 5>), dim3(grid), dim3(512), 0, s, a); \
+    if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0, false>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4, W_>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 5) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 5, W_>), dim3(grid), dim3(512), 0, s, a); \
     else if (pipe) {                                                                                        \
-      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 3>), dim3(grid), dim3(512), 0, s, a); \
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 0>), dim3(grid), dim3(512), 0, s, a); \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1, W_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2, W_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 3, W_>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 0, W_>), dim3(grid), dim3(512), 0, s, a); \
     } else {                                                                                                \
-      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3>), dim3(grid), dim3(512), 0, s, a); \
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0>), dim3(grid), dim3(512), 0, s, a); \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1, W_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2, W_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3, W_>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0, W_>), dim3(grid), dim3(512), 0, s, a); \
     }                                                                                                       \
+  } while (0)
+#define HALOP_LAUNCH(NCH_, BN_)                  \
+  do {                                           \
+    if (wide) HALOP_LAUNCH_W(NCH_, BN_, true);   \
+    else HALOP_LAUNCH_W(NCH_, BN_, false);       \
   } while (0)
     if (one_chunk) HALOP_LAUNCH(1, 64);
     else HALOP_LAUNCH(2, 32);
+#undef HALOP_LAUNCH_W
 #undef HALOP_LAUNCH
     return 1;
   }

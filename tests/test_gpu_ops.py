@@ -364,7 +364,7 @@ def test_halop_relu_dropout_epilogue(cin, cout):
                 ops.set_option("halo_persist", None)
             assert kname.startswith("igemm_fwd_halop_kernel") == bool(persist), kname
             if persist and drop:
-                assert kname.endswith(", false, 5>"), kname
+                assert kname.split(", ")[3:5] == ["false", "5"], kname
             res[(persist, drop)] = out.double()
     yp, yn, y0 = res[(1, rate)], res[(0, rate)], res[(1, 0.0)]
     pos = y0 > 1e-2 * y0.abs().max()        # clearly positive before dropout: kept or dropped, never ReLU-zeroed
@@ -430,7 +430,7 @@ def test_halop_mask_addend_epilogue(mode):
             ops.set_option("halo_persist", None)
         assert kname.startswith("igemm_fwd_halop_kernel") == bool(persist), kname
         if persist:
-            assert kname.endswith(", false, 4>"), kname
+            assert kname.split(", ")[3:5] == ["false", "4"], kname
         res.append(torch.cat(outs, -1).double())
     tol = 2 ** -7 * ref.abs() + 1e-3 * ref.abs().max()
     assert ((res[0] - ref).abs() - tol).max().item() < 0, (res[0] - ref).abs().max().item()
@@ -686,6 +686,83 @@ def test_halop_pipelined_epilogue_matches(parts, cout, split, grid, epi):
         assert torch.equal(a_, b_)
     if epi == "stats":
         assert relerr(res[1][1], res[0][1]) < 1e-5
+
+
+HALOP_WIDE_CASES = [
+    # name, source channels, Nout, epilogue, split, up
+    ("1ch_stats", [64], 64, "stats", False, 1),
+    ("1ch_relu_stats", [64], 64, "relu_stats", False, 1),
+    ("1ch_plain_n48", [64], 48, "plain", False, 1),
+    ("1ch_split128", [64], 128, "relu", True, 1),
+    ("1ch_up2_stats", [64], 64, "stats", False, 2),
+    ("2ch_stats", [64, 64], 128, "stats", False, 1),
+    ("2ch_relu_n64", [128], 64, "relu", False, 1),
+    ("2ch_split", [128], 128, "plain", True, 1),
+    ("1ch_mask", [64], 64, "mask", False, 1),
+    ("2ch_mask_split", [128], 128, "mask", True, 1),
+    ("1ch_dropout", [64], 64, "dropout", False, 1),
+]
+
+
+@pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
+@pytest.mark.parametrize("case", HALOP_WIDE_CASES, ids=[c[0] for c in HALOP_WIDE_CASES])
+def test_halop_wide_store_matches(case, grid):
+    """Persistent halo kernel with 16-B epilogue stores (halop_wide=2: channel quads of two 16-channel groups
+    joined by permlane16_swap; by default the tile-serial forms only) vs the 8-B quad stores (halop_wide=0): the same values in
+    every channel of the outputs (plain, split, ragged N = 48 against a 64-wide block), and BatchNorm sums
+    to f32 order, for every epilogue form (statistics, ReLU, ReLU-backward mask + addend, dropout), the
+    pipelined one-chunk and the two-chunk forms, an upsampled source; a 3-block grid walks many tiles."""
+    name, parts, nout, epi, split, up = case
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(61)
+    N, S = 2, 32
+    xs = [torch.randn(N, S // up, S // up, c, generator=g).to(DEV, dt) for c in parts]
+    cin = sum(parts)
+    W = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV)
+    mk = torch.randn(N, S, S, nout, generator=g).to(DEV, dt)
+    ad = torch.randn(N, S, S, nout, generator=g).to(DEV, dt)
+    res = []
+    for wide in (1, 0):
+        ops.set_option("halop_wide", 2 * wide)   # 2: every (non-BNR) form, the pipelined ones included
+        if grid:
+            ops.set_option("halo_persist_grid", grid)
+        try:
+            st = torch.zeros(2, nout, device=DEV)
+            kw = dict(srcB=xs[1] if len(xs) > 1 else None, up=up == 2)
+            if epi in ("stats", "relu", "relu_stats", "plain", "dropout"):
+                kw.update(bias=bias, relu=epi in ("relu", "relu_stats", "dropout"))
+            if epi in ("stats", "relu_stats"):
+                kw.update(bn_stats=(st[0], st[1]))
+            if epi == "dropout":
+                kw.update(dropout_rate=0.3, dropout_seed=77)
+            if split:
+                o1 = torch.full((N, S, S, 64), 7.0, dtype=dt, device=DEV)
+                o2 = torch.full((N, S, S, nout - 64 + 8), 7.0, dtype=dt, device=DEV)   # wider stride than stored
+                if epi == "mask":
+                    kw.update(mask=mk[..., :64].contiguous(), mask_scale=1.5, mask2=mk[..., 64:].contiguous(),
+                              mask2_scale=0.5)
+                ops.conv_fwd(xs[0], W, nout, out=o1, out_mode=2, out2=o2, split_c=64, **kw)
+                outs = [o1, o2]
+            else:
+                o = torch.full((N, S, S, 64 if nout < 64 else nout), 7.0, dtype=dt, device=DEV)
+                if epi == "mask":
+                    kw.update(mask=mk, mask_scale=1.5, addend=ad)
+                ops.conv_fwd(xs[0], W, nout, out=o, **kw)
+                outs = [o]
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("halop_wide", None)
+            ops.set_option("halo_persist_grid", None)
+        # igemm_fwd_halop_kernel<BNR, NCH, BN, PIPE, EPI, WIDE>
+        assert kname.startswith("igemm_fwd_halop_kernel") and kname.split(", ")[5] == ("true>" if wide else "false>"), kname
+        res.append(([t.clone() for t in outs], st.clone()))
+    for a_, b_ in zip(res[0][0], res[1][0]):
+        assert torch.equal(a_, b_), (a_.double() - b_.double()).abs().max().item()
+    if nout < 64:   # the pad channels of the 64-stride output: untouched by either form
+        assert (res[0][0][0][..., nout:] == 7.0).all()
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.parametrize("parts,cout", [([128], 64), ([64, 64], 64), ([128], 128), ([64, 64], 128)])

@@ -65,6 +65,11 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L2,L3,L4" \
           --variants "tap64p_wide=0;tap64p_wide=1" > gpurun_out/wide_kernels.log 2>&1 &&
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_wide=0;tap64p_wide=1" > gpurun_out/wide_ab.log 2>&1 ;;
+    hwide) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
+          -k "halop or halo_ or upsample_gather or two_chunks" > gpurun_out/hwide_tests.log 2>&1 &&
+        timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd,bnr --layers "L0 64,L0 128,L1 128" \
+          --variants "halop_wide=0;halop_wide=1" > gpurun_out/hwide_kernels.log 2>&1 &&
+        timeout -k 10 300 python tools/ab_step.py --variant opt --opts "halop_wide=0;halop_wide=1" > gpurun_out/hwide_ab.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
