@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 class AdpError(RuntimeError):

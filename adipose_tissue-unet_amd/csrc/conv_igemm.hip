@@ -1187,6 +1187,11 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
     a.bna_inv_count = 1.f / bn->count;
     if (!(std::is_same<T, bf16>::value && adp::option("conv_fast", 2) == 2 && adp::wgrad_bna_fusable(a))) {
       a.bna_dA = nullptr;
+      if (!dY) {   // dz not wanted by the caller: the two-launch form computes it in library scratch
+        dY = adp::scratch(1, (size_t)a.M * dy_stride * (std::is_same<T, bf16>::value ? 2 : 4));
+        if (!dY) return -2;
+        a.dY = dY;
+      }
       if (adp_bn_bwd_apply(std::is_same<T, bf16>::value ? ADP_BF16 : ADP_F32, (size_t)a.M, dy_stride, bn->dA, bn->z,
                            bn->scale, bn->shift, bn->mean, bn->invstd, bn->gamma, bn->dgamma, bn->dbeta, bn->count,
                            const_cast<void*>(dY), s))
@@ -1197,6 +1202,11 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
     if (!adp::launch_wgrad_tap64(a, s)) {
       if (a.bna_dA) {   // no kernel took the fused form: dY = bn_bwd_apply(dA, z) first, then the fallback
         a.bna_dA = nullptr;
+        if (!dY) {
+          dY = adp::scratch(1, (size_t)a.M * dy_stride * 2);
+          if (!dY) return -2;
+          a.dY = dY;
+        }
         if (adp_bn_bwd_apply(ADP_BF16, (size_t)a.M, dy_stride, bn->dA, bn->z, bn->scale, bn->shift, bn->mean,
                              bn->invstd, bn->gamma, bn->dgamma, bn->dbeta, bn->count, const_cast<void*>(dY), s))
           return -2;
@@ -1303,7 +1313,8 @@ extern "C" int adp_conv_fwd(int dtype, const adp_conv_desc* d, const adp_conv_io
 extern "C" int adp_conv_wgrad_bn(int dtype, const adp_conv_desc* d, const adp_conv_io* io, const adp_bn_bwd_args* bn,
                                  void* dY, int dy_stride, float* dW, float* dB, adp_stream_t st) {
   hipStream_t s = (hipStream_t)st;
-  ADP_REQUIRE(d && io && bn && bn->dA && bn->z && dY && dW, "adp_conv_wgrad_bn: null argument");
+  ADP_REQUIRE(d && io && bn && bn->dA && bn->z && dW, "adp_conv_wgrad_bn: null argument");
+  ADP_REQUIRE(dY || !dB, "adp_conv_wgrad_bn: dY may be NULL only without dB (nothing then reads dz)");
   adp::set_launch_stream(s);
   ADP_REQUIRE(bn->scale && bn->shift && bn->mean && bn->invstd && bn->gamma && bn->dgamma && bn->dbeta && bn->count > 0,
               "adp_conv_wgrad_bn: BatchNorm vectors and count");

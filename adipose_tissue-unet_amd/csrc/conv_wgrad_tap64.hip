@@ -30,6 +30,9 @@ constexpr int WG_RSRC3 = 0x00020000;       // raw buffer descriptor word 3 (gfx9
 __device__ __forceinline__ void wg_buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
 }
+__device__ __forceinline__ void wg_glds16(const void* p, void* lds) {
+  __builtin_amdgcn_global_load_lds(p, (lds_void*)lds, 16, 0, 0);
+}
 
 
 #define W64_BAR()                          \
@@ -85,6 +88,9 @@ ADP_DEV v2u32_w wg_lds_r8(uint32_t lds_addr) {
 }
 ADP_DEV void wg_lds_w16(uint32_t lds_addr, v4u32_w v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr), "v"(v) : "memory");
+}
+ADP_DEV void wg_lds_w8(uint32_t lds_addr, v2u32_w v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(lds_addr), "v"(v) : "memory");
 }
 ADP_DEV uint32_t lds_off(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
@@ -460,8 +466,9 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   // 2 GiB): a halo pixel outside the image is an out-of-range offset and reads as zeros
   const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(inA ? a.srcA : a.srcB), 0, a.Nimg * a.Hs * a.Ws * xcs * 2, WG_RSRC3);
+  // (BNA with dY null: nothing reads dz, a zero-size resource drops its stores)
   const __amdgpu_buffer_rsrc_t rsD =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.dY, 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dY, 0, a.dY ? a.Nimg * a.Ho * a.Wo * a.dy_stride * 2 : 0, WG_RSRC3);
   const __amdgpu_buffer_rsrc_t rsBA = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(BNA ? a.bna_dA : a.dY), 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
   const __amdgpu_buffer_rsrc_t rsBZ = __builtin_amdgcn_make_buffer_rsrc(
@@ -763,14 +770,22 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
 // B = "virtual" fragments whose 16 columns are two taps x 8 channels (column j = k = 8 tap + c), read
 // with ds_read_b64_tr_b16 from the halo rows of the two taps (the tenth tap column reads a zero row).
 // Wave partials meet in LDS (ds_add_f32); one f32 atomic per dW element per block.
+// BNA (adp_conv_wgrad_bn on the input layer, unet_bn enc0_conv1): dY = bn_bwd_apply(dA, z) is computed
+// here instead of read. Two patches ahead, dA goes by LDS-DMA into the slots of the stage's dY image dY
+// would have taken and z into registers (two register sets, the loop unrolled by two); at its patch each
+// thread applies bn_bwd_apply_kernel's arithmetic (same rounding: bit-identical dz) to its own slots in
+// place. dz is not stored: the launcher takes this form only for dY = NULL (the input layer has no data
+// gradient, so nothing reads dz). Replaces the apply pass (dA + z read, dz written) and the dz read.
+template <bool BNA>
 __global__ __launch_bounds__(512, 1) void igemm_wgrad_cin8_kernel(WgradArgs a) {
   constexpr int NTH = 512, PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
   constexpr int HSLOT = NTH * 16;                  // halo region: one 16-B row per thread (rows >= 340: 0)
   constexpr int GD = PH * PW * 8 / NTH;            // dY 16-B chunks per thread
   constexpr int STAGE = HSLOT + PH * PW * 128, NST = 3;
   constexpr int ZROW = HROWS;                      // an all-zero halo row
-  static_assert(NST * STAGE <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[NST * STAGE];
+  constexpr int CST = BNA ? 6 * 64 * 4 : 0;        // BNA: per-channel scale, shift, mean, P, Q, R
+  static_assert(NST * STAGE + CST <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NST * STAGE + CST];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = patch row
@@ -781,27 +796,37 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_cin8_kernel(WgradArgs a) {
   const bf16* X = reinterpret_cast<const bf16*>(a.srcA);
   const bf16* D = reinterpret_cast<const bf16*>(a.dY);
 
-  auto issue = [&](int k) {   // 1 + GD LDS-DMA instructions per thread
+  auto patch_origin = [&](int k, int& img, int& y0, int& x0) {
     const int t = lin + k * G;
     const int px = t % tx_n, r = t / tx_n;
-    const int y0 = (r % ty_n) * PH, img = r / ty_n, x0 = px * PW;
+    y0 = (r % ty_n) * PH; img = r / ty_n; x0 = px * PW;
+  };
+  auto issue_halo = [&](int k) {   // 1 LDS-DMA instruction per thread
+    int img, y0, x0;
+    patch_origin(k, img, y0, x0);
     unsigned char* st = smem + (k % NST) * STAGE;
-    {
-      const int hr = tid;
-      const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
-      const bool ok = hr < HROWS && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
-      const void* p = ok ? (const void*)(X + (size_t)((img * a.Hs + gy) * a.Ws + gx) * a.CAs)
-                         : (const void*)wg64_zero_page;
-      __builtin_amdgcn_global_load_lds(p, (lds_void*)(st + wave * 64 * 16), 16, 0, 0);
-    }
+    const int hr = tid;
+    const int gy = y0 - 1 + hr / HW, gx = x0 - 1 + hr % HW;
+    const bool ok = hr < HROWS && gy >= 0 && gy < a.Hs && gx >= 0 && gx < a.Ws;
+    const void* p = ok ? (const void*)(X + (size_t)((img * a.Hs + gy) * a.Ws + gx) * a.CAs)
+                       : (const void*)wg64_zero_page;
+    wg_glds16(p, st + wave * 64 * 16);
+  };
+  // element offset of this thread's dY chunk i of patch k (the same for dA, z and dz)
+  auto chunk_off = [&](int k, int i) {
+    int img, y0, x0;
+    patch_origin(k, img, y0, x0);
+    const int idx = i * NTH + tid;
+    const int pr = idx >> 3, pos = idx & 7;
+    const size_t m = (size_t)(img * a.Ho + y0 + (pr >> 5)) * a.Wo + x0 + (pr & 31);
+    return m * a.dy_stride + 8 * (pos ^ gsw<128>(pr));
+  };
+  auto issue = [&](int k) {   // 1 + GD LDS-DMA instructions per thread
+    issue_halo(k);
+    unsigned char* st = smem + (k % NST) * STAGE;
 #pragma unroll
-    for (int i = 0; i < GD; ++i) {
-      const int idx = i * NTH + tid;
-      const int pr = idx >> 3, pos = idx & 7;
-      const size_t m = (size_t)(img * a.Ho + y0 + (pr >> 5)) * a.Wo + x0 + (pr & 31);
-      __builtin_amdgcn_global_load_lds(D + m * a.dy_stride + 8 * (pos ^ gsw<128>(pr)),
-                                       (lds_void*)(st + HSLOT + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
-    }
+    for (int i = 0; i < GD; ++i)
+      wg_glds16(D + chunk_off(k, i), st + HSLOT + (size_t)(i * NTH + wave * 64) * 16);
   };
   const int g = lane >> 4, ii = lane & 15, q = ii >> 2, pp = ii & 3;
   const int rr0 = 16 * (g >> 1) + 4 * (g & 1) + q;
@@ -821,19 +846,8 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_cin8_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nt > 0) issue(0);
-  if (nt > 1) issue(1);
   const uint32_t sbase = lds_off(smem);
-  for (int k = 0; k < nt; ++k) {
-    if (k + 2 < nt) {
-      issue(k + 2);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + GD)) : "memory");
-    } else if (k + 1 < nt) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + GD) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    W64_BAR();   // patch k landed for every wave
+  auto compute = [&](int k) {   // patch k of stage k % NST, landed and visible to every wave
     const uint32_t hb = sbase + (k % NST) * STAGE, db = hb + HSLOT;
     bf16x8 fd[4], fx[5];
 #pragma unroll
@@ -859,10 +873,109 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_cin8_kernel(WgradArgs a) {
       for (int kb = 0; kb < 5; ++kb)
         acc[nb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd[nb], fx[kb], acc[nb][kb], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    W64_BAR();   // stage k % NST is free for patch k + 3
+  };
+
+  if constexpr (!BNA) {
+    if (nt > 0) issue(0);
+    if (nt > 1) issue(1);
+    for (int k = 0; k < nt; ++k) {
+      if (k + 2 < nt) {
+        issue(k + 2);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + GD)) : "memory");
+      } else if (k + 1 < nt) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + GD) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      W64_BAR();   // patch k landed for every wave
+      compute(k);
+      W64_BAR();   // stage k % NST is free for patch k + 3
+    }
+  } else {
+    // per-channel constants of bn_bwd_apply_kernel; this thread's chunks all hold channel group bcg
+    // (gsw<128> depends on row bits 1-2, which the thread's rows i * 64 + tid / 8 share)
+    const __amdgpu_buffer_rsrc_t rsDA = __builtin_amdgcn_make_buffer_rsrc((void*)a.bna_dA, 0, a.M * a.dy_stride * 2, WG_RSRC3);
+    const __amdgpu_buffer_rsrc_t rsZ = __builtin_amdgcn_make_buffer_rsrc((void*)a.bna_z, 0, a.M * a.dy_stride * 2, WG_RSRC3);
+    const int bcg = (tid & 7) ^ gsw<128>(tid >> 3);
+    float* bk = reinterpret_cast<float*>(smem + NST * STAGE);
+    if (tid < 64) {
+      const float kk = a.bna_gamma[tid] * a.bna_invstd[tid];
+      bk[0 * 64 + tid] = a.bna_sc[tid];
+      bk[1 * 64 + tid] = a.bna_sh[tid];
+      bk[2 * 64 + tid] = a.bna_mean[tid];
+      bk[3 * 64 + tid] = kk;
+      bk[4 * 64 + tid] = -kk * a.bna_invstd[tid] * a.bna_dgamma[tid] * a.bna_inv_count;
+      bk[5 * 64 + tid] = -kk * a.bna_dbeta[tid] * a.bna_inv_count;
+    }
+    __syncthreads();
+    typedef unsigned v4u_c __attribute__((ext_vector_type(4)));
+    // dA by LDS-DMA into the stage's dY image (the slots this thread would have DMA'd dY into), z into
+    // registers (2 GD + 1 vector-memory ops per patch with the halo)
+    auto load_ops = [&](int k, v4u_c (&zr)[GD]) {
+      issue_halo(k);
+      unsigned char* st = smem + (k % NST) * STAGE;
+#pragma unroll
+      for (int i = 0; i < GD; ++i) {
+        const unsigned off = (unsigned)(chunk_off(k, i) * 2);
+        wg_buf_lds16(rsDA, st + HSLOT + (size_t)(i * NTH + wave * 64) * 16, off);
+        zr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsZ, off, 0, 0);
+      }
+    };
+    // dz of this thread's slots of patch k, in place (its own DMA wrote them: no barrier needed before);
+    // 8 B at a time (no 16-B result held: registers)
+    auto apply = [&](int k, const v4u_c (&zr)[GD]) {
+      const uint32_t dimg = sbase + (k % NST) * STAGE + HSLOT;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {   // 4 channels at a time: bounds the registers held
+        float c[6][4];
+#pragma unroll
+        for (int qq = 0; qq < 6; ++qq) {
+          const float4 v = wg_lds_f4(sbase + NST * STAGE + (qq * 64 + bcg * 8 + 4 * half) * 4);
+          c[qq][0] = v.x; c[qq][1] = v.y; c[qq][2] = v.z; c[qq][3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < GD; ++i) {
+          const uint32_t slot = dimg + (uint32_t)(i * NTH + tid) * 16 + 8 * half;
+          const v2u32_w dv = wg_lds_r8(slot);
+          const unsigned zw[2] = {zr[i][2 * half], zr[i][2 * half + 1]};
+          const bf16* d = reinterpret_cast<const bf16*>(&dv);
+          const bf16* zz = reinterpret_cast<const bf16*>(zw);
+          bf16 o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {   // bn_bwd_apply_kernel's arithmetic and rounding
+            const float zf = (float)zz[j];
+            const float dbv = fmaf(zf, c[0][j], c[1][j]) > 0.f ? (float)d[j] : 0.f;
+            o[j] = (bf16)fmaf(c[3][j], dbv, fmaf(c[4][j], zf - c[2][j], c[5][j]));
+          }
+          wg_lds_w8(slot, *reinterpret_cast<const v2u32_w*>(o));
+        }
+      }
+    };
+    constexpr int OPS = 1 + 2 * GD;   // vector-memory ops of one patch's loads
+    v4u_c z0[GD], z1[GD];
+    // patch k: its loads (issued two patches ago) retired, its dz into the stage, the loads of patch
+    // k + 2 into the freed registers, then the multiply. Ops younger than patch k's loads at the wait: the
+    // loads of patch k + 1 (OPS)
+    auto step = [&](int k, v4u_c (&zr)[GD]) {
+      if (k + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      apply(k, zr);
+      if (k + 2 < nt) load_ops(k + 2, zr);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      W64_BAR();   // patch k's halo and dz image visible to every wave
+      compute(k);
+      W64_BAR();   // stage k % NST is free for patch k + 3
+    };
+    if (nt > 0) load_ops(0, z0);
+    if (nt > 1) load_ops(1, z1);
+    for (int k = 0; k < nt; k += 2) {
+      step(k, z0);
+      if (k + 1 < nt) step(k + 1, z1);
+    }
   }
   if (nt == 0) return;
   // wave partials -> LDS [64][80] f32 -> one atomic per element into dW[n][k], k < 72
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* red = reinterpret_cast<float*>(smem);
   for (int i = tid; i < 64 * 80; i += NTH) red[i] = 0.f;
   __syncthreads();
@@ -881,6 +994,10 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_cin8_kernel(WgradArgs a) {
 }
 
 #undef W64_BAR
+
+// (explicit instantiations: without them hipcc emitted no host stub for the <false> form)
+template __global__ void igemm_wgrad_cin8_kernel<false>(WgradArgs);
+template __global__ void igemm_wgrad_cin8_kernel<true>(WgradArgs);
 
 // dW[n][k] += sum over the splits of part[split][n][k] (n < Nout, k < K = Kpad), 4 floats per thread.
 // blockIdx.y = group of SG consecutive splits: one group adds with a plain read-modify-write, several
@@ -966,11 +1083,21 @@ static bool halop_ok(const WgradArgs& a) {
 // BatchNorm-backward apply fused into the halo weight gradient: every block of input chunk c recomputes
 // its output block's dY tile, so only layers with at most wgrad_bna_maxch (default 1) 64-channel input
 // chunks take it (levels 0-1 of unet_bn; deeper layers re-read dA/z once per chunk)
+// shapes of the input-layer weight-gradient kernel (one 8-channel source, 64 outputs)
+static bool cin8_ok(const WgradArgs& a) {
+  return option("wgrad_cin8", 1) && !a.scA && a.CAs == 8 && a.CBs == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
+         a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
+         a.Nout == 64 && a.dy_mode == 0 && a.K == 72 && a.Kpad >= 72 && a.dy_stride % 8 == 0 && a.dy_stride >= 64;
+}
 bool wgrad_bna_fusable(const WgradArgs& a) {
   // (launch_wgrad_tap64 takes the halo kernel only with wgrad_tap64 != 0: with it off, the fused form would
   //  fall through to a kernel that reads a dY nothing has computed)
-  return a.bna_dA && a.bna_z && option("wgrad_tap64", 1) != 0 && option("wgrad_bna", 1) &&
-         option("wgrad_halop_waves", 8) == 8 && halop_ok(a) && (a.CAs + a.CBs) / 64 <= option("wgrad_bna_maxch", 1);
+  if (!(a.bna_dA && a.bna_z && option("wgrad_tap64", 1) != 0 && option("wgrad_bna", 1))) return false;
+  // the input layer (option wgrad_cin8_bna), when nothing reads dz (dY = NULL: the kernel stores none);
+  // dA / z through buffer resources below 2 GiB
+  if (cin8_ok(a) && !a.dY && option("wgrad_cin8_bna", 1) && (size_t)a.M * a.dy_stride * 2 < ((size_t)1 << 31))
+    return true;
+  return option("wgrad_halop_waves", 8) == 8 && halop_ok(a) && (a.CAs + a.CBs) / 64 <= option("wgrad_bna_maxch", 1);
 }
 
 // configurations: 0 = 256x256 (8 waves, 128x64 per wave), 1 = 128x256 (8 waves, 64x64),
@@ -978,13 +1105,16 @@ bool wgrad_bna_fusable(const WgradArgs& a) {
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   const int mode = option("wgrad_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
-  if (option("wgrad_cin8", 1) && !a.bna_dA && !a.scA && a.CAs == 8 && a.CBs == 0 && a.kh == 3 && a.kw == 3 && a.dil == 1 &&
-      a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % 8 == 0 && a.Wo % 32 == 0 &&
-      a.Nout == 64 && a.dy_mode == 0 && a.K == 72 && a.Kpad >= 72 && a.dy_stride % 8 == 0 && a.dy_stride >= 64) {
+  if (cin8_ok(a)) {   // (bna_dA set: the caller checked wgrad_bna_fusable)
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
     const int grid = std::max(1, std::min(tiles, option("wgrad_cin8_grid", 256)));
-    adp::set_kernel("igemm_wgrad_cin8_kernel");
-    hipLaunchKernelGGL(igemm_wgrad_cin8_kernel, dim3(grid), dim3(512), 0, s, a);
+    if (a.bna_dA) {
+      adp::set_kernel("igemm_wgrad_cin8_kernel<true>");
+      hipLaunchKernelGGL((igemm_wgrad_cin8_kernel<true>), dim3(grid), dim3(512), 0, s, a);
+    } else {
+      adp::set_kernel("igemm_wgrad_cin8_kernel<false>");
+      hipLaunchKernelGGL((igemm_wgrad_cin8_kernel<false>), dim3(grid), dim3(512), 0, s, a);
+    }
     return 1;
   }
   const int cin = a.CAs + a.CBs;

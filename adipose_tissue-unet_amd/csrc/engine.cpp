@@ -1258,7 +1258,8 @@ struct adp_handle {
       CL(bn_wgrad(en + "_conv2", N, b(("az" + k + "_1").c_str()), nullptr, dA2, z2, dz2, s));
       void* dA1 = b(("dA_z" + k + "_1").c_str());
       CL(bn_dgrad(en + "_conv2", N, dz2, dA1, en + "_conv1", z1, s));
-      void* dz1 = b(("dz_z" + k + "_1").c_str());
+      // (the input layer has no data gradient: its dz is not stored, the fused input-layer form then runs)
+      void* dz1 = i == 0 ? nullptr : b(("dz_z" + k + "_1").c_str());
       const void* src = i == 0 ? b("x") : b(("pool" + std::to_string(i - 1)).c_str());
       CL(bn_wgrad(en + "_conv1", N, src, nullptr, dA1, z1, dz1, s));
       if (i > 0) {

@@ -1031,7 +1031,9 @@ class UNetBN(UNetEngine):
             self._bn_bwd_wgrad(f"enc{i}_conv2", dA2, z2, dz2, l2, a[f"az{i}_1"])
             dA1 = gb(f"dA_z{i}_1", z1)
             self.dgrad(l2, dz2, dA1, bn_reduce=self._bn_red(f"enc{i}_conv1", z1))
-            dz1 = gb(f"dz_z{i}_1", z1)
+            # (the input layer has no data gradient: with the fused BN-backward weight gradient nothing reads
+            # its dz, which is then never stored)
+            dz1 = gb(f"dz_z{i}_1", z1) if i > 0 or not self.fuse_bn_wgrad else None
             l1 = L[f"enc{i}_conv1"]
             src = a["x"] if i == 0 else a[f"pool{i - 1}"]
             self._bn_bwd_wgrad(f"enc{i}_conv1", dA1, z1, dz1, l1, src)

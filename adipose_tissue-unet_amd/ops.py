@@ -247,10 +247,14 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     """dW (+)= X_tap^T dY (f32 accumulators, caller zeroes). shuffle_c>0: dY is a ConvT output.
     bn_apply=(dA, z, scale, shift, mean, invstd, gamma, dgamma, dbeta, count): dY is first computed as
     bn_bwd_apply(dA, z, ...) and stored (adp_conv_wgrad_bn: fused into the weight-gradient launch where the
-    halo kernel takes the shape, bit-identical to bn_bwd_apply + conv_wgrad)."""
+    halo kernel takes the shape, bit-identical to bn_bwd_apply + conv_wgrad). With bn_apply, dY may be None
+    (and dB None) when nothing reads dz: the fused forms then store nothing (the input layer, which has no
+    data gradient)."""
     Wdummy = torch.empty(0)
     _act(srcA, "srcA")
-    _act(dY, "dY")
+    _check(dY is not None or (bn_apply is not None and dB is None), "dY is None only with bn_apply and no dB")
+    dYs = dY if dY is not None else bn_apply[0]   # (its shape stands for dz's)
+    _act(dYs, "dY")
     N, Hs, Ws, CA = srcA.shape
     CB = 0 if srcB is None else srcB.shape[3]
     K = kh * kw * (CA + CB)
@@ -269,9 +273,9 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     d.Nout = nout
     if shuffle_c:
         d.out_mode, d.shuffle_c = 1, shuffle_c
-        _check(tuple(dY.shape[:3]) == (N, 2 * Ho, 2 * Wo), "convT dY shape mismatch")
+        _check(tuple(dYs.shape[:3]) == (N, 2 * Ho, 2 * Wo), "convT dY shape mismatch")
     else:
-        _check(tuple(dY.shape[:3]) == (N, Ho, Wo) and dY.shape[3] >= nout, "dY shape mismatch")
+        _check(tuple(dYs.shape[:3]) == (N, Ho, Wo) and dYs.shape[3] >= nout, "dY shape mismatch")
     io.srcA, io.srcB = ptr(srcA), ptr(srcB)
     if bnA is not None:
         io.bn_scaleA, io.bn_shiftA = ptr(bnA[0]), ptr(bnA[1])
@@ -286,13 +290,13 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     nbytes = _nbytes(srcA) + _nbytes(srcB) + _nbytes(dY) + 4.0 * nout * Kpad
     if bn_apply is not None:
         dA, z, sc, sh, mu, ist, gam, dg, dbt, count = bn_apply
-        _check(not shuffle_c and dA.shape == z.shape == dY.shape and dY.shape[3] == nout and
-               dA.dtype == z.dtype == dY.dtype, "bn_apply: dA, z, dY of one [N, Ho, Wo, nout] shape")
+        _check(not shuffle_c and dA.shape == z.shape == dYs.shape and dYs.shape[3] == nout and
+               dA.dtype == z.dtype == dYs.dtype, "bn_apply: dA, z, dY of one [N, Ho, Wo, nout] shape")
         bn = BnBwdArgs(ptr(dA), ptr(z), ptr(sc), ptr(sh), ptr(mu), ptr(ist), ptr(gam), ptr(dg), ptr(dbt),
                        float(count))
         _timed(dc, flops,
                lambda: call("adp_conv_wgrad_bn", dc, C.byref(d), C.byref(io), C.byref(bn), ptr(dY),
-                            int(dY.shape[3]), ptr(dW), ptr(dB), stream_ptr()), nbytes + 2 * _nbytes(dA))
+                            int(dYs.shape[3]), ptr(dW), ptr(dB), stream_ptr()), nbytes + 2 * _nbytes(dA))
         return
     _timed(dc, flops,
            lambda: call("adp_conv_wgrad", dc, C.byref(d), C.byref(io), ptr(dY), int(dY.shape[3]), ptr(dW),

@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 14 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 15 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
@@ -37,7 +37,8 @@ extern "C" {
                               v10: adp_bn_bwd_apply_head, adp_head_sigmoid_bwd_bnr with dx = NULL, adp_conv_wgrad_bn;
                               v11: adp_sum_bf16; v12: adp_timing / adp_timing_read, unet_bn handle preset;
                               v13: adp_vec_mul (eval BatchNorm folded into the fp8 dequantisation scale);
-                              v14: adp_scale_rows (eval BatchNorm folded into bf16 / f32 forward weights) */
+                              v14: adp_scale_rows (eval BatchNorm folded into bf16 / f32 forward weights);
+                              v15: adp_conv_wgrad_bn with dY = NULL (dz not stored), input-layer fused form */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -146,7 +147,10 @@ typedef struct adp_bn_bwd_args {
 /* adp_bn_bwd_apply(bn -> dY) followed by adp_conv_wgrad(dY), as one launch where the persistent halo
  * weight-gradient kernel takes the shape (3x3 stride-1 layers with <= 2 64-channel input chunks): dz is
  * computed while the weight gradient loads its tiles and stored into dY (for the data-gradient launch),
- * bit-identical to the two-launch form, which runs otherwise. */
+ * bit-identical to the two-launch form, which runs otherwise. dY may be NULL when dB is NULL and nothing
+ * reads dz (the input layer has no data gradient): the fused forms then store nothing -- and the
+ * input-layer kernel (one 8-channel source, 64 outputs) takes the fused form too -- while the two-launch
+ * form computes dz in library scratch. */
 int adp_conv_wgrad_bn(int dtype, const adp_conv_desc* d, const adp_conv_io* io, const adp_bn_bwd_args* bn,
                       void* dY, int dy_stride, float* dW, float* dB, adp_stream_t s);
 

@@ -985,6 +985,56 @@ def test_wgrad_bn_apply_fused(N, H, W, parts, cout, dtn, fused, maxch):
     assert relerr(dW2.cpu(), dW1.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("N,H,W,grid", [(2, 64, 64, None), (1, 32, 96, None), (3, 16, 32, 5), (2, 64, 64, 7)])
+@pytest.mark.parametrize("opt", [None, "wgrad_cin8_bna", "wgrad_bna"])
+def test_wgrad_bn_apply_input_layer_no_dz(N, H, W, grid, opt):
+    """adp_conv_wgrad_bn with dY = NULL (nothing reads dz): on the input layer (one 8-channel source, 64
+    outputs) the persistent input-layer kernel computes dz = bn_bwd_apply(dA, z) from dA (LDS-DMA) and z
+    (registers) in its stage images and stores none; dW equals adp_bn_bwd_apply + adp_conv_wgrad to f32
+    summation order. Options wgrad_cin8_bna=0 / wgrad_bna=0 take the two-launch form through library scratch;
+    small grids (5 / 7 blocks) walk many patches per block, an odd count exercising the unrolled tail."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(37)
+    cout = 64
+    x = torch.randn(N, H, W, 8, generator=g).to(DEV, dt)
+    z = (torch.randn(N, H, W, cout, generator=g) * 2).to(DEV, dt)
+    dA = torch.randn(N, H, W, cout, generator=g).to(DEV, dt)
+    vec = lambda: (torch.rand(cout, generator=g) + 0.5).to(DEV)   # noqa: E731
+    sc, sh, mu, ist, gam = vec(), vec() - 1.0, vec() - 1.0, vec(), vec()
+    dg, db = torch.randn(cout, generator=g).to(DEV), torch.randn(cout, generator=g).to(DEV)
+    count = N * H * W
+    dz1 = torch.full_like(z, 7.0)
+    dW1 = torch.zeros((cout, 96), device=DEV)   # Kpad = 72 rounded to 32
+    dW2 = torch.zeros_like(dW1)
+    ops.bn_bwd_apply(dA, z, sc, sh, mu, ist, gam, dg, db, count, dz1)
+    ops.conv_wgrad(x, dz1, dW1, cout)
+    assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_cin8_kernel<false>"
+    if opt:
+        ops.set_option(opt, 0)
+    if grid:
+        ops.set_option("wgrad_cin8_grid", grid)
+    try:
+        ops.conv_wgrad(x, None, dW2, cout, bn_apply=(dA, z, sc, sh, mu, ist, gam, dg, db, count))
+        kname = _lib.lib().adp_last_kernel().decode()
+        torch.cuda.synchronize()
+    finally:
+        for o_ in (opt, "wgrad_cin8_grid"):
+            if o_:
+                ops.set_option(o_, None)
+    assert kname == "igemm_wgrad_cin8_kernel<%s>" % ("false" if opt else "true"), kname
+    assert relerr(dW2.cpu(), dW1.cpu()) < 1e-5
+    if grid is None and opt is None:   # a halo-kernel layer with dY = NULL: fused, dz not stored
+        xs = torch.randn(N, H, W, 64, generator=g).to(DEV, dt)
+        dW3 = torch.zeros((cout, 9 * 64), device=DEV)
+        dW4 = torch.zeros_like(dW3)
+        ops.conv_wgrad(xs, dz1, dW3, cout)
+        ops.conv_wgrad(xs, None, dW4, cout, bn_apply=(dA, z, sc, sh, mu, ist, gam, dg, db, count))
+        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_halop_kernel<8, true")
+        torch.cuda.synchronize()
+        assert relerr(dW4.cpu(), dW3.cpu()) < 1e-5
+
+
 @pytest.mark.parametrize("opt", ["wgrad_tap64", "wgrad_halop", "wgrad_bna"])
 def test_wgrad_bn_apply_with_kernel_options_off(opt):
     """adp_conv_wgrad_bn with the halo weight-gradient kernel switched off (wgrad_tap64 = 0 is a documented

@@ -70,6 +70,10 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd,bnr --layers "L0 64,L0 128,L1 128" \
           --variants "halop_wide=0;halop_wide=1" > gpurun_out/hwide_kernels.log 2>&1 &&
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "halop_wide=0;halop_wide=1" > gpurun_out/hwide_ab.log 2>&1 ;;
+    cin8bna) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_network.py tests/test_engine.py \
+          tests/test_abi.py -v --timeout 200 --timeout-method thread -k "wgrad or unet_bn or engine or abi or cin8" \
+          > gpurun_out/cin8bna_tests.log 2>&1 &&
+        timeout -k 10 300 python tools/ab_step.py --variant opt --opts "wgrad_cin8_bna=0;wgrad_cin8_bna=1" > gpurun_out/cin8bna_ab.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
