@@ -82,6 +82,36 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
         for (int mb = 0; mb < 4; ++mb)
           acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mb][ks], xb[u][ks], acc[mb], 0, 0, 0);
       const int m = mm[u];
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      if (a.wide_st) {
+        // 16-B stores: the quads of 16-channel blocks mb and mb + 1 joined by v_permlane16_swap (lane row h4
+        // then holds channels 16 (mb + (h4 & 1)) + 8 (h4 >> 1) .. + 7), before the lane-divergent tail test
+        const bool mv = g0 + u < groups && m < a.M;
+        C8v2u32 o2[4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          const bool qv = mv && 16 * mb + 4 * h4 < a.Nout;
+          float v[4];
+          bf16x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = acc[mb][i] + bias[mb][i];
+            if (a.relu) v[i] = fmaxf(v[i], 0.f);
+            if (qv) { s1[mb][i] += v[i]; s2[mb][i] += v[i] * v[i]; }
+            o[i] = (bf16)v[i];
+          }
+          o2[mb] = __builtin_bit_cast(C8v2u32, o);
+        }
+#pragma unroll
+        for (int p = 0; p < 4; p += 2) {
+          const auto e0 = __builtin_amdgcn_permlane16_swap(o2[p].x, o2[p + 1].x, false, false);
+          const auto e1 = __builtin_amdgcn_permlane16_swap(o2[p].y, o2[p + 1].y, false, false);
+          const int cw = 16 * (p + (h4 & 1)) + 8 * (h4 >> 1);
+          if (mv && cw < a.Nout)
+            *reinterpret_cast<uint4*>(out + (size_t)m * a.out_stride + cw) = make_uint4(e0[0], e1[0], e0[1], e1[1]);
+        }
+        continue;
+      }
       if (g0 + u >= groups || m >= a.M) continue;
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
@@ -95,7 +125,6 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
           s1[mb][i] += v[i];
           s2[mb][i] += v[i] * v[i];
         }
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
         bf16x4 o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = (bf16)v[i];
@@ -285,6 +314,8 @@ int launch_fwd_cin8(FwdArgs& a, hipStream_t s) {
       a.Kpad < (a.K + 31) / 32 * 32 || a.Nout > 64 || a.Nout % 8 != 0 || a.out_mode != 0 || !a.out ||
       a.out_stride % 4 != 0 || a.addend || a.mask || a.accum || a.drop_rate > 0.f || a.bnr_z)
     return 0;
+  // 16-B output stores (option cin8_wide): every 8-channel run wholly inside or outside Nout (Nout % 8 == 0)
+  a.wide_st = option("cin8_wide", 1) && a.out_stride % 8 == 0;
   const int ks = (a.K + 31) / 32;
   if (ks == 1) launch_cin8<1>(a, s);
   else if (ks == 2) launch_cin8<2>(a, s);

@@ -1252,7 +1252,8 @@ def test_cin8_input_layer_bn_stats(S, cout):
                                                      (1, 10, 3, 24, 1, True), (5, 8, 3, 64, 1, False)])
 def test_cin8_pipelined_matches_plain(N, S, cin, cout, dil, relu):
     """The pipelined branch-free input-layer kernel (igemm_fwd_cin8p_kernel, buffer accesses with
-    out-of-range padding / tail offsets) against the plain one (option cin8_pf=0): same MFMA order, so the
+    out-of-range padding / tail offsets) against the plain one (option cin8_pf=0; with 16-B stores of
+    permlane16_swap-joined quads, and with 8-B stores, cin8_wide=0): same MFMA order, so the
     stored outputs are bit-identical; BatchNorm sums equal up to the order of the per-wave atomics; pad
     channels stored as zeros. Ragged images (13x13, 10x10, 8x8) leave partial 16-pixel groups."""
     from adipose_amd._lib import lib
@@ -1262,8 +1263,9 @@ def test_cin8_pipelined_matches_plain(N, S, cin, cout, dil, relu):
     b[:cout] = bias.to(DEV)
     src = nhwc_pad(xs[0], l.cin_s[0], torch.bfloat16)
     res = {}
-    for pf in (1, 0):
-        ops.set_option("cin8_pf", pf)
+    for pf in (1, 0, "narrow"):   # "narrow": the plain form with 8-B stores (option cin8_wide=0)
+        ops.set_option("cin8_pf", 1 if pf == 1 else 0)
+        ops.set_option("cin8_wide", 0 if pf == "narrow" else 1)
         try:
             out = torch.full((N, S, S, l.cout_s), 7.0, dtype=torch.bfloat16, device=DEV)
             s1 = torch.zeros(l.cout_s, device=DEV)
@@ -1273,8 +1275,11 @@ def test_cin8_pipelined_matches_plain(N, S, cin, cout, dil, relu):
             res[pf] = (out.clone(), s1.clone(), s2.clone(), lib().adp_last_kernel().decode())
         finally:
             ops.set_option("cin8_pf", None)
+            ops.set_option("cin8_wide", None)
     assert res[1][3].startswith("igemm_fwd_cin8p_kernel") and res[0][3].startswith("igemm_fwd_cin8_kernel")
-    assert torch.equal(res[1][0], res[0][0])
+    assert torch.equal(res[1][0], res[0][0]) and torch.equal(res["narrow"][0], res[0][0])
+    for k in (1, 2):
+        assert torch.allclose(res["narrow"][k], res[0][k], rtol=1e-5, atol=1e-3)
     if l.cout_s > cout:   # (pad channels: zero weight rows, zero bias -> stored zeros, as the plain form)
         assert res[1][0][..., cout:].abs().max().item() == 0.0
     ref = oracle_fwd([rb(xs[0], torch.bfloat16)], rb(kern, torch.bfloat16), bias, dil, False, relu=relu)

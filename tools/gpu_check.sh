@@ -74,6 +74,10 @@ for s in $STEPS; do
           tests/test_abi.py -v --timeout 200 --timeout-method thread -k "wgrad or unet_bn or engine or abi or cin8" \
           > gpurun_out/cin8bna_tests.log 2>&1 &&
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "wgrad_cin8_bna=0;wgrad_cin8_bna=1" > gpurun_out/cin8bna_ab.log 2>&1 ;;
+    cin8w) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
+          -k "cin8" > gpurun_out/cin8w_tests.log 2>&1 &&
+        timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats --layers "L0 in8" \
+          --variants "cin8_wide=0;cin8_wide=1" > gpurun_out/cin8w_kernels.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
