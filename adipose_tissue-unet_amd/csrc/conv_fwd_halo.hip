@@ -462,11 +462,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     const unsigned off = n0 + c0 < nlim ? (unsigned)((m * ostride + ocol0 + c0) * 2) : 0x80000000u;
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32_h, o), rsO, off, 0, 0);
   };
-  // WIDE: units (mf, nf) and (mf, nf + 1), nf even, as one 16-B store per lane
-  auto epi_pair = [&](int mf, int nf, const f32x4& av0, const f32x4& av1, uint2 zv0, uint2 zv1, int mrow_,
-                      uint2 dv0 = uint2{0u, 0u}, uint2 dv1 = uint2{0u, 0u}) {
-    const v2u32_h o0 = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf, av0, zv0, mrow_, dv0));
-    const v2u32_h o1 = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf + 1, av1, zv1, mrow_, dv1));
+  // WIDE: the stored quads o0 / o1 of units (mf, nf) and (mf, nf + 1), nf even, as one 16-B store per lane
+  auto epi_join = [&](int mf, int nf, v2u32_h o0, v2u32_h o1, int mrow_) {
     const auto e0 = __builtin_amdgcn_permlane16_swap(o0.x, o1.x, false, false);
     const auto e1 = __builtin_amdgcn_permlane16_swap(o0.y, o1.y, false, false);
     typedef unsigned int v4u32_h __attribute__((ext_vector_type(4)));
@@ -475,6 +472,13 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     const unsigned off = n0 + cw < nlim ? (unsigned)((m * ostride + ocol0 + cw) * 2) : 0x80000000u;
     __builtin_amdgcn_raw_buffer_store_b128(st, rsO, off, 0, 0);
   };
+  auto epi_pair = [&](int mf, int nf, const f32x4& av0, const f32x4& av1, uint2 zv0, uint2 zv1, int mrow_,
+                      uint2 dv0 = uint2{0u, 0u}, uint2 dv1 = uint2{0u, 0u}) {
+    const v2u32_h o0 = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf, av0, zv0, mrow_, dv0));
+    const v2u32_h o1 = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf + 1, av1, zv1, mrow_, dv1));
+    epi_join(mf, nf, o0, o1, mrow_);
+  };
+  v2u32_h pend = {0u, 0u};   // WIDE, pipelined: the first unit of a pair, stored at the next tap
   // every unit of an accumulator set, in the store form of the launch
   auto epi_all = [&](const f32x4 (&av)[2][NF], const uint2 (&zv)[2][NF], int mrow_, const uint2 (&dv)[EPI == 4 ? 2 : 1][NF]) {
     if constexpr (WIDE) {
@@ -546,14 +550,22 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
           // previous tile's epilogue unit u in tap u + 1 (the z loads had a tap's time to land), its VALU
           // spread between this step's MFMAs
           constexpr bool unit_here = EPI_PREV;
-          const bool with_unit = unit_here && cc == 0 && kq == 0 && t >= 1 && t - 1 < (WIDE ? NF : 2 * NF);
+          const bool with_unit = unit_here && cc == 0 && kq == 0 && t >= 1 && t - 1 < 2 * NF;
           if (with_unit) {
-            const int u = t - 1, mf = u & 1;
-            if constexpr (WIDE) {   // pair u: units (u & 1, 2 (u >> 1)) and (u & 1, 2 (u >> 1) + 1)
-              const int nf = 2 * (u >> 1);
-              epi_pair(mf, nf, accp[mf][nf], accp[mf][nf + 1], zreg[mf][nf], zreg[mf][nf + 1], mrowp);
+            const int u = t - 1;
+            if constexpr (WIDE) {
+              // pair p = u >> 1 = units (p & 1, 2 (p >> 1)) and (p & 1, 2 (p >> 1) + 1), its two halves in
+              // consecutive taps (the per-tap VALU of the narrow form): the first unit's quad is held in
+              // registers, the second tap joins it with its own and stores 16 B
+              const int p = u >> 1, mf = p & 1, nf = 2 * (p >> 1);
+              if ((u & 1) == 0) {
+                pend = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp));
+              } else {
+                epi_join(mf, nf, pend, __builtin_bit_cast(v2u32_h, epi_vals(mf, nf + 1, accp[mf][nf + 1],
+                                                                            zreg[mf][nf + 1], mrowp)), mrowp);
+              }
             } else {
-              const int nf = u >> 1;
+              const int mf = u & 1, nf = u >> 1;
               epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
             }
           }
@@ -680,14 +692,14 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     const int pm = option("halop_pipe", 1);
     const bool pipe = !bnr && !maskepi && !dropepi && (pm == 2 || (pm == 1 && one_chunk));
     const int epi = bnr ? 0 : dropepi ? 5 : maskepi ? 4 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
-    // WIDE (option halop_wide: 0 off, 1 the tile-serial forms, 2 every form): 16-B stores of channel-quad
-    // pairs when every 8-channel run of the store is wholly inside or outside its limit. Not the BN-backward
-    // reduction forms (two units' z quads and constants at once spill) and by default not the pipelined
-    // ones (a pair unit between two taps' MFMAs: level-0 64->64 forward with statistics -5 %); the two-chunk
-    // forward with statistics +4 % (profiles/r03_halop_wide_ab.txt)
-    const int wm = option("halop_wide", 1);
-    const bool wide = !bnr && (wm == 2 || (wm == 1 && !pipe)) && a.Nout % 8 == 0 &&
-                      (a.out_mode != 2 || a.split_c % 8 == 0);
+    // WIDE (option halop_wide: 0 off, 1 the tile-serial forms, 2 every form, 3 every form but the pipelined
+    // ones with statistics): 16-B stores of channel-quad pairs when every 8-channel run of the store is wholly
+    // inside or outside its limit. Not the BN-backward reduction forms (two units' z quads and constants at
+    // once spill). Measured (profiles/r03_halop_wide_ab.txt): two-chunk forward with statistics +4 %, one-chunk
+    // pipelined forward +6 %, one-chunk pipelined forward with statistics -2..-5 % (kept narrow)
+    const int wm = option("halop_wide", 3);
+    const bool wide = !bnr && (wm == 2 || (wm == 1 && !pipe) || (wm == 3 && !(pipe && (epi == 1 || epi == 3)))) &&
+                      a.Nout % 8 == 0 && (a.out_mode != 2 || a.split_c % 8 == 0);
     adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
                     pipe ? "true" : "false", epi, wide ? "true" : "false");
 #define HALOP_LAUNCH_W(NCH_, BN_, W_)                                                                       \

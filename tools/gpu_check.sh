@@ -78,6 +78,11 @@ for s in $STEPS; do
           -k "cin8" > gpurun_out/cin8w_tests.log 2>&1 &&
         timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats --layers "L0 in8" \
           --variants "cin8_wide=0;cin8_wide=1" > gpurun_out/cin8w_kernels.log 2>&1 ;;
+    hpipe) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
+          -k "halop or halo_ or two_chunks" > gpurun_out/hpipe_tests.log 2>&1 &&
+        timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L0 64" \
+          --variants "halop_wide=1;halop_wide=2" > gpurun_out/hpipe_kernels.log 2>&1 &&
+        timeout -k 10 300 python tools/ab_step.py --variant opt --opts "halop_wide=1;halop_wide=2" > gpurun_out/hpipe_ab.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
