@@ -764,7 +764,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
       else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
-      P_BAR();   // stage cs landed for every wave, and nobody reads the stage being refilled any more
+      // (timing-only ablation, fwd_debug bit 9: no barrier -- the stages race, the values are garbage)
+      if (!(a.debug_flags & 512)) P_BAR();   // stage cs landed for every wave, nobody reads the stage being refilled
       if constexpr (ZALL) {
         if (!zissued && lk > k) {   // the loader is past this tile: z before the next tile's first stage
           load_zall(m0c);
