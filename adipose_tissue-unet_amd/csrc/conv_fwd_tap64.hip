@@ -264,6 +264,40 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   // cluster, so one wave of each SIMD multiplies while the other issues
   constexpr int NW = WM * WN;
   const bool late = a.stagger && NW == 8 && ((__builtin_amdgcn_readfirstlane(wave) >> 2) & 1);
+  // KPIPE (option tap64_kpipe): the step's barrier sits in the middle of the previous step. After its third
+  // MFMA cluster a wave has read all of stage t it will read (B half 0 was preloaded), so there it waits for
+  // stage t + 1 (issued one step earlier), passes the barrier while that cluster's MFMAs run, refills stage t
+  // with step t + 2, issues the fourth cluster and preloads stage t + 1's B half 0 behind it. The same
+  // fragments and MFMA order: bit-identical.
+  if (a.kpipe) {
+    auto issue_step = [&](int b_) {
+      const Kt kk = kinfo();
+      issueA(0, kk, b_); issueB(0, kk, b_); issueB(1, kk, b_); issueA(1, kk, b_);
+    };
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    T64_BAR();   // stage 0 landed for every wave
+    if (nk > 1) issue_step(1);
+    readB(0, 0, fb0);
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      readA(buf, 0, fa);
+      mma(fa, fb0, 0, 0);
+      readB(buf, 1, fb1);
+      mma(fa, fb1, 0, 1);
+      readA(buf, 1, fa);
+      mma(fa, fb1, 1, 1);
+      if (t + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (only step t + 1 is in flight)
+        T64_BAR();   // stage t read by every wave; stage t + 1 landed
+        if (!late && t + 2 < nk) issue_step(buf);
+      }
+      mma(fa, fb0, 1, 0);
+      if (t + 1 < nk) {
+        readB(buf ^ 1, 0, fb0);
+        if (late && t + 2 < nk) issue_step(buf);
+      }
+    }
+  } else
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -422,6 +456,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   // the persistent kernel for the 256x256 and 256x128 tiles (BNR launches: option tap64p_bnr)
   if ((cfg == 0 || cfg == 1) && !a.f8 && !a.f32 && (!a.bnr_z || option("tap64p_bnr", 1)) && launch_fwd_tap64p(a, s, cfg))
     return 1;
+  a.kpipe = option("tap64_kpipe", 0);   // (the persistent launch above reads its own option into kpipe)
   if (a.f32 && cfg == 0) cfg = 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);

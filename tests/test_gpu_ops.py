@@ -231,6 +231,56 @@ def test_tap64p_halo_matches(mode, grid, tile, wide):
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
 
 
+@pytest.mark.parametrize("tile", [256, 128], ids=["256x256x2", "256x128x3"])
+@pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
+@pytest.mark.parametrize("mode", ["one_chunk", "concat", "ragged_n", "split", "up2", "deep"])
+def test_tap64p_kpipe_matches(mode, grid, tile):
+    """Halo forms of the persistent forward with the software-pipelined K loop (option tap64p_kpipe=1: the
+    step's barrier in the middle of the previous step, the refill issued there, the next step's first B
+    fragments preloaded behind the fourth MFMA cluster) against the default loop: the same K order and
+    fragments, so the stored outputs are identical and the BatchNorm sums agree to f32 order. 3 / 7-block
+    grids walk many tiles (tile-boundary preload after the epilogue, counted waits with epilogues in the
+    window); 'deep' has 4 input chunks (halo ring turns)."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(19)
+    N, H, W_ = 2, 32, 64
+    parts = {"one_chunk": [64], "concat": [64, 128], "ragged_n": [128], "split": [128, 64], "up2": [192],
+             "deep": [256]}[mode]
+    nout = {"ragged_n": 320}.get(mode, 256)
+    if tile == 128:
+        nout = {"ragged_n": 192}.get(mode, 128 if mode != "split" else 256)
+    up = mode == "up2"
+    cin = sum(parts)
+    srcs = [torch.randn(N, H // (2 if up else 1), W_ // (2 if up else 1), c, generator=g).to(DEV, dt) for c in parts]
+    Wt = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV)
+    res = []
+    for kp in (1, 0):
+        outs = [torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)]
+        kw = dict(srcB=srcs[1] if len(srcs) > 1 else None, bias=bias, relu=mode != "split", up=up)
+        if mode == "split":
+            outs = [torch.zeros(N, H, W_, 128, dtype=dt, device=DEV), torch.zeros(N, H, W_, nout - 128, dtype=dt, device=DEV)]
+            kw.update(out_mode=2, out2=outs[1], split_c=128)
+        st = torch.zeros(2, nout, device=DEV)
+        opts = dict(fwd_tap64=2 if tile == 256 else 3, fwd_halo=0, fwd_w4=0, tap64p_kpipe=kp)
+        if grid:
+            opts["tap64_persist_grid"] = grid
+        for k_, v_ in opts.items():
+            ops.set_option(k_, v_)
+        try:
+            ops.conv_fwd(srcs[0], Wt, nout, out=outs[0], bn_stats=(st[0], st[1]), **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for k_ in opts:
+                ops.set_option(k_, None)
+        assert kname.startswith("igemm_fwd_tap64p_kernel<256, %d, %d, false, true, false" % (tile, 2 if tile == 256 else 3)), kname
+        res.append((torch.cat(outs, -1), st.double()))
+    (y1, s1), (y0, s0) = res
+    assert torch.equal(y1, y0), (y1.double() - y0.double()).abs().max().item()
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
 @pytest.mark.parametrize("mode", ["one_chunk", "concat", "ragged_n", "split", "up2"])
 def test_tap64p_wreg_matches_dma(mode, grid):
@@ -570,6 +620,65 @@ def test_tap64_persistent_matches(mode, grid, cfg, wide):
     for a_, b_ in zip(res[0][0], res[1][0]):
         assert torch.equal(a_, b_)
     assert relerr(res[1][1], res[0][1]) < 1e-5
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4], ids=["256x256", "256x128", "512x64"])
+@pytest.mark.parametrize("mode", ["plain", "concat", "bnr", "convt_dgrad", "f32"])
+def test_tap64_kpipe_matches(mode, cfg):
+    """Non-persistent tap64 kernel with the software-pipelined K loop (option tap64_kpipe=1: the barrier in
+    the middle of the previous step, the refill of step t + 2 issued there, B half 0 of the next step
+    preloaded behind the fourth MFMA cluster) against the default loop: bit-identical outputs and equal
+    BatchNorm sums (statistics or the fused BN-backward reduction); bf16 and exact-f32 forms."""
+    g = torch.Generator().manual_seed(23)
+    dt = torch.float32 if mode == "f32" else torch.bfloat16
+    kw, bnr = {}, None
+    if mode != "convt_dgrad":
+        N, S = 2, 23
+        parts = [64, 128] if mode == "concat" else ([64] if mode == "f32" else [128])
+        cin = sum(parts)
+        nout = 256 if mode != "plain" else 320
+        srcs = [torch.randn(N, S, S, c, generator=g).to(DEV, dt) for c in parts]
+        W = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+        args = (srcs[0], W, nout)
+        if len(srcs) > 1:
+            kw["srcB"] = srcs[1]
+        out_shape = (N, S, S, nout)
+        if mode == "bnr":
+            z = torch.randn(N, S, S, nout, generator=g).to(DEV, dt)
+            vec = [(torch.rand(nout, generator=g) + 0.5).to(DEV) for _ in range(4)]
+            bnr = (z, vec[0], vec[1] - 1.0, vec[2] - 1.0, vec[3])
+        else:
+            kw.update(bias=torch.randn(nout, generator=g).to(DEV), relu=True)
+        stats_c = nout
+    else:   # ConvTranspose data gradient: stride-2 4-tap gather over the 2x-resolution gradient
+        N, S, cin, cs = 2, 21, 256, 64
+        dt_ = torch.randn(N, 2 * S, 2 * S, cs, generator=g).to(DEV, dt)
+        W = (torch.randn(cin, 4 * cs, generator=g) * 0.05).to(DEV, dt)
+        args = (dt_, W, cin)
+        out_shape = (N, S, S, cin)
+        kw.update(kh=2, kw=2, dil=1, pad=0, stride=2, Ho=S, Wo=S)
+        stats_c = cin
+    res = []
+    for kp in (1, 0):
+        out = torch.zeros(out_shape, dtype=dt, device=DEV)
+        st = torch.zeros(2, stats_c, device=DEV)
+        opts = dict(tap64_persist=0, fwd_tap64=cfg, fwd_halo=0, tap64_kpipe=kp)
+        for k_, v_ in opts.items():
+            ops.set_option(k_, v_)
+        try:
+            if bnr is not None:
+                ops.conv_fwd(*args, out=out, bn_reduce=bnr + (st[1], st[0]), **kw)
+            else:
+                ops.conv_fwd(*args, out=out, bn_stats=(st[0], st[1]), **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for k_ in opts:
+                ops.set_option(k_, None)
+        assert kname.startswith("igemm_fwd_tap64_kernel<"), kname
+        res.append((out.clone(), st.clone()))
+    assert torch.equal(res[0][0], res[1][0]), (res[0][0].double() - res[1][0].double()).abs().max().item()
+    assert relerr(res[0][1], res[1][1]) < 1e-5
 
 
 def test_halo_fused_epilogues():

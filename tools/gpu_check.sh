@@ -85,6 +85,13 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "halop_wide=1;halop_wide=2" > gpurun_out/hpipe_ab.log 2>&1 ;;
     barab) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd --layers "L2 256,L3 512->512,L4 1024->1024" \
           --variants "fwd_debug=0;fwd_debug=512;fwd_debug=32;fwd_debug=544;fwd_debug=16;fwd_debug=560" > gpurun_out/barab_kernels.log 2>&1 ;;
+    kpipe) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
+          -k "kpipe or tap64p_halo or tap64_persistent or tap64_matches or f32" > gpurun_out/kpipe_tests.log 2>&1 &&
+        timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L2 256,L3 512->512,L4 1024->1024,L1 256" \
+          --variants "tap64p_kpipe=0;tap64p_kpipe=1" > gpurun_out/kpipe_kernels.log 2>&1 &&
+        timeout -k 10 300 python tools/bench_kernels.py --kinds bnr --layers "L2 256,L3 512->512,L4 1024->1024" \
+          --variants "tap64_kpipe=0;tap64_kpipe=1" > gpurun_out/kpipe_bnr_kernels.log 2>&1 &&
+        timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_kpipe=0,tap64_kpipe=0;tap64p_kpipe=1,tap64_kpipe=1" > gpurun_out/kpipe_ab.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
