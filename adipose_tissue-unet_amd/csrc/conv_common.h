@@ -38,7 +38,7 @@ struct FwdArgs {
   int out_f8;
   int stagger;           // persistent forward: waves 4-7 issue their LDS-DMA after the first MFMA cluster
   int wide_st;           // persistent forward: 16-B epilogue stores (channel pairs joined by permlane16_swap)
-  int kpipe;             // persistent halo forward: mid-step barrier, next step's first fragments preloaded
+  int kpipe;             // tap64 kernel: mid-step barrier, next step's B half 0 preloaded (option tap64_kpipe)
   int debug_flags;       // timing-only ablations (option "fwd_debug"): bit1 skips the BN-statistics atomics
   float* stat;           // BatchNorm accumulator replicas (adp::stat_scratch) for bn_sum / bnr_* launches
   int defer_fold;        // bn_sum launch whose replica sums adp_bn_finalize_fold adds in (adp_conv_desc)

@@ -456,7 +456,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   // the persistent kernel for the 256x256 and 256x128 tiles (BNR launches: option tap64p_bnr)
   if ((cfg == 0 || cfg == 1) && !a.f8 && !a.f32 && (!a.bnr_z || option("tap64p_bnr", 1)) && launch_fwd_tap64p(a, s, cfg))
     return 1;
-  a.kpipe = option("tap64_kpipe", 0);   // (the persistent launch above reads its own option into kpipe)
+  a.kpipe = option("tap64_kpipe", 0);   // (opt-in: +1-1.5 % on the BN-backward data gradients, profiles/r03_kpipe_ab.txt)
   if (a.f32 && cfg == 0) cfg = 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);

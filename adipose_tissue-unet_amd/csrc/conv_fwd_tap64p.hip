@@ -715,100 +715,6 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   }
   if constexpr (WREG) load_w(0);   // (the first load_next stores them into stage 0)
   const int total = mine * nk;
-  // ---- KPIPE (halo forms, option tap64p_kpipe): the step's barrier moves from the top of step gs to the
-  // middle of step gs - 1. After its third MFMA cluster a wave has read everything of stage cs it will read
-  // (the B halves; A comes from the halo slot), so there it waits for the NEXT step's stage, passes the
-  // barrier (the third cluster's MFMAs still running: the barrier latency hides behind them), refills the
-  // freed stage cs (the loader now NST steps ahead: the prologue fills all NST stages), issues its fourth
-  // cluster and then preloads the next step's first B fragments, whose LDS latency hides behind that
-  // cluster (A too would hold 48 more registers across the fourth cluster: spills). The same MFMAs, fragments and K order: bit-identical outputs. The wait counts carry over with
-  // the waited step s = gs + 1, except that an epilogue is younger than the stage of s when it ended a tile
-  // at step >= s - NST (it follows the refill of the step that ended it).
-  bool kp_done = false;
-  if constexpr (HALO && !WREG && !F8) {   // (fp8: its operand registers leave no room, it would spill)
-    if (a.kpipe) {
-      kp_done = true;
-      int kl_epi = -NST - 1;   // step of the latest epilogue
-      auto kp_wait = [&](int s_) {   // this wave's pieces of the stage of step s_ landed
-        if (a.debug_flags & 64) {
-        } else if (s_ + NST - 2 >= total) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (kl_epi >= s_ - NST) {
-          if (wide) {
-            if (NST == 2 && hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W + 1 < 63 ? VM_EPI_W + 1 : 63) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W) : "memory");
-          } else if (NST == 2 && hg_last) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI + 1 < 63 ? VM_EPI + 1 : 63) : "memory");
-          } else {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
-          }
-        } else if (NST == 2 && hg_last) {
-          asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
-        }
-      };
-      auto set_tap = [&](int k_, int t_) {
-        const int c = t_ / 9, tp = t_ - 9 * c;
-        hslot = (k_ * nch + c) & 1;
-        hdy = tp / 3;
-        hdx = tp - 3 * hdy;
-      };
-#pragma unroll
-      for (int i = 0; i < NST; ++i) load_next();
-      int gs = 0, cs = 0;
-      kp_wait(0);
-      if (!(a.debug_flags & 512)) P_BAR();
-      readB(cs, 0, fb0);
-      for (int k = 0; k < mine; ++k) {
-        const int m0c = tile_m0(k);
-#pragma unroll
-        for (int i = 0; i < 2 * MIQ; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int t = 0; t < nk; ++t, ++gs) {
-          set_tap(k, t);
-          rA(cs, 0);
-          mma(fa, fb0, 0, 0);
-          readB(cs, 1, fb1);
-          mma(fa, fb1, 0, 1);
-          rA(cs, 1);
-          mma(fa, fb1, 1, 1);
-          const bool more = gs + 1 < total;
-          if (more) {
-            kp_wait(gs + 1);
-            if (!(a.debug_flags & 512)) P_BAR();   // stage cs read by every wave; the next stage landed
-            if (!late) load_next();
-          }
-          mma(fa, fb0, 1, 0);
-          const int ncs = cs == NST - 1 ? 0 : cs + 1;
-          if (more) {
-            // (at a tile's last step the preload follows the epilogue: fragments held across it would spill)
-            if (t + 1 < nk) readB(ncs, 0, fb0);
-            if (late) load_next();
-          }
-          cs = ncs;
-        }
-        kl_epi = gs - 1;
-        auto preload_next_tile = [&]() {
-          if (k + 1 < mine) readB(cs, 0, fb0);
-        };
-        if (a.debug_flags & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue
-#pragma unroll
-          for (int i = 0; i < 2 * MIQ; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-          kl_epi = -NST - 1;
-          preload_next_tile();
-          continue;
-        }
-        if (wide) epilogue_wide(m0c);
-        else epilogue(m0c);
-        preload_next_tile();
-      }
-    }
-  }
-  if (!kp_done) {
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i) load_next();
   int gs = 0, cs = 0, last_epi = -NST;   // step, its stage, step of the latest epilogue
@@ -883,7 +789,6 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     if (wide) epilogue_wide(m0c);
     else epilogue(m0c);
   }
-  }
 
   // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
   if (!stats || (a.debug_flags & 2)) return;
@@ -936,7 +841,8 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   a.stagger = option("tap64p_stagger", 1);
   // 16-B epilogue stores (bf16, no BN-backward reduction; whole 16-channel groups, split on 32 channels):
   // level 2 forward +6 %, level 3 +3 %, step -1.4 %, bit-identical (profiles/r03_wide_store_ab.txt)
-  a.kpipe = option("tap64p_kpipe", 0);
+  // (a software-pipelined K loop -- barrier in the middle of the previous step, B half 0 preloaded -- measured
+  //  1.5-5 % slower here and was removed: profiles/r03_kpipe_ab.txt)
   a.wide_st = option("tap64p_wide", 1) && !a.f8 && !a.bnr_z && a.Nout % 16 == 0 &&
               (a.out_mode != 2 || a.split_c % 32 == 0);
   int cfg = option("tap64p_cfg", 0);

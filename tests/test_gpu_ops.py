@@ -231,56 +231,6 @@ def test_tap64p_halo_matches(mode, grid, tile, wide):
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
 
 
-@pytest.mark.parametrize("tile", [256, 128], ids=["256x256x2", "256x128x3"])
-@pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
-@pytest.mark.parametrize("mode", ["one_chunk", "concat", "ragged_n", "split", "up2", "deep"])
-def test_tap64p_kpipe_matches(mode, grid, tile):
-    """Halo forms of the persistent forward with the software-pipelined K loop (option tap64p_kpipe=1: the
-    step's barrier in the middle of the previous step, the refill issued there, the next step's first B
-    fragments preloaded behind the fourth MFMA cluster) against the default loop: the same K order and
-    fragments, so the stored outputs are identical and the BatchNorm sums agree to f32 order. 3 / 7-block
-    grids walk many tiles (tile-boundary preload after the epilogue, counted waits with epilogues in the
-    window); 'deep' has 4 input chunks (halo ring turns)."""
-    dt = torch.bfloat16
-    g = torch.Generator().manual_seed(19)
-    N, H, W_ = 2, 32, 64
-    parts = {"one_chunk": [64], "concat": [64, 128], "ragged_n": [128], "split": [128, 64], "up2": [192],
-             "deep": [256]}[mode]
-    nout = {"ragged_n": 320}.get(mode, 256)
-    if tile == 128:
-        nout = {"ragged_n": 192}.get(mode, 128 if mode != "split" else 256)
-    up = mode == "up2"
-    cin = sum(parts)
-    srcs = [torch.randn(N, H // (2 if up else 1), W_ // (2 if up else 1), c, generator=g).to(DEV, dt) for c in parts]
-    Wt = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
-    bias = torch.randn(nout, generator=g).to(DEV)
-    res = []
-    for kp in (1, 0):
-        outs = [torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)]
-        kw = dict(srcB=srcs[1] if len(srcs) > 1 else None, bias=bias, relu=mode != "split", up=up)
-        if mode == "split":
-            outs = [torch.zeros(N, H, W_, 128, dtype=dt, device=DEV), torch.zeros(N, H, W_, nout - 128, dtype=dt, device=DEV)]
-            kw.update(out_mode=2, out2=outs[1], split_c=128)
-        st = torch.zeros(2, nout, device=DEV)
-        opts = dict(fwd_tap64=2 if tile == 256 else 3, fwd_halo=0, fwd_w4=0, tap64p_kpipe=kp)
-        if grid:
-            opts["tap64_persist_grid"] = grid
-        for k_, v_ in opts.items():
-            ops.set_option(k_, v_)
-        try:
-            ops.conv_fwd(srcs[0], Wt, nout, out=outs[0], bn_stats=(st[0], st[1]), **kw)
-            torch.cuda.synchronize()
-            kname = _lib.lib().adp_last_kernel().decode()
-        finally:
-            for k_ in opts:
-                ops.set_option(k_, None)
-        assert kname.startswith("igemm_fwd_tap64p_kernel<256, %d, %d, false, true, false" % (tile, 2 if tile == 256 else 3)), kname
-        res.append((torch.cat(outs, -1), st.double()))
-    (y1, s1), (y0, s0) = res
-    assert torch.equal(y1, y0), (y1.double() - y0.double()).abs().max().item()
-    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-3)
-
-
 @pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
 @pytest.mark.parametrize("mode", ["one_chunk", "concat", "ragged_n", "split", "up2"])
 def test_tap64p_wreg_matches_dma(mode, grid):
