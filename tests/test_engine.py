@@ -252,7 +252,12 @@ def test_native_unet_bn_train_step_matches_python(dtype):
         ref = tr.read_metrics()
         got = eng.train_step(x, y, lr, cfg)
         for k in ("loss", "main_out_loss", "main_out_dice_coef", "main_out_binary_accuracy"):
-            assert abs(got[k] - ref[k]) <= tol * max(1.0, abs(ref[k])), (step, k, got[k], ref[k])
+            t_k = tol
+            if k == "main_out_binary_accuracy" and step > 0:
+                # (a count metric: one pixel at the 0.5 threshold is 1 / (B S^2) = 1.2e-4 here; on step-2 weights
+                # that differ at the rounding level a few pixels may sit on the other side of it)
+                t_k = max(tol, 8.0 / (B * S_ * S_))
+            assert abs(got[k] - ref[k]) <= t_k * max(1.0, abs(ref[k])), (step, k, got[k], ref[k])
         if step == 0:
             _compare_grads(eng.get_grads(), {n: net.get_layer_grads(n) for n in net.layers}, dtype, "step-1 grads")
     w_eng = eng.get_weights()
