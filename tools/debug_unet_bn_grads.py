@@ -78,11 +78,14 @@ bufmap = {"enc0_conv1": ("z0_1", "dz_z0_1", "dA_z0_1"), "enc0_conv2": ("z0_2", "
           "dec0_conv1": ("y0_1", "dz_y0_1", "dA_y0_1"), "dec0_conv2": ("y0_2", "dz_y0_2", "y0_2")}
 for name, (zk, dzk, dak) in bufmap.items():
     z = a[zk].cpu()
-    dz = net.buf("g/" + dzk, tuple(a[zk].shape), a[zk].dtype).cpu()
     da = net.buf("g/" + dak, tuple(a[zk].shape), a[zk].dtype).cpu()
+    # (enc0_conv1's dz is not stored with the fused BN-backward weight gradient: nothing reads it)
+    dzs = "n/a"
+    if not (name == "enc0_conv1" and net.fuse_bn_wgrad):
+        dz = net.buf("g/" + dzk, tuple(a[zk].shape), a[zk].dtype).cpu()
+        dzs = f"{rel(dz, inter['z/' + name].grad):.2e}"
     print(name, "z", f"{rel(z, inter['z/' + name].detach()):.2e}",
-          "dA", f"{rel(da, inter['a/' + name].grad):.2e}",
-          "dz", f"{rel(dz, inter['z/' + name].grad):.2e}")
+          "dA", f"{rel(da, inter['a/' + name].grad):.2e}", "dz", dzs)
 for name, ts in W.items():
     got = net.get_layer_grads(name)
     print("grad", name, [f"{rel(gi, t.grad):.2e}" for gi, t in zip(got, ts)])
