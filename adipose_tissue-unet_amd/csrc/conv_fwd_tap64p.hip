@@ -597,17 +597,21 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // 16-B store per (pixel, pair of groups) instead of two 8-B ones, 64 contiguous bytes of a pixel per
   // instruction instead of 32. Needs Nout % 16 == 0 and a split point on a 32-channel boundary (host).
   auto epilogue_wide = [&](int m0) {
-    if constexpr (!BNR && !F8) {
+    if constexpr (!BNR) {
       int tidv = tid;
       asm volatile("" : "+v"(tidv));
       const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
 #pragma unroll
       for (int np = 0; np < 4; np += 2) {
-        float bias[2][4];
+        float bias[2][4], wsc[2][4];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const float4 b4 = p_lds_f4(&cst[0][wc * 64 + (np + j) * 16 + 4 * h4]);
           bias[j][0] = b4.x; bias[j][1] = b4.y; bias[j][2] = b4.z; bias[j][3] = b4.w;
+          if constexpr (F8) {   // the per-column dequantisation scale (bf16 output)
+            const float4 w4 = p_lds_f4(&cst[1][wc * 64 + (np + j) * 16 + 4 * h4]);
+            wsc[j][0] = w4.x; wsc[j][1] = w4.y; wsc[j][2] = w4.z; wsc[j][3] = w4.w;
+          }
         }
         // this lane's 8-channel run after the exchange, and its store target
         const int cw = n0 + wc * 64 + 16 * (np + (h4 & 1)) + 8 * (h4 >> 1);
@@ -632,7 +636,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
             bf16x4 o;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              x[r] = acc[mt][np + j][r] + bias[j][r];
+              x[r] = F8 ? fmaf(acc[mt][np + j][r], wsc[j][r], bias[j][r]) : acc[mt][np + j][r] + bias[j][r];
               if (a.relu) x[r] = fmaxf(x[r], 0.f);
               o[r] = (bf16)x[r];
             }
@@ -674,7 +678,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       }
     }
   };
-  const bool wide = !BNR && !F8 && a.wide_st;
+  const bool wide = !BNR && a.wide_st;   // (fp8: bf16 output only, the launcher checks)
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
@@ -843,7 +847,9 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // level 2 forward +6 %, level 3 +3 %, step -1.4 %, bit-identical (profiles/r03_wide_store_ab.txt)
   // (a software-pipelined K loop -- barrier in the middle of the previous step, B half 0 preloaded -- measured
   //  1.5-5 % slower here and was removed: profiles/r03_kpipe_ab.txt)
-  a.wide_st = option("tap64p_wide", 1) && !a.f8 && !a.bnr_z && a.Nout % 16 == 0 &&
+  // fp8 launches with a bf16 output take them too (option tap64p_wide_f8); fp8 outputs keep 4-B stores
+  a.wide_st = option("tap64p_wide", 1) && (!a.f8 || (option("tap64p_wide_f8", 0) && !a.out_f8)) && !a.bnr_z &&
+              a.Nout % 16 == 0 &&
               (a.out_mode != 2 || a.split_c % 32 == 0);
   int cfg = option("tap64p_cfg", 0);
   if (cfg < 1 || cfg > 3) {

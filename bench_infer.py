@@ -32,6 +32,7 @@ V3_FWD_GFLOP_1024 = 896.3
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--mode", default="wsi", choices=["wsi", "tiles", "fp8"])
+    p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
     p.add_argument("--levels", type=int, default=5, help="unet_bn levels (mode fp8)")
     p.add_argument("--train-steps", type=int, default=60, help="mode fp8: bf16 training steps before the comparison")
     p.add_argument("--gpus", type=int, default=1)
@@ -149,6 +150,8 @@ def main():
     from adipose_amd.data import synthetic_tile, to_gray
     from adipose_amd.nets import AdiposeV3Net
     from adipose_amd.predictor import INFER_CPAD, HipUnetPredictor, SlidingWindowInference
+    for kv in args.opt:
+        ops.set_option(kv.split("=")[0], int(kv.split("=")[1]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

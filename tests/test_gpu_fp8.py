@@ -137,9 +137,10 @@ def test_fp8_persistent_halo_form(cinA, cinB, cout, H, W, relu, kern):
     bias = torch.randn(cout, generator=g) * 0.1
     W8, sc = pack8(Wf)
     outs = []
-    for persist in (1, 0):
+    for persist, wide in ((1, 1), (0, 0), (1, 0)):   # (tap64p_wide_f8: 16-B stores of joined channel quads)
         out = torch.zeros(B, H, W, cout, dtype=torch.bfloat16, device=DEV)
         ops.set_option("tap64p_f8", persist)
+        ops.set_option("tap64p_wide_f8", wide)
         try:
             ops.conv_fwd(xa8.to(DEV), W8, cout, out=out, srcB=None if xb8 is None else xb8.to(DEV),
                          bias=bias.to(DEV), kh=3, kw=3, relu=relu, w_scale=sc)
@@ -147,8 +148,11 @@ def test_fp8_persistent_halo_form(cinA, cinB, cout, H, W, relu, kern):
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
             ops.set_option("tap64p_f8", None)
+            ops.set_option("tap64p_wide_f8", None)
         assert (kname == kern) == bool(persist), kname
         outs.append(out.cpu().float().double())
+    assert torch.equal(outs[0], outs[2])   # wide and 8-B stores: the same values
+    outs = outs[:2]
     x_cat = xa8 if xb8 is None else torch.cat([xa8.float(), xb8.float()], -1).to(F8)
     ref = ref_conv(x_cat, W8, sc, cout, 3, 1, cin, bias=bias, relu=relu)
     for got in outs:
@@ -172,9 +176,10 @@ def test_fp8_convtranspose_pixel_shuffle(cin, cout, H, out_fp8):
     bias = torch.randn(cout, generator=g) * 0.1
     W8, sc = pack8(Wf)
     outs = []
-    for persist in (1, 0):
+    for persist, wide in ((1, 1), (0, 0), (1, 0)):   # (tap64p_wide_f8: bf16 outputs only)
         out = torch.zeros(B, 2 * H, 2 * H, cout, dtype=F8 if out_fp8 else torch.bfloat16, device=DEV)
         ops.set_option("tap64p_f8", persist)
+        ops.set_option("tap64p_wide_f8", wide)
         try:
             ops.conv_fwd(x8.to(DEV), W8, 4 * cout, out=out, bias=bias.to(DEV), kh=1, kw=1, pad=0, out_mode=1,
                          shuffle_c=cout, w_scale=sc)
@@ -182,9 +187,11 @@ def test_fp8_convtranspose_pixel_shuffle(cin, cout, H, out_fp8):
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
             ops.set_option("tap64p_f8", None)
+            ops.set_option("tap64p_wide_f8", None)
         assert kname.startswith("igemm_fwd_tap64p_kernel") == bool(persist), kname
         outs.append(out.cpu())
     assert torch.equal(outs[0].view(torch.uint8), outs[1].view(torch.uint8))
+    assert torch.equal(outs[0].view(torch.uint8), outs[2].view(torch.uint8))
     Wd = W8.float().double().cpu() * sc.double().cpu()[:, None]
     y = torch.einsum("bhwc,nc->bhwn", x8.float().double(), Wd)        # (B,H,W,4*cout)
     ref = torch.zeros(B, 2 * H, 2 * H, cout, dtype=torch.float64)

@@ -94,6 +94,12 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_kpipe=0,tap64_kpipe=0;tap64p_kpipe=1,tap64_kpipe=1" > gpurun_out/kpipe_ab.log 2>&1 ;;
     bnrcfg) timeout -k 10 300 python tools/bench_kernels.py --kinds bnr --layers "L2 256,L3 512->512,L4 1024->1024,L3 1024->512,L1 256" \
           --variants "tap64p_cfg=0;tap64p_cfg=2;tap64_kpipe=1;tap64p_cfg=1,tap64p_bnr=2" > gpurun_out/bnrcfg_kernels.log 2>&1 ;;
+    f8wide) timeout -k 10 400 python -u -m pytest tests/test_gpu_fp8.py -v --timeout 120 --timeout-method thread \
+          > gpurun_out/f8wide_tests.log 2>&1 &&
+        for i in 1 2; do
+          timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_wide_f8=0 > gpurun_out/f8wide_off_$i.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_wide_f8=1 > gpurun_out/f8wide_on_$i.log 2>&1 || exit 1
+        done ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
