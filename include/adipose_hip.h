@@ -113,7 +113,10 @@ const char* adp_source_hash(void);
  * the built-in default. Kernel selection: "conv_fast" (2 = LDS-DMA kernels, default; 1 = register-staged;
  * 0 = generic), "fwd_tap64" / "wgrad_tap64" (0 off, 1 auto, 2+c force tile configuration c),
  * "tap64_bal", "tap64_korder", "wgrad_ra", "wgrad_blocks", "wgrad_min_chunk", "wgrad_glds_tn64";
- * "wgrad_debug" is a timing-only ablation (bit 0 skips the dW atomics: results invalid). */
+ * epilogue store width (round 3, bit-identical either way): "tap64p_wide" (1), "tap64p_wide_f8" (0), "halop_wide"
+ * (0 off, 1 tile-serial forms, 2 all, 3 default: all but the pipelined statistics forms), "cin8_wide" (1);
+ * "wgrad_cin8_bna" (1: the input layer's fused BN-backward weight gradient when dY = NULL), "tap64_kpipe" (0:
+ * mid-step barrier in the tap64 K loop); "wgrad_debug" / "fwd_debug" are timing-only ablations (results invalid). */
 int adp_set_option(const char* name, int value);
 /* Per-launch timing of the conv kernels (bench roofline; no reference counterpart). mode 1: clear the record
  * and start recording a HIP event pair around the MAIN kernel of every adp_conv_fwd / adp_conv_wgrad(_bn)
