@@ -101,6 +101,8 @@ for s in $STEPS; do
           timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_wide_f8=1 > gpurun_out/f8wide_on_$i.log 2>&1 || exit 1
         done ;;
     contention) timeout -k 10 400 python -u tools/contention_probe.py > gpurun_out/contention.log 2>&1 ;;
+    pipe2) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L0 128,L1 128" \
+          --variants "halop_pipe=1;halop_pipe=2;halop_pipe=2,halop_wide=2" > gpurun_out/pipe2_kernels.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
