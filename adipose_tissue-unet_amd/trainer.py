@@ -58,10 +58,14 @@ def dp_row_normaliser(world, batch_local, rows_kept):
 
 
 class GradBuckets:
-    """Bucketed, backward-overlapped SUM all-reduce over the flat gradient buffer."""
+    """Bucketed, backward-overlapped SUM all-reduce over the flat gradient buffer. overlap=False launches every
+    bucket at finish() instead (the same sums): while an RCCL bucket holds CUs, a persistent conv kernel's
+    blocks that find no free CU run after the others, so an overlapped bucket can cost as much as an exposed one
+    (profiles/r03_contention_probe.txt); the switch is there to measure both on a multi-GPU node."""
 
-    def __init__(self, net, bucket_bytes=16 << 20, group=None):
+    def __init__(self, net, bucket_bytes=16 << 20, group=None, overlap=True):
         self.group = group
+        self.overlap = overlap
         self.world = dist.get_world_size(group)
         ps = net.ps
         # layer -> [start, end) span in the flat buffer (a layer's params are contiguous)
@@ -92,6 +96,8 @@ class GradBuckets:
         self.works = []
 
     def ready(self, lname):
+        if not self.overlap:
+            return
         for i, p in enumerate(self.pending):
             if lname in p:
                 p.discard(lname)
@@ -120,7 +126,7 @@ class Trainer:
 
     def __init__(self, net, loss_cfg: LossConfig | None = None, *, optimizer="adam", lr=1e-4, beta1=0.9,
                  beta2=0.999, eps=1e-7, weight_decay=0.01, process_group=None, distributed=None,
-                 bucket_bytes=16 << 20):
+                 bucket_bytes=16 << 20, overlap_allreduce=True):
         self.net = net
         self.cfg = loss_cfg or LossConfig()
         self.opt = optimizer.lower()
@@ -133,7 +139,8 @@ class Trainer:
         self.distributed = dist.is_available() and dist.is_initialized() if distributed is None else distributed
         self.group = process_group
         self.world = dist.get_world_size(process_group) if self.distributed else 1
-        self.buckets = GradBuckets(net, bucket_bytes, process_group) if self.distributed and self.world > 1 else None
+        self.buckets = (GradBuckets(net, bucket_bytes, process_group, overlap=overlap_allreduce)
+                        if self.distributed and self.world > 1 else None)
         self.stats = torch.zeros((3, 8), dtype=torch.float64, device=dev)   # per head: loss_rows sums
         self.lossbuf = torch.zeros(4, dtype=torch.float64, device=dev)
         self._dp = {}

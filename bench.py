@@ -36,6 +36,8 @@ def parse():
     p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
+    p.add_argument("--allreduce", default="overlap", choices=["overlap", "after"],
+                   help="N > 1: gradient buckets all-reduced as the backward completes them (default) or all after it")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="collective backend for N > 1 (nccl = RCCL; gloo only to rehearse the multi-rank plumbing with "
                         "several ranks on one GPU)")
@@ -174,7 +176,7 @@ def main():
         net = AdiposeV3Net(B, S, dtype=args.dtype, device=dev, seed=865, cpad=args.cpad)
         cfg = LossConfig()
         C = None
-    tr = Trainer(net, cfg, lr=1e-4, distributed=world > 1)
+    tr = Trainer(net, cfg, lr=1e-4, distributed=world > 1, overlap_allreduce=args.allreduce == "overlap")
 
     # synthetic histology tiles, resident in HBM before timing (per-rank shard of the data)
     xs, ys = synthetic_batch(B, S, channels=3, seed=865 + rank)
@@ -263,7 +265,8 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (seeded histology-like tiles, resident in HBM)",
         "config": {"workload": wl, "preset": args.preset, "levels": args.levels if args.preset == "unet_bn" else 4,
-                   "tile": S, "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}"},
+                   "tile": S, "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}",
+                   "allreduce": args.allreduce if world > 1 else None},
         "train_loss": round(met["loss"], 5), "dice_val": round(val["main_out_dice_coef"], 5),
         "roofline": roof, "cpu_baseline": cpu,
     }

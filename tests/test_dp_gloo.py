@@ -14,6 +14,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -62,7 +63,7 @@ def run_ranks(fn, world=WORLD):
 
 
 # ------------------------------------------------------------------------------- grad buckets
-def _buckets_fn(rank, world):
+def _buckets_fn(rank, world, overlap=True):
     import _adipose_pkg  # noqa: F401
     from adipose_amd.nets import ParamStore
     from adipose_amd.trainer import GradBuckets
@@ -80,19 +81,32 @@ def _buckets_fn(rank, world):
     g = torch.Generator().manual_seed(100 + rank)
     net.ps.grad.copy_(torch.randn(net.ps.total, generator=g))
     before = net.ps.grad.clone()
-    gb = GradBuckets(net, bucket_bytes=16 << 10)    # small buckets -> several launches
+    gb = GradBuckets(net, bucket_bytes=16 << 10, overlap=overlap)    # small buckets -> several launches
     gb.begin()
     for name in reversed(list(sizes)):
         if name != "l2":                              # l2's hook never fires: finish() must cover it
             gb.ready(name)
+    launched_before_finish = sum(gb.launched)
     gb.finish()
-    return {"before": before, "after": net.ps.grad.clone(), "nbuckets": len(gb.buckets)}
+    return {"before": before, "after": net.ps.grad.clone(), "nbuckets": len(gb.buckets),
+            "launched_before_finish": launched_before_finish}
 
 
-def test_grad_buckets_sum_allreduce():
-    res = run_ranks(_buckets_fn)
+def _buckets_after_fn(rank, world):
+    return _buckets_fn(rank, world, overlap=False)
+
+
+@pytest.mark.parametrize("fn", [_buckets_fn, _buckets_after_fn], ids=["overlap", "after_backward"])
+def test_grad_buckets_sum_allreduce(fn):
+    """Bucketed SUM all-reduce: launched from the backward's ready-hooks (overlap) or all at finish()
+    (GradBuckets(overlap=False), bench.py --allreduce after): the same sums either way."""
+    res = run_ranks(fn)
     total = sum(res[r]["before"] for r in range(WORLD))
     assert res[0]["nbuckets"] > 2
+    if fn is _buckets_after_fn:
+        assert res[0]["launched_before_finish"] == 0
+    else:
+        assert res[0]["launched_before_finish"] > 0
     for r in range(WORLD):
         np.testing.assert_allclose(res[r]["after"], total, rtol=0, atol=1e-5)
 
