@@ -91,12 +91,13 @@ def _snapshot(net):
             "weights": {n: [a.copy() for a in net.get_layer_weights(n)] for n in names}}
 
 
-def _train_fn(rank, world):
+def _train_fn(rank, world, overlap=True):
     from adipose_amd.trainer import LossConfig, Trainer
     x, y = _data()
     sl = slice(rank * B_LOCAL, (rank + 1) * B_LOCAL)
     net = _net(B_LOCAL)
-    tr = Trainer(net, LossConfig(), lr=LR, distributed=True, bucket_bytes=1 << 20)   # several buckets
+    tr = Trainer(net, LossConfig(), lr=LR, distributed=True, bucket_bytes=1 << 20,   # several buckets
+                 overlap_allreduce=overlap)
     assert tr.buckets is not None and len(tr.buckets.buckets) > 2
     tr.train_step(torch.from_numpy(x[sl]).cuda(), torch.from_numpy(y[sl]).cuda())
     met = tr.read_metrics()
@@ -106,9 +107,14 @@ def _train_fn(rank, world):
     return out
 
 
-def test_dp_train_step_world2_matches_single_device_batch():
+def _train_after_fn(rank, world):
+    return _train_fn(rank, world, overlap=False)
+
+
+@pytest.mark.parametrize("fn", [_train_fn, _train_after_fn], ids=["overlap", "after_backward"])
+def test_dp_train_step_world2_matches_single_device_batch(fn):
     from adipose_amd.trainer import LossConfig, Trainer
-    res = run_ranks(_train_fn)
+    res = run_ranks(fn)
     x, y = _data()
     net = _net(WORLD * B_LOCAL)
     tr = Trainer(net, LossConfig(), lr=LR)

@@ -109,6 +109,8 @@ for s in $STEPS; do
     dp2after) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29518 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline --allreduce after \
            > gpurun_out/bench_dp2_gloo_after.log 2>&1 ;;
+    dptests) timeout -k 10 400 python -u -m pytest tests/test_gpu_dp.py -v --timeout 200 --timeout-method thread \
+           > gpurun_out/dp_tests.log 2>&1 ;;
     diag) timeout -k 10 300 python -u tools/diag_bn_determinism.py > gpurun_out/diag_bn.log 2>&1 &&
           timeout -k 10 300 python -u tools/diag_f32_freeze.py > gpurun_out/diag_freeze.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
