@@ -24,6 +24,7 @@ def main():
     p.add_argument("--blocks", default="0,8,16,32,64")
     p.add_argument("--spin-ms", type=float, default=20.0)
     p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--opt", action="append", default=[], help="name=value native option")
     args = p.parse_args()
     import numpy as np
     import torch
@@ -33,6 +34,9 @@ def main():
     from adipose_amd.nets import UNetBN
     from adipose_amd.trainer import LossConfig, Trainer
 
+    from adipose_amd import ops
+    for kv in args.opt:
+        ops.set_option(kv.split("=")[0], int(kv.split("=")[1]))
     spin = ctypes.CDLL(os.path.join(ROOT, "tools", "libspin.so"))
     dev = torch.device("cuda", 0)
     B, S = 4, 1024
@@ -80,6 +84,7 @@ def main():
         res[f"K{k}"] = {"ms": [round(v, 3) for v in times[k]], "min": round(min(times[k]), 3),
                         "extra_ms": round(min(times[k]) - base, 3) if base else None,
                         "cu_share_model_ms": round(res["spin_ms"] * k / 256, 3)}
+    res["opts"] = args.opt
     print(json.dumps(res))
 
 

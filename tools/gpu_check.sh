@@ -103,6 +103,8 @@ for s in $STEPS; do
     contention) timeout -k 10 400 python -u tools/contention_probe.py > gpurun_out/contention.log 2>&1 ;;
     pipe2) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L0 128,L1 128" \
           --variants "halop_pipe=1;halop_pipe=2;halop_pipe=2,halop_wide=2" > gpurun_out/pipe2_kernels.log 2>&1 ;;
+    contention2) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 \
+          --opt tap64_persist_grid=1000000 --opt halo_persist_grid=1000000 > gpurun_out/contention_nonpersist.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
            --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
