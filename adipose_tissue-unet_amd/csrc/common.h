@@ -130,6 +130,11 @@ float* stat_scratch();   // [STAT_REPL][2][STAT_CMAX] f32, or nullptr (error set
 // adp_bn_finalize_fold with the same three may take the replicas next (stat_scratch_fold clears the record)
 int defer_fold_begin(int C, const float* sum, hipStream_t s);
 float* stat_scratch_fold(int C, const float* sum, hipStream_t s);
+int bn_fold_reset(hipStream_t s);   // adp_bn_fold_reset
+// dynamic tile claiming: a zeroed slot of CLAIM_INTS counters for one persistent launch (a ring of CLAIM_SLOTS per
+// device, handed out in turn; a launch leaves its slot zeroed again), or nullptr (error set)
+constexpr int CLAIM_SLOTS = 64, CLAIM_INTS = 64;
+int* claim_slot();
 // per-device growable scratch (slot 0: weight-gradient split partials); growing synchronises the device
 void* scratch(int slot, size_t bytes);
 int stat_fold(int C, float* dst0, float* dst1, hipStream_t s);   // elementwise.hip

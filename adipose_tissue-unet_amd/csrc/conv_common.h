@@ -43,6 +43,7 @@ struct FwdArgs {
   float* stat;           // BatchNorm accumulator replicas (adp::stat_scratch) for bn_sum / bnr_* launches
   int defer_fold;        // bn_sum launch whose replica sums adp_bn_finalize_fold adds in (adp_conv_desc)
   int f32;               // f32 launch on the LDS-DMA tap kernel (32-channel K steps, f32 MFMA)
+  int* claim;            // persistent kernels: dynamic tile claiming counters (adp::claim_slot), nullptr = static lists
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
@@ -133,6 +134,43 @@ ADP_DEV int xcd_remap(int bid, int nwg) {
   int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (bid >> 3);
+}
+
+// ------------------------------------------------ dynamic tile claiming (persistent kernels)
+// A persistent kernel whose blocks walk static tile lists (lin, lin + G, ...) runs ~2x long when a kernel on
+// another stream (RCCL's all-reduce blocks) holds a few CUs: the blocks that find no free CU run their whole
+// list after the others (profiles/r03_contention_probe.txt). With claiming, a block takes its next tile from
+// a per-N-column counter (claim[col], vector atomics at agent scope, one tile ahead of the multiply so the
+// cross-tile prefetch stays), and a block that starts late finds the work taken. claim[nclaim] counts the
+// blocks that are done; the last one re-zeroes the counters, so the next launch on the slot starts from 0.
+// (the prologue's synchronous claim of a block's first two tiles; the atomic optimizer's wave form is fine here)
+ADP_DEV int claim_next2(int* cnt) {
+  return __hip_atomic_fetch_add(cnt, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// In the K loop the claim must not stall: a compiler-visible atomic gets an immediate s_waitcnt vmcnt(0) (the
+// atomic optimizer broadcasts its result at once, and loop-carried copies of a pending result wait too), which
+// drains the LDS-DMA prefetch. claim_issue is the atomic as inline asm (one lane), and claim_publish waits for
+// it with the count of the vector-memory ops issued after it (NYOUNG, exact: a larger count could pass while
+// the atomic is still in flight) and stores the raw value into the LDS ring, all in ONE asm block, in the same
+// loop iteration (no copy of the pending register can exist in between)
+ADP_DEV int claim_issue(int* cnt) {
+  int r;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(r) : "v"(cnt), "v"(1) : "memory");
+  return r;
+}
+template <int NYOUNG>
+ADP_DEV void claim_publish(int* lds, int r) {
+  const unsigned addr = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  asm volatile("s_waitcnt vmcnt(%2)\n\tds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r),
+               "n"(NYOUNG < 63 ? NYOUNG : 0) : "memory");
+}
+// every block calls this exactly once, after its last claim (thread 0; nclaim counters + the done count)
+ADP_DEV void claim_block_done(int* claim, int nclaim, int G) {
+  const int done = __hip_atomic_fetch_add(claim + nclaim, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (done == G - 1) {
+    for (int i = 0; i < nclaim; ++i) __hip_atomic_store(claim + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(claim + nclaim, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // XOR swizzle of the 16-B chunks of a 128-B LDS row (rows of 64 bf16): chunk c of row r is stored at

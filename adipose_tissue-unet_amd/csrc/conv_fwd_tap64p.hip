@@ -51,6 +51,14 @@ __device__ __forceinline__ void p_lds_add(float* p, float v) {
   const unsigned addr = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)p;
   asm volatile("ds_add_f32 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
+// the claimed-tile ring (dynamic claiming): inline-asm LDS read for the same reason (the prefetch stream is
+// in flight whenever the loader reads a tile id)
+__device__ __forceinline__ int p_lds_i32(const int* p) {
+  int r;
+  const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
 
 #define P_BAR()                            \
   do {                                     \
@@ -74,7 +82,8 @@ __device__ __forceinline__ void p_lds_add(float* p, float v) {
 constexpr int P_HROWS = 340;   // 10 x 34 halo pixels of an 8 x 32 patch
 template <int BM, int BN, int NST, bool BNR, bool HALO = false>
 constexpr int tap64p_lds() {
-  return HALO ? NST * BN * 128 + 2 * P_HROWS * 128 + 7 * BN * 4 : NST * (BM + BN) * 128 + 7 * BN * 4;
+  // (+16 B: the ring of claimed tile ids, dynamic claiming)
+  return (HALO ? NST * BN * 128 + 2 * P_HROWS * 128 + 7 * BN * 4 : NST * (BM + BN) * 128 + 7 * BN * 4) + 16;
 }
 __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_halo.hip: conflict-free)
 
@@ -122,6 +131,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   float (*cst)[BN] = reinterpret_cast<float (*)[BN]>(smem + OC);   // epilogue constants:
                                                                   // bias | scale shift mean invstd (BNR)
   float (*sacc)[BN] = reinterpret_cast<float (*)[BN]>(smem + OC + 5 * BN * 4);   // block's BN sums
+  int* ring = reinterpret_cast<int*>(smem + OC + 7 * BN * 4);   // dynamic claiming: tile ids of local tiles k & 3
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WN, wc = wave % WN;
@@ -129,9 +139,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   prio_static<ADP_PRIO_FWD>(wave);
   const int lin = xcd_remap(blockIdx.x, G);
   const int ntiles = a.nblocks;
-  const int mine = lin < ntiles ? (ntiles - lin + G - 1) / G : 0;
-  if (mine == 0) return;   // uniform per block
-  const int n0 = (lin % a.ntile_n) * BN;
+  // tiles: static lists (lin, lin + G, ...: `mine` of them) or claimed one tile ahead from the counter of the
+  // block's N column (dyn, conv_common.h); either way a block keeps one N column
+  // (the fp8 eval forms and the opt-in register-staged form keep static lists: no spare registers there)
+  const bool dyn = !F8 && !WREG && a.claim != nullptr;
+  const int ntn = a.ntile_n, ntm = ntiles / ntn, col = lin % ntn;
+  const int mine = dyn ? 0 : (lin < ntiles ? (ntiles - lin + G - 1) / G : 0);
+  if (!dyn && mine == 0) return;   // uniform per block
+  const int n0 = col * BN;
   const int pos = lane & 7;
   const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
   const int Cin_s = a.CAs + a.CBs;
@@ -149,6 +164,18 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     sacc[1][tid] = 0.f;
   }
   // (ordered before the epilogue by the first K step's barrier)
+  if (dyn) {   // the first two tiles, before anything is staged (claims of one tile then follow in the K loop)
+    if (tid == 0) {
+      const int t = claim_next2(a.claim + col);
+      ring[0] = t;
+      ring[1] = t + 1;
+    }
+    __syncthreads();
+    if (ring[0] >= ntm) {   // (uniform) every tile is taken: a block that started late
+      if (tid == 0) claim_block_done(a.claim, ntn, G);
+      return;
+    }
+  }
 
   const int npix = a.Nimg * a.Hs * a.Ws;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.srcA, 0, npix * a.CAs * ES, P_RSRC3);
@@ -229,8 +256,15 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // tile (p = 32 * patch row + column) is output pixel m0 + (p >> 5) * Wo + (p & 31)
   const int ptx = HALO ? a.Wo / 32 : 1, pty = HALO ? a.Ho / 8 : 1;
   struct PatchO { int img, y0, x0; };
-  auto patch_of = [&](int k) {
-    const int t = (lin + k * G) / a.ntile_n;
+  // tile id (M-tile / patch index) of the block's local tile k, -1 past the end of its work. dyn: the ring slot
+  // was written at the top of the compute step whose stage is the loader's first step of tile k - 1, before
+  // that step's barrier -- ahead of every reader (the loader needs tile k from step NST - 1 of tile k - 1 on)
+  auto tile_id = [&](int k) -> int {
+    if (!dyn) return k < mine ? lin / ntn + k * (G / ntn) : -1;
+    const int t = __builtin_amdgcn_readfirstlane(p_lds_i32(ring + (k & 3)));   // (uniform: scalar registers)
+    return t < ntm ? t : -1;   // (a claim past the last tile: the work is taken)
+  };
+  auto patch_t = [&](int t) {
     PatchO P;
     P.x0 = (t % ptx) * 32;
     const int r = t / ptx;
@@ -238,12 +272,12 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     P.img = r / pty;
     return P;
   };
-  auto tile_m0 = [&](int k) {
+  auto m0_of = [&](int t) {   // first output pixel of tile t
     if constexpr (HALO) {
-      const PatchO P = patch_of(k);
+      const PatchO P = patch_t(t);
       return (P.img * a.Ho + P.y0) * a.Wo + P.x0;
     }
-    return ((lin + k * G) / a.ntile_n) * BM;
+    return t * BM;
   };
   auto pix = [&](int m0, int p) { return HALO ? m0 + (p >> 5) * a.Wo + (p & 31) : m0 + p; };
   const bool no_dma = (a.debug_flags & 32) != 0;   // timing-only ablation (fwd_debug bit 5): the K loop
@@ -252,11 +286,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // HALO: one 16-B group g of the halo of chunk c of tile k into slot `slot`; returns whether this wave
   // issued an instruction (the last group covers 160 of 512 threads: waves 3-7 skip it)
   const int nch = Cin_s / KSTEP;
-  auto issue_halo = [&](int k, int c, int g, int slot) {
+  auto issue_halo = [&](int t, int c, int g, int slot) {
     const int idx = g * NTH + tid;
     if (g == GH - 1 && __builtin_amdgcn_readfirstlane(g * NTH + wave * 64) >= P_HROWS * 8) return false;
     if (idx < P_HROWS * 8) {
-      const PatchO P = patch_of(k);
+      const PatchO P = patch_t(t);
       const int hr = idx >> 3, hp = idx & 7;
       // (yi, xi) in the conv's input grid, which is the source upsampled x up (nearest: source pixel
       // (yi >> 1, xi >> 1) for up = 2, the UpSampling2D of train_adipose_unet_v3.py:691 folded in)
@@ -273,9 +307,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     return true;
   };
   // WREG: the halo group g of chunk c of tile k through a register (ok = false: an out-of-range load, 0)
-  auto load_halo_reg = [&](int k, int c, int g, bool ok) -> v4u32_t {
+  auto load_halo_reg = [&](int t, int c, int g, bool ok) -> v4u32_t {
     const int idx = g * NTH + tid;
-    const PatchO P = patch_of(k);
+    const PatchO P = patch_t(t);
     const int hr = idx >> 3, hp = idx & 7;
     const int yi = P.y0 - 1 + hr / 34, xi = P.x0 - 1 + hr % 34;
     const int ci = c * KSTEP;
@@ -320,33 +354,42 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
                                       lane * 16) = wst[h][i];
     }
   };
+  // the loader's bookkeeping after issuing stream step lsteps = (tile lk, step lt)
+  int lsteps = 0, lk_tile = -1;
+  auto advance = [&]() {
+    ++lsteps;
+    ls = ls == NST - 1 ? 0 : ls + 1;
+    if (++lt == nk) { lt = 0; ++lk; }
+  };
   auto load_next_halo = [&]() {
     hg_last = false;
-    if (lk >= mine) return;
+    if (lt == 0) lk_tile = tile_id(lk);
+    if (lk_tile < 0) return;   // stream exhausted (uniform)
     if (no_dma && nissued >= NST - 1) {   // (timing-only ablation, fwd_debug bit 5: bookkeeping only)
-      ls = ls == NST - 1 ? 0 : ls + 1;
-      if (++lt == nk) { lt = 0; ++lk; }
+      advance();
       return;
     }
     ++nissued;
     const int c = lt / 9, tp = lt - 9 * c;
+    // one group of the next chunk of the stream rides on taps NST-1 .. NST-1+GH-1: its tile (the next tile's
+    // at the last chunk; -1 past the end of the block's work) and its slot (e + 1) & 1, e = this chunk's index
+    const bool hwin = tp >= NST - 1 && tp < NST - 1 + GH;
+    const int t2 = !hwin ? -1 : c + 1 < nch ? lk_tile : tile_id(lk + 1);
+    const int nc2 = c + 1 < nch ? c + 1 : 0, e = lk * nch + c;
     if constexpr (WREG) {
       // the halo group loaded at the previous step into its slot (or, if none, into this thread's first
       // weight slot of stage ls, which store_w overwrites next), this step's staged weights into stage ls,
       // then the next halo group (taps NST-1 .. NST-1+GH-1 of a chunk) and the next step's weights into
-      // registers. No LDS-DMA: every wait is the compiler's, on registers.
+      // registers (the next tile's first step after a tile's last: the same rows for every tile). No LDS-DMA:
+      // every wait is the compiler's, on registers.
       store_halo_reg(hpend_g, hpend_slot, hreg, hpend, (unsigned)(ls * STAGE + OB0 + wave * 8 * ROWB + lane * 16));
       store_w(ls);
-      const int e = lk * nch + c;
-      const int nk2 = c + 1 < nch ? lk : lk + 1, nc2 = c + 1 < nch ? c + 1 : 0;
-      hpend = tp >= NST - 1 && tp < NST - 1 + GH && nk2 < mine;
+      hpend = hwin && t2 >= 0;
       hpend_g = hpend ? tp - (NST - 1) : 0;
       hpend_slot = (e + 1) & 1;
-      hreg = load_halo_reg(nk2 < mine ? nk2 : lk, nc2, hpend_g, hpend);
-      const int lt2 = lt + 1 < nk ? lt + 1 : 0, lk2 = lt + 1 < nk ? lk : lk + 1;
-      load_w(lk2 < mine ? lt2 : lt);
-      ls = ls == NST - 1 ? 0 : ls + 1;
-      if (++lt == nk) { lt = 0; ++lk; }
+      hreg = load_halo_reg(hpend ? t2 : lk_tile, nc2, hpend_g, hpend);
+      load_w(lt + 1 < nk ? lt + 1 : 0);
+      advance();
       return;
     }
     {   // weights of (tap tp, chunk c): GEMM K rows kt = tp * nch + c
@@ -361,29 +404,24 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         }
       }
     }
-    if (tp >= NST - 1 && tp < NST - 1 + GH) {   // one group of the next chunk of the stream
-      const int e = lk * nch + c;   // stream index of this chunk; the next one goes to slot (e + 1) & 1
-      const int nk2 = c + 1 < nch ? lk : lk + 1, nc2 = c + 1 < nch ? c + 1 : 0;
-      if (nk2 < mine) hg_last = issue_halo(nk2, nc2, tp - (NST - 1), (e + 1) & 1);
-    }
-    ls = ls == NST - 1 ? 0 : ls + 1;
-    if (++lt == nk) { lt = 0; ++lk; }
+    if (t2 >= 0) hg_last = issue_halo(t2, nc2, tp - (NST - 1), (e + 1) & 1);
+    advance();
   };
   auto load_next = [&]() {
     if constexpr (HALO) { load_next_halo(); return; }
-    if (lk >= mine) return;   // stream exhausted (uniform)
+    if (lt == 0) lk_tile = tile_id(lk);
+    if (lk_tile < 0) return;   // stream exhausted (uniform)
     if (no_dma && nissued >= NST - 1) {   // (keep the loader's bookkeeping, issue nothing)
-      if (++lt == nk) { lt = 0; ++lk; }
+      advance();
       return;
     }
     ++nissued;
     if (lt == 0) {
-      setup_rows(tile_m0(lk));
+      setup_rows(m0_of(lk_tile));
       it_ci = it_ty = it_tx = it_kt = 0;
     }
     issue(kinfo(), ls);
-    ls = ls == NST - 1 ? 0 : ls + 1;
-    if (++lt == nk) { lt = 0; ++lk; }
+    advance();
   };
 
   const int r16 = lane & 15, h4 = lane >> 4;
@@ -712,18 +750,21 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // drains everything.
   if constexpr (WREG) {   // the first chunk's whole halo ahead of the stream (registers -> LDS)
 #pragma unroll
-    for (int g = 0; g < GH; ++g) store_halo_reg(g, 0, load_halo_reg(0, 0, g, true), true, (unsigned)(OB0 + tid * 16));
+    for (int g = 0; g < GH; ++g)
+      store_halo_reg(g, 0, load_halo_reg(tile_id(0), 0, g, true), true, (unsigned)(OB0 + tid * 16));
   } else if constexpr (HALO) {   // the first chunk's whole halo ahead of the stream
+    const int t0 = tile_id(0);
 #pragma unroll
-    for (int g = 0; g < GH; ++g) issue_halo(0, 0, g, 0);
+    for (int g = 0; g < GH; ++g) issue_halo(t0, 0, g, 0);
   }
   if constexpr (WREG) load_w(0);   // (the first load_next stores them into stage 0)
-  const int total = mine * nk;
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i) load_next();
   int gs = 0, cs = 0, last_epi = -NST;   // step, its stage, step of the latest epilogue
-  for (int k = 0; k < mine; ++k) {
-    const int m0c = tile_m0(k);
+  for (int k = 0;; ++k) {
+    const int tk = tile_id(k);
+    if (tk < 0) break;   // the block's work is done (uniform)
+    const int m0c = m0_of(tk);
 #pragma unroll
     for (int i = 0; i < 2 * MIQ; ++i)
 #pragma unroll
@@ -743,7 +784,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           // the stage and the halo groups were written by every wave's ds_write at earlier steps
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         } else if (a.debug_flags & 64) {   // timing-only ablation (fwd_debug bit 6): LDS-DMA issued, never waited for
-        } else if (gs + NST - 2 >= total) {
+        } else if (gs + NST - 2 >= lsteps) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (last_epi > gs - NST) {
           if (wide) {
@@ -763,7 +804,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         hslot = (k * nch + c) & 1;
         hdy = tp / 3;
         hdx = tp - 3 * hdy;
-      } else if (gs + NST - 2 >= total) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (gs + NST - 2 >= lsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else if (last_epi > gs - NST && wide) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W) : "memory");
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
       else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
@@ -777,8 +818,24 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           zstep = gs;
         }
       }
+      // dyn: when the loader starts tile lk at this step, thread 0 claims tile lk + 1 (an atomic the compiler
+      // does not wait for: claim_issue) and publishes it after the multiply, waiting only for the atomic (the
+      // step's own LDS-DMA pieces, issued after it, stay in flight); the next barrier makes it visible, ahead
+      // of the loader's first use (step NST - 1 of tile lk for the halo form, the next tile's first step else)
+      bool claim_now = false;
+      int cslot = 0, cval = 0;
+      if (dyn && lt == 0) {
+        lk_tile = tile_id(lk);
+        claim_now = lk_tile >= 0;
+        cslot = (lk + 1) & 3;
+        if (claim_now && tid == 0) cval = claim_issue(a.claim + col);
+      }
       if (!late) load_next();
       compute(cs, late);
+      if (claim_now && tid == 0) {
+        if (WREG || no_dma) claim_publish<0>(ring + cslot, cval);
+        else claim_publish<LOPS>(ring + cslot, cval);
+      }
       cs = cs == NST - 1 ? 0 : cs + 1;
     }
     last_epi = gs - 1;
@@ -794,6 +851,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     else epilogue(m0c);
   }
 
+  if (dyn && tid == 0) claim_block_done(a.claim, ntn, G);   // (every claim of the block has returned)
   // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
   if (!stats || (a.debug_flags & 2)) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -863,6 +921,9 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   int grid = std::min(a.nblocks, option("tap64_persist_grid", 256));
   grid -= grid % a.ntile_n;
   if (grid <= 0) grid = a.ntile_n;
+  // dynamic tile claiming (option tap64p_claim): robust to CUs held by another stream's kernels (RCCL)
+  a.claim = nullptr;
+  if (option("tap64p_claim", 0) && a.ntile_n + 1 <= CLAIM_INTS) a.claim = claim_slot();   // (nullptr: static lists)
   const bool bnr = a.bnr_z != nullptr;
   // the halo form (option tap64p_halo): 3x3 stride-1 'same' layers whose output tiles into 8 x 32 patches
   const bool halo_shape = !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&

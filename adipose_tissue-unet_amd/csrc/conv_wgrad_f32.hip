@@ -202,11 +202,13 @@ __global__ __launch_bounds__(WN * WK * 64, 1) void igemm_wgrad_f32_kernel(WgradA
       for (int r = 0; r < 4; ++r) blk[(rq + r) * ES + kb * 16 + col] = acc[nb][kb][r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (a.part) {
+      // the reduce adds whole Nout x Kpad slabs: the K..Kpad-1 pad columns are written as zeros (the tiles
+      // cover them, ntile_k * TK >= round_up(K, 64) >= Kpad), never left with another launch's scratch
       float* slab = a.part + (size_t)split * a.Nout * a.Kpad;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int n = n0 + wn * 64 + nb * 16 + i;
-        if (n < a.Nout && kk < a.K) slab[(size_t)n * a.Kpad + kk] = blk[i * ES + lane];
+        if (n < a.Nout && kk < a.Kpad) slab[(size_t)n * a.Kpad + kk] = kk < a.K ? blk[i * ES + lane] : 0.f;
       }
     } else {
 #pragma unroll

@@ -882,7 +882,44 @@ static float* stat_scratch_impl(bool fold, int C, const float* sum, hipStream_t 
   return p;
 }
 float* stat_scratch() { return stat_scratch_impl(false, 0, nullptr, nullptr); }
+// drop a deferred fold that never reached its adp_bn_finalize_fold (an error or exception between the two) and
+// re-zero the replicas it left its sums in, stream-ordered on s; a no-op when nothing is pending
+int bn_fold_reset(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { set_error("adp_bn_fold_reset: hipGetDevice failed"); return -2; }
+  {
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    PendingFold& pf = pending_folds()[dev];
+    if (!pf.on) return 0;
+    pf.on = false;
+  }
+  float* p = stat_scratch();
+  if (!p) return -2;
+  if (hipMemsetAsync(p, 0, sizeof(float) * STAT_REPL * 2 * STAT_CMAX, s) != hipSuccess) {
+    set_error("adp_bn_fold_reset: clearing the accumulator replicas failed");
+    return -2;
+  }
+  return 0;
+}
 float* stat_scratch_fold(int C, const float* sum, hipStream_t s) { return stat_scratch_impl(true, C, sum, s); }
+int* claim_slot() {
+  static std::mutex mu;
+  static std::map<int, std::pair<int*, unsigned>> per_dev;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) { set_error("claim_slot: hipGetDevice failed"); return nullptr; }
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = per_dev[dev];
+  if (!e.first) {
+    const size_t bytes = sizeof(int) * CLAIM_SLOTS * CLAIM_INTS;
+    if (hipMalloc(&e.first, bytes) != hipSuccess || hipMemset(e.first, 0, bytes) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+      e.first = nullptr;
+      set_error("claim_slot: allocation of the tile-claiming counters failed");
+      return nullptr;
+    }
+  }
+  return e.first + (size_t)(e.second++ % CLAIM_SLOTS) * CLAIM_INTS;
+}
 void* scratch(int slot, size_t bytes) {
   static std::mutex mu;
   static std::map<std::pair<int, int>, std::pair<void*, size_t>> bufs;
@@ -1075,6 +1112,8 @@ extern "C" int adp_bn_finalize(int C, float count, const float* sum, const float
                      sum, sq, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean, rvar);
   return adp::check_launch("adp_bn_finalize");
 }
+
+extern "C" int adp_bn_fold_reset(adp_stream_t st) { return adp::bn_fold_reset((hipStream_t)st) ? -2 : 0; }
 
 extern "C" int adp_bn_finalize_fold(int C, float count, float* sum, float* sq, const float* gamma, const float* beta,
                                     float eps, float momentum, float* scale, float* shift, float* mean, float* invstd,

@@ -40,6 +40,7 @@
 
 namespace adp {
 void set_error(const std::string& msg);
+int option(const char* name, int dflt);
 }
 
 namespace {
@@ -179,6 +180,7 @@ struct adp_handle {
   std::vector<hipEvent_t> bev;        // one "layers done" event per bucket
   hipEvent_t comm_done = nullptr;
   bool dp_active = false;
+  float* Gsnap = nullptr;             // adp_debug_grad_flat(which = 1): G as each bucket's all-reduce was issued
   std::string comm_err;
 
   ~adp_handle() {
@@ -191,6 +193,7 @@ struct adp_handle {
     for (auto e : bev) (void)hipEventDestroy(e);
     if (comm_done) (void)hipEventDestroy(comm_done);
     if (cstream) (void)hipStreamDestroy(cstream);
+    if (Gsnap) (void)hipFree(Gsnap);
     for (auto& l : dense) {
       if (!train_on || cfg.dtype != ADP_DTYPE_F32) (void)hipFree(l.W);
       if (!train_on) (void)hipFree(l.b);
@@ -758,6 +761,13 @@ struct adp_handle {
     bk.launched = true;
     CK(hipEventRecord(bev[bi], s));
     CK(hipStreamWaitEvent(cstream, bev[bi], 0));
+    if (adp::option("dp_snapshot", 0)) {   // test hook: what the all-reduce is about to read
+      if (!Gsnap) {
+        CK(hipMalloc(reinterpret_cast<void**>(&Gsnap), sizeof(float) * nflat));
+        CK(hipMemset(Gsnap, 0, sizeof(float) * nflat));
+      }
+      CK(hipMemcpyAsync(Gsnap + bk.lo, G + bk.lo, sizeof(float) * (bk.hi - bk.lo), hipMemcpyDeviceToDevice, cstream));
+    }
     NC(rccl().allreduce(G + bk.lo, G + bk.lo, bk.hi - bk.lo, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm),
                         cstream));
     return 0;
@@ -771,6 +781,15 @@ struct adp_handle {
     pend[bi].erase(id);
     if (pend[bi].empty() && !buckets[bi].launched) return dp_launch(bi, s);
     return 0;
+  }
+  // error path between dp_begin and dp_finish: buckets already issued may still read G on the communication
+  // stream, so the compute stream waits for them before anything (the next step's zero-fill) writes G again
+  void dp_abort(hipStream_t s) {
+    if (!dp_active) return;
+    dp_active = false;
+    bool any = false;
+    for (auto& b : buckets) any = any || b.launched;
+    if (any && hipEventRecord(comm_done, cstream) == hipSuccess) (void)hipStreamWaitEvent(s, comm_done, 0);
   }
   int dp_finish(hipStream_t s) {
     if (!dp_active) return 0;
@@ -786,6 +805,9 @@ struct adp_handle {
 
   // ================================================================ unet_bn (nets.UNetBN)
   int ch_of(int lvl) const { return base << lvl; }
+  // the input layer's weight gradient computes dz = bn_bwd_apply(dA, z) inside the fused cin8 kernel (bf16, 64
+  // outputs: igemm_wgrad_cin8_kernel<true>) and stores none; other shapes need a dz buffer for the apply pass
+  bool in_dz_fused() const { return cfg.dtype == ADP_DTYPE_BF16 && base == 64; }
   int side(int lvl) const { return S >> lvl; }
   BnLayer& L(const std::string& n) { return bl[bl_idx.at(n)]; }
   void* wfwd(const BnLayer& l) {   // forward-layout weights in the compute dtype
@@ -903,7 +925,7 @@ struct adp_handle {
       const std::string k = std::to_string(i);
       rc = act("z" + k + "_1", i) || act("z" + k + "_2", i) || act("az" + k + "_1", i) || act("az" + k + "_2", i) ||
            act("dA_z" + k + "_2", i) || act("dz_z" + k + "_2", i) || act("dA_z" + k + "_1", i) ||
-           act("dz_z" + k + "_1", i);
+           ((i == 0 && in_dz_fused()) ? 0 : act("dz_z" + k + "_1", i));
       if (!rc && i < Lv - 1)
         rc = act("y" + k + "_1", i) || act("y" + k + "_2", i) || act("ay" + k + "_1", i) || act("ay" + k + "_2", i) ||
              act("t" + k, i) || act("dz_y" + k + "_2", i) || act("dA_y" + k + "_1", i) ||
@@ -1258,8 +1280,9 @@ struct adp_handle {
       CL(bn_wgrad(en + "_conv2", N, b(("az" + k + "_1").c_str()), nullptr, dA2, z2, dz2, s));
       void* dA1 = b(("dA_z" + k + "_1").c_str());
       CL(bn_dgrad(en + "_conv2", N, dz2, dA1, en + "_conv1", z1, s));
-      // (the input layer has no data gradient: its dz is not stored, the fused input-layer form then runs)
-      void* dz1 = i == 0 ? nullptr : b(("dz_z" + k + "_1").c_str());
+      // (the input layer has no data gradient: its dz is not stored where the fused input-layer form runs, bf16
+      // with 64 base channels; elsewhere the two-launch form writes it into the handle's own buffer)
+      void* dz1 = (i == 0 && in_dz_fused()) ? nullptr : b(("dz_z" + k + "_1").c_str());
       const void* src = i == 0 ? b("x") : b(("pool" + std::to_string(i - 1)).c_str());
       CL(bn_wgrad(en + "_conv1", N, src, nullptr, dA1, z1, dz1, s));
       if (i > 0) {
@@ -1594,6 +1617,21 @@ extern "C" int adp_get_grad(adp_handle* h, const char* layer, int slot, float* h
   return h->v3_get_grad(layer, slot, host);
 }
 
+extern "C" int adp_debug_grad_flat(adp_handle* h, int which, float* host, size_t n) {
+  if (!h || (which != 0 && which != 1)) { adp::set_error("adp_debug_grad_flat: bad arguments (which 0 or 1)"); return -1; }
+  if (!h->train_on || !h->G || h->step == 0) { adp::set_error("adp_debug_grad_flat: no training step has run"); return -1; }
+  if (n != h->nflat || !host) {
+    adp::set_error("adp_debug_grad_flat: n must be the flat gradient size " + std::to_string(h->nflat));
+    return -1;
+  }
+  const float* src = which == 0 ? h->G : h->Gsnap;
+  if (!src) { adp::set_error("adp_debug_grad_flat: no snapshot (set option dp_snapshot = 1, train with a communicator)"); return -1; }
+  if (hipSetDevice(h->device) != hipSuccess) { adp::set_error("adp_debug_grad_flat: hipSetDevice failed"); return -2; }
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(host, src, sizeof(float) * n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 extern "C" int adp_forward(adp_handle* h, const float* images, int n, long long img_stride, float mean, float std_,
                            int tta_mode, float* prob, adp_stream_t st) {
   if (!h || !images || !prob || n < 0 || tta_mode < 0 || tta_mode > 3) {
@@ -1683,6 +1721,7 @@ extern "C" int adp_train_step(adp_handle* h, const float* x, const float* y, int
   }
   hipStream_t s = (hipStream_t)st;
   if (hipSetDevice(h->device) != hipSuccess) { adp::set_error("adp_train_step: hipSetDevice failed"); return -2; }
+  CL(adp_bn_fold_reset(st));   // a failed earlier step may have left a deferred BatchNorm fold pending
   if (!bn) {
     CL(h->ensure_train());
     if (h->dirty) CL(h->upload(s));
@@ -1744,7 +1783,7 @@ extern "C" int adp_train_step(adp_handle* h, const float* x, const float* y, int
   CL(h->dp_begin(frozen));
   const int brc = bn ? h->bn_backward(N, s) : h->backward(N, keep, full, s);
   if (brc) {
-    h->dp_active = false;
+    h->dp_abort(s);
     return brc;
   }
   CL(h->dp_finish(s));

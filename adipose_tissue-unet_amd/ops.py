@@ -471,6 +471,12 @@ def fill(dst, value):
     call("adp_fill_f32", dst.numel(), float(value), ptr(dst), stream_ptr())
 
 
+def bn_fold_reset():
+    """Drop a deferred BatchNorm fold left pending by a failed step and re-zero the accumulator replicas
+    (adp_bn_fold_reset, stream-ordered; a no-op when nothing is pending)."""
+    call("adp_bn_fold_reset", stream_ptr())
+
+
 def bn_finalize(count, ssum, ssq, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean=None, rvar=None,
                 fold=False):
     """fold=True: first add the statistics the previous conv_fwd(..., defer_fold=True) left in the

@@ -110,6 +110,13 @@ class GradBuckets:
         self.works.append(dist.all_reduce(self.ps.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                           async_op=True))
 
+    def abort(self):
+        """Error path of a backward: the buckets already issued may still read the gradient buffer on the RCCL
+        stream; the current stream waits for them before anything (the next step's zero-fill) writes it."""
+        for w in self.works:
+            w.wait()
+        self.works = []
+
     def finish(self):
         # every gradient is final here: reduce any bucket a ready-hook did not launch (a layer that never
         # reported, or frozen-only buckets, whose zero gradients are harmless to sum)
@@ -230,6 +237,7 @@ class Trainer:
         net = self.net
         B = y.shape[0]
         a = net.acts(B)
+        ops.bn_fold_reset()   # a failed earlier step may have left a deferred BatchNorm fold pending
         ops.prep_input(x_norm, a["x"], mean=0.0, std=1.0)
         self.iterations += 1
         outs = net.forward(B, train=True, seed=self.iterations)
@@ -241,6 +249,10 @@ class Trainer:
             net.grad_hook = self.buckets.ready
         try:
             net.backward(grads)
+        except BaseException:
+            if self.buckets is not None:
+                self.buckets.abort()
+            raise
         finally:
             net.grad_hook = None
         if self.buckets is not None:

@@ -122,21 +122,43 @@ def workload_label(args):
     return wl + (f" (BASELINE configs[{cfg}])" if cfg is not None else " (not a BASELINE config)")
 
 
-def committed_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary that holds it
-    (profiles/<round>_traffic.json, written by tools/profile_round.sh from rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes of the bench command of that workload); (None, None) if absent."""
+def committed_traffic(kernel, workload, build):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of THIS workload
+    (profiles/<round>_traffic.json, written by tools/profile_round.sh from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    of the bench command, with the workload label and library build record of that run under "_meta");
+    (None, None, None) when no summary of this workload holds the kernel — a profile of another workload is
+    never used. The third value says whether the profiled library build is the one running now."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
+        meta = d.get("_meta") or {}
+        if meta.get("workload") != workload:
+            continue
         e = d.get(kernel)
         if e and e.get("traffic_bytes") is not None:
-            return int(e["traffic_bytes"]), os.path.basename(f)
-    return None, None
+            return int(e["traffic_bytes"]), os.path.basename(f), meta.get("build") == build
+    return None, None, None
+
+
+def committed_dice_val(workload):
+    """Dice@val of this workload from the newest committed bench_converge.py run (profiles/*_converge*.json):
+    training on a stream of distinct tiles, validation on the 64-tile seeded val stream. The
+    throughput run itself trains one resident batch, which says nothing about Dice."""
+    import glob
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_converge*.json")))):
+        try:
+            d = json.loads(open(f).read().strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            continue
+        if d.get("workload") == workload:
+            return {"dice_val": d.get("dice_val"), "dice_val_thr": d.get("dice_val_thr"), "steps": d.get("steps"),
+                    "train_seconds": d.get("train_seconds"), "time_to_target": d.get("time_to_target"),
+                    "target": d.get("target"), "fp8": d.get("fp8"), "source": os.path.basename(f)}
+    return None
 
 
 def main():
@@ -146,7 +168,7 @@ def main():
     import torch.distributed as dist
 
     import _adipose_pkg  # noqa: F401
-    from adipose_amd import ops
+    from adipose_amd import _lib, ops
     from adipose_amd.data import synthetic_batch
     from adipose_amd.nets import AdiposeV3Net, UNetBN
     from adipose_amd.trainer import LossConfig, Trainer
@@ -211,15 +233,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     met = tr.read_metrics()
-    # Dice@val: forward (eval) on a separate seeded synthetic val stream of this workload
-    xv, yv = synthetic_batch(B, S, channels=3, seed=865 + 10_000 + rank)
-    xv = xv.astype(np.float32)
-    if C is None:
-        from adipose_amd.data import to_gray
-        xv = to_gray(xv)
-    tr.eval_step(torch.from_numpy((xv - mean) / (std + 1e-10)).to(dev).contiguous(),
-                 torch.from_numpy(yv).to(dev).contiguous())
-    val = tr.read_metrics()
 
     summ = timer.summary()
     if rank != 0:
@@ -240,11 +253,14 @@ def main():
                          "alg_gbs": round(v[3] / (v[2] * 1e-3) / 1e9, 1),
                          "share_of_step": round(v[2] / step_ms, 4)}
                   for k, v in sorted(summ.items(), key=lambda kv: -kv[1][2])}
-    traffic, tsrc = committed_traffic(kname)
+    wl = workload_label(args)
+    build = _lib.lib().adp_source_hash().decode()[:16]
+    traffic, tsrc, same_build = committed_traffic(kname, wl, build)
     alg_bytes = abytes / n
     roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2),
             "peak": MI355X_PEAK[dname], "unit": "TFLOP/s", "frac": round(achieved / MI355X_PEAK[dname], 4),
             "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc,
+            "traffic_same_build": same_build,
             "algorithmic_bytes": round(alg_bytes),
             "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
             "avg_launch_ms": round(ms / n, 4), "launches": n,
@@ -258,7 +274,6 @@ def main():
             cpu = cpu_baseline(args)
         except Exception as e:  # report, never fake
             cpu = {"value": None, "error": repr(e)}
-    wl = workload_label(args)
     line = {
         "metric": "1024^2 tiles/sec (train)", "value": round(value, 4), "unit": "tiles/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -267,7 +282,8 @@ def main():
         "config": {"workload": wl, "preset": args.preset, "levels": args.levels if args.preset == "unet_bn" else 4,
                    "tile": S, "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}",
                    "allreduce": args.allreduce if world > 1 else None},
-        "train_loss": round(met["loss"], 5), "dice_val": round(val["main_out_dice_coef"], 5),
+        "build": build,
+        "train_loss": round(met["loss"], 5), "dice_val": committed_dice_val(wl),
         "roofline": roof, "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

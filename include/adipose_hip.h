@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 15 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 16 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
@@ -38,7 +38,8 @@ extern "C" {
                               v11: adp_sum_bf16; v12: adp_timing / adp_timing_read, unet_bn handle preset;
                               v13: adp_vec_mul (eval BatchNorm folded into the fp8 dequantisation scale);
                               v14: adp_scale_rows (eval BatchNorm folded into bf16 / f32 forward weights);
-                              v15: adp_conv_wgrad_bn with dY = NULL (dz not stored), input-layer fused form */
+                              v15: adp_conv_wgrad_bn with dY = NULL (dz not stored), input-layer fused form;
+                              v16: adp_bn_fold_reset, adp_debug_grad_flat */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -221,6 +222,10 @@ int adp_bn_finalize(int C, float count, const float* sum, const float* sqsum, co
 int adp_bn_finalize_fold(int C, float count, float* sum, float* sqsum, const float* gamma, const float* beta,
                          float eps, float momentum, float* scale, float* shift, float* mean, float* invstd,
                          float* running_mean, float* running_var, adp_stream_t s);
+/* Drops a bn_defer_fold record that never reached its adp_bn_finalize_fold (an error or exception between the
+ * two) and re-zeroes the replicas, stream-ordered on s; a no-op when nothing is pending. Trainer steps and
+ * adp_train_step call it first, so a failed step cannot poison the replicas for the rest of the process. */
+int adp_bn_fold_reset(adp_stream_t s);
 /* a = relu(z*scale + shift), the post-BatchNorm activation, materialised once per layer */
 int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* scale, const float* shift,
                  void* out, adp_stream_t s);
@@ -436,6 +441,12 @@ int adp_get_param(adp_handle* h, const char* layer, int slot, float* host, size_
 /* The gradient of a parameter slot from the last adp_train_step (after its all-reduce), same layout as
  * adp_get_param; synchronous. Errors before the first step and for the running-statistics slots. */
 int adp_get_grad(adp_handle* h, const char* layer, int slot, float* host, size_t n);
+/* Test hook of the bucketed all-reduce (v16): which = 0 copies the whole flat gradient buffer of the last
+ * adp_train_step (n = its element count, adp_debug_grad_flat(h, 0, NULL, 0) -> error message names it);
+ * which = 1 copies the snapshot taken on the communication stream as each bucket's all-reduce was issued,
+ * recorded only while option "dp_snapshot" is 1. With a one-rank communicator (the in-place SUM changes
+ * nothing) the two are equal iff no gradient was written after its bucket started. Synchronous. */
+int adp_debug_grad_flat(adp_handle* h, int which, float* host, size_t n);
 /* predict_single / TTA (segmentation_inference.py:153-229): images = n device f32 (S,S) raw gray tiles
  * img_stride floats apart (<= 0: dense); prob = n device f32 (S,S) main_out probabilities;
  * (x - mean)/(std + 1e-10) on load; tta_mode 0 none, 1 minimal (id, flipH), 2 basic (+flipV, rot90),

@@ -121,8 +121,12 @@ def _compare_weights(a, b, lr, steps):
                 per.append((k, i, nb, d.size, float(d.max())))
     # Adam's first steps move every weight by ~lr * sign(g): a gradient that is zero up to rounding may
     # take either sign in two f32 atomic summation orders, so a few elements may differ by <= 2 lr (measured:
-    # up to 0.17 % of the weights by more than 1e-6, all in layers with many near-zero gradients)
-    assert worst <= 2 * lr * steps + 1e-6 and n_big <= 1e-2 * n_all, (worst, n_big, n_all, per[:8])
+    # up to 0.17 % of the weights by more than 1e-6, all in layers with many near-zero gradients). A wrong or
+    # missing gradient term moves most of its layer's weights by ~lr: every layer is bounded on its own (10 % of
+    # its elements, at least 4), so one bad layer fails even when it is small against the whole net
+    assert worst <= 2 * lr * steps + 1e-6 and n_big <= 3e-3 * n_all, (worst, n_big, n_all, per[:8])
+    bad = [p for p in per if p[2] > max(4, 0.1 * p[3])]
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("freeze", [False, True])
@@ -353,6 +357,49 @@ def test_native_unet_bn_bucketed_comm_and_errors():
         call("adp_get_grad", a._h, b"enc0_conv1", 3, np.zeros(64, np.float32).ctypes.data, 64)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("preset", ["adipose_v3", "unet_bn"])
+def test_bucket_allreduce_reads_final_gradients(weights, preset):
+    """The native step's overlapped bucket all-reduce (engine.cpp dp_launch) may only start once every gradient
+    of its bucket is written. With a one-rank communicator the in-place SUM changes nothing, so the test takes a
+    snapshot of each bucket on the communication stream at the moment its all-reduce is issued (option
+    dp_snapshot, adp_debug_grad_flat) and requires it to equal the final gradient buffer element for element: a
+    gradient written after its bucket started would differ (frozen-encoder step included)."""
+    from adipose_amd import ops
+    from adipose_amd._lib import AdpError, call
+    from adipose_amd.engine import NativeAdiposeV3, NativeUNetBN, comm_destroy, comm_init, comm_unique_id, train_cfg
+    if preset == "adipose_v3":
+        e = NativeAdiposeV3(tile=S, max_batch=2, dtype="bf16")
+        e.set_weights(weights)
+        x, y = _train_data(11)
+        cfgs = [train_cfg(), train_cfg(freeze_encoder=True)]
+    else:
+        w, x, y = _bn_case(3, S, 2, seed=7)
+        e = NativeUNetBN(tile=S, max_batch=2, dtype="bf16", levels=3)
+        e.set_weights(w)
+        cfgs = [train_cfg(use_hard_mining=False)]
+    comm = comm_init(1, comm_unique_id(), 0)
+    e.set_comm(comm)
+    ops.set_option("dp_snapshot", 1)
+    try:
+        for cfg in cfgs:
+            e.train_step(x, y, 1e-3, cfg)
+            with pytest.raises(AdpError) as err:   # a size query: the message names the flat size
+                call("adp_debug_grad_flat", e._h, 0, None, 0)
+            n = int(str(err.value).rsplit(" ", 1)[-1])
+            g = np.zeros(n, np.float32)
+            snap = np.zeros(n, np.float32)
+            call("adp_debug_grad_flat", e._h, 0, g.ctypes.data, n)
+            call("adp_debug_grad_flat", e._h, 1, snap.ctypes.data, n)
+            assert np.abs(g).max() > 0
+            diff = np.flatnonzero(g != snap)
+            assert diff.size == 0, (preset, diff.size, diff[:8])
+    finally:
+        ops.set_option("dp_snapshot", 0)
+        e.set_comm(None)
+        comm_destroy(comm)
+        e.close()
 
 
 def test_c_client_trains_both_presets():

@@ -171,11 +171,12 @@ def test_tap64_configs(cfg):
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("claim", [0, 1], ids=["static", "claimed"])
 @pytest.mark.parametrize("wide", [0, 1], ids=["st8", "st16"])
 @pytest.mark.parametrize("tile", [256, 128], ids=["256x256x2", "256x128x3"])
 @pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
 @pytest.mark.parametrize("mode", ["plain", "one_chunk", "concat", "split"])
-def test_tap64p_halo_matches(mode, grid, tile, wide):
+def test_tap64p_halo_matches(mode, grid, tile, wide, claim):
     """Halo form of the persistent 256x256 forward (A operand read from a 10x34 halo moved into LDS once per
     64-channel chunk, chunk-major K stream, next chunk's halo issued one group per step) vs a float64
     reference convolution of the same bf16 operands, and vs the gathered form (tap64p_halo=0) to within the
@@ -211,6 +212,7 @@ def test_tap64p_halo_matches(mode, grid, tile, wide):
         ops.set_option("tap64p_halo", halo)
         ops.set_option("fwd_w4", 0)   # (the four-wave form takes the Nout % 256 == 0 shapes: its own test)
         ops.set_option("tap64p_wide", wide)
+        ops.set_option("tap64p_claim", claim)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
@@ -218,7 +220,7 @@ def test_tap64p_halo_matches(mode, grid, tile, wide):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4", "tap64p_wide"):
+            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4", "tap64p_wide", "tap64p_claim"):
                 ops.set_option(o_, None)
         assert kname.startswith("igemm_fwd_tap64p_kernel<256, %d, %d, false, %s, false" % (
             tile, 2 if tile == 256 else 3, "true" if halo else "false")), kname
@@ -229,6 +231,53 @@ def test_tap64p_halo_matches(mode, grid, tile, wide):
     torch.testing.assert_close(sh_, sg, rtol=1e-4, atol=1e-2)
     rf = ref.reshape(-1, nout)
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
+
+
+@pytest.mark.parametrize("form", ["halo256", "halo128", "gather_dil2", "convt"])
+def test_tap64p_claim_counters_reset(form):
+    """Dynamic tile claiming (option tap64p_claim): every launch takes its tiles from a counter slot of the
+    library's ring (adp::claim_slot, 64 slots) and the last block to finish re-zeroes it. 150 launches -- more
+    than two turns of the ring, grids of 256 / 7 / 1 blocks, several N columns -- must all equal the static
+    launch bit for bit: a slot left non-zero would make a later launch skip tiles (stale output rows)."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(31)
+    N, H, W_ = 2, 32, 64
+    kw = {}
+    if form == "convt":
+        cin, cs = 128, 64
+        x = torch.randn(N, H, W_, cin, generator=g).to(DEV, dt)
+        Wt = (torch.randn(4 * cs, cin, generator=g) * 0.05).to(DEV, dt)
+        nout, oshape = 4 * cs, (N, 2 * H, 2 * W_, cs)
+        kw.update(bias=torch.randn(cs, generator=g).to(DEV), kh=1, kw=1, pad=0, out_mode=1, shuffle_c=cs)
+        opts = dict(fwd_tap64=2, tap64p_cfg=3)
+    else:
+        cin, nout = 128, 512
+        x = torch.randn(N, H, W_, cin, generator=g).to(DEV, dt)
+        Wt = (torch.randn(nout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+        oshape = (N, H, W_, nout)
+        kw.update(bias=torch.randn(nout, generator=g).to(DEV), relu=True)
+        opts = dict(fwd_tap64=2 if form != "halo128" else 3, fwd_halo=0, fwd_w4=0)
+        if form == "gather_dil2":
+            kw.update(dil=2, pad=2)
+    outs = []
+    try:
+        for k_, v_ in opts.items():
+            ops.set_option(k_, v_)
+        for i in range(150):
+            claim = 0 if i == 0 else 1
+            ops.set_option("tap64p_claim", claim)
+            ops.set_option("tap64_persist_grid", (None, 7, 1)[i % 3] if i else None)
+            o = torch.full(oshape, float("nan"), dtype=dt, device=DEV)
+            ops.conv_fwd(x, Wt, nout, out=o, **kw)
+            outs.append(o)
+        torch.cuda.synchronize()
+        kname = _lib.lib().adp_last_kernel().decode()
+    finally:
+        for k_ in list(opts) + ["tap64p_claim", "tap64_persist_grid"]:
+            ops.set_option(k_, None)
+    assert kname.startswith("igemm_fwd_tap64p_kernel"), kname
+    for i, o in enumerate(outs[1:], 1):
+        assert torch.equal(o, outs[0]), (i, torch.isnan(o.float()).sum().item())
 
 
 @pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
@@ -488,18 +537,20 @@ def test_upsample_gather_halo_forms(form, grid):
     torch.testing.assert_close(sp, sn, rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("claim", [0, 1], ids=["static", "claimed"])
 @pytest.mark.parametrize("wide", [0, 1], ids=["st8", "st16"])
 @pytest.mark.parametrize("cfg", [1, 2, 3], ids=["256x256x2", "256x128x3", "128x256x3"])
 @pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
 @pytest.mark.parametrize("mode", ["plain", "concat", "convt_shuffle", "split", "convt_dgrad", "bnr", "dilated"])
-def test_tap64_persistent_matches(mode, grid, cfg, wide):
+def test_tap64_persistent_matches(mode, grid, cfg, wide, claim):
     """Persistent tap64 kernel (conv_fwd_tap64p.hip: one K-step stream over the block's tiles through an
     NST-stage LDS ring, register epilogue with 8-B buffer stores, or with 16-B stores of channel pairs joined
     by permlane16_swap: option tap64p_wide) in its three tile / ring forms vs the
     non-persistent kernel on the same launch: bit-identical outputs and equal BatchNorm sums (statistics,
     or the fused BatchNorm-backward reduction for bnr); a 3-block grid makes every block walk many tiles
     (ragged last M tile, partial N tile), so the cross-tile prefetch and the counted vmcnt waits are
-    exercised."""
+    exercised. claimed: the persistent blocks take their tiles from an atomic counter (option tap64p_claim),
+    which changes which block computes a tile, not how: still bit-identical."""
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(11)
     kw = {}
@@ -552,6 +603,7 @@ def test_tap64_persistent_matches(mode, grid, cfg, wide):
         ops.set_option("fwd_tap64", 2)   # the 256x256 configuration (small problems would pick narrower tiles)
         ops.set_option("tap64p_cfg", cfg)
         ops.set_option("tap64p_wide", wide)
+        ops.set_option("tap64p_claim", claim)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
@@ -562,7 +614,7 @@ def test_tap64_persistent_matches(mode, grid, cfg, wide):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("tap64_persist", "fwd_tap64", "tap64_persist_grid", "tap64p_cfg", "tap64p_wide"):
+            for o_ in ("tap64_persist", "fwd_tap64", "tap64_persist_grid", "tap64p_cfg", "tap64p_wide", "tap64p_claim"):
                 ops.set_option(o_, None)
         res.append(([o.clone() for o in outs], st.clone(), kname))
     assert res[0][2].startswith("igemm_fwd_tap64_kernel") and res[1][2].startswith("igemm_fwd_tap64p_kernel"), \
@@ -1631,6 +1683,18 @@ def test_deferred_bn_fold_is_guarded():
         ops.bn_finalize(N * H * 32, s0, q0, gamma, beta, 1e-5, 0.1, sc, sh, mu, ist, fold=True)
     ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()))   # the replicas are usable again
     torch.cuda.synchronize()
+    # a deferred fold that never reaches its finalize (an error between the two): adp_bn_fold_reset drops the
+    # record and re-zeroes the replicas, so the next statistics launch runs and its sums are not polluted
+    ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()), defer_fold=True)
+    with pytest.raises(ops.AdpError):
+        ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()))
+    ops.bn_fold_reset()
+    ops.bn_fold_reset()   # nothing pending: a no-op
+    s1, q1 = vec(), vec()
+    ops.conv_fwd(x, W, C, out=out, bn_stats=(s1, q1))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(s1, s_ref, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(q1, q_ref, rtol=1e-5, atol=1e-3)
 
 
 F32_TAP_CASES = [

@@ -15,6 +15,9 @@ for s in $STEPS; do
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 ;;
     prof) bash tools/profile_round.sh "$TAG" > gpurun_out/prof.log 2>&1 ;;
+    converge) timeout -k 10 480 python bench_converge.py --fp8 > gpurun_out/converge.json 2> gpurun_out/converge.err ;;
+    convergev3) timeout -k 10 480 python bench_converge.py --preset adipose_v3 --batch 2 \
+                  > gpurun_out/converge_v3.json 2> gpurun_out/converge_v3.err ;;
     proff32) bash tools/profile_round.sh "${TAG}_f32" --preset adipose_v3 --dtype f32 --size 1024 --batch 2 \
                --steps 5 --warmup 2 > gpurun_out/prof_f32.log 2>&1 ;;
     nettests) timeout -k 10 600 python -u -m pytest tests/test_gpu_network.py -x -v --timeout 120 \
@@ -100,6 +103,12 @@ for s in $STEPS; do
           timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_wide_f8=0 > gpurun_out/f8wide_off_$i.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_wide_f8=1 > gpurun_out/f8wide_on_$i.log 2>&1 || exit 1
         done ;;
+    native) timeout -k 10 400 python -u -m pytest tests/test_gpu_native_size.py -x -v -s --timeout 200 \
+              --timeout-method thread > gpurun_out/native_tests.log 2>&1 ;;
+    claimab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_claim=0;tap64p_claim=1" \
+               > gpurun_out/claim_ab.log 2>&1 ;;
+    claimprobe) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 --opt tap64p_claim=1 \
+               > gpurun_out/contention_claim.log 2>&1 ;;
     contention) timeout -k 10 400 python -u tools/contention_probe.py > gpurun_out/contention.log 2>&1 ;;
     pipe2) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L0 128,L1 128" \
           --variants "halop_pipe=1;halop_pipe=2;halop_pipe=2,halop_wide=2" > gpurun_out/pipe2_kernels.log 2>&1 ;;

@@ -27,6 +27,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d "$OUT" -o fetch -- python
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d "$OUT" -o write -- python3 $BENCH > "$OUT/write.log" 2>&1
 cp "$OUT/kt_kernel_stats.csv" "$OUT/kernel_stats.csv"
 grep '^{"metric"' "$OUT/kt.log" | tail -1 > "$OUT/bench.json" || true
-python3 tools/traffic_summary.py "$OUT/fetch_counter_collection.csv" "$OUT/write_counter_collection.csv" "$OUT/traffic.json"
+python3 tools/traffic_summary.py "$OUT/fetch_counter_collection.csv" "$OUT/write_counter_collection.csv" "$OUT/traffic.json" \
+  "$OUT/bench.json"
 python3 tools/kstats.py "$OUT/kernel_stats.csv" 14 > "$OUT/kernel_breakdown.txt"
 echo done

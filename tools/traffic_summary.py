@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """HBM traffic per launch, per kernel instantiation, from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-usage: python tools/traffic_summary.py FETCH_counter_collection.csv WRITE_counter_collection.csv OUT.json
+usage: python tools/traffic_summary.py FETCH_counter_collection.csv WRITE_counter_collection.csv OUT.json [BENCH.json]
+
+BENCH.json (the bench line of the profiled command): its workload label and library build record go under
+"_meta", so bench.py only ever quotes a summary of the workload it is running (committed_traffic).
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read (16 B/lane loads and LDS-DMA alike), so read bytes = 2 x FETCH_SIZE KiB;
@@ -40,6 +43,12 @@ def main():
         wr = sum(w) / len(w) if w else None
         out[k] = {"launches": max(len(f), len(w)), "read_bytes": rd, "write_bytes": wr,
                   "traffic_bytes": (rd or 0.0) + (wr or 0.0) if rd is not None and wr is not None else None}
+    if len(sys.argv) > 4:
+        try:
+            b = json.loads(open(sys.argv[4]).read().strip().splitlines()[-1])
+            out["_meta"] = {"workload": b["config"]["workload"], "build": b.get("build")}
+        except (OSError, ValueError, IndexError, KeyError) as e:
+            print(f"no workload label from {sys.argv[4]}: {e!r}")
     json.dump(out, open(sys.argv[3], "w"), indent=1, sort_keys=True)
     print(f"{len(out)} kernels -> {sys.argv[3]}")
 
