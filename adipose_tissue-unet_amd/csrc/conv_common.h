@@ -66,6 +66,7 @@ struct WgradArgs {
   const float* bna_sc; const float* bna_sh; const float* bna_mean; const float* bna_invstd;
   const float* bna_gamma; const float* bna_dgamma; const float* bna_dbeta;
   float bna_inv_count;
+  int* claim;           // persistent halo weight gradient: dynamic tile claiming counters (nullptr: static lists)
 };
 
 // LDS-only workgroup barrier for epilogues: this wave's LDS traffic complete, then s_barrier. Unlike
@@ -143,6 +144,15 @@ ADP_DEV int xcd_remap(int bid, int nwg) {
 // a per-N-column counter (claim[col], vector atomics at agent scope, one tile ahead of the multiply so the
 // cross-tile prefetch stays), and a block that starts late finds the work taken. claim[nclaim] counts the
 // blocks that are done; the last one re-zeroes the counters, so the next launch on the slot starts from 0.
+// read of a claimed tile id from the block's LDS ring as inline asm: a plain LDS read gets an s_waitcnt vmcnt(0)
+// in front whenever LDS-DMA or a claim atomic may be in flight (the compiler cannot tell the ring from the DMA
+// targets), which would drain the prefetch or wait for the pending claim
+ADP_DEV int claim_ring_read(const int* p) {
+  int r;
+  const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr) : "memory");
+  return __builtin_amdgcn_readfirstlane(r);
+}
 // (the prologue's synchronous claim of a block's first two tiles; the atomic optimizer's wave form is fine here)
 ADP_DEV int claim_next2(int* cnt) {
   return __hip_atomic_fetch_add(cnt, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -263,7 +263,9 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 // with v_permlane16_swap into 8-channel runs (lane row h4 then holds channels 16 (nf + (h4 & 1)) + 8 (h4 >> 1)
 // .. + 7 of its pixel): one 16-B store per pair of units instead of two 8-B ones (the persistent forward's
 // tap64p_wide); needs the store limit (Nout, or split_c for the first part) on an 8-channel boundary
-template <bool BNR, int NCH, int BN, bool PIPE, int EPI, bool WIDE = false>
+// DYN: tiles claimed from a counter (a.claim) instead of the static list -- a compile-time form, since the
+// claimed tile id and the pending claim cost registers the tightest forms do not have
+template <bool BNR, int NCH, int BN, bool PIPE, int EPI, bool WIDE = false, bool DYN = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   static_assert(!BNR || EPI == 0, "the BN-backward reduction launch stores the plain product");
   static_assert(EPI < 4 || !PIPE, "mask / addend quads, the dropout hash and two accumulator sets: registers");
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   constexpr int GW = 9 * NCH * BN * 8 / NTH;                // resident weight chunks per thread
   constexpr int WTAP = NCH * BN * ROWB;
   constexpr int OFF_W = HBUF, OFF_C = OFF_W + 9 * WTAP;
-  constexpr int SMEM = OFF_C + 5 * BN * 4;                  // + per-channel epilogue constants
+  constexpr int SMEM = OFF_C + 5 * BN * 4 + 16;             // + per-channel epilogue constants, claimed-tile ring
   static_assert(GW * NTH == 9 * NCH * BN * 8, "weights must split evenly");
   static_assert(SMEM <= 160 * 1024, "LDS");
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -289,8 +291,12 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
   const int T = a.nblocks, G = gridDim.x;
   const int lin = xcd_remap(blockIdx.x, G);
-  const int nt = lin < T ? (T - lin + G - 1) / G : 0;
-  if (nt == 0) return;
+  // tiles: the static list lin, lin + G, ... (nt of them), or (dyn, conv_common.h) claimed from the counter of
+  // the block's output block: the first two in the prologue, then tile k + 2 at the start of tile k (its value
+  // is needed at the start of tile k + 1, for the halo prefetch), published at the end of tile k
+  constexpr bool dyn = DYN;
+  const int nt = dyn ? 0 : (lin < T ? (T - lin + G - 1) / G : 0);
+  if (!dyn && nt == 0) return;
   const int Wrows = (a.Nout + 63) / 64 * 64;
   // ntile_n = NT output blocks of BN channels: tile t = NT * patch + block, the grid is a multiple of
   // NT, so a block keeps one output block (its resident weights) and the blocks of a patch run side by
@@ -305,8 +311,28 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   const int nlim = a.out_mode == 2 && !second ? a.split_c : a.Nout;
   const int Cin_s = a.CAs + a.CBs;
 
+  int* ring = reinterpret_cast<int*>(smem + OFF_C + 5 * BN * 4);
+  const int npatch = T / NT;
+  if (dyn) {
+    if (tid == 0) {
+      const int t = claim_next2(a.claim + nh);
+      ring[0] = t;
+      ring[1] = t + 1;
+    }
+    __syncthreads();
+    if (ring[0] >= npatch) {   // (uniform) the work is taken: a block that started late
+      if (tid == 0) claim_block_done(a.claim, NT, G);
+      return;
+    }
+  }
+  // patch index of the block's local tile k, -1 past its end
+  auto tile_id = [&](int k) -> int {
+    if (!dyn) return k < nt ? lin / NT + k * (G / NT) : -1;
+    const int t = claim_ring_read(ring + (k & 3));
+    return t < npatch ? t : -1;
+  };
   auto tile_origin = [&](int k, int& img, int& y0, int& x0) {
-    const int t = (lin + k * G) / NT;
+    const int t = tile_id(k);
     const int px = t % tx_n, r = t / tx_n;
     y0 = (r % ty_n) * PH;
     img = r / ty_n;
@@ -503,7 +529,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   // previous tile's epilogue units run between this tile's taps -- or (!PIPE) this tile's epilogue
   auto run_tile = [&](int k, auto with_prev) {
     constexpr bool EPI_PREV = decltype(with_prev)::value;
-    const bool more = k + 1 < nt;
+    const bool more = tile_id(k + 1) >= 0;
+    // dyn: claim tile k + 2 now (a compiler-visible atomic in a file built without the atomic optimizer, whose
+    // wave form would wait for the result at once: the wait lands before its use at the end of this tile)
+    int claimed = 0;
+    if (dyn && more && tid == 0) claimed = __hip_atomic_fetch_add(a.claim + nh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int img, y0, x0;
     tile_origin(k, img, y0, x0);
     const int mrow = (img * a.Ho + y0 + wave) * a.Wo + x0;   // first output pixel of this wave's row
@@ -600,15 +630,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < GH; ++i)
         if (i * NTH + tid < HCH) *reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16) = hreg[i];
+      if (dyn && tid == 0) ring[(k + 2) & 3] = claimed;   // (slot of tile k - 2: long done)
       LDS_BAR();
     }
   };
   run_tile(0, std::false_type{});
-  for (int k = 1; k < nt; ++k) run_tile(k, std::integral_constant<bool, PIPE>{});
+  for (int k = 1; tile_id(k) >= 0; ++k) run_tile(k, std::integral_constant<bool, PIPE>{});
   if constexpr (PIPE) {   // the last tile's epilogue
     if constexpr (BNR) load_z(mrowp, zreg);
     epi_all(accp, zreg, mrowp, dreg);
   }
+  if (dyn && tid == 0) claim_block_done(a.claim, NT, G);   // (every claim of the block has returned)
   if (!stats || (a.debug_flags & 2)) return;   // (uniform)
   float* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
 #pragma unroll
@@ -700,24 +732,35 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     const int wm = option("halop_wide", 3);
     const bool wide = !bnr && (wm == 2 || (wm == 1 && !pipe) || (wm == 3 && !(pipe && (epi == 1 || epi == 3)))) &&
                       a.Nout % 8 == 0 && (a.out_mode != 2 || a.split_c % 8 == 0);
-    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
-                    pipe ? "true" : "false", epi, wide ? "true" : "false");
-#define HALOP_LAUNCH_W(NCH_, BN_, W_)                                                                       \
+    // dynamic tile claiming (option halop_claim; nullptr from claim_slot: static lists). Not the one-chunk
+    // BN-backward-reduction form nor the pipelined forms with statistics: their claimed forms spill (the
+    // latter run in the forward pass only, where no all-reduce holds CUs)
+    a.claim = option("halop_claim", 0) && nt_n + 1 <= CLAIM_INTS && !(bnr && one_chunk) && !(pipe && (epi == 1 || epi == 3))
+                  ? claim_slot() : nullptr;
+    const bool dyn = a.claim != nullptr;
+    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
+                    pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false");
+#define HALOP_LAUNCH_WD(NCH_, BN_, W_, D_)                                                                       \
   do {                                                                                                      \
-    if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0, false>), dim3(grid), dim3(512), 0, s, a); \
-    else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4, W_>), dim3(grid), dim3(512), 0, s, a); \
-    else if (epi == 5) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 5, W_>), dim3(grid), dim3(512), 0, s, a); \
+    if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0, false, D_>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 5) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 5, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
     else if (pipe) {                                                                                        \
-      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1, W_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2, W_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 3, W_>), dim3(grid), dim3(512), 0, s, a); \
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 0, W_>), dim3(grid), dim3(512), 0, s, a); \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 3, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 0, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
     } else {                                                                                                \
-      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1, W_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2, W_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3, W_>), dim3(grid), dim3(512), 0, s, a); \
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0, W_>), dim3(grid), dim3(512), 0, s, a); \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
     }                                                                                                       \
+  } while (0)
+#define HALOP_LAUNCH_W(NCH_, BN_, W_)                   \
+  do {                                                  \
+    if (dyn) HALOP_LAUNCH_WD(NCH_, BN_, W_, true);      \
+    else HALOP_LAUNCH_WD(NCH_, BN_, W_, false);         \
   } while (0)
 #define HALOP_LAUNCH(NCH_, BN_)                  \
   do {                                           \
@@ -727,6 +770,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     if (one_chunk) HALOP_LAUNCH(1, 64);
     else HALOP_LAUNCH(2, 32);
 #undef HALOP_LAUNCH_W
+#undef HALOP_LAUNCH_WD
 #undef HALOP_LAUNCH
     return 1;
   }

@@ -51,15 +51,6 @@ __device__ __forceinline__ void p_lds_add(float* p, float v) {
   const unsigned addr = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)p;
   asm volatile("ds_add_f32 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
-// the claimed-tile ring (dynamic claiming): inline-asm LDS read for the same reason (the prefetch stream is
-// in flight whenever the loader reads a tile id)
-__device__ __forceinline__ int p_lds_i32(const int* p) {
-  int r;
-  const unsigned addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr) : "memory");
-  return r;
-}
-
 #define P_BAR()                            \
   do {                                     \
     asm volatile("" ::: "memory");         \
@@ -261,7 +252,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // that step's barrier -- ahead of every reader (the loader needs tile k from step NST - 1 of tile k - 1 on)
   auto tile_id = [&](int k) -> int {
     if (!dyn) return k < mine ? lin / ntn + k * (G / ntn) : -1;
-    const int t = __builtin_amdgcn_readfirstlane(p_lds_i32(ring + (k & 3)));   // (uniform: scalar registers)
+    const int t = claim_ring_read(ring + (k & 3));   // (uniform: scalar registers)
     return t < ntm ? t : -1;   // (a claim past the last tile: the work is taken)
   };
   auto patch_t = [&](int t) {

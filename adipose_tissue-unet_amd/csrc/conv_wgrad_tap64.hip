@@ -445,7 +445,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   static_assert(GH + GD <= 2 * PH, "the next patch's LDS-DMA groups are spread over the 8 patch rows");
   static_assert(!BNA || (NW == 8 && GD * NTH == DCH), "BNA: 8 waves, whole dY groups");
   constexpr int BNA_ROW = 3;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE + (BNA ? 6 * 64 * 4 : 0)];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE + (BNA ? 6 * 64 * 4 : 0) + 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap
@@ -459,7 +459,26 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   const int lin0 = xcd_remap(blockIdx.x, gridDim.x);
   const int combo = lin0 % combos, lin = lin0 / combos;
   const int ch = combo % nch, nblk = combo / nch;
-  const int nt = lin < T ? (T - lin + G - 1) / G : 0;
+  // patches: the static list lin, lin + G, ... (nt of them), or (dyn, conv_common.h) claimed from the counter
+  // of the block's (chunk, output block) combination: the first two in the prologue, then patch k + 2 at the
+  // start of patch k (a compiler-visible atomic: this file is built without the atomic optimizer), published
+  // after the drain at the end of patch k, before its barrier
+  const bool dyn = a.claim != nullptr;
+  int* ring = reinterpret_cast<int*>(smem + 2 * STAGE + (BNA ? 6 * 64 * 4 : 0));
+  const int nt = dyn ? 0 : (lin < T ? (T - lin + G - 1) / G : 0);
+  if (dyn) {
+    if (tid == 0) {
+      const int t = claim_next2(a.claim + combo);
+      ring[0] = t;
+      ring[1] = t + 1;
+    }
+    __syncthreads();
+  }
+  auto tile_id = [&](int k) -> int {
+    if (!dyn) return k < nt ? lin + k * G : -1;
+    const int t = claim_ring_read(ring + (k & 3));
+    return t < T ? t : -1;
+  };
   const bool inA = ch * 64 < a.CAs;
   const int xcs = inA ? a.CAs : a.CBs;
   // operands through buffer resources over the whole source / dY tensors (the launcher keeps each below
@@ -498,7 +517,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   struct Patch { int y0, x0, pbx, pbd; };
   auto patch = [&](int k) {
     Patch P;
-    const int t = lin + k * G;
+    const int t = tile_id(k);
     const int px = t % tx_n, r = t / tx_n;
     const int img = r / ty_n;
     P.y0 = (r % ty_n) * PH;
@@ -662,7 +681,8 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   acc8[0] = acc8[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nb8 = wave >> 1, cb8 = 2 * (wave & 1);
 
-  if (nt > 0) {
+  const bool any = tile_id(0) >= 0;
+  if (any) {
     const Patch P0 = patch(0);
     if constexpr (BNA) {
 #pragma unroll
@@ -679,10 +699,13 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     W64_BAR();
   }
-  for (int k = 0; k < nt; ++k) {
+  for (int k = 0; any; ++k) {
     const int buf = k & 1;
-    const bool more = k + 1 < nt;
+    const bool more = tile_id(k + 1) >= 0;
     const Patch Pn = patch(more ? k + 1 : k);
+    int claimed = 0;
+    if (dyn && more && tid == 0)
+      claimed = __hip_atomic_fetch_add(a.claim + combo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (BNA) {
       int lz = lane;
       asm volatile("" : "+v"(lz));
@@ -727,8 +750,12 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next patch landed
+    if (dyn && more && tid == 0) ring[(k + 2) & 3] = claimed;   // (slot of patch k - 2: long done)
     W64_BAR();                                          // and nobody reads this buffer any more
+    if (!more) break;
   }
+  if (dyn && tid == 0) claim_block_done(a.claim, combos, gridDim.x);   // (every claim of the block has returned)
+  if (!any) return;   // (dyn: a block that started late found the work taken)
   if (a.debug_flags & 1) {
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
@@ -1124,6 +1151,8 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     const int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
     const int grid = per * combos;
     a.debug_flags = option("wgrad_debug", 0);
+    // dynamic patch claiming (option wgrad_halop_claim; nullptr from claim_slot: static lists)
+    a.claim = option("wgrad_halop_claim", 0) && combos + 1 <= CLAIM_INTS ? claim_slot() : nullptr;
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {
         adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8>");

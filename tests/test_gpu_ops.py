@@ -1220,6 +1220,102 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
 
+CLAIM_HALO_CASES = [
+    # name, source channels, Nout, forward kwargs kind
+    ("fwd_1ch_relu", [64], 64, "relu"),
+    ("fwd_1ch_128", [64], 128, "plain"),
+    ("fwd_2ch_stats", [64, 64], 128, "stats"),
+    ("fwd_2ch_bnr", [128], 64, "bnr"),
+    ("fwd_1ch_mask", [64], 64, "mask"),
+    ("fwd_2ch_split", [128], 128, "split"),
+    ("fwd_1ch_up2", [64], 64, "up"),
+    ("wgrad_1ch", [64], 64, "wgrad"),
+    ("wgrad_2src", [64, 64], 128, "wgrad"),
+    ("wgrad_bna", [64], 64, "wgrad_bna"),
+]
+
+
+@pytest.mark.parametrize("grid", [None, 7, 1], ids=["chip_grid", "7_blocks", "1_block"])
+@pytest.mark.parametrize("case", CLAIM_HALO_CASES, ids=[c[0] for c in CLAIM_HALO_CASES])
+def test_halo_kernels_claimed_match_static(case, grid):
+    """Dynamic tile claiming in the persistent halo kernels (options halop_claim, wgrad_halop_claim): the tiles a
+    block takes change, their arithmetic does not. Forward forms (plain / ReLU / statistics / BN-backward
+    reduction / mask / split / upsample gather): stored outputs bit-identical to the static lists, BatchNorm sums
+    to f32 order; weight gradient (plain, two sources, fused BN apply): dW to f32 order (per-block f32 atomics),
+    dz bit-identical. Each claimed launch runs three times (the counter slot re-zeroed by its last block)."""
+    name, parts, cout, kind = case
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(51)
+    N, H, W_ = 2, 64, 64
+    up = kind == "up"
+    Hs, Ws = (H // 2, W_ // 2) if up else (H, W_)
+    srcs = [torch.randn(N, Hs, Ws, c, generator=g).to(DEV, dt) for c in parts]
+    cin = sum(parts)
+    vec = lambda n: (torch.rand(n, generator=g) + 0.5).to(DEV)   # noqa: E731
+    wopt = "wgrad_halop_claim" if kind.startswith("wgrad") else "halop_claim"
+
+    def run():
+        if kind.startswith("wgrad"):
+            dZ = torch.randn(N, H, W_, cout, generator=torch.Generator().manual_seed(5)).to(DEV, dt)
+            dW = torch.zeros((cout, 9 * cin), device=DEV)
+            if kind == "wgrad_bna":
+                gg = torch.Generator().manual_seed(6)
+                z = (torch.randn(N, H, W_, cout, generator=gg) * 2).to(DEV, dt)
+                v = [(torch.rand(cout, generator=gg) + 0.5).to(DEV) for _ in range(7)]
+                dz = torch.zeros_like(z)
+                ops.conv_wgrad(srcs[0], dz, dW, cout, bn_apply=(dZ, z, v[0], v[1] - 1.0, v[2] - 1.0, v[3], v[4], v[5],
+                                                                 v[6], N * H * W_))
+                return [dz], [dW]
+            ops.conv_wgrad(srcs[0], dZ, dW, cout, srcB=srcs[1] if len(srcs) > 1 else None)
+            return [], [dW]
+        gw = torch.Generator().manual_seed(7)
+        Wt = (torch.randn(cout, 9 * cin, generator=gw) * 0.03).to(DEV, dt)
+        out = torch.zeros(N, H, W_, cout, dtype=dt, device=DEV)
+        st = torch.zeros(2, cout, device=DEV)
+        kw = dict(srcB=srcs[1] if len(srcs) > 1 else None, up=up)
+        outs = [out]
+        if kind == "bnr":
+            z = torch.randn(N, H, W_, cout, generator=gw).to(DEV, dt)
+            v = [(torch.rand(cout, generator=gw) + 0.5).to(DEV) for _ in range(4)]
+            ops.conv_fwd(srcs[0], Wt, cout, out=out, bn_reduce=(z, v[0], v[1] - 1.0, v[2] - 1.0, v[3], st[1], st[0]), **kw)
+        elif kind == "mask":
+            m = torch.randn(N, H, W_, cout, generator=gw).to(DEV, dt)
+            ops.conv_fwd(srcs[0], Wt, cout, out=out, mask=m, **kw)
+        elif kind == "split":
+            o2 = torch.zeros(N, H, W_, cout - 64, dtype=dt, device=DEV)
+            out = torch.zeros(N, H, W_, 64, dtype=dt, device=DEV)
+            outs = [out, o2]
+            ops.conv_fwd(srcs[0], Wt, cout, out=out, out_mode=2, out2=o2, split_c=64, **kw)
+        else:
+            b = torch.randn(cout, generator=gw).to(DEV)
+            ops.conv_fwd(srcs[0], Wt, cout, out=out, bias=b, relu=kind in ("relu", "up"),
+                         bn_stats=(st[0], st[1]) if kind == "stats" else None, **kw)
+        return outs, [st]
+
+    res = []
+    try:
+        if grid:
+            ops.set_option("halo_persist_grid", grid)
+            ops.set_option("wgrad_halop_grid", grid)
+        for claim in (0, 1, 1, 1):
+            ops.set_option(wopt, claim)
+            ex, fl = run()
+            torch.cuda.synchronize()
+            res.append((ex, fl, _lib.lib().adp_last_kernel().decode()))
+    finally:
+        for o_ in ("halo_persist_grid", "wgrad_halop_grid", wopt):
+            ops.set_option(o_, None)
+    k0 = res[0][2]
+    assert k0.startswith("igemm_wgrad_halop_kernel" if kind.startswith("wgrad") else "igemm_fwd_halop_kernel"), k0
+    for ex, fl, kn in res[1:]:
+        if not kind.startswith("wgrad") and kind != "bnr":
+            assert kn.endswith("true>"), kn   # the claimed form ran (DYN)
+        for a_, b_ in zip(ex, res[0][0]):
+            assert torch.equal(a_, b_)
+        for a_, b_ in zip(fl, res[0][1]):
+            assert relerr(a_, b_) < 1e-5
+
+
 @pytest.mark.parametrize("N,Hs,Ws,parts,cout", [(2, 8, 16, [64], 64), (1, 16, 32, [128], 128), (2, 8, 32, [192], 192)])
 def test_wgrad_persistent_halo_upsample(N, Hs, Ws, parts, cout):
     """Halo weight gradient with the nearest-x2 upsample folded into its input gather (adipose_v3's

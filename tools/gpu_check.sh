@@ -105,10 +105,10 @@ for s in $STEPS; do
         done ;;
     native) timeout -k 10 400 python -u -m pytest tests/test_gpu_native_size.py -x -v -s --timeout 200 \
               --timeout-method thread > gpurun_out/native_tests.log 2>&1 ;;
-    claimab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_claim=0;tap64p_claim=1" \
+    claimab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_claim=0;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1" \
                > gpurun_out/claim_ab.log 2>&1 ;;
-    claimprobe) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 --opt tap64p_claim=1 \
-               > gpurun_out/contention_claim.log 2>&1 ;;
+    claimprobe) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 --opt tap64p_claim=1 --opt halop_claim=1 \
+               --opt wgrad_halop_claim=1 > gpurun_out/contention_claim.log 2>&1 ;;
     contention) timeout -k 10 400 python -u tools/contention_probe.py > gpurun_out/contention.log 2>&1 ;;
     pipe2) timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L0 128,L1 128" \
           --variants "halop_pipe=1;halop_pipe=2;halop_pipe=2,halop_wide=2" > gpurun_out/pipe2_kernels.log 2>&1 ;;
