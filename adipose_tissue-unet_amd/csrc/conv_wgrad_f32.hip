@@ -234,6 +234,196 @@ __global__ void wgrad_f32_reduce_kernel(int splits, size_t slab, const float4* p
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Persistent halo form of the f32 weight gradient (3x3, stride 1, dilation 1, 'same'; f32 channel strides that are
+// multiples of 32 from one or two sources, Nout a multiple of 32; the nearest-x2 input gather of adipose_v3's
+// up*_conv1 layers): the f32 counterpart of igemm_wgrad_halop_kernel (conv_wgrad_tap64.hip). The gathered kernel
+// above re-reads every input pixel once per tap and tiles K = 9 Cin_s in 64-wide blocks that run part-empty on
+// adipose_v3's 44 * 2^l widths; here a block keeps one (32-channel input chunk, 64-channel output block) pair
+// and walks 4 x 32 output patches: per patch the 6 x 34 input halo (26 KiB) and the 128 x 64 dY tile (32 KiB)
+// are moved into LDS once by LDS-DMA (double-buffered: the next patch's pieces ride on the rows of this one),
+// and wave w keeps the 16 x 16 dW block (output rows 16 (w >> 1), input columns 16 (w & 1)) of all nine taps in
+// 36 accumulator registers. A 4-pixel k step of v_mfma_f32_16x16x4_f32 reads one f32 of dY^T and, per tap, one
+// f32 of the shifted halo (ds_read_b32, 16 consecutive channels of one pixel per 16 lanes); the 16-B chunk q of
+// row r sits at q ^ 4 (r & 1), so the two rows a 32-lane group reads fall into disjoint banks. Exact f32
+// products, f32 accumulation; one f32 atomic add per dW element and block at the end.
+constexpr int HF_PH = 4, HF_PW = 32, HF_HW = HF_PW + 2, HF_HROWS = (HF_PH + 2) * HF_HW;   // 204 halo pixels
+// LDS read with a compile-time byte offset on a per-lane base: the uniform part of every fragment address of the
+// unrolled k loop is an immediate, so the loop holds 4 base registers instead of 320 addresses
+template <int OFF>
+ADP_DEV float wf_rdo(uint32_t addr) {
+  float r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
+  return r;
+}
+// k step S of a patch (pixel row S / 8, pixels 4 (S % 8) .. + 3): dY^T element and the 9 tap-shifted halo elements
+template <int S>
+ADP_DEV void hf_read(uint32_t abase, const uint32_t (&bbase)[3], float& A, float (&B)[9]) {
+  constexpr int r = S / 8, xs = S % 8;
+  A = wf_rdo<(r * HF_PW + 4 * xs) * 256>(abase);
+  B[0] = wf_rdo<((r + 0) * HF_HW + 4 * xs) * 128>(bbase[0]);
+  B[1] = wf_rdo<((r + 0) * HF_HW + 4 * xs) * 128>(bbase[1]);
+  B[2] = wf_rdo<((r + 0) * HF_HW + 4 * xs) * 128>(bbase[2]);
+  B[3] = wf_rdo<((r + 1) * HF_HW + 4 * xs) * 128>(bbase[0]);
+  B[4] = wf_rdo<((r + 1) * HF_HW + 4 * xs) * 128>(bbase[1]);
+  B[5] = wf_rdo<((r + 1) * HF_HW + 4 * xs) * 128>(bbase[2]);
+  B[6] = wf_rdo<((r + 2) * HF_HW + 4 * xs) * 128>(bbase[0]);
+  B[7] = wf_rdo<((r + 2) * HF_HW + 4 * xs) * 128>(bbase[1]);
+  B[8] = wf_rdo<((r + 2) * HF_HW + 4 * xs) * 128>(bbase[2]);
+}
+// the 32 k steps of a patch, software-pipelined one step deep (the reads of step S + 1 in flight while step S
+// multiplies); at the first step of each pixel row the row's share of the next patch's LDS-DMA goes out
+template <int S, typename RowIssue>
+ADP_DEV void hf_steps(uint32_t abase, const uint32_t (&bbase)[3], float (&fa)[2], float (&fb)[2][9], f32x4 (&acc)[9],
+                      const RowIssue& row_issue) {
+  constexpr int NS = HF_PH * HF_PW / 4, cur = S & 1;
+  if constexpr (S % 8 == 0) row_issue(S / 8);
+  if constexpr (S + 1 < NS) {
+    hf_read<S + 1>(abase, bbase, fa[cur ^ 1], fb[cur ^ 1]);
+    wf_lgkm<10>();
+  } else {
+    wf_lgkm<0>();
+  }
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur], fb[cur][t], acc[t], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+  if constexpr (S + 1 < NS) hf_steps<S + 1>(abase, bbase, fa, fb, acc, row_issue);
+}
+__global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs a) {
+  constexpr int NTH = 512, CI = 32, NB = 64;
+  constexpr int HRB = CI * 4, DRB = NB * 4;                    // LDS row bytes: halo pixel, dY pixel
+  constexpr int NPIX = HF_PH * HF_PW;                          // 128 output pixels per patch
+  constexpr int HBUF = HF_HROWS * HRB, DBUF = NPIX * DRB, STAGE = HBUF + DBUF;
+  constexpr int HCH = HF_HROWS * (HRB / 16), DCH = NPIX * (DRB / 16);   // 16-B pieces per patch
+  constexpr int GH = (HCH + NTH - 1) / NTH, GD = DCH / NTH;
+  static_assert(GD * NTH == DCH && GH + GD <= 2 * HF_PH, "pieces: two per patch row");
+  static_assert(2 * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave >> 1, wc = wave & 1;
+  const int tx_n = a.Wo / HF_PW, ty_n = a.Ho / HF_PH;
+  const int Cin_s = a.CAs + a.CBs, nch = Cin_s / CI, nnb = (a.Nout + NB - 1) / NB, combos = nch * nnb;
+  const int T = a.Nimg * tx_n * ty_n, G = gridDim.x / combos;
+  const int lin0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int combo = lin0 % combos, lin = lin0 / combos;
+  const int ch = combo % nch, nblk = combo / nch;
+  const int nt = lin < T ? (T - lin + G - 1) / G : 0;
+  if (nt == 0) return;   // (uniform)
+  const bool inA = ch * CI < a.CAs;
+  const int xcs = inA ? a.CAs : a.CBs;
+  const int us = a.up >> 1;
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(inA ? a.srcA : a.srcB), 0, a.Nimg * a.Hs * a.Ws * xcs * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsD =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dY, 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 4, 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  // per-thread constant parts of the gathers (a halo row holds CI channels in 8 chunks, a dY row NB in 16)
+  const int xc0 = (inA ? ch * CI : ch * CI - a.CAs) * 4;
+  int hy[GH], hx[GH], hoff[GH];
+#pragma unroll
+  for (int i = 0; i < GH; ++i) {
+    const int idx = i * NTH + tid, hr = idx >> 3, pos = idx & 7;
+    hy[i] = hr / HF_HW - 1;
+    hx[i] = hr % HF_HW - 1;
+    hoff[i] = xc0 + 16 * (pos ^ (4 * (hr & 1)));
+  }
+  int dpix[GD], doff[GD];
+  bool dok[GD];
+#pragma unroll
+  for (int i = 0; i < GD; ++i) {
+    const int idx = i * NTH + tid, pr = idx >> 4, q = (idx & 15) ^ (4 * (pr & 1));
+    dpix[i] = (pr >> 5) * a.Wo + (pr & 31);
+    doff[i] = (nblk * NB + 4 * q) * 4;
+    dok[i] = nblk * NB + 4 * q < a.Nout;
+  }
+  struct Patch { int img, y0, x0, pbd; };
+  auto patch = [&](int k) {
+    Patch P;
+    const int t = lin + k * G;
+    const int px = t % tx_n, r = t / tx_n;
+    P.img = r / ty_n;
+    P.y0 = (r % ty_n) * HF_PH;
+    P.x0 = px * HF_PW;
+    P.pbd = (P.img * a.Ho + P.y0) * a.Wo + P.x0;
+    return P;
+  };
+  auto issue_h = [&](const Patch& P, int i, int buf) {
+    const int idx = i * NTH + tid;
+    if (i < GH - 1 || idx < HCH) {
+      const int gy = P.y0 + hy[i], gx = P.x0 + hx[i];
+      const bool ok = (unsigned)gy < (unsigned)(a.Hs << us) && (unsigned)gx < (unsigned)(a.Ws << us);
+      const unsigned off =
+          ok ? (unsigned)(((P.img * a.Hs + (gy >> us)) * a.Ws + (gx >> us)) * xcs * 4 + hoff[i]) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsX, (lds_void*)(smem + buf * STAGE + (size_t)(i * NTH + wave * 64) * 16),
+                                               16, off, 0, 0, 0);
+    }
+  };
+  auto issue_d = [&](const Patch& P, int i, int buf) {
+    const unsigned off = dok[i] ? (unsigned)((P.pbd + dpix[i]) * a.dy_stride * 4 + doff[i]) : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rsD, (lds_void*)(smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16), 16, off, 0, 0, 0);
+  };
+  // the next patch's pieces, two per patch row (halo first)
+  auto issue_row = [&](const Patch& P, int r, int buf) {
+#pragma unroll
+    for (int g = 0; g < GH + GD; ++g)
+      if (g / 2 == r) {
+        if (g < GH) issue_h(P, g, buf);
+        else issue_d(P, g - GH, buf);
+      }
+  };
+
+  f32x4 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int li = lane & 15, lg = lane >> 4;
+  const int ncol = wn * 16 + li, ccol = wc * 16 + li;   // this lane's dY column (output channel), X column
+  const uint32_t sbase = wf_lds(smem);
+  // per-lane parts of the fragment addresses: row r * 32 + 4 xs + lg of the dY tile, row (r + dy) * 34 + 4 xs +
+  // lg + dx of the halo; the rows' swizzle parity is that of lg (+ dx), the rest of the address is uniform
+  const uint32_t a_lane = lg * DRB + ((((ncol >> 2) ^ (4 * (lg & 1))) << 4) | ((ncol & 3) << 2));
+  uint32_t b_lane[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+    b_lane[dx] = (lg + dx) * HRB + ((((ccol >> 2) ^ (4 * ((lg + dx) & 1))) << 4) | ((ccol & 3) << 2));
+
+  {
+    const Patch P0 = patch(0);
+#pragma unroll
+    for (int i = 0; i < GH; ++i) issue_h(P0, i, 0);
+#pragma unroll
+    for (int i = 0; i < GD; ++i) issue_d(P0, i, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int k = 0; k < nt; ++k) {
+    const int buf = k & 1;
+    const bool more = k + 1 < nt;
+    const Patch Pn = patch(more ? k + 1 : k);
+    const uint32_t hb = sbase + buf * STAGE;
+    const uint32_t abase = hb + HBUF + a_lane;
+    const uint32_t bbase[3] = {hb + b_lane[0], hb + b_lane[1], hb + b_lane[2]};
+    float fa[2], fb[2][9];
+    hf_read<0>(abase, bbase, fa[0], fb[0]);
+    hf_steps<0>(abase, bbase, fa, fb, acc, [&](int r) { if (more) issue_row(Pn, r, buf ^ 1); });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next patch landed
+    __syncthreads();                                    // and nobody reads this stage any more
+  }
+  // dW[n][tap * Cin_s + ch * CI + ccol] += acc[tap][r], n = nblk * NB + wn * 16 + 4 lg + r
+  const int kc = ch * CI + ccol;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nblk * NB + wn * 16 + 4 * lg + r;
+      if (n < a.Nout) atomicAdd(a.dW + (size_t)n * a.Kpad + t * Cin_s + kc, acc[t][r]);
+    }
+}
+
 template <int WN, int WK>
 void launch_f32cfg(WgradArgs& a, hipStream_t s) {
   constexpr int TN = WN * 64, TK = WK * 64;
@@ -269,8 +459,25 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
   // opt-in: on adipose_v3's f32 layers (44 * 2^l channels, K = 9 Cin_s) its 64-granular N tiles and 128-512-wide
   // K tiles run 39-66 % full, and it measured 62-64 TF against the register-staged kernel's 84 TF
   // (profiles/r03_wgrad_f32_ab.txt)
-  if (!option("wgrad_f32", 0) || a.scA || a.scB || a.bna_dA) return 0;
+  if (a.scA || a.scB || a.bna_dA) return 0;
   const int Cin_s = a.CAs + a.CBs;
+  // the persistent halo form (option wgrad_f32_halo): 3x3 stride-1 'same' layers of 32-channel multiples
+  if (option("wgrad_f32_halo", 1) && a.kh == 3 && a.kw == 3 && a.dil == 1 && a.pad == 1 && a.stride == 1 &&
+      (a.up == 1 || a.up == 2) && a.Ho == a.Hs * a.up && a.Wo == a.Ws * a.up && a.Ho % HF_PH == 0 &&
+      a.Wo % HF_PW == 0 && a.CAs % 32 == 0 && a.CBs % 32 == 0 && a.Nout % 32 == 0 && a.dy_mode == 0 &&
+      a.K == 9 * Cin_s && a.Kpad >= a.K && a.dy_stride % 4 == 0 && a.dy_stride >= a.Nout &&
+      a.srcA && (!a.CBs || a.srcB) &&
+      (size_t)a.Nimg * a.Hs * a.Ws * std::max(a.CAs, a.CBs) * 4 < ((size_t)1 << 31) &&
+      (size_t)a.M * a.dy_stride * 4 < ((size_t)1 << 31)) {
+    const int combos = (Cin_s / 32) * ((a.Nout + 63) / 64);
+    const int tiles = a.Nimg * (a.Ho / HF_PH) * (a.Wo / HF_PW);
+    const int per = std::max(1, std::min(tiles, option("wgrad_f32_halo_grid", 256) / combos));
+    adp::set_kernel("igemm_wgrad_halo_f32_kernel");
+    hipLaunchKernelGGL(igemm_wgrad_halo_f32_kernel, dim3(per * combos), dim3(512), 0, s, a);
+    adp::kernel_end();
+    return 1;
+  }
+  if (!option("wgrad_f32", 0)) return 0;
   if (a.CAs % 4 != 0 || a.CBs % 4 != 0 || a.K != a.kh * a.kw * Cin_s || a.Kpad % 4 != 0 || a.Kpad < a.K ||
       a.dy_stride % 4 != 0 || a.Nout % 4 != 0 || (a.dy_mode == 1 && a.Cps % 4 != 0))
     return 0;

@@ -1220,6 +1220,58 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
 
+F32_HALO_WGRAD_CASES = [
+    # name, N, H, W (output grid), source channel strides, Nout, up
+    ("c64_64", 2, 32, 64, [64], 64, False),
+    ("c96_96_ragged_n", 1, 16, 64, [96], 96, False),
+    ("concat_64_64", 2, 16, 32, [64, 64], 64, False),
+    ("up2_96_64", 2, 32, 64, [96], 64, True),
+    ("up2_352_192", 1, 16, 32, [352], 192, True),
+    ("c192_352", 1, 8, 32, [192], 352, False),
+]
+
+
+@pytest.mark.parametrize("case", F32_HALO_WGRAD_CASES, ids=[c[0] for c in F32_HALO_WGRAD_CASES])
+def test_wgrad_f32_halo(case):
+    """Persistent halo form of the f32 weight gradient (igemm_wgrad_halo_f32_kernel: 32-channel input chunks,
+    64-wide output blocks, 4 x 32 patches, exact v_mfma_f32_16x16x4_f32) vs autograd of the fp32 oracle conv
+    (<= 1e-4 of the largest element) and vs the register-staged f32 kernel (option wgrad_f32_halo=0) on the
+    same operands: adipose_v3's f32 channel strides (64 / 96 / 192 / 352: Nout not a multiple of 64 leaves a
+    part-empty output block), a concat input, the nearest-x2 input gather of the up*_conv1 layers."""
+    name, N, H, W_, parts, cout, up = case
+    g = torch.Generator().manual_seed(61)
+    Hs, Ws = (H // 2, W_ // 2) if up else (H, W_)
+    xs = [torch.randn(N, Hs, Ws, c, generator=g) for c in parts]
+    dZ = torch.randn(N, H, W_, cout, generator=g)
+    cin = sum(parts)
+    kern = (torch.randn(3, 3, cin, cout, generator=g) * 0.05).requires_grad_(True)
+    x = torch.cat(xs, -1)
+    if up:
+        x = R.upsample_nearest2(x)
+    (R.conv2d_same(x, kern, None, relu=False) * dZ).sum().backward()
+    xd = [t.to(DEV).contiguous() for t in xs]
+    dzd = torch.zeros(N, H, W_, cout, device=DEV)   # (the network's dZ stride: cout_s)
+    dzd[..., :cout] = dZ.to(DEV)
+    K = 9 * cin
+    res = []
+    for halo in (1, 0):
+        dW = torch.zeros(((cout + 63) // 64 * 64, K), device=DEV)
+        ops.set_option("wgrad_f32_halo", halo)
+        try:
+            ops.conv_wgrad(xd[0], dzd, dW, cout, srcB=xd[1] if len(xd) > 1 else None, up=up)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("wgrad_f32_halo", None)
+        res.append((dW[:cout].cpu(), kname))
+    assert res[0][1] == "igemm_wgrad_halo_f32_kernel", res[0][1]
+    assert res[1][1] != "igemm_wgrad_halo_f32_kernel", res[1][1]
+    # packed [n][tap * Cin + c] -> Keras (ky, kx, c, n)
+    got = res[0][0].view(cout, 3, 3, cin).permute(1, 2, 3, 0)
+    assert relerr(got, kern.grad) < 1e-4, relerr(got, kern.grad)
+    assert relerr(res[0][0], res[1][0]) < 1e-5
+
+
 CLAIM_HALO_CASES = [
     # name, source channels, Nout, forward kwargs kind
     ("fwd_1ch_relu", [64], 64, "relu"),
