@@ -866,8 +866,8 @@ def test_halop_wide_store_matches(case, grid):
         finally:
             ops.set_option("halop_wide", None)
             ops.set_option("halo_persist_grid", None)
-        # igemm_fwd_halop_kernel<BNR, NCH, BN, PIPE, EPI, WIDE>
-        assert kname.startswith("igemm_fwd_halop_kernel") and kname.split(", ")[5] == ("true>" if wide else "false>"), kname
+        # igemm_fwd_halop_kernel<BNR, NCH, BN, PIPE, EPI, WIDE, DYN>
+        assert kname.startswith("igemm_fwd_halop_kernel") and kname.split(", ")[5] == ("true" if wide else "false"), kname
         res.append(([t.clone() for t in outs], st.clone()))
     for a_, b_ in zip(res[0][0], res[1][0]):
         assert torch.equal(a_, b_), (a_.double() - b_.double()).abs().max().item()
@@ -1001,12 +1001,14 @@ def test_wgrad_f32_lds_kernel(case):
         dW = torch.zeros(nout, (K + 31) // 32 * 32, device=DEV)
         dB = torch.zeros(shuf if shuf else nout, device=DEV)
         ops.set_option("wgrad_f32", f32k)
+        ops.set_option("wgrad_f32_halo", 0)   # (the persistent halo form has its own test)
         try:
             ops.conv_wgrad(xa.to(DEV), dY.to(DEV), dW, nout, dB=dB, **kw)
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
             ops.set_option("wgrad_f32", None)
+            ops.set_option("wgrad_f32_halo", None)
         assert kname.startswith("igemm_wgrad_f32_kernel") == bool(f32k), kname
         res.append((dW.cpu().double(), dB.cpu().double()))
     (w1, b1), (w0, b0) = res
