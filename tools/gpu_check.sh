@@ -109,6 +109,11 @@ for s in $STEPS; do
               --timeout-method thread > gpurun_out/native_tests.log 2>&1 ;;
     claimab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_claim=0;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1" \
                > gpurun_out/claim_ab.log 2>&1 ;;
+    claimk) timeout -k 10 400 python tools/bench_kernels.py --kinds fwd,fwd_stats,bnr,wgrad \
+              --layers "L0 64->64,L0 128->64,L1 128->128,L2 256->256,L3 512->512,L4 1024->1024" \
+              --variants "tap64p_claim=0,halop_claim=0,wgrad_halop_claim=0;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1" \
+              > gpurun_out/claim_kernels.log 2>&1 ;;
+    probe0) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 > gpurun_out/contention_static.log 2>&1 ;;
     claimprobe) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 --opt tap64p_claim=1 --opt halop_claim=1 \
                --opt wgrad_halop_claim=1 > gpurun_out/contention_claim.log 2>&1 ;;
     contention) timeout -k 10 400 python -u tools/contention_probe.py > gpurun_out/contention.log 2>&1 ;;
