@@ -44,6 +44,7 @@ struct FwdArgs {
   int defer_fold;        // bn_sum launch whose replica sums adp_bn_finalize_fold adds in (adp_conv_desc)
   int f32;               // f32 launch on the LDS-DMA tap kernel (32-channel K steps, f32 MFMA)
   int* claim;            // persistent kernels: dynamic tile claiming counters (adp::claim_slot), nullptr = static lists
+  int claim_chunk;       // tiles per claim (halo forward: consecutive patches taken together)
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
@@ -67,6 +68,7 @@ struct WgradArgs {
   const float* bna_gamma; const float* bna_dgamma; const float* bna_dbeta;
   float bna_inv_count;
   int* claim;           // persistent halo weight gradient: dynamic tile claiming counters (nullptr: static lists)
+  int claim_chunk;      // patches per claim
 };
 
 // LDS-only workgroup barrier for epilogues: this wave's LDS traffic complete, then s_barrier. Unlike
@@ -168,11 +170,15 @@ ADP_DEV int claim_issue(int* cnt) {
   asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(r) : "v"(cnt), "v"(1) : "memory");
   return r;
 }
+// (NYOUNG < 0: the caller's own wait already covers the atomic -- no vmcnt wait here)
 template <int NYOUNG>
 ADP_DEV void claim_publish(int* lds, int r) {
   const unsigned addr = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
-  asm volatile("s_waitcnt vmcnt(%2)\n\tds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r),
-               "n"(NYOUNG < 63 ? NYOUNG : 0) : "memory");
+  if constexpr (NYOUNG < 0)
+    asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%2)\n\tds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r),
+                 "n"(NYOUNG < 63 ? NYOUNG : 0) : "memory");
 }
 // every block calls this exactly once, after its last claim (thread 0; nclaim counters + the done count)
 ADP_DEV void claim_block_done(int* claim, int nclaim, int G) {

@@ -291,9 +291,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
   const int T = a.nblocks, G = gridDim.x;
   const int lin = xcd_remap(blockIdx.x, G);
-  // tiles: the static list lin, lin + G, ... (nt of them), or (dyn, conv_common.h) claimed from the counter of
-  // the block's output block: the first two in the prologue, then tile k + 2 at the start of tile k (its value
-  // is needed at the start of tile k + 1, for the halo prefetch), published at the end of tile k
+  // tiles: the static list lin, lin + G, ... (nt of them), or (dyn, conv_common.h) super-tiles of CH consecutive
+  // patches claimed from the counter of the block's output block: super-tiles 0 and 1 are the block's static
+  // ones (nothing to wait for at the start), claim value c is super-tile 2 G / NT + c; super-tile s + 2 is
+  // claimed at the start of super-tile s and published at the end of its first tile (the halo prefetch needs a
+  // tile's successor at the start of the tile)
   constexpr bool dyn = DYN;
   const int nt = dyn ? 0 : (lin < T ? (T - lin + G - 1) / G : 0);
   if (!dyn && nt == 0) return;
@@ -313,23 +315,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 
   int* ring = reinterpret_cast<int*>(smem + OFF_C + 5 * BN * 4);
   const int npatch = T / NT;
-  if (dyn) {
-    if (tid == 0) {
-      const int t = claim_next2(a.claim + nh);
-      ring[0] = t;
-      ring[1] = t + 1;
-    }
-    __syncthreads();
-    if (ring[0] >= npatch) {   // (uniform) the work is taken: a block that started late
-      if (tid == 0) claim_block_done(a.claim, NT, G);
-      return;
-    }
-  }
+  const int CH = dyn ? a.claim_chunk : 1, nsup = (npatch + CH - 1) / CH;
+  auto sup_id = [&](int sidx) -> int {   // dyn: super-tile index of the block's local super-tile sidx, -1 past the end
+    const int v = sidx < 2 ? lin / NT + sidx * (G / NT) : 2 * (G / NT) + claim_ring_read(ring + (sidx & 3));
+    return v < nsup ? v : -1;
+  };
   // patch index of the block's local tile k, -1 past its end
   auto tile_id = [&](int k) -> int {
     if (!dyn) return k < nt ? lin / NT + k * (G / NT) : -1;
-    const int t = claim_ring_read(ring + (k & 3));
-    return t < npatch ? t : -1;
+    const int v = sup_id(k / CH);
+    const int t = v * CH + k % CH;
+    return v >= 0 && t < npatch ? t : -1;
   };
   auto tile_origin = [&](int k, int& img, int& y0, int& x0) {
     const int t = tile_id(k);
@@ -532,8 +528,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     const bool more = tile_id(k + 1) >= 0;
     // dyn: claim tile k + 2 now (a compiler-visible atomic in a file built without the atomic optimizer, whose
     // wave form would wait for the result at once: the wait lands before its use at the end of this tile)
+    // (a claim is published at the end of this tile, inside `if (more)`: claim_now implies more)
+    const bool claim_now = dyn && k % CH == 0 && more && sup_id(k / CH + 1) >= 0;
     int claimed = 0;
-    if (dyn && more && tid == 0) claimed = __hip_atomic_fetch_add(a.claim + nh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (claim_now && tid == 0) claimed = __hip_atomic_fetch_add(a.claim + nh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int img, y0, x0;
     tile_origin(k, img, y0, x0);
     const int mrow = (img * a.Ho + y0 + wave) * a.Wo + x0;   // first output pixel of this wave's row
@@ -630,7 +628,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < GH; ++i)
         if (i * NTH + tid < HCH) *reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16) = hreg[i];
-      if (dyn && tid == 0) ring[(k + 2) & 3] = claimed;   // (slot of tile k - 2: long done)
+      if (claim_now && tid == 0) ring[(k / CH + 2) & 3] = claimed;   // (slot of super-tile s - 2: long done)
       LDS_BAR();
     }
   };
@@ -737,6 +735,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     // latter run in the forward pass only, where no all-reduce holds CUs)
     a.claim = option("halop_claim", 0) && nt_n + 1 <= CLAIM_INTS && !(bnr && one_chunk) && !(pipe && (epi == 1 || epi == 3))
                   ? claim_slot() : nullptr;
+    a.claim_chunk = std::max(1, option("halop_claim_chunk", 4));   // patches per claim
     const bool dyn = a.claim != nullptr;
     adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
                     pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false");

@@ -155,18 +155,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     sacc[1][tid] = 0.f;
   }
   // (ordered before the epilogue by the first K step's barrier)
-  if (dyn) {   // the first two tiles, before anything is staged (claims of one tile then follow in the K loop)
-    if (tid == 0) {
-      const int t = claim_next2(a.claim + col);
-      ring[0] = t;
-      ring[1] = t + 1;
-    }
-    __syncthreads();
-    if (ring[0] >= ntm) {   // (uniform) every tile is taken: a block that started late
-      if (tid == 0) claim_block_done(a.claim, ntn, G);
-      return;
-    }
-  }
+  // dyn: a block's first tile is its static one (lin / ntn: no claim to wait for at the start); claim value c is
+  // tile G / ntn + c
 
   const int npix = a.Nimg * a.Hs * a.Ws;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.srcA, 0, npix * a.CAs * ES, P_RSRC3);
@@ -252,7 +242,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // that step's barrier -- ahead of every reader (the loader needs tile k from step NST - 1 of tile k - 1 on)
   auto tile_id = [&](int k) -> int {
     if (!dyn) return k < mine ? lin / ntn + k * (G / ntn) : -1;
-    const int t = claim_ring_read(ring + (k & 3));   // (uniform: scalar registers)
+    if (k == 0) return lin / ntn;
+    const int t = G / ntn + claim_ring_read(ring + (k & 3));   // (uniform: scalar registers)
     return t < ntm ? t : -1;   // (a claim past the last tile: the work is taken)
   };
   auto patch_t = [&](int t) {
@@ -749,6 +740,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     for (int g = 0; g < GH; ++g) issue_halo(t0, 0, g, 0);
   }
   if constexpr (WREG) load_w(0);   // (the first load_next stores them into stage 0)
+  // dyn: the claim of tile 1 goes out before the prologue's stages, so the wait at the top of step 0 covers it
+  int c1val = 0;
+  if (dyn && tid == 0) c1val = claim_issue(a.claim + col);
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i) load_next();
   int gs = 0, cs = 0, last_epi = -NST;   // step, its stage, step of the latest epilogue
@@ -800,6 +794,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
       else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
+      if (dyn && gs == 0 && tid == 0) claim_publish<-1>(ring + 1, c1val);   // tile 1 (claimed in the prologue)
       // (timing-only ablation, fwd_debug bit 9: no barrier -- the stages race, the values are garbage)
       if (!(a.debug_flags & 512)) P_BAR();   // stage cs landed for every wave, nobody reads the stage being refilled
       if constexpr (ZALL) {

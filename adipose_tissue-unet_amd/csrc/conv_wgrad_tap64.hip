@@ -459,25 +459,24 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   const int lin0 = xcd_remap(blockIdx.x, gridDim.x);
   const int combo = lin0 % combos, lin = lin0 / combos;
   const int ch = combo % nch, nblk = combo / nch;
-  // patches: the static list lin, lin + G, ... (nt of them), or (dyn, conv_common.h) claimed from the counter
-  // of the block's (chunk, output block) combination: the first two in the prologue, then patch k + 2 at the
-  // start of patch k (a compiler-visible atomic: this file is built without the atomic optimizer), published
-  // after the drain at the end of patch k, before its barrier
+  // patches: the static list lin, lin + G, ... (nt of them), or (dyn, conv_common.h) super-patches of CH
+  // consecutive patches claimed from the counter of the block's (chunk, output block) combination: super-patches
+  // 0 and 1 are the block's static ones, claim value c is super-patch 2 G + c; super-patch s + 2 is claimed at the
+  // start of super-patch s (a compiler-visible atomic: this file is built without the atomic optimizer) and
+  // published after the drain at the end of its first patch, before that patch's barrier
   const bool dyn = a.claim != nullptr;
   int* ring = reinterpret_cast<int*>(smem + 2 * STAGE + (BNA ? 6 * 64 * 4 : 0));
   const int nt = dyn ? 0 : (lin < T ? (T - lin + G - 1) / G : 0);
-  if (dyn) {
-    if (tid == 0) {
-      const int t = claim_next2(a.claim + combo);
-      ring[0] = t;
-      ring[1] = t + 1;
-    }
-    __syncthreads();
-  }
+  const int CH = dyn ? a.claim_chunk : 1, nsup = (T + CH - 1) / CH;
+  auto sup_id = [&](int sidx) -> int {
+    const int v = sidx < 2 ? lin + sidx * G : 2 * G + claim_ring_read(ring + (sidx & 3));
+    return v < nsup ? v : -1;
+  };
   auto tile_id = [&](int k) -> int {
     if (!dyn) return k < nt ? lin + k * G : -1;
-    const int t = claim_ring_read(ring + (k & 3));
-    return t < T ? t : -1;
+    const int v = sup_id(k / CH);
+    const int t = v * CH + k % CH;
+    return v >= 0 && t < T ? t : -1;
   };
   const bool inA = ch * 64 < a.CAs;
   const int xcs = inA ? a.CAs : a.CBs;
@@ -703,8 +702,9 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     const int buf = k & 1;
     const bool more = tile_id(k + 1) >= 0;
     const Patch Pn = patch(more ? k + 1 : k);
+    const bool claim_now = dyn && k % CH == 0 && more && sup_id(k / CH + 1) >= 0;
     int claimed = 0;
-    if (dyn && more && tid == 0)
+    if (claim_now && tid == 0)
       claimed = __hip_atomic_fetch_add(a.claim + combo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (BNA) {
       int lz = lane;
@@ -750,7 +750,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next patch landed
-    if (dyn && more && tid == 0) ring[(k + 2) & 3] = claimed;   // (slot of patch k - 2: long done)
+    if (claim_now && tid == 0) ring[(k / CH + 2) & 3] = claimed;   // (slot of super-patch s - 2: long done)
     W64_BAR();                                          // and nobody reads this buffer any more
     if (!more) break;
   }
@@ -1153,6 +1153,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     a.debug_flags = option("wgrad_debug", 0);
     // dynamic patch claiming (option wgrad_halop_claim; nullptr from claim_slot: static lists)
     a.claim = option("wgrad_halop_claim", 0) && combos + 1 <= CLAIM_INTS ? claim_slot() : nullptr;
+    a.claim_chunk = std::max(1, option("wgrad_halop_claim_chunk", 4));   // patches per claim
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {
         adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8>");

@@ -104,7 +104,7 @@ for s in $STEPS; do
           timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_wide_f8=1 > gpurun_out/f8wide_on_$i.log 2>&1 || exit 1
         done ;;
     quick) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
-             -k "wide_store or f32_lds or f32_halo or claim" > gpurun_out/quick_tests.log 2>&1 ;;
+             -k "wide_store or f32_lds or f32_halo or claim or halop or wgrad_persistent or tap64p" > gpurun_out/quick_tests.log 2>&1 ;;
     native) timeout -k 10 400 python -u -m pytest tests/test_gpu_native_size.py -x -v -s --timeout 200 \
               --timeout-method thread > gpurun_out/native_tests.log 2>&1 ;;
     claimab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_claim=0;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1" \
