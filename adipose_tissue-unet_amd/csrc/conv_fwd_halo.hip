@@ -327,6 +327,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     const int t = v * CH + k % CH;
     return v >= 0 && t < npatch ? t : -1;
   };
+  if (dyn && tile_id(0) < 0) {   // (uniform) more blocks than super-tiles: nothing static for this one
+    if (tid == 0) claim_block_done(a.claim, NT, G);
+    return;
+  }
   auto tile_origin = [&](int k, int& img, int& y0, int& x0) {
     const int t = tile_id(k);
     const int px = t % tx_n, r = t / tx_n;
@@ -736,6 +740,10 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     a.claim = option("halop_claim", 0) && nt_n + 1 <= CLAIM_INTS && !(bnr && one_chunk) && !(pipe && (epi == 1 || epi == 3))
                   ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("halop_claim_chunk", 4));   // patches per claim
+    if (a.claim) {   // (no more blocks per output block than super-tiles)
+      const int nsup = (tiles / nt_n + a.claim_chunk - 1) / a.claim_chunk;
+      grid = std::max(nt_n, std::min(grid, nsup * nt_n));
+    }
     const bool dyn = a.claim != nullptr;
     adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
                     pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false");

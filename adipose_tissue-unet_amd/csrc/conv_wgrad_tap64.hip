@@ -1148,12 +1148,13 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   if (halop_ok(a)) {   // option wgrad_halop: 0 off, else every eligible shape
     const int combos = (cin / 64) * (a.Nout / 64);
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
-    const int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
-    const int grid = per * combos;
+    int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
     a.debug_flags = option("wgrad_debug", 0);
     // dynamic patch claiming (option wgrad_halop_claim; nullptr from claim_slot: static lists)
     a.claim = option("wgrad_halop_claim", 0) && combos + 1 <= CLAIM_INTS ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("wgrad_halop_claim_chunk", 4));   // patches per claim
+    if (a.claim) per = std::min(per, (tiles + a.claim_chunk - 1) / a.claim_chunk);   // (<= super-patches)
+    const int grid = per * combos;
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {
         adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8>");
