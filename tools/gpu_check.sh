@@ -113,6 +113,10 @@ for s in $STEPS; do
               --layers "L0 64->64,L0 128->64,L1 128->128,L2 256->256,L3 512->512,L4 1024->1024" \
               --variants "tap64p_claim=0,halop_claim=0,wgrad_halop_claim=0;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1" \
               > gpurun_out/claim_kernels.log 2>&1 ;;
+    claimchunk) timeout -k 10 400 python tools/bench_kernels.py --kinds fwd,wgrad \
+              --layers "L0 64->64,L0 128->64,L1 128->128,L2 256->256" \
+              --variants "halop_claim=0,wgrad_halop_claim=0;halop_claim=1,wgrad_halop_claim=1,halop_claim_chunk=1,wgrad_halop_claim_chunk=1;halop_claim=1,wgrad_halop_claim=1;halop_claim=1,wgrad_halop_claim=1,halop_claim_chunk=16,wgrad_halop_claim_chunk=16;halop_claim=1,wgrad_halop_claim=1,halop_claim_chunk=64,wgrad_halop_claim_chunk=64" \
+              > gpurun_out/claim_chunk.log 2>&1 ;;
     probe0) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 > gpurun_out/contention_static.log 2>&1 ;;
     claimprobe) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 --opt tap64p_claim=1 --opt halop_claim=1 \
                --opt wgrad_halop_claim=1 > gpurun_out/contention_claim.log 2>&1 ;;
