@@ -737,7 +737,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     // dynamic tile claiming (option halop_claim; nullptr from claim_slot: static lists). Not the one-chunk
     // BN-backward-reduction form nor the pipelined forms with statistics: their claimed forms spill (the
     // latter run in the forward pass only, where no all-reduce holds CUs)
-    a.claim = option("halop_claim", 0) && nt_n + 1 <= CLAIM_INTS && !(bnr && one_chunk) && !(pipe && (epi == 1 || epi == 3))
+    a.claim = option("halop_claim", option("dp_claim", 0)) && nt_n + 1 <= CLAIM_INTS && !(bnr && one_chunk) && !(pipe && (epi == 1 || epi == 3))
                   ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("halop_claim_chunk", 4));   // patches per claim
     if (a.claim) {   // (no more blocks per output block than super-tiles)

@@ -909,7 +909,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   if (grid <= 0) grid = a.ntile_n;
   // dynamic tile claiming (option tap64p_claim): robust to CUs held by another stream's kernels (RCCL)
   a.claim = nullptr;
-  if (option("tap64p_claim", 0) && a.ntile_n + 1 <= CLAIM_INTS) a.claim = claim_slot();   // (nullptr: static lists)
+  if (option("tap64p_claim", option("dp_claim", 0)) && a.ntile_n + 1 <= CLAIM_INTS) a.claim = claim_slot();   // (nullptr: static lists)
   const bool bnr = a.bnr_z != nullptr;
   // the halo form (option tap64p_halo): 3x3 stride-1 'same' layers whose output tiles into 8 x 32 patches
   const bool halo_shape = !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&

@@ -1151,7 +1151,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     int per = std::max(1, std::min(tiles, option("wgrad_halop_grid", 256) / combos));
     a.debug_flags = option("wgrad_debug", 0);
     // dynamic patch claiming (option wgrad_halop_claim; nullptr from claim_slot: static lists)
-    a.claim = option("wgrad_halop_claim", 0) && combos + 1 <= CLAIM_INTS ? claim_slot() : nullptr;
+    a.claim = option("wgrad_halop_claim", option("dp_claim", 0)) && combos + 1 <= CLAIM_INTS ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("wgrad_halop_claim_chunk", 4));   // patches per claim
     if (a.claim) per = std::min(per, (tiles + a.claim_chunk - 1) / a.claim_chunk);   // (<= super-patches)
     const int grid = per * combos;
