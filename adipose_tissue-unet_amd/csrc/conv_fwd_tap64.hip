@@ -456,6 +456,8 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   // the persistent kernel for the 256x256 and 256x128 tiles (BNR launches: option tap64p_bnr)
   if ((cfg == 0 || cfg == 1) && !a.f8 && !a.f32 && (!a.bnr_z || option("tap64p_bnr", 1)) && launch_fwd_tap64p(a, s, cfg))
     return 1;
+  // f32: the persistent halo form for the 256x128 choice (3x3 stride-1 layers; falls through otherwise)
+  if (cfg == 1 && a.f32 && launch_fwd_tap64p(a, s, 1)) return 1;
   a.kpipe = option("tap64_kpipe", 0);   // (opt-in: +1-1.5 % on the BN-backward data gradients, profiles/r03_kpipe_ab.txt)
   if (a.f32 && cfg == 0) cfg = 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);

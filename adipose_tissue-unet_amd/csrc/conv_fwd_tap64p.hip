@@ -86,12 +86,19 @@ __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_ha
 // registers one step ahead (4 x 16-B buffer loads per thread) and written into the free stage with ds_write
 // when the step is issued: the LDS-DMA issue (60-185 cycles per 1-KiB wave piece, what the K loop waited on:
 // profiles/r02_tap64p_halo_ablation.txt) is left to the <= 1 halo group per step.
-template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false>
+// F32 (halo form, 256x128 / 3 stages; the f32 path of adipose_v3, every drop-in CLI's default dtype): the same
+// byte schedule with 32-channel K steps (a 128-B row is 32 f32 channels). The two 16-B fragments a lane reads per
+// row are 8 f32 of k = 16 s + 4 h4 + e (s = 0, 1; e = 0..3): eight exact v_mfma_f32_16x16x4_f32 per 16x16 block,
+// the e-th of half s taking element e -- lane group h4 then supplies k = 16 s + 4 h4 + e to it, and A and B share
+// that permutation, so every k of the step enters the dot product once. f32 epilogue: 16-B stores of a lane's
+// channel quad.
+template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false, bool F32 = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   static_assert(!F8 || !BNR, "fp8: no BN-backward reduction");
   static_assert(!WREG || (HALO && NST == 2 && !F8), "register-staged weights: the bf16 2-stage halo form");
-  constexpr int NTH = 512, ROWB = 128, ES = F8 ? 1 : 2, KSTEP = F8 ? 128 : 64;
-  constexpr int OES = 2;   // output / z element bytes (bf16)
+  static_assert(!F32 || (HALO && !BNR && !F8 && !WREG), "f32: the halo form");
+  constexpr int NTH = 512, ROWB = 128, ES = F8 ? 1 : (F32 ? 4 : 2), KSTEP = F8 ? 128 : (F32 ? 32 : 64);
+  constexpr int OES = F32 ? 4 : 2;   // output / z element bytes (bf16; f32)
   constexpr int WN = BN / 64, WM = 8 / WN, TM = BM / WM;
   static_assert(WN * WM == 8 && TM % 32 == 0 && TM >= 64, "wave layout");
   static_assert(!HALO || (!BNR && BM == 256 && ((BN == 256 && NST == 2) || (BN == 128 && NST == 3))),
@@ -454,6 +461,21 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       prio_lo<ADP_PRIO_FWD>();
       return;
     }
+    if constexpr (F32) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              acc[ha * MIQ + mi][hb * 2 + ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                  __builtin_bit_cast(f32x4, fb[ni][s])[e], __builtin_bit_cast(f32x4, fa[mi][s])[e],
+                  acc[ha * MIQ + mi][hb * 2 + ni], 0, 0, 0);
+      prio_lo<ADP_PRIO_FWD>();
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -562,8 +584,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           if (a.relu) x[r] = fmaxf(x[r], 0.f);
         }
         bf16x4 o;
+        if constexpr (!F32) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)x[r];
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)x[r];
+        }
         int pix = m;
         if (shuffle) {
           const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
@@ -571,7 +595,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         }
         // (timing-only ablation, fwd_debug bit 7: every store to an out-of-range offset, dropped)
         const unsigned off = v && !(a.debug_flags & 128) ? (unsigned)((pix * ostr + cq) * oes) : P_OOB;
-        if (o8) {   // 4 channels -> 4 e4m3 bytes (f8x8_from_f's saturating encode)
+        if constexpr (F32) {
+          const f32x4 o4 = {x[0], x[1], x[2], x[3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, o4), rsO, off, 0, 0);
+        } else if (o8) {   // 4 channels -> 4 e4m3 bytes (f8x8_from_f's saturating encode)
           float c8[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) c8[r] = fminf(fmaxf(x[r], -FP8_MAX), FP8_MAX);
@@ -617,7 +644,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // 16-B store per (pixel, pair of groups) instead of two 8-B ones, 64 contiguous bytes of a pixel per
   // instruction instead of 32. Needs Nout % 16 == 0 and a split point on a 32-channel boundary (host).
   auto epilogue_wide = [&](int m0) {
-    if constexpr (!BNR) {
+    if constexpr (!BNR && !F32) {
       int tidv = tid;
       asm volatile("" : "+v"(tidv));
       const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
@@ -698,7 +725,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       }
     }
   };
-  const bool wide = !BNR && a.wide_st;   // (fp8: bf16 output only, the launcher checks)
+  const bool wide = !BNR && !F32 && a.wide_st;   // (fp8: bf16 output only, the launcher checks)
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
@@ -868,17 +895,20 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
                a.CAs % 128 != 0 || a.CBs % 128 != 0))
     return 0;
   if (a.addend || a.mask || a.mask2 || a.accum || a.drop_rate > 0.f || a.scA || a.scB) return 0;
+  // f32: the 256x128 halo form (the tap64 256x128 choice, option tap64p_f32), no BN-backward reduction
+  if (a.f32 && (!option("tap64p_f32", 1) || tile != 1 || a.bnr_z)) return 0;
   if (a.up != 1 && (a.up != 2 || a.bnr_z)) return 0;   // up = 2: the halo form only (below)
   if (a.out_mode == 1 && (a.Cps % 8 != 0 || a.Nout % a.Cps != 0)) return 0;
   if (a.out_mode == 2 && (a.split_c % 16 != 0 || a.out2_stride % 8 != 0)) return 0;
   if (a.out_stride % 8 != 0 || (a.bnr_z && a.bnr_zs % 8 != 0)) return 0;
   const int Cin_s = a.CAs + a.CBs;
-  if (a.CAs % 64 != 0 || a.CBs % 64 != 0 || a.K != a.kh * a.kw * Cin_s || a.K % 64 != 0 || a.Kpad != a.K) return 0;
+  const int ks = a.f32 ? 32 : 64, es = a.f32 ? 4 : 2;   // K-step channels (bf16 / f32), element bytes
+  if (a.CAs % ks != 0 || a.CBs % ks != 0 || a.K != a.kh * a.kw * Cin_s || a.K % ks != 0 || a.Kpad != a.K) return 0;
   // buffer-resource offsets: every operand below 2 GiB
   const size_t lim = (size_t)1 << 31, pix = (size_t)a.Nimg * a.Hs * a.Ws;
-  const size_t outb = a.out_mode == 1 ? (size_t)a.M * 4 * a.out_stride * 2 : (size_t)a.M * a.out_stride * 2;
-  if (pix * a.CAs * 2 >= lim || pix * a.CBs * 2 >= lim || outb >= lim ||
-      (size_t)((a.Nout + 63) / 64 * 64) * a.Kpad * 2 >= lim || (a.out2 && (size_t)a.M * a.out2_stride * 2 >= lim) ||
+  const size_t outb = a.out_mode == 1 ? (size_t)a.M * 4 * a.out_stride * es : (size_t)a.M * a.out_stride * es;
+  if (pix * a.CAs * es >= lim || pix * a.CBs * es >= lim || outb >= lim ||
+      (size_t)((a.Nout + 63) / 64 * 64) * a.Kpad * es >= lim || (a.out2 && (size_t)a.M * a.out2_stride * es >= lim) ||
       (a.bnr_z && (size_t)a.M * a.bnr_zs * 2 >= lim))
     return 0;
   // auto (tools/bench_kernels.py, bench_convt.py; profiles/r02_tap64p_cfg_ab.txt): the tap64 256x128 choice
@@ -892,7 +922,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // (a software-pipelined K loop -- barrier in the middle of the previous step, B half 0 preloaded -- measured
   //  1.5-5 % slower here and was removed: profiles/r03_kpipe_ab.txt)
   // fp8 launches with a bf16 output take them too (option tap64p_wide_f8); fp8 outputs keep 4-B stores
-  a.wide_st = option("tap64p_wide", 1) && (!a.f8 || (option("tap64p_wide_f8", 0) && !a.out_f8)) && !a.bnr_z &&
+  a.wide_st = option("tap64p_wide", 1) && !a.f32 && (!a.f8 || (option("tap64p_wide_f8", 0) && !a.out_f8)) && !a.bnr_z &&
               a.Nout % 16 == 0 &&
               (a.out_mode != 2 || a.split_c % 32 == 0);
   int cfg = option("tap64p_cfg", 0);
@@ -916,6 +946,13 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
                           a.dil == 1 && a.pad == 1 && a.stride == 1 && a.Ho == a.Hs * a.up && a.Wo == a.Ws * a.up &&
                           a.Ho % 8 == 0 && a.Wo % 32 == 0;
   if (a.up != 1 && !(halo_shape && (cfg == 1 || (cfg == 2 && option("tap64p_halo128", 1))))) return 0;
+  if (a.f32) {
+    if (!halo_shape || cfg != 2) return 0;
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true>");
+    hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true>), dim3(grid), dim3(512), 0,
+                       s, a);
+    return 1;
+  }
   if (a.f8 && !(halo_shape && (cfg == 1 || cfg == 2))) {   // gather form (ConvTranspose, fp8 output)
     adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, true, false>", BM, BN, cfg == 1 ? 2 : 3);
     if (cfg == 1) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, false, true>), dim3(grid), dim3(512), 0, s, a);

@@ -57,6 +57,30 @@ def dp_row_normaliser(world, batch_local, rows_kept):
     return float(world * batch_local * rows_kept)
 
 
+def plan_buckets(ps, bucket_bytes):
+    """[(layer names, lo, hi)]: the flat gradient buffer cut into spans of about bucket_bytes, in the order the
+    backward pass completes them (from the end of the buffer), each span whole layers."""
+    spans = {}   # layer -> [start, end) span in the flat buffer (a layer's params are contiguous)
+    for name, (off, shape, _) in ps.entries.items():
+        lname = name.rsplit("/", 1)[0]
+        n = int(np.prod(shape))
+        lo, hi = spans.get(lname, (off, off))
+        spans[lname] = (min(lo, off), max(hi, off + ops.round_up(n, 64)))
+    order = sorted(spans.items(), key=lambda kv: kv[1][0], reverse=True)
+    buckets = []
+    cur, cur_lo, cur_hi = [], None, None
+    for lname, (lo, hi) in order:
+        if cur and (cur_hi - lo) * 4 > bucket_bytes:
+            buckets.append((set(cur), cur_lo, cur_hi))
+            cur, cur_hi = [], None
+        cur.append(lname)
+        cur_lo = lo
+        cur_hi = hi if cur_hi is None else cur_hi
+    if cur:
+        buckets.append((set(cur), cur_lo, cur_hi))
+    return buckets
+
+
 class GradBuckets:
     """Bucketed, backward-overlapped SUM all-reduce over the flat gradient buffer. overlap=False launches every
     bucket at finish() instead (the same sums): while an RCCL bucket holds CUs, a persistent conv kernel's
@@ -67,27 +91,8 @@ class GradBuckets:
         self.group = group
         self.overlap = overlap
         self.world = dist.get_world_size(group)
-        ps = net.ps
-        # layer -> [start, end) span in the flat buffer (a layer's params are contiguous)
-        spans = {}
-        for name, (off, shape, _) in ps.entries.items():
-            lname = name.rsplit("/", 1)[0]
-            n = int(np.prod(shape))
-            lo, hi = spans.get(lname, (off, off))
-            spans[lname] = (min(lo, off), max(hi, off + ops.round_up(n, 64)))
-        order = sorted(spans.items(), key=lambda kv: kv[1][0], reverse=True)  # backward completes from the end
-        self.buckets = []
-        cur, cur_lo, cur_hi = [], None, None
-        for lname, (lo, hi) in order:
-            if cur and (cur_hi - lo) * 4 > bucket_bytes:
-                self.buckets.append((set(cur), cur_lo, cur_hi))
-                cur, cur_hi = [], None
-            cur.append(lname)
-            cur_lo = lo
-            cur_hi = hi if cur_hi is None else cur_hi
-        if cur:
-            self.buckets.append((set(cur), cur_lo, cur_hi))
-        self.ps = ps
+        self.buckets = plan_buckets(net.ps, bucket_bytes)
+        self.ps = net.ps
         self.works = []
 
     def begin(self, frozen=()):

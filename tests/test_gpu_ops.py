@@ -233,6 +233,67 @@ def test_tap64p_halo_matches(mode, grid, tile, wide, claim):
     torch.testing.assert_close(sh_[0], rf.sum(0), rtol=2e-3, atol=1.0)
 
 
+@pytest.mark.parametrize("claim", [0, 1], ids=["static", "claimed"])
+@pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
+@pytest.mark.parametrize("mode", ["plain", "concat", "up", "split", "n352"])
+def test_tap64p_f32_halo(mode, grid, claim):
+    """f32 halo form of the persistent forward (igemm_fwd_tap64p_kernel<256, 128, 3, ..., F32>: 32-channel K steps,
+    eight exact v_mfma_f32_16x16x4_f32 per 16x16 block and step) vs a float64 convolution of the same f32 operands
+    (<= 1e-5 of the largest element: only the f32 accumulation differs) and vs the non-persistent f32 tap64 kernel
+    (option tap64p_f32=0) to the same bound; BatchNorm sums to f32 order. adipose_v3's f32 channel strides (96 /
+    192 / 352: a ragged last N tile), two sources, the nearest-x2 upsample gather, a split store."""
+    dt = torch.float32
+    g = torch.Generator().manual_seed(21)
+    N, H, W_ = 2, 32, 64
+    parts, nout, up = {"plain": ([96], 96, 1), "concat": ([64, 128], 192, 1), "up": ([192], 96, 2),
+                       "split": ([96, 96], 192, 1), "n352": ([352], 352, 1)}[mode]
+    Hs, Ws = H // up, W_ // up
+    cin = sum(parts)
+    srcs = [torch.randn(N, Hs, Ws, c, generator=g).to(DEV, dt) for c in parts]
+    Wt = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV)
+    x = torch.cat([t.double() for t in srcs], -1).permute(0, 3, 1, 2)
+    if up == 2:
+        x = x.repeat_interleave(2, 2).repeat_interleave(2, 3)
+    wk = Wt[:nout].double().view(nout, 3, 3, cin).permute(0, 3, 1, 2)
+    ref = F.conv2d(x, wk, padding=1).permute(0, 2, 3, 1) + bias.double()
+    relu = mode != "split"
+    if relu:
+        ref = ref.clamp_min(0.0)
+    res = []
+    for persist in (1, 0):
+        outs = [torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)]
+        kw = dict(srcB=srcs[1] if len(srcs) > 1 else None, bias=bias, relu=relu, up=up == 2)
+        if mode == "split":
+            outs = [torch.zeros(N, H, W_, 96, dtype=dt, device=DEV), torch.zeros(N, H, W_, nout - 96, dtype=dt, device=DEV)]
+            kw.update(out_mode=2, out2=outs[1], split_c=96)
+        st = torch.zeros(2, nout, device=DEV)
+        ops.set_option("tap64p_f32", persist)
+        ops.set_option("tap64p_claim", claim)
+        if grid:
+            ops.set_option("tap64_persist_grid", grid)
+        try:
+            ops.conv_fwd(srcs[0], Wt, nout, out=outs[0], bn_stats=(st[0], st[1]), **kw)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for o_ in ("tap64p_f32", "tap64p_claim", "tap64_persist_grid"):
+                ops.set_option(o_, None)
+        if persist:
+            assert kname == "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true>", kname
+        else:
+            assert kname.startswith("igemm_fwd_tap64_kernel<4, 2, 64"), kname
+        res.append((torch.cat(outs, -1).double(), st.double()))
+    (yp, sp), (yt, stt) = res
+    scale = ref.abs().max().item()
+    assert (yp - ref).abs().max().item() < 1e-5 * scale
+    assert (yp - yt).abs().max().item() < 1e-5 * scale
+    rf = ref.reshape(-1, nout)
+    torch.testing.assert_close(sp[0], rf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(sp[1], (rf * rf).sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(sp, stt, rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("form", ["halo256", "halo128", "gather_dil2", "convt"])
 def test_tap64p_claim_counters_reset(form):
     """Dynamic tile claiming (option tap64p_claim): every launch takes its tiles from a counter slot of the

@@ -7,6 +7,13 @@ one training step on the default stream; the step's wall time is compared with s
 only lost K of 256 CUs for the spin's duration grows by about spin_ms * K / 256; a persistent kernel whose
 late blocks wait for a held CU grows by up to its own duration.
 usage: python tools/contention_probe.py [--blocks 0,8,16,32,64] [--spin-ms 20] [--rounds 3]
+
+--buckets: the data-parallel schedule instead of one long hold. The step runs with the Trainer's gradient buckets
+(trainer.plan_buckets, 16 MB), and each bucket's all-reduce is stood in for by a side-stream sleep kernel of
+--bucket-ms holding K CUs, started when the backward has finished the bucket's layers (overlap) or all of them at
+the end of the backward (after), as RCCL's kernels would be on a node. Arms: static tile lists / claimed tiles
+(option dp_claim) x overlap / after; "exposed_model_ms" is what the buckets cost run back to back on an idle chip.
+usage: python tools/contention_probe.py --buckets [--blocks 8,32] [--bucket-ms 0.3] [--rounds 3]
 """
 import argparse
 import ctypes
@@ -25,6 +32,8 @@ def main():
     p.add_argument("--spin-ms", type=float, default=20.0)
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--opt", action="append", default=[], help="name=value native option")
+    p.add_argument("--buckets", action="store_true")
+    p.add_argument("--bucket-ms", type=float, default=0.3)
     args = p.parse_args()
     import numpy as np
     import torch
@@ -69,6 +78,8 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t) * 1e3
 
+    if args.buckets:
+        return bucket_probe(args, tr, x, y, spin, side, per_iter_ms, res, ops)
     ks = [int(v) for v in args.blocks.split(",")]
     times = {k: [] for k in ks}
     for _ in range(args.rounds):
@@ -85,6 +96,82 @@ def main():
                         "extra_ms": round(min(times[k]) - base, 3) if base else None,
                         "cu_share_model_ms": round(res["spin_ms"] * k / 256, 3)}
     res["opts"] = args.opt
+    print(json.dumps(res))
+
+
+class _Done:
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        import torch
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+def bucket_probe(args, tr, x, y, spin, side, per_iter_ms, res, ops):
+    """The Trainer's bucket schedule with each all-reduce replaced by a CU-holding sleep on a side stream."""
+    import torch
+    from adipose_amd import trainer as trmod
+    iters = max(1, int(args.bucket_ms / per_iter_ms))
+    state = {"k": 0}
+
+    class SpinBuckets(trmod.GradBuckets):
+        def __init__(self, net, overlap):   # no process group: one GPU stands in for a rank
+            self.group, self.overlap, self.world = None, overlap, 1
+            self.buckets = trmod.plan_buckets(net.ps, 16 << 20)
+            self.ps, self.works = net.ps, []
+
+        def _launch(self, i):
+            self.launched[i] = True
+            ev = torch.cuda.Event()
+            ev.record()
+            side.wait_event(ev)
+            spin.spin_launch(state["k"], iters, 98304, ctypes.c_void_p(side.cuda_stream))
+            done = torch.cuda.Event()
+            done.record(side)
+            self.works.append(_Done(done))
+
+    real_all_reduce = trmod.dist.all_reduce
+    trmod.dist.all_reduce = lambda *a, **k: None   # the Dice-sum reduce: 24 doubles, no CUs worth holding
+    arms = {}
+    ks = [int(v) for v in args.blocks.split(",") if int(v) > 0]
+    sb = {ov: SpinBuckets(tr.net, ov) for ov in (True, False)}
+    res["n_buckets"] = len(sb[True].buckets)
+    res["bucket_iters"] = iters
+
+    def step():
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        tr.train_step(x, y)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) * 1e3
+
+    try:
+        for _ in range(2):
+            for claim in (0, 1):
+                ops.set_option("dp_claim", claim)
+                tr.buckets = None
+                arms.setdefault(f"none/claim{claim}", []).append(step())
+                for k in ks:
+                    state["k"] = k
+                    for ov in (True, False):
+                        tr.buckets = sb[ov]
+                        step()    # warm
+                        for _ in range(args.rounds):
+                            arms.setdefault(f"K{k}/claim{claim}/{'overlap' if ov else 'after'}", []).append(step())
+    finally:
+        trmod.dist.all_reduce = real_all_reduce
+        tr.buckets = None
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(res["n_buckets"]):
+        spin.spin_launch(8, iters, 98304, ctypes.c_void_p(side.cuda_stream))
+    torch.cuda.synchronize()
+    res["exposed_model_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+    base = {c: min(arms[f"none/claim{c}"]) for c in (0, 1)}
+    for name, v in arms.items():
+        c = int(name.split("claim")[1][0])
+        res[name] = {"min": round(min(v), 3), "extra_ms": round(min(v) - base[c], 3), "n": len(v)}
     print(json.dumps(res))
 
 
