@@ -118,18 +118,20 @@ void set_kernel(const char* fmt, ...);
 void set_launch_stream(hipStream_t s);
 void kernel_end();
 // Replicated per-channel accumulators for the BatchNorm sums (statistics of a conv output, or the
-// BN-backward dbeta/dgamma reductions). f32 atomics execute at the memory side and serialise per
-// address, so thousands of blocks adding into the same C floats queue behind each other (measured:
+// BN-backward dbeta/dgamma reductions). Atomics execute at the memory side and serialise per
+// address, so thousands of blocks adding into the same C values queue behind each other (measured:
 // ~17 ns per add per address, 1.75 ms per training step); blocks add into replica (block & 63)
 // instead and stat_fold() sums the replicas into the caller's accumulators and re-zeroes them.
+// The replicas are f64 (round 4): each producer adds f32 partials summed in a fixed order, and f64 sums
+// of them in the atomics' run-dependent order round to the same f32 (deterministic BatchNorm statistics).
 // Per device, lazily allocated and zeroed; launches that use it must be ordered on one stream.
 constexpr int STAT_REPL = 64, STAT_CMAX = 2048;
-float* stat_scratch();   // [STAT_REPL][2][STAT_CMAX] f32, or nullptr (error set) if allocation failed or a
+double* stat_scratch();   // [STAT_REPL][2][STAT_CMAX] f64, or nullptr (error set) if allocation failed or a
                          // deferred fold is pending
 // bn_defer_fold bookkeeping: a launch that leaves its sums in the replicas records (C, sum, stream); only the
 // adp_bn_finalize_fold with the same three may take the replicas next (stat_scratch_fold clears the record)
 int defer_fold_begin(int C, const float* sum, hipStream_t s);
-float* stat_scratch_fold(int C, const float* sum, hipStream_t s);
+double* stat_scratch_fold(int C, const float* sum, hipStream_t s);
 int bn_fold_reset(hipStream_t s);   // adp_bn_fold_reset
 // dynamic tile claiming: a zeroed slot of CLAIM_INTS counters for one persistent launch (a ring of CLAIM_SLOTS per
 // device, handed out in turn; a launch leaves its slot zeroed again), or nullptr (error set)

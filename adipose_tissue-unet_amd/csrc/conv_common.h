@@ -40,11 +40,12 @@ struct FwdArgs {
   int wide_st;           // persistent forward: 16-B epilogue stores (channel pairs joined by permlane16_swap)
   int kpipe;             // tap64 kernel: mid-step barrier, next step's B half 0 preloaded (option tap64_kpipe)
   int debug_flags;       // timing-only ablations (option "fwd_debug"): bit1 skips the BN-statistics atomics
-  float* stat;           // BatchNorm accumulator replicas (adp::stat_scratch) for bn_sum / bnr_* launches
+  double* stat;          // BatchNorm accumulator replicas (f64) (adp::stat_scratch) for bn_sum / bnr_* launches
   int defer_fold;        // bn_sum launch whose replica sums adp_bn_finalize_fold adds in (adp_conv_desc)
   int f32;               // f32 launch on the LDS-DMA tap kernel (32-channel K steps, f32 MFMA)
   int* claim;            // persistent kernels: dynamic tile claiming counters (adp::claim_slot), nullptr = static lists
   int claim_chunk;       // tiles per claim (halo forward: consecutive patches taken together)
+  int claim_full;        // claiming: every tile claimed, none static (option claim_full; conv_common.h)
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
@@ -69,6 +70,7 @@ struct WgradArgs {
   float bna_inv_count;
   int* claim;           // persistent halo weight gradient: dynamic tile claiming counters (nullptr: static lists)
   int claim_chunk;      // patches per claim
+  int claim_full;       // every super-patch claimed, none static (option claim_full)
 };
 
 // LDS-only workgroup barrier for epilogues: this wave's LDS traffic complete, then s_barrier. Unlike
@@ -180,6 +182,11 @@ ADP_DEV void claim_publish(int* lds, int r) {
     asm volatile("s_waitcnt vmcnt(%2)\n\tds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r),
                  "n"(NYOUNG < 63 ? NYOUNG : 0) : "memory");
 }
+// claim_full (option claim_full): a block's first two tiles are claimed too -- one synchronous claim of two at
+// the start (claim_next2) -- instead of being its static ones. With static first tiles a block whose CU is
+// held by another stream's kernel when the launch starts still owns them and runs them after everyone else
+// is done (+4.3 ms per step with 8 CUs held for 20 ms: profiles/r04_contention_probe.txt); claimed, a late
+// block finds the work taken and leaves. The price is the claim's round trip at the start of every block.
 // every block calls this exactly once, after its last claim (thread 0; nclaim counters + the done count)
 ADP_DEV void claim_block_done(int* claim, int nclaim, int G) {
   const int done = __hip_atomic_fetch_add(claim + nclaim, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -417,9 +424,9 @@ ADP_DEV void epi_bn_flush(const FwdArgs& a, float* red, int n0, int tid, const f
       const int c = a.out_mode == 1 ? nn % a.Cps : nn;
       // replica of this block (folded into bn_sum/bn_sq or bnr_dbeta/bnr_dgamma by the launcher)
       const unsigned blk = blockIdx.x + blockIdx.y * gridDim.x;
-      float* rep = a.stat + (size_t)(blk & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
-      atomicAdd(rep + c, s);
-      atomicAdd(rep + adp::STAT_CMAX + c, q);
+      double* rep = a.stat + (size_t)(blk & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+      atomicAdd(rep + c, (double)s);
+      atomicAdd(rep + adp::STAT_CMAX + c, (double)q);
     }
   }
 }

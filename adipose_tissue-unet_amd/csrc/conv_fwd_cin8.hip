@@ -140,9 +140,9 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
       const float x = row16_sum(s1[mb][i]), y = row16_sum(s2[mb][i]);
       const int co = 16 * mb + 4 * h4 + i;
       if (r16 == 0 && co < a.Nout) {   // this wave's replica; the launcher folds them into bn_sum / bn_sq
-        float* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
-        atomicAdd(rep + co, x);
-        atomicAdd(rep + adp::STAT_CMAX + co, y);
+        double* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+        atomicAdd(rep + co, (double)x);
+        atomicAdd(rep + adp::STAT_CMAX + co, (double)y);
       }
     }
 }
@@ -271,9 +271,9 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8p_kernel(FwdArgs a) {
       const float x = row16_sum(s1[mb][i]), y = row16_sum(s2[mb][i]);
       const int co = 16 * mb + 4 * h4 + i;
       if (r16 == 0 && co < a.Nout) {
-        float* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
-        atomicAdd(rep + co, x);
-        atomicAdd(rep + adp::STAT_CMAX + co, y);
+        double* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+        atomicAdd(rep + co, (double)x);
+        atomicAdd(rep + adp::STAT_CMAX + co, (double)y);
       }
     }
 }

@@ -297,6 +297,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   // claimed at the start of super-tile s and published at the end of its first tile (the halo prefetch needs a
   // tile's successor at the start of the tile)
   constexpr bool dyn = DYN;
+  const bool full = dyn && a.claim_full;   // every super-tile claimed (0 and 1 by one claim at the start)
   const int nt = dyn ? 0 : (lin < T ? (T - lin + G - 1) / G : 0);
   if (!dyn && nt == 0) return;
   const int Wrows = (a.Nout + 63) / 64 * 64;
@@ -317,7 +318,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   const int npatch = T / NT;
   const int CH = dyn ? a.claim_chunk : 1, nsup = (npatch + CH - 1) / CH;
   auto sup_id = [&](int sidx) -> int {   // dyn: super-tile index of the block's local super-tile sidx, -1 past the end
-    const int v = sidx < 2 ? lin / NT + sidx * (G / NT) : 2 * (G / NT) + claim_ring_read(ring + (sidx & 3));
+    const int v = full ? claim_ring_read(ring + (sidx & 3))
+                       : sidx < 2 ? lin / NT + sidx * (G / NT) : 2 * (G / NT) + claim_ring_read(ring + (sidx & 3));
     return v < nsup ? v : -1;
   };
   // patch index of the block's local tile k, -1 past its end
@@ -327,12 +329,19 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     const int t = v * CH + k % CH;
     return v >= 0 && t < npatch ? t : -1;
   };
-  if (dyn && tile_id(0) < 0) {   // (uniform) more blocks than super-tiles: nothing static for this one
+  if (full) {
+    if (tid == 0) {
+      const int r = claim_next2(a.claim + nh);
+      ring[0] = r;
+      ring[1] = r + 1;
+    }
+    __syncthreads();
+  }
+  if (dyn && tile_id(0) < 0) {   // (uniform) more blocks than super-tiles (full: the work is taken already)
     if (tid == 0) claim_block_done(a.claim, NT, G);
     return;
   }
-  auto tile_origin = [&](int k, int& img, int& y0, int& x0) {
-    const int t = tile_id(k);
+  auto tile_origin = [&](int t, int& img, int& y0, int& x0) {   // (t: the patch index from tile_id)
     const int px = t % tx_n, r = t / tx_n;
     y0 = (r % ty_n) * PH;
     img = r / ty_n;
@@ -369,11 +378,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
                         : (const void*)halo_zero_page;
     __builtin_amdgcn_global_load_lds(p, (lds_void*)(smem + OFF_W + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
   }
+  int img0, y00, x00;
+  tile_origin(tile_id(0), img0, y00, x00);
 #pragma unroll
   for (int i = 0; i < GH; ++i) {
     if (i * NTH + tid < HCH) {
-      int img0, y00, x00;
-      tile_origin(0, img0, y00, x00);
       const uint4* p = halo_src(img0, y00, x00, i);
       __builtin_amdgcn_global_load_lds(p ? (const void*)p : (const void*)halo_zero_page,
                                        (lds_void*)(smem + (size_t)(i * NTH + wave * 64) * 16), 16, 0, 0);
@@ -526,10 +535,14 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   uint2 zreg[2][NF], dreg[EPI == 4 ? 2 : 1][NF];
   int mrowp = 0;
   // one tile: prefetch the next tile's halo into registers, nine taps, then (PIPE) nothing -- the
-  // previous tile's epilogue units run between this tile's taps -- or (!PIPE) this tile's epilogue
-  auto run_tile = [&](int k, auto with_prev) {
+  // previous tile's epilogue units run between this tile's taps -- or (!PIPE) this tile's epilogue.
+  // tk = tile_id(k); returns tile_id(k + 1) (dyn: each is an LDS read of the claim ring with its own lgkmcnt
+  // wait, so the ids are read once per tile and carried)
+  auto run_tile = [&](int k, int tk, auto with_prev) -> int {
     constexpr bool EPI_PREV = decltype(with_prev)::value;
-    const bool more = tile_id(k + 1) >= 0;
+    if constexpr (!DYN) tk = tile_id(k);   // (static lists: arithmetic -- nothing carried across the taps)
+    const int tn = tile_id(k + 1);
+    const bool more = tn >= 0;
     // dyn: claim tile k + 2 now (a compiler-visible atomic in a file built without the atomic optimizer, whose
     // wave form would wait for the result at once: the wait lands before its use at the end of this tile)
     // (a claim is published at the end of this tile, inside `if (more)`: claim_now implies more)
@@ -537,7 +550,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     int claimed = 0;
     if (claim_now && tid == 0) claimed = __hip_atomic_fetch_add(a.claim + nh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int img, y0, x0;
-    tile_origin(k, img, y0, x0);
+    tile_origin(tk, img, y0, x0);
     const int mrow = (img * a.Ho + y0 + wave) * a.Wo + x0;   // first output pixel of this wave's row
     if constexpr (BNR) load_z(EPI_PREV ? mrowp : mrow, zreg);
     if constexpr (EPI == 4) {
@@ -547,7 +560,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     uint4 hreg[GH];
     if (more) {
       int img1, y01, x01;
-      tile_origin(k + 1, img1, y01, x01);
+      tile_origin(DYN ? tn : tile_id(k + 1), img1, y01, x01);
 #pragma unroll
       for (int i = 0; i < GH; ++i) {
         const uint4* p = halo_src(img1, y01, x01, i);
@@ -635,16 +648,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       if (claim_now && tid == 0) ring[(k / CH + 2) & 3] = claimed;   // (slot of super-tile s - 2: long done)
       LDS_BAR();
     }
+    return DYN ? tn : tile_id(k + 1);
   };
-  run_tile(0, std::false_type{});
-  for (int k = 1; tile_id(k) >= 0; ++k) run_tile(k, std::integral_constant<bool, PIPE>{});
+  int tnext = run_tile(0, tile_id(0), std::false_type{});
+  for (int k = 1; tnext >= 0; ++k) tnext = run_tile(k, tnext, std::integral_constant<bool, PIPE>{});
   if constexpr (PIPE) {   // the last tile's epilogue
     if constexpr (BNR) load_z(mrowp, zreg);
     epi_all(accp, zreg, mrowp, dreg);
   }
   if (dyn && tid == 0) claim_block_done(a.claim, NT, G);   // (every claim of the block has returned)
   if (!stats || (a.debug_flags & 2)) return;   // (uniform)
-  float* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+  double* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
@@ -652,8 +666,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       const float x = row16_sum(s1[nf][i]), y = row16_sum(s2[nf][i]);
       const int c = n0 + nf * 16 + 4 * h4 + i;
       if (r16 == 0 && c < a.Nout) {
-        atomicAdd(d0 + c, x);
-        atomicAdd(d0 + adp::STAT_CMAX + c, y);
+        atomicAdd(d0 + c, (double)x);
+        atomicAdd(d0 + adp::STAT_CMAX + c, (double)y);
       }
     }
 }
@@ -740,6 +754,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     a.claim = option("halop_claim", option("dp_claim", 0)) && nt_n + 1 <= CLAIM_INTS && !(bnr && one_chunk) && !(pipe && (epi == 1 || epi == 3))
                   ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("halop_claim_chunk", 4));   // patches per claim
+    a.claim_full = option("claim_full", 0);
     if (a.claim) {   // (no more blocks per output block than super-tiles)
       const int nsup = (tiles / nt_n + a.claim_chunk - 1) / a.claim_chunk;
       grid = std::max(nt_n, std::min(grid, nsup * nt_n));

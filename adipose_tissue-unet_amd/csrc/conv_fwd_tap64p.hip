@@ -45,11 +45,13 @@ __device__ __forceinline__ float4 p_lds_f4(const float* p) {
   return r;
 }
 
-// the block's BatchNorm sums: LDS float add as inline asm for the same reason (no lgkmcnt wait: nothing
-// reads sacc before the final barrier, which is preceded by an explicit lgkmcnt(0))
-__device__ __forceinline__ void p_lds_add(float* p, float v) {
+// the block's BatchNorm sums: LDS f64 add as inline asm for the same reason (no lgkmcnt wait: nothing
+// reads sacc before the final barrier, which is preceded by an explicit lgkmcnt(0)). f64: the waves of one
+// channel set add their per-tile f32 partials in a run-dependent order, which f64 sums absorb (common.h)
+__device__ __forceinline__ void p_lds_add(double* p, float v) {
   const unsigned addr = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)p;
-  asm volatile("ds_add_f32 %0, %1" ::"v"(addr), "v"(v) : "memory");
+  const double d = (double)v;
+  asm volatile("ds_add_f64 %0, %1" ::"v"(addr), "v"(d) : "memory");
 }
 #define P_BAR()                            \
   do {                                     \
@@ -74,7 +76,8 @@ constexpr int P_HROWS = 340;   // 10 x 34 halo pixels of an 8 x 32 patch
 template <int BM, int BN, int NST, bool BNR, bool HALO = false>
 constexpr int tap64p_lds() {
   // (+16 B: the ring of claimed tile ids, dynamic claiming)
-  return (HALO ? NST * BN * 128 + 2 * P_HROWS * 128 + 7 * BN * 4 : NST * (BM + BN) * 128 + 7 * BN * 4) + 16;
+  // (constants: 5 f32 rows; the block's BatchNorm sums: 2 f64 rows)
+  return (HALO ? NST * BN * 128 + 2 * P_HROWS * 128 + 9 * BN * 4 : NST * (BM + BN) * 128 + 9 * BN * 4) + 16;
 }
 __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_halo.hip: conflict-free)
 
@@ -128,8 +131,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   constexpr int OC = NST * STAGE + (HALO ? 2 * HBUF : 0);
   float (*cst)[BN] = reinterpret_cast<float (*)[BN]>(smem + OC);   // epilogue constants:
                                                                   // bias | scale shift mean invstd (BNR)
-  float (*sacc)[BN] = reinterpret_cast<float (*)[BN]>(smem + OC + 5 * BN * 4);   // block's BN sums
-  int* ring = reinterpret_cast<int*>(smem + OC + 7 * BN * 4);   // dynamic claiming: tile ids of local tiles k & 3
+  double (*sacc)[BN] = reinterpret_cast<double (*)[BN]>(smem + OC + 5 * BN * 4);   // block's BN sums (f64)
+  int* ring = reinterpret_cast<int*>(smem + OC + 9 * BN * 4);   // dynamic claiming: tile ids of local tiles k & 3
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WN, wc = wave % WN;
@@ -141,6 +144,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // block's N column (dyn, conv_common.h); either way a block keeps one N column
   // (the fp8 eval forms and the opt-in register-staged form keep static lists: no spare registers there)
   const bool dyn = !F8 && !WREG && a.claim != nullptr;
+  const bool full = dyn && a.claim_full;   // every tile claimed (tiles 0 and 1 by one claim at the start)
+  int r2 = 0;
+  if (full && tid == 0) r2 = claim_next2(a.claim + lin % a.ntile_n);   // (its wait lands at the cst stores)
   const int ntn = a.ntile_n, ntm = ntiles / ntn, col = lin % ntn;
   const int mine = dyn ? 0 : (lin < ntiles ? (ntiles - lin + G - 1) / G : 0);
   if (!dyn && mine == 0) return;   // uniform per block
@@ -158,8 +164,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     cst[2][tid] = (BNR && v) ? a.bnr_sh[n] : 0.f;
     cst[3][tid] = (BNR && v) ? a.bnr_mean[n] : 0.f;
     cst[4][tid] = (BNR && v) ? a.bnr_invstd[n] : 0.f;
-    sacc[0][tid] = 0.f;
-    sacc[1][tid] = 0.f;
+    sacc[0][tid] = 0.0;
+    sacc[1][tid] = 0.0;
   }
   // (ordered before the epilogue by the first K step's barrier)
   // dyn: a block's first tile is its static one (lin / ntn: no claim to wait for at the start); claim value c is
@@ -249,8 +255,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // that step's barrier -- ahead of every reader (the loader needs tile k from step NST - 1 of tile k - 1 on)
   auto tile_id = [&](int k) -> int {
     if (!dyn) return k < mine ? lin / ntn + k * (G / ntn) : -1;
-    if (k == 0) return lin / ntn;
-    const int t = G / ntn + claim_ring_read(ring + (k & 3));   // (uniform: scalar registers)
+    if (k == 0 && !full) return lin / ntn;
+    const int t = (full ? 0 : G / ntn) + claim_ring_read(ring + (k & 3));   // (uniform: scalar registers)
     return t < ntm ? t : -1;   // (a claim past the last tile: the work is taken)
   };
   auto patch_t = [&](int t) {
@@ -757,19 +763,28 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // The wait counts what was issued after the stage: the NST - 2 younger stages and, when a tile ended
   // inside that window, its EPI_OPS epilogue ops; near the end of the stream (fewer younger stages) it
   // drains everything.
+  if (full) {   // the first two tiles (a block that starts late finds them past the end and leaves)
+    if (tid == 0) {
+      ring[0] = r2;
+      ring[1] = r2 + 1;
+    }
+    __syncthreads();
+  }
   if constexpr (WREG) {   // the first chunk's whole halo ahead of the stream (registers -> LDS)
 #pragma unroll
     for (int g = 0; g < GH; ++g)
       store_halo_reg(g, 0, load_halo_reg(tile_id(0), 0, g, true), true, (unsigned)(OB0 + tid * 16));
   } else if constexpr (HALO) {   // the first chunk's whole halo ahead of the stream
     const int t0 = tile_id(0);
+    if (t0 >= 0) {
 #pragma unroll
-    for (int g = 0; g < GH; ++g) issue_halo(t0, 0, g, 0);
+      for (int g = 0; g < GH; ++g) issue_halo(t0, 0, g, 0);
+    }
   }
   if constexpr (WREG) load_w(0);   // (the first load_next stores them into stage 0)
   // dyn: the claim of tile 1 goes out before the prologue's stages, so the wait at the top of step 0 covers it
   int c1val = 0;
-  if (dyn && tid == 0) c1val = claim_issue(a.claim + col);
+  if (dyn && !full && tid == 0) c1val = claim_issue(a.claim + col);
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i) load_next();
   int gs = 0, cs = 0, last_epi = -NST;   // step, its stage, step of the latest epilogue
@@ -821,7 +836,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
       else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
-      if (dyn && gs == 0 && tid == 0) claim_publish<-1>(ring + 1, c1val);   // tile 1 (claimed in the prologue)
+      if (dyn && !full && gs == 0 && tid == 0) claim_publish<-1>(ring + 1, c1val);   // tile 1 (claimed in the prologue)
       // (timing-only ablation, fwd_debug bit 9: no barrier -- the stages race, the values are garbage)
       if (!(a.debug_flags & 512)) P_BAR();   // stage cs landed for every wave, nobody reads the stage being refilled
       if constexpr (ZALL) {
@@ -869,7 +884,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   if (!stats || (a.debug_flags & 2)) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  float* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+  double* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
   if (tid < BN) {
     const int n = n0 + tid;
     if (n < a.Nout) {
@@ -940,6 +955,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // dynamic tile claiming (option tap64p_claim): robust to CUs held by another stream's kernels (RCCL)
   a.claim = nullptr;
   if (option("tap64p_claim", option("dp_claim", 0)) && a.ntile_n + 1 <= CLAIM_INTS) a.claim = claim_slot();   // (nullptr: static lists)
+  a.claim_full = option("claim_full", 0);
   const bool bnr = a.bnr_z != nullptr;
   // the halo form (option tap64p_halo): 3x3 stride-1 'same' layers whose output tiles into 8 x 32 patches
   const bool halo_shape = !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&

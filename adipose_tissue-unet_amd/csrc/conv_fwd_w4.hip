@@ -351,11 +351,11 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
     if (a.debug_flags & 2) return;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    float* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+    double* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
     const int n = n0 + tid;
     if (n < a.Nout) {
-      atomicAdd(rep + n, sacc[tid]);
-      atomicAdd(rep + adp::STAT_CMAX + n, sacc[256 + tid]);
+      atomicAdd(rep + n, (double)sacc[tid]);
+      atomicAdd(rep + adp::STAT_CMAX + n, (double)sacc[256 + tid]);
     }
   }
 }

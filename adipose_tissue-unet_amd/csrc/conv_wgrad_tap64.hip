@@ -465,11 +465,13 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   // start of super-patch s (a compiler-visible atomic: this file is built without the atomic optimizer) and
   // published after the drain at the end of its first patch, before that patch's barrier
   const bool dyn = a.claim != nullptr;
+  const bool full = dyn && a.claim_full;   // every super-patch claimed (0 and 1 by one claim at the start)
   int* ring = reinterpret_cast<int*>(smem + 2 * STAGE + (BNA ? 6 * 64 * 4 : 0));
   const int nt = dyn ? 0 : (lin < T ? (T - lin + G - 1) / G : 0);
   const int CH = dyn ? a.claim_chunk : 1, nsup = (T + CH - 1) / CH;
   auto sup_id = [&](int sidx) -> int {
-    const int v = sidx < 2 ? lin + sidx * G : 2 * G + claim_ring_read(ring + (sidx & 3));
+    const int v = full ? claim_ring_read(ring + (sidx & 3))
+                       : sidx < 2 ? lin + sidx * G : 2 * G + claim_ring_read(ring + (sidx & 3));
     return v < nsup ? v : -1;
   };
   auto tile_id = [&](int k) -> int {
@@ -514,9 +516,8 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   }
   // patch k of this block -> origin (image row base, y0, x0) and the pixel indices of its (y0, x0)
   struct Patch { int y0, x0, pbx, pbd; };
-  auto patch = [&](int k) {
+  auto patch = [&](int t) {   // (t: the patch index from tile_id, read once per patch and carried)
     Patch P;
-    const int t = tile_id(k);
     const int px = t % tx_n, r = t / tx_n;
     const int img = r / ty_n;
     P.y0 = (r % ty_n) * PH;
@@ -680,9 +681,18 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   acc8[0] = acc8[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nb8 = wave >> 1, cb8 = 2 * (wave & 1);
 
-  const bool any = tile_id(0) >= 0;
+  if (full) {   // the first two super-patches (a block that starts late finds them past the end)
+    if (tid == 0) {
+      const int r = claim_next2(a.claim + combo);
+      ring[0] = r;
+      ring[1] = r + 1;
+    }
+    __syncthreads();
+  }
+  int tcur = tile_id(0);
+  const bool any = tcur >= 0;
   if (any) {
-    const Patch P0 = patch(0);
+    const Patch P0 = patch(tcur);
     if constexpr (BNA) {
 #pragma unroll
       for (int i = 0; i < GD; ++i) issue_d(P0, i, 0);
@@ -700,8 +710,9 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   }
   for (int k = 0; any; ++k) {
     const int buf = k & 1;
-    const bool more = tile_id(k + 1) >= 0;
-    const Patch Pn = patch(more ? k + 1 : k);
+    const int tn = tile_id(k + 1);
+    const bool more = tn >= 0;
+    const Patch Pn = patch(more ? tn : tcur);
     const bool claim_now = dyn && k % CH == 0 && more && sup_id(k / CH + 1) >= 0;
     int claimed = 0;
     if (claim_now && tid == 0)
@@ -753,6 +764,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     if (claim_now && tid == 0) ring[(k / CH + 2) & 3] = claimed;   // (slot of super-patch s - 2: long done)
     W64_BAR();                                          // and nobody reads this buffer any more
     if (!more) break;
+    tcur = tn;
   }
   if (dyn && tid == 0) claim_block_done(a.claim, combos, gridDim.x);   // (every claim of the block has returned)
   if (!any) return;   // (dyn: a block that started late found the work taken)
@@ -1153,6 +1165,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     // dynamic patch claiming (option wgrad_halop_claim; nullptr from claim_slot: static lists)
     a.claim = option("wgrad_halop_claim", option("dp_claim", 0)) && combos + 1 <= CLAIM_INTS ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("wgrad_halop_claim_chunk", 4));   // patches per claim
+    a.claim_full = option("claim_full", 0);
     if (a.claim) per = std::min(per, (tiles + a.claim_chunk - 1) / a.claim_chunk);   // (<= super-patches)
     const int grid = per * combos;
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable

@@ -19,7 +19,7 @@ inline int nblk(size_t n, int cap = 8192) {
 }
 
 // replica of this block in the BatchNorm accumulator scratch (see adp::stat_scratch)
-ADP_DEV float* stat_replica(float* scratch, unsigned block) {
+ADP_DEV double* stat_replica(double* scratch, unsigned block) {
   return scratch + (size_t)(block & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
 }
 
@@ -209,7 +209,7 @@ __global__ void maxpool_bwd_kernel(int N, int H, int W, int C, const T* src, con
 template <typename T, bool SRC>
 __global__ __launch_bounds__(TPB) void maxpool_bwd_bnr_kernel(int N, int H, int W, int C, const T* src, const T* dpool, const T* addend,
                                        T* dsrc, const T* z, const float* sc, const float* sh, const float* mean,
-                                       const float* invstd, float* stat) {
+                                       const float* invstd, double* stat) {
   const int G = C >> 3, lanes = TPB / G;
   const int g = threadIdx.x % G, pl = threadIdx.x / G;
   const unsigned Ho = H >> 1, Wo = W >> 1, P = (unsigned)N * Ho * Wo;
@@ -293,9 +293,9 @@ __global__ __launch_bounds__(TPB) void maxpool_bwd_bnr_kernel(int N, int H, int 
       a += red[0][(l * G + gg) * 8 + j];
       b += red[1][(l * G + gg) * 8 + j];
     }
-    float* rep = stat_replica(stat, blockIdx.x);
-    atomicAdd(rep + c, a);                   // folded into dbeta / dgamma by stat_fold_kernel
-    atomicAdd(rep + adp::STAT_CMAX + c, b);
+    double* rep = stat_replica(stat, blockIdx.x);
+    atomicAdd(rep + c, (double)a);           // folded into dbeta / dgamma by stat_fold_kernel
+    atomicAdd(rep + adp::STAT_CMAX + c, (double)b);
   }
 }
 
@@ -413,59 +413,58 @@ __global__ void bn_finalize_kernel(int C, float count, const float* sum, const f
 
 // dst{0,1}[c] += sum over the replicas of scratch[r][{0,1}][c]; the replicas are re-zeroed
 // block = 64 channels x 4 replica groups of STAT_REPL / 4: a thread sums 16 replicas (and zeroes them),
-// the four partial sums meet in LDS (a launch-latency-bound fold: 4x shorter dependent chain)
-__global__ void stat_fold_kernel(int C, float* scratch, float* dst0, float* dst1) {
-  constexpr int RG = 4, RPER = adp::STAT_REPL / RG;
-  __shared__ float part[2][RG][64];
+// the four partial sums meet in LDS (a launch-latency-bound fold: 4x shorter dependent chain). The replicas
+// are f64 and every producer adds an f32 partial whose own order is fixed (one wave's or one block's pixels
+// in a fixed sequence): f64 addition of those partials in any order agrees to ~1e-16 relative, far below
+// the f32 rounding of the result, so the folded sums -- and the BatchNorm scale / shift / mean / invstd and
+// dgamma / dbeta made from them -- are the same bits from run to run (f32 atomics in run-dependent order made
+// bf16 runs of one network differ by rounding flips: profiles/r03_bf16_bn_nondeterminism.txt)
+ADP_DEV void fold_replicas(int C, int c, int rg, double* scratch, double& s0, double& s1) {
+  constexpr int RPER = adp::STAT_REPL / 4;
+  s0 = 0.0;
+  s1 = 0.0;
+  if (c >= C) return;
+#pragma unroll 4
+  for (int r = rg * RPER; r < (rg + 1) * RPER; ++r) {
+    double* p = scratch + (size_t)r * 2 * adp::STAT_CMAX + c;
+    s0 += p[0];
+    s1 += p[adp::STAT_CMAX];
+    p[0] = 0.0;
+    p[adp::STAT_CMAX] = 0.0;
+  }
+}
+__global__ void stat_fold_kernel(int C, double* scratch, float* dst0, float* dst1) {
+  __shared__ double part[2][4][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  float s0 = 0.f, s1 = 0.f;
-  if (c < C) {
-#pragma unroll 4
-    for (int r = rg * RPER; r < (rg + 1) * RPER; ++r) {
-      float* p = scratch + (size_t)r * 2 * adp::STAT_CMAX + c;
-      s0 += p[0];
-      s1 += p[adp::STAT_CMAX];
-      p[0] = 0.f;
-      p[adp::STAT_CMAX] = 0.f;
-    }
-  }
+  double s0, s1;
+  fold_replicas(C, c, rg, scratch, s0, s1);
   part[0][rg][cl] = s0;
   part[1][rg][cl] = s1;
   __syncthreads();
   if (rg == 0 && c < C) {
-    dst0[c] += (part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]);
-    if (dst1) dst1[c] += (part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]);
+    dst0[c] += (float)((part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]));
+    if (dst1) dst1[c] += (float)((part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]));
   }
 }
 
 // stat_fold_kernel + bn_finalize_kernel in one launch: the replica sums are added into sum / sq (and
 // re-zeroed), then the BatchNorm scale / shift / mean / invstd (and running statistics) of those sums
-__global__ void bn_fold_finalize_kernel(int C, float* scratch, float* sum, float* sq, float count,
+__global__ void bn_fold_finalize_kernel(int C, double* scratch, float* sum, float* sq, float count,
                                         const float* gamma, const float* beta, float eps, float momentum,
                                         float* scale, float* shift, float* mean, float* invstd, float* rmean,
                                         float* rvar) {
-  constexpr int RG = 4, RPER = adp::STAT_REPL / RG;
-  __shared__ float part[2][RG][64];
+  __shared__ double part[2][4][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  float s0 = 0.f, s1 = 0.f;
-  if (c < C) {
-#pragma unroll 4
-    for (int r = rg * RPER; r < (rg + 1) * RPER; ++r) {
-      float* p = scratch + (size_t)r * 2 * adp::STAT_CMAX + c;
-      s0 += p[0];
-      s1 += p[adp::STAT_CMAX];
-      p[0] = 0.f;
-      p[adp::STAT_CMAX] = 0.f;
-    }
-  }
+  double s0, s1;
+  fold_replicas(C, c, rg, scratch, s0, s1);
   part[0][rg][cl] = s0;
   part[1][rg][cl] = s1;
   __syncthreads();
   if (rg != 0 || c >= C) return;
-  const float ts = sum[c] + ((part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]));
-  const float tq = sq[c] + ((part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]));
+  const float ts = sum[c] + (float)((part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]));
+  const float tq = sq[c] + (float)((part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]));
   sum[c] = ts;
   sq[c] = tq;
   // = bn_finalize_kernel (training statistics, count > 0)
@@ -488,7 +487,7 @@ __global__ void bn_fold_finalize_kernel(int C, float* scratch, float* sum, float
 template <typename T>
 __global__ void bn_bwd_reduce_kernel(size_t M, int C, const T* dA, const T* z, const float* sc,
                                      const float* sh, const float* mean, const float* invstd,
-                                     float* dgamma, float* dbeta, float* stat) {
+                                     float* dgamma, float* dbeta, double* stat) {
   const int G = C >> 3;
   const int lanes = TPB / G;           // pixels processed per block iteration
   const int g = threadIdx.x % G, pl = threadIdx.x / G;
@@ -524,9 +523,9 @@ __global__ void bn_bwd_reduce_kernel(size_t M, int C, const T* dA, const T* z, c
       a += red[0][(l * G + gg) * 8 + j];
       b += red[1][(l * G + gg) * 8 + j];
     }
-    float* rep = stat_replica(stat, blockIdx.x);
-    atomicAdd(rep + c, a);
-    atomicAdd(rep + adp::STAT_CMAX + c, b);
+    double* rep = stat_replica(stat, blockIdx.x);
+    atomicAdd(rep + c, (double)a);
+    atomicAdd(rep + adp::STAT_CMAX + c, (double)b);
   }
 }
 
@@ -846,9 +845,9 @@ int defer_fold_begin(int C, const float* sum, hipStream_t s) {
   pending_folds()[dev] = PendingFold{true, C, sum, s};
   return 0;
 }
-static float* stat_scratch_impl(bool fold, int C, const float* sum, hipStream_t s) {
+static double* stat_scratch_impl(bool fold, int C, const float* sum, hipStream_t s) {
   static std::mutex mu;
-  static std::map<int, float*> per_dev;
+  static std::map<int, double*> per_dev;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("stat_scratch: hipGetDevice failed"); return nullptr; }
   {
@@ -871,8 +870,8 @@ static float* stat_scratch_impl(bool fold, int C, const float* sum, hipStream_t 
   std::lock_guard<std::mutex> lk(mu);
   auto it = per_dev.find(dev);
   if (it != per_dev.end()) return it->second;
-  const size_t bytes = sizeof(float) * STAT_REPL * 2 * STAT_CMAX;
-  float* p = nullptr;
+  const size_t bytes = sizeof(double) * STAT_REPL * 2 * STAT_CMAX;
+  double* p = nullptr;
   if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     set_error("stat_scratch: allocation of the BatchNorm accumulator replicas failed");
@@ -881,7 +880,7 @@ static float* stat_scratch_impl(bool fold, int C, const float* sum, hipStream_t 
   per_dev[dev] = p;
   return p;
 }
-float* stat_scratch() { return stat_scratch_impl(false, 0, nullptr, nullptr); }
+double* stat_scratch() { return stat_scratch_impl(false, 0, nullptr, nullptr); }
 // drop a deferred fold that never reached its adp_bn_finalize_fold (an error or exception between the two) and
 // re-zero the replicas it left its sums in, stream-ordered on s; a no-op when nothing is pending
 int bn_fold_reset(hipStream_t s) {
@@ -893,15 +892,15 @@ int bn_fold_reset(hipStream_t s) {
     if (!pf.on) return 0;
     pf.on = false;
   }
-  float* p = stat_scratch();
+  double* p = stat_scratch();
   if (!p) return -2;
-  if (hipMemsetAsync(p, 0, sizeof(float) * STAT_REPL * 2 * STAT_CMAX, s) != hipSuccess) {
+  if (hipMemsetAsync(p, 0, sizeof(double) * STAT_REPL * 2 * STAT_CMAX, s) != hipSuccess) {
     set_error("adp_bn_fold_reset: clearing the accumulator replicas failed");
     return -2;
   }
   return 0;
 }
-float* stat_scratch_fold(int C, const float* sum, hipStream_t s) { return stat_scratch_impl(true, C, sum, s); }
+double* stat_scratch_fold(int C, const float* sum, hipStream_t s) { return stat_scratch_impl(true, C, sum, s); }
 int* claim_slot() {
   static std::mutex mu;
   static std::map<int, std::pair<int*, unsigned>> per_dev;
@@ -946,7 +945,7 @@ void* scratch(int slot, size_t bytes) {
 }
 int stat_fold(int C, float* dst0, float* dst1, hipStream_t s) { return stat_fold_at(0, C, dst0, dst1, s); }
 int stat_fold_at(int c0, int C, float* dst0, float* dst1, hipStream_t s) {
-  float* sc = stat_scratch();
+  double* sc = stat_scratch();
   if (!sc) return -1;
   hipLaunchKernelGGL(stat_fold_kernel, dim3((C + 63) / 64), dim3(256), 0, s, C, sc + c0, dst0, dst1);
   return check_launch("stat_fold");
@@ -1036,7 +1035,7 @@ extern "C" int adp_maxpool2_bwd_bnr(int dtype, int N, int H, int W, int C, const
   const size_t P = (size_t)N * (H / 2) * (W / 2);
   const int blocks = (int)std::max<size_t>(1, std::min<size_t>((P + lanes - 1) / lanes,
                                                                (size_t)adp::option("pool_bnr_blocks", 2048)));
-  float* stat = adp::stat_scratch();
+  double* stat = adp::stat_scratch();
   if (!stat) return -1;
   DTYPE_SWITCH(dtype, T,
                if (src) hipLaunchKernelGGL((maxpool_bwd_bnr_kernel<T, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st,
@@ -1121,7 +1120,7 @@ extern "C" int adp_bn_finalize_fold(int C, float count, float* sum, float* sq, c
   ADP_REQUIRE(C > 0 && C <= adp::STAT_CMAX && count > 0 && sum && sq && gamma && beta && scale && shift && mean &&
                   invstd,
               "adp_bn_finalize_fold: bad arguments (training statistics, C <= 2048)");
-  float* sc = adp::stat_scratch_fold(C, sum, (hipStream_t)st);
+  double* sc = adp::stat_scratch_fold(C, sum, (hipStream_t)st);
   if (!sc) return -1;
   hipLaunchKernelGGL(bn_fold_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)st, C, sc, sum, sq,
                      count, gamma, beta, eps, momentum, scale, shift, mean, invstd, rmean, rvar);
@@ -1134,7 +1133,7 @@ extern "C" int adp_bn_bwd_reduce(int dtype, size_t M, int C, const void* dA, con
   ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB, "adp_bn_bwd_reduce: C must be a multiple of 8 and <= 2048");
   int lanes = TPB / (C / 8);
   int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, 2048);
-  float* stat = adp::stat_scratch();
+  double* stat = adp::stat_scratch();
   if (!stat) return -1;
   DTYPE_SWITCH(dtype, T,
                hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, C,

@@ -124,7 +124,7 @@ template <typename T, int NOUT, bool BNR = false>
 __global__ __launch_bounds__(TPB) void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* sc,
                                 const float* sh, const float* p, const float* dp, const T* addend,
                                 const T* mask, float ms, T* dx, float* dW, float* db, const float* bmean = nullptr,
-                                const float* binv = nullptr, float* stat = nullptr) {
+                                const float* binv = nullptr, double* stat = nullptr) {
   const int G = Cs >> 3;                 // groups per pixel
   const int lanes = TPB / G;
   const int g = threadIdx.x % G, pl = threadIdx.x / G;
@@ -221,19 +221,19 @@ __global__ __launch_bounds__(TPB) void head_bwd_kernel(size_t M, int Cs, int Cin
   // BNR: every sum goes to this block's replica of the accumulator scratch (adp::stat_scratch; same-address
   // f32 atomics from thousands of blocks serialise), folded by the host wrapper: row 0 [0, Cs) dbeta,
   // row 1 [0, Cs) dgamma, row 0 [Cs, Cs + Cin) dW, row 0 Cs + Cin db
-  float* rep = BNR ? stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX : nullptr;
+  double* rep = BNR ? stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX : nullptr;
   for (int c = threadIdx.x; c < Cin; c += TPB) {
     int gg = c >> 3, j = c & 7;
     float s = 0.f;
     for (int l = 0; l < lanes; ++l) s += red[(l * G + gg) * 8 + j];
-    if (BNR) atomicAdd(rep + Cs + c, s);
+    if (BNR) atomicAdd(rep + Cs + c, (double)s);
     else if (NOUT == 2) { atomicAdd(dW + c, -s); atomicAdd(dW + Cin + c, s); }
     else atomicAdd(dW + c, s);
   }
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int l = 0; l < lanes; ++l) s += redb[l * G];
-    if (BNR) atomicAdd(rep + Cs + Cin, s);
+    if (BNR) atomicAdd(rep + Cs + Cin, (double)s);
     else if (NOUT == 2) { atomicAdd(db, -s); atomicAdd(db + 1, s); }
     else atomicAdd(db, s);
   }
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(TPB) void head_bwd_kernel(size_t M, int Cs, int Cin
         const int gg = c >> 3, j = c & 7;
         float t = 0.f;
         for (int l = 0; l < lanes; ++l) t += red[(l * G + gg) * 8 + j];
-        atomicAdd(rep + (pass ? adp::STAT_CMAX : 0) + c, t);
+        atomicAdd(rep + (pass ? adp::STAT_CMAX : 0) + c, (double)t);
       }
     }
   }
@@ -559,7 +559,7 @@ extern "C" int adp_head_sigmoid_bwd_bnr(int dtype, size_t M, int Cs, int Cin, co
   ADP_REQUIRE(Cs % 8 == 0 && Cs / 8 <= TPB && Cin <= Cs && z && sc && sh && mean && invstd && dgamma && dbeta,
               "adp_head_sigmoid_bwd_bnr: Cs % 8 == 0, Cin <= Cs, all BatchNorm pointers");
   ADP_REQUIRE(Cs + Cin + 1 <= adp::STAT_CMAX, "adp_head_sigmoid_bwd_bnr: Cs + Cin too large");
-  float* stat = adp::stat_scratch();
+  double* stat = adp::stat_scratch();
   if (!stat) return -1;
   const int lanes = TPB / (Cs / 8);
   // every block resident at once (measured at level 0: 233 us with 2 blocks per CU, 286 us with 4096)

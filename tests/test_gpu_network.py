@@ -257,6 +257,35 @@ def test_unet_bn_fallback_paths_match_default(flag):
             assert c > 0.98, (flag, n, c)
 
 
+@pytest.mark.parametrize("levels,S", [(3, 64), (5, 128)])
+def test_unet_bn_bf16_runs_are_deterministic(levels, S):
+    """Two identical bf16 training forward + backward passes give bit-identical outputs, BatchNorm statistics and
+    data-gradient chains: since round 4 the BatchNorm sums (forward statistics in every conv epilogue and the
+    fused BN-backward reductions) are f64 replicas fed f32 partials of a fixed order (csrc/common.h), where f32
+    atomics in run-dependent order used to make runs differ by bf16 rounding flips (per-layer gradient cosines down
+    to 0.9895: profiles/r03_bf16_bn_nondeterminism.txt). The weight gradients themselves are still f32 atomic sums
+    over blocks, whose order can move the last bits of an element; nothing downstream of them in the step reads
+    them, so they stay within 1e-5 of each other."""
+    B = 2
+    w = R.unet_bn_keras_weights(levels=levels, base=64, in_ch=3, seed=5)
+    x, y = synth_batch(B, S, C=3, seed=9)
+    net = UNetBN(B, S, levels=levels, base=64, in_ch=3, dtype="bf16", device=DEV)
+    net.set_weights(w)
+    tr = Trainer(net, LossConfig(use_hard_mining=False))
+    runs = []
+    for _ in range(3):
+        outs, _ = _unet_bn_step(net, tr, x, y, B)
+        runs.append((outs["main_out"].clone(), {n: [torch.as_tensor(g).clone() for g in net.get_layer_grads(n)]
+                                                for n in w}))
+    p0, g0 = runs[0]
+    for p1, g1 in runs[1:]:
+        assert torch.equal(p0, p1), (p0 - p1).abs().max().item()
+        for n in w:
+            for a, b in zip(g0[n], g1[n]):
+                r = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-30)
+                assert r <= 1e-5, (n, r)
+
+
 def test_unet_bn_repeated_steps_and_double_backward():
     """The per-step statistic arena (BatchNorm sums zeroed once per training forward, the ConvTranspose
     bias-gradient sums once per backward) must not carry anything over: a second training forward +

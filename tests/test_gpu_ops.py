@@ -270,6 +270,7 @@ def test_tap64p_f32_halo(mode, grid, claim):
         st = torch.zeros(2, nout, device=DEV)
         ops.set_option("tap64p_f32", persist)
         ops.set_option("tap64p_claim", claim)
+        ops.set_option("fwd_tap64", 3)   # the 256x128 tile (these small launches would score 256x64 higher)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
@@ -277,7 +278,7 @@ def test_tap64p_f32_halo(mode, grid, claim):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("tap64p_f32", "tap64p_claim", "tap64_persist_grid"):
+            for o_ in ("tap64p_f32", "tap64p_claim", "tap64_persist_grid", "fwd_tap64"):
                 ops.set_option(o_, None)
         if persist:
             assert kname == "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true>", kname

@@ -9,6 +9,6 @@ TMP=$(mktemp -d /tmp/adp_ref.XXXXXX)
 git -C "$ROOT" archive "$REV" adipose_tissue-unet_amd/csrc include | tar -x -C "$TMP"
 mkdir -p "$ROOT/ab"
 TAG=$(git -C "$ROOT" rev-parse --short "$REV")
-make -C "$TMP/adipose_tissue-unet_amd/csrc" -j8 OUT="$ROOT/ab/libadipose_$TAG.so" > "$TMP/build.log" 2>&1 || { tail -20 "$TMP/build.log"; exit 1; }
+make -C "$TMP/adipose_tissue-unet_amd/csrc" -j8 OUT="$ROOT/ab/libadipose_$TAG.so" "$ROOT/ab/libadipose_$TAG.so" > "$TMP/build.log" 2>&1 || { tail -20 "$TMP/build.log"; exit 1; }
 rm -rf "$TMP"
 echo "$ROOT/ab/libadipose_$TAG.so"

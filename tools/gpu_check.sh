@@ -135,6 +135,16 @@ for s in $STEPS; do
            > gpurun_out/dp_tests.log 2>&1 ;;
     diag) timeout -k 10 300 python -u tools/diag_bn_determinism.py > gpurun_out/diag_bn.log 2>&1 &&
           timeout -k 10 300 python -u tools/diag_f32_freeze.py > gpurun_out/diag_freeze.log 2>&1 ;;
+    pmcdom) bash tools/pmc_dom.sh > gpurun_out/pmc_dom.log 2>&1 ;;
+    abref) bash tools/ab_libs.sh "$(ls ab/libadipose_*.so | head -n 1)" adipose_tissue-unet_amd/libadipose_hip.so 3 \
+             bench.py --no-cpu-baseline --steps 10 > gpurun_out/ab_ref.log 2>&1 ;;
+    claimk3) timeout -k 10 500 python tools/bench_kernels.py --kinds fwd,fwd_stats,bnr,wgrad \
+              --layers "L0 64->64,L0 128->64,L1 128->128,L2 256->256,L3 512->512,L4 1024->1024" \
+              --variants "tap64p_claim=0,halop_claim=0,wgrad_halop_claim=0;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1,claim_full=1" \
+              > gpurun_out/claim_kernels3.log 2>&1 ;;
+    probefull) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 --opt tap64p_claim=1 --opt halop_claim=1 \
+               --opt wgrad_halop_claim=1 --opt claim_full=1 > gpurun_out/contention_full.log 2>&1 ;;
+    bndet) timeout -k 10 300 python -u tools/diag_bn_grads.py > gpurun_out/diag_bn_grads.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   rc=$?
