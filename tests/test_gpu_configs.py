@@ -152,10 +152,13 @@ def unet_bn_slice_vs_oracle(L, S, B, seed):
         net.backward(grads)
         torch.cuda.synchronize()
         err = (outs["main_out"].cpu() - p).abs().max().item()
+        print(f"[gate] unet_bn slice L{L} S{S} B{B} {dtype}: forward max {err:.3e} mean "
+              f"{(outs['main_out'].cpu() - p).abs().mean().item():.3e}")
         # (bf16: storage rounding through 8 BatchNorm layers; 0.044 measured at a logit near the 0.5 boundary)
         assert err < (1e-4 if dtype == "f32" else 6e-2), (dtype, err)
         assert (outs["main_out"].cpu() - p).abs().mean().item() < (1e-5 if dtype == "f32" else 5e-3)
         bad = []
+        worst_c = 1.0
         for name, ts in W.items():
             for si, (gi, t) in enumerate(zip(net.get_layer_grads(name), ts)):
                 c = cos(torch.as_tensor(gi), t.grad)
@@ -169,6 +172,10 @@ def unet_bn_slice_vs_oracle(L, S, B, seed):
                         bad.append((name, si, r, c))
                 elif c <= 0.95:
                     bad.append((name, si, c))
+                if dtype == "bf16":
+                    worst_c = min(worst_c, c)
+        if dtype == "bf16":
+            print(f"[gate] unet_bn slice L{L} S{S} B{B} bf16: lowest gradient cosine vs the f32 oracle {worst_c:.5f}")
         assert not bad, (dtype, bad)
         del net, tr
         torch.cuda.empty_cache()

@@ -144,6 +144,8 @@ for s in $STEPS; do
               > gpurun_out/claim_kernels3.log 2>&1 ;;
     probefull) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 --opt tap64p_claim=1 --opt halop_claim=1 \
                --opt wgrad_halop_claim=1 --opt claim_full=1 > gpurun_out/contention_full.log 2>&1 ;;
+    gates) timeout -k 10 600 python -u -m pytest -s -v --timeout 300 --timeout-method thread tests/test_gpu_configs.py \
+             tests/test_gpu_network.py -k "slice_vs_oracle or fallback_paths" > gpurun_out/gates.log 2>&1 ;;
     bndet) timeout -k 10 300 python -u tools/diag_bn_grads.py > gpurun_out/diag_bn_grads.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
