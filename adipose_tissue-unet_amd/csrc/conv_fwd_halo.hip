@@ -754,10 +754,12 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     a.claim = option("halop_claim", option("dp_claim", 0)) && nt_n + 1 <= CLAIM_INTS && !(bnr && one_chunk) && !(pipe && (epi == 1 || epi == 3))
                   ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("halop_claim_chunk", 4));   // patches per claim
-    a.claim_full = option("claim_full", 0);
+    a.claim_full = 0;
     if (a.claim) {   // (no more blocks per output block than super-tiles)
       const int nsup = (tiles / nt_n + a.claim_chunk - 1) / a.claim_chunk;
       grid = std::max(nt_n, std::min(grid, nsup * nt_n));
+      // claim_full only with at least 4 super-tiles per block (its first claim takes two at once)
+      a.claim_full = option("claim_full", 0) && nsup >= 4 * (grid / nt_n);
     }
     const bool dyn = a.claim != nullptr;
     adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,

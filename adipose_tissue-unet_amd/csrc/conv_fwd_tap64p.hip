@@ -731,6 +731,104 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       }
     }
   };
+  // wide_st = 2: the same 16-B stores in line order. epilogue_wide writes the first 64 B of the wave's 128-B pixel
+  // lines (groups 0-1) for all 2 * MIQ pixel groups and only then the second 64 B (groups 2-3): 16 store instructions
+  // apart, and with every CU of an XCD in its epilogue at once (8 waves x 128 pixels x 64 B = 64 KiB per CU, 2 MiB per
+  // XCD between the two halves of a line) the L2 writes many lines back in halves -- PMC WRITE_SIZE 1.48x the output
+  // bytes on every level (profiles/r04c_pmc_dom.txt). Here the two halves of each pixel line leave in consecutive
+  // instructions. Same values, same stores: bit-identical.
+  auto epilogue_lines = [&](int m0) {
+    if constexpr (!BNR && !F32) {
+      int tidv = tid;
+      asm volatile("" : "+v"(tidv));
+      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+      float bias[4][4], wsc[4][4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float4 b4 = p_lds_f4(&cst[0][wc * 64 + nt * 16 + 4 * h4]);
+        bias[nt][0] = b4.x; bias[nt][1] = b4.y; bias[nt][2] = b4.z; bias[nt][3] = b4.w;
+        if constexpr (F8) {
+          const float4 w4 = p_lds_f4(&cst[1][wc * 64 + nt * 16 + 4 * h4]);
+          wsc[nt][0] = w4.x; wsc[nt][1] = w4.y; wsc[nt][2] = w4.z; wsc[nt][3] = w4.w;
+        }
+      }
+      // per pair of groups (np = 0, 2): this lane's 8-channel run after the exchange and its store target
+      int cqp[2], subp[2], ostrp[2];
+      bool cvp[2];
+      __amdgpu_buffer_rsrc_t rsOp[2];
+#pragma unroll
+      for (int pi = 0; pi < 2; ++pi) {
+        const int np = 2 * pi;
+        const int cw = n0 + wc * 64 + 16 * (np + (h4 & 1)) + 8 * (h4 >> 1);
+        cvp[pi] = cw < a.Nout;
+        subp[pi] = 0;
+        cqp[pi] = cw;
+        if (shuffle) { subp[pi] = cw / a.Cps; cqp[pi] = cw - subp[pi] * a.Cps; }
+        const bool second = split && __builtin_amdgcn_readfirstlane(n0 + wc * 64 + np * 16) >= a.split_c;
+        if (second) cqp[pi] = cw - a.split_c;
+        ostrp[pi] = second ? a.out2_stride : a.out_stride;
+        rsOp[pi] = __builtin_amdgcn_make_buffer_rsrc(second ? a.out2 : a.out, 0, second ? out2_bytes : (int)out_bytes,
+                                                     P_RSRC3);
+      }
+      float s1[4][4] = {}, s2[4][4] = {};
+#pragma unroll
+      for (int mt = 0; mt < 2 * MIQ; ++mt) {
+        const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
+        const bool mv = m < a.M;
+#pragma unroll
+        for (int pi = 0; pi < 2; ++pi) {
+          v2u32 o2[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int nt = 2 * pi + j;
+            const bool qv = mv && n0 + wc * 64 + nt * 16 + 4 * h4 < a.Nout;   // (statistics: own quad)
+            float x[4];
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              x[r] = F8 ? fmaf(acc[mt][nt][r], wsc[nt][r], bias[nt][r]) : acc[mt][nt][r] + bias[nt][r];
+              if (a.relu) x[r] = fmaxf(x[r], 0.f);
+              o[r] = (bf16)x[r];
+            }
+            o2[j] = __builtin_bit_cast(v2u32, o);
+            if (stats && qv) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) { s1[nt][r] += x[r]; s2[nt][r] += x[r] * x[r]; }
+            }
+          }
+          const auto e0 = __builtin_amdgcn_permlane16_swap(o2[0].x, o2[1].x, false, false);
+          const auto e1 = __builtin_amdgcn_permlane16_swap(o2[0].y, o2[1].y, false, false);
+          const v4u32_t st = {e0[0], e1[0], e0[1], e1[1]};
+          int pixo = m;
+          if (shuffle) {
+            const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+            pixo = (img * Hq + 2 * yo + (subp[pi] >> 1)) * Wq + 2 * xo + (subp[pi] & 1);
+          }
+          const unsigned off =
+              mv && cvp[pi] && !(a.debug_flags & 128) ? (unsigned)((pixo * ostrp[pi] + cqp[pi]) * OES) : P_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(st, rsOp[pi], off, 0, 0);
+        }
+      }
+      if (stats) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s1[nt][r] = row16_sum(s1[nt][r]);
+            s2[nt][r] = row16_sum(s2[nt][r]);
+          }
+          if (r16 == 0) {
+            const int cl = wc * 64 + nt * 16 + 4 * h4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              p_lds_add(&sacc[0][cl + r], s1[nt][r]);
+              p_lds_add(&sacc[1][cl + r], s2[nt][r]);
+            }
+          }
+        }
+      }
+    }
+  };
   const bool wide = !BNR && !F32 && a.wide_st;   // (fp8: bf16 output only, the launcher checks)
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
@@ -875,7 +973,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       last_epi = -NST;   // (no epilogue ops were issued)
       continue;
     }
-    if (wide) epilogue_wide(m0c);
+    if (wide && a.wide_st == 2) epilogue_lines(m0c);
+    else if (wide) epilogue_wide(m0c);
     else epilogue(m0c);
   }
 
@@ -937,9 +1036,12 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // (a software-pipelined K loop -- barrier in the middle of the previous step, B half 0 preloaded -- measured
   //  1.5-5 % slower here and was removed: profiles/r03_kpipe_ab.txt)
   // fp8 launches with a bf16 output take them too (option tap64p_wide_f8); fp8 outputs keep 4-B stores
-  a.wide_st = option("tap64p_wide", 1) && !a.f32 && (!a.f8 || (option("tap64p_wide_f8", 0) && !a.out_f8)) && !a.bnr_z &&
-              a.Nout % 16 == 0 &&
-              (a.out_mode != 2 || a.split_c % 32 == 0);
+  // (tap64p_wide = 2: the same stores in line order, epilogue_lines)
+  const int wide_opt = option("tap64p_wide", 1);
+  a.wide_st = wide_opt && !a.f32 && (!a.f8 || (option("tap64p_wide_f8", 0) && !a.out_f8)) && !a.bnr_z &&
+              a.Nout % 16 == 0 && (a.out_mode != 2 || a.split_c % 32 == 0)
+                  ? (wide_opt == 2 ? 2 : 1)
+                  : 0;
   int cfg = option("tap64p_cfg", 0);
   if (cfg < 1 || cfg > 3) {
     if (a.bnr_z && tile != 1 && option("tap64p_bnr", 1) < 2) return 0;
@@ -955,7 +1057,9 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // dynamic tile claiming (option tap64p_claim): robust to CUs held by another stream's kernels (RCCL)
   a.claim = nullptr;
   if (option("tap64p_claim", option("dp_claim", 0)) && a.ntile_n + 1 <= CLAIM_INTS) a.claim = claim_slot();   // (nullptr: static lists)
-  a.claim_full = option("claim_full", 0);
+  // claim_full: only with at least 4 tiles per block (its first claim takes tiles 0 and 1 at once: with fewer,
+  // the blocks that start first would take two tiles each and leave the rest idle -- 2x on a 1-tile-per-block launch)
+  a.claim_full = option("claim_full", 0) && mt >= 4 * (grid / a.ntile_n);
   const bool bnr = a.bnr_z != nullptr;
   // the halo form (option tap64p_halo): 3x3 stride-1 'same' layers whose output tiles into 8 x 32 patches
   const bool halo_shape = !bnr && option("tap64p_halo", 1) && a.out_mode != 1 && a.kh == 3 && a.kw == 3 &&

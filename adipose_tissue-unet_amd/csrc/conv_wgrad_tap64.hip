@@ -1165,8 +1165,9 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     // dynamic patch claiming (option wgrad_halop_claim; nullptr from claim_slot: static lists)
     a.claim = option("wgrad_halop_claim", option("dp_claim", 0)) && combos + 1 <= CLAIM_INTS ? claim_slot() : nullptr;
     a.claim_chunk = std::max(1, option("wgrad_halop_claim_chunk", 4));   // patches per claim
-    a.claim_full = option("claim_full", 0);
     if (a.claim) per = std::min(per, (tiles + a.claim_chunk - 1) / a.claim_chunk);   // (<= super-patches)
+    // claim_full only with at least 4 super-patches per block (its first claim takes two at once)
+    a.claim_full = option("claim_full", 0) && (tiles + a.claim_chunk - 1) / a.claim_chunk >= 4 * per;
     const int grid = per * combos;
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {

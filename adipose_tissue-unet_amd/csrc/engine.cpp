@@ -1675,11 +1675,9 @@ extern "C" int adp_set_comm(adp_handle* h, void* comm) {
   if (!h) { adp::set_error("adp_set_comm: null handle"); return -1; }
   if (comm && !rccl().ok) { adp::set_error("adp_set_comm: librccl.so.1 not loadable"); return -3; }
   h->comm = comm;
-  // data parallel over more than one rank: the persistent kernels claim their tiles (option dp_claim, the
-  // default of tap64p_claim / halop_claim / wgrad_halop_claim), so RCCL's blocks holding CUs during the
-  // overlapped bucket all-reduces do not leave whole static tile lists waiting
-  int n = 1;
-  if (comm && rccl().count(static_cast<ncclComm_t>(comm), &n) == ncclSuccess && n > 1) adp_set_option("dp_claim", 1);
+  // (the persistent kernels keep their static tile lists under data parallelism: in the bucket schedule a held
+  // CU frees within one bucket's all-reduce, and static lists measured cheaper than claimed tiles end to end --
+  // DESIGN.md §5, profiles/r04c_bucket_probe.log; option dp_claim=1 turns claiming on)
   return 0;
 }
 

@@ -153,11 +153,10 @@ class Trainer:
         self.world = dist.get_world_size(process_group) if self.distributed else 1
         self.buckets = (GradBuckets(net, bucket_bytes, process_group, overlap=overlap_allreduce)
                         if self.distributed and self.world > 1 else None)
-        if self.buckets is not None:
-            # data parallel: the persistent kernels claim their tiles from counters (option dp_claim, the default
-            # of tap64p_claim / halop_claim / wgrad_halop_claim): RCCL's blocks hold CUs while the overlapped
-            # buckets reduce, and static tile lists would leave whole blocks waiting for them
-            ops.set_option("dp_claim", 1)
+        # (data parallel keeps the persistent kernels' static tile lists: with the bucket schedule -- each bucket's
+        # all-reduce holding CUs for a fraction of a millisecond -- static lists cost the overlapped step +0.4-0.5 ms
+        # against +0.7 ms with claimed tiles, whose kernels are 3-11 % slower on an idle chip, and +1.9-2.2 ms for
+        # the exposed all-reduce: profiles/r04c_bucket_probe.log, DESIGN.md §5. Option dp_claim=1 turns claiming on.)
         self.stats = torch.zeros((3, 8), dtype=torch.float64, device=dev)   # per head: loss_rows sums
         self.lossbuf = torch.zeros(4, dtype=torch.float64, device=dev)
         self._dp = {}

@@ -154,9 +154,11 @@ def unet_bn_slice_vs_oracle(L, S, B, seed):
         err = (outs["main_out"].cpu() - p).abs().max().item()
         print(f"[gate] unet_bn slice L{L} S{S} B{B} {dtype}: forward max {err:.3e} mean "
               f"{(outs['main_out'].cpu() - p).abs().mean().item():.3e}")
-        # (bf16: storage rounding through 8 BatchNorm layers; 0.044 measured at a logit near the 0.5 boundary)
-        assert err < (1e-4 if dtype == "f32" else 6e-2), (dtype, err)
-        assert (outs["main_out"].cpu() - p).abs().mean().item() < (1e-5 if dtype == "f32" else 5e-3)
+        # (bf16: storage rounding through 8 BatchNorm layers, at a logit near the 0.5 boundary. Since round 4 the
+        # BatchNorm sums are deterministic, so this is one fixed value per build rather than a run-dependent spread:
+        # 4.06e-2 max / 2.71e-3 mean measured (profiles/r04c_gates.log); round 3 allowed 6e-2 / 5e-3 for the spread)
+        assert err < (1e-4 if dtype == "f32" else 5e-2), (dtype, err)
+        assert (outs["main_out"].cpu() - p).abs().mean().item() < (1e-5 if dtype == "f32" else 3.5e-3)
         bad = []
         worst_c = 1.0
         for name, ts in W.items():
@@ -170,7 +172,7 @@ def unet_bn_slice_vs_oracle(L, S, B, seed):
                     r = rel_err(gi, t.grad)
                     if r >= 5e-2 or c < 0.9999:
                         bad.append((name, si, r, c))
-                elif c <= 0.95:
+                elif c <= 0.965:   # (bf16 vs the f32 oracle: 0.974 lowest measured, profiles/r04c_gates.log)
                     bad.append((name, si, c))
                 if dtype == "bf16":
                     worst_c = min(worst_c, c)

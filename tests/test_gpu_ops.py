@@ -171,8 +171,8 @@ def test_tap64_configs(cfg):
     assert relerr(st[1, :cout], (rs * rs).sum(0)) < 2e-2
 
 
-@pytest.mark.parametrize("claim", [0, 1], ids=["static", "claimed"])
-@pytest.mark.parametrize("wide", [0, 1], ids=["st8", "st16"])
+@pytest.mark.parametrize("claim", [0, 1, 2], ids=["static", "claimed", "claimed_full"])
+@pytest.mark.parametrize("wide", [0, 1, 2], ids=["st8", "st16", "st16_lines"])
 @pytest.mark.parametrize("tile", [256, 128], ids=["256x256x2", "256x128x3"])
 @pytest.mark.parametrize("grid", [None, 3, 7], ids=["chip_grid", "3_blocks", "7_blocks"])
 @pytest.mark.parametrize("mode", ["plain", "one_chunk", "concat", "split"])
@@ -212,7 +212,8 @@ def test_tap64p_halo_matches(mode, grid, tile, wide, claim):
         ops.set_option("tap64p_halo", halo)
         ops.set_option("fwd_w4", 0)   # (the four-wave form takes the Nout % 256 == 0 shapes: its own test)
         ops.set_option("tap64p_wide", wide)
-        ops.set_option("tap64p_claim", claim)
+        ops.set_option("tap64p_claim", min(claim, 1))
+        ops.set_option("claim_full", 1 if claim == 2 else 0)   # (every tile claimed: the 3 / 7-block grids)
         if grid:
             ops.set_option("tap64_persist_grid", grid)
         try:
@@ -220,7 +221,8 @@ def test_tap64p_halo_matches(mode, grid, tile, wide, claim):
             torch.cuda.synchronize()
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
-            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4", "tap64p_wide", "tap64p_claim"):
+            for o_ in ("fwd_tap64", "fwd_halo", "tap64p_halo", "tap64_persist_grid", "fwd_w4", "tap64p_wide", "tap64p_claim",
+                       "claim_full"):
                 ops.set_option(o_, None)
         assert kname.startswith("igemm_fwd_tap64p_kernel<256, %d, %d, false, %s, false" % (
             tile, 2 if tile == 256 else 3, "true" if halo else "false")), kname
@@ -1358,7 +1360,8 @@ def test_halo_kernels_claimed_match_static(case, grid):
     block takes change, their arithmetic does not. Forward forms (plain / ReLU / statistics / BN-backward
     reduction / mask / split / upsample gather): stored outputs bit-identical to the static lists, BatchNorm sums
     to f32 order; weight gradient (plain, two sources, fused BN apply): dW to f32 order (per-block f32 atomics),
-    dz bit-identical. Each claimed launch runs three times (the counter slot re-zeroed by its last block)."""
+    dz bit-identical. Each claimed launch runs three times (the counter slot re-zeroed by its last block), then twice
+    with every super-tile claimed (option claim_full, one-patch claims so that the 1 / 7-block grids take it)."""
     name, parts, cout, kind = case
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(51)
@@ -1413,13 +1416,16 @@ def test_halo_kernels_claimed_match_static(case, grid):
         if grid:
             ops.set_option("halo_persist_grid", grid)
             ops.set_option("wgrad_halop_grid", grid)
-        for claim in (0, 1, 1, 1):
-            ops.set_option(wopt, claim)
+        for claim in (0, 1, 1, 1, 2, 2):
+            ops.set_option(wopt, min(claim, 1))
+            if claim == 2:
+                ops.set_option("claim_full", 1)
+                ops.set_option(wopt + "_chunk", 1)
             ex, fl = run()
             torch.cuda.synchronize()
             res.append((ex, fl, _lib.lib().adp_last_kernel().decode()))
     finally:
-        for o_ in ("halo_persist_grid", "wgrad_halop_grid", wopt):
+        for o_ in ("halo_persist_grid", "wgrad_halop_grid", wopt, "claim_full", wopt + "_chunk"):
             ops.set_option(o_, None)
     k0 = res[0][2]
     assert k0.startswith("igemm_wgrad_halop_kernel" if kind.startswith("wgrad") else "igemm_fwd_halop_kernel"), k0

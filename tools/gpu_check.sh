@@ -146,6 +146,19 @@ for s in $STEPS; do
                --opt wgrad_halop_claim=1 --opt claim_full=1 > gpurun_out/contention_full.log 2>&1 ;;
     gates) timeout -k 10 600 python -u -m pytest -s -v --timeout 300 --timeout-method thread tests/test_gpu_configs.py \
              tests/test_gpu_network.py -k "slice_vs_oracle or fallback_paths" > gpurun_out/gates.log 2>&1 ;;
+    ctests) timeout -k 10 600 python -u -m pytest -s -v --timeout 200 --timeout-method thread tests/test_gpu_ops.py \
+              tests/test_gpu_configs.py tests/test_gpu_network.py \
+              -k "claim or fallback_paths or slice_vs_oracle or deterministic" > gpurun_out/ctests.log 2>&1 ;;
+    bprobe) timeout -k 10 500 python -u tools/contention_probe.py --buckets --blocks 8,32 > gpurun_out/bucket_probe.log 2>&1 ;;
+    bprobefull) timeout -k 10 500 python -u tools/contention_probe.py --buckets --blocks 8,32 --opt claim_full=1 \
+              > gpurun_out/bucket_probe_full.log 2>&1 ;;
+    wtests) timeout -k 10 600 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_gpu_ops.py \
+              -k "tap64p_halo_matches or tap64_persistent_matches" > gpurun_out/wtests.log 2>&1 ;;
+    wlines) timeout -k 10 400 python tools/bench_kernels.py --kinds fwd,fwd_stats --layers "L2 256->256,L3 512->512,L4 1024->1024" \
+              --variants "tap64p_wide=1;tap64p_wide=2" > gpurun_out/wlines_kernels.log 2>&1 ;;
+    wlinespmc) bash tools/pmc_dom.sh "L2 256->256,L3 512->512,L4 1024->1024" fwd,fwd_stats "tap64p_wide=2" \
+              > gpurun_out/pmc_dom.log 2>&1 ;;
+    wab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_wide=1;tap64p_wide=2" > gpurun_out/wlines_ab.log 2>&1 ;;
     bndet) timeout -k 10 300 python -u tools/diag_bn_grads.py > gpurun_out/diag_bn_grads.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
