@@ -1036,8 +1036,10 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // (a software-pipelined K loop -- barrier in the middle of the previous step, B half 0 preloaded -- measured
   //  1.5-5 % slower here and was removed: profiles/r03_kpipe_ab.txt)
   // fp8 launches with a bf16 output take them too (option tap64p_wide_f8); fp8 outputs keep 4-B stores
-  // (tap64p_wide = 2: the same stores in line order, epilogue_lines)
-  const int wide_opt = option("tap64p_wide", 1);
+  // tap64p_wide = 2 (default since round 4): the same stores in line order (epilogue_lines): PMC writes 1.48x ->
+  // 1.00x the output bytes on levels 2-4, the kernel +1.0-1.3 % on levels 2-3, step 23.51 -> 23.43 ms
+  // (profiles/r04c_wlines_*.txt); 1 = the pair-major order of round 3
+  const int wide_opt = option("tap64p_wide", 2);
   a.wide_st = wide_opt && !a.f32 && (!a.f8 || (option("tap64p_wide_f8", 0) && !a.out_f8)) && !a.bnr_z &&
               a.Nout % 16 == 0 && (a.out_mode != 2 || a.split_c % 32 == 0)
                   ? (wide_opt == 2 ? 2 : 1)
