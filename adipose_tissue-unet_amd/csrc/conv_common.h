@@ -446,6 +446,8 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s);
 // layers with Nout % 256 == 0; called by launch_fwd_tap64p for its 256x256 halo shapes.
 int launch_fwd_w4(FwdArgs& a, hipStream_t s);
 int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)
+// conv_fwd_halo_f8.hip: fp8 forward of 3x3 layers with 64-channel sources (one, or two concatenated)
+int launch_fwd_halop_f8(FwdArgs& a, hipStream_t s);
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
 // conv_wgrad_f32.hip: f32 weight gradient on LDS-DMA staging (32-pixel stages, exact f32 MFMA)

@@ -83,6 +83,34 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
           acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mb][ks], xb[u][ks], acc[mb], 0, 0, 0);
       const int m = mm[u];
       typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      if (a.out_f8) {
+        // fp8 e4m3 output (UNetBN.forward_fp8's level-0 operand; no statistics): each 16-channel block's quad is one
+        // dword; a 4 x 4 transpose over the lane rows (v_permlane16_swap, then v_permlane32_swap) leaves lane row h4
+        // with channels 16 h4 .. + 15 of its pixel, one 16-B store (Nout == 64, the launcher checks)
+        const bool mv = g0 + u < groups && m < a.M;
+        unsigned d[4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          float c8[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v = acc[mb][i] + bias[mb][i];
+            if (a.relu) v = fmaxf(v, 0.f);
+            c8[i] = fminf(fmaxf(v, -FP8_MAX), FP8_MAX);
+          }
+          int qv = __builtin_amdgcn_cvt_pk_fp8_f32(c8[0], c8[1], 0, false);
+          qv = __builtin_amdgcn_cvt_pk_fp8_f32(c8[2], c8[3], qv, true);
+          d[mb] = (unsigned)qv;
+        }
+        const auto p01 = __builtin_amdgcn_permlane16_swap(d[0], d[1], false, false);
+        const auto p23 = __builtin_amdgcn_permlane16_swap(d[2], d[3], false, false);
+        const auto q02 = __builtin_amdgcn_permlane32_swap(p01[0], p23[0], false, false);
+        const auto q13 = __builtin_amdgcn_permlane32_swap(p01[1], p23[1], false, false);
+        if (mv)
+          *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(a.out) + (size_t)m * a.out_stride + 16 * h4) =
+              make_uint4(q02[0], q13[0], q02[1], q13[1]);
+        continue;
+      }
       if (a.wide_st) {
         // 16-B stores: the quads of 16-channel blocks mb and mb + 1 joined by v_permlane16_swap (lane row h4
         // then holds channels 16 (mb + (h4 & 1)) + 8 (h4 >> 1) .. + 7), before the lane-divergent tail test
@@ -286,7 +314,7 @@ void launch_cin8_u(FwdArgs& a, hipStream_t s) {
   const int waves = std::max(1, std::min((groups + UNR - 1) / UNR, adp::option("cin8_waves", 2048)));
   const size_t HWo = (size_t)a.Ho * a.Wo;
   const size_t src_bytes = ((size_t)a.M + HWo - 1) / HWo * a.Hs * a.Ws * 16, out_bytes = (size_t)a.M * a.out_stride * 2;
-  if (adp::option("cin8_pf", 0) && src_bytes < (1ull << 31) && out_bytes < (1ull << 31)) {
+  if (adp::option("cin8_pf", 0) && !a.out_f8 && src_bytes < (1ull << 31) && out_bytes < (1ull << 31)) {
     adp::set_kernel("igemm_fwd_cin8p_kernel<%d, %d>", KS, UNR);
     hipLaunchKernelGGL((igemm_fwd_cin8p_kernel<KS, UNR>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
     return;
@@ -314,6 +342,8 @@ int launch_fwd_cin8(FwdArgs& a, hipStream_t s) {
       a.Kpad < (a.K + 31) / 32 * 32 || a.Nout > 64 || a.Nout % 8 != 0 || a.out_mode != 0 || !a.out ||
       a.out_stride % 4 != 0 || a.addend || a.mask || a.accum || a.drop_rate > 0.f || a.bnr_z)
     return 0;
+  // fp8 output (desc out_fp8 on a bf16 launch): 64 channels, 16-B aligned pixel rows, no statistics
+  if (a.out_f8 && (a.Nout != 64 || a.out_stride % 16 != 0 || a.bn_sum)) return 0;
   // 16-B output stores (option cin8_wide): every 8-channel run wholly inside or outside Nout (Nout % 8 == 0)
   a.wide_st = option("cin8_wide", 1) && a.out_stride % 8 == 0;
   const int ks = (a.K + 31) / 32;

@@ -1062,6 +1062,11 @@ int launch_fwd_f8(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) 
                   (d->out_mode == 0 || d->out_mode == 1) && a.out,
               "adp_conv_fwd(fp8): plain or pixel-shuffle store only (no BN / addend / mask / accum / dropout)");
   ADP_REQUIRE(d->out_mode != 1 || (d->shuffle_c > 0 && d->Nout % d->shuffle_c == 0), "adp_conv_fwd: bad shuffle_c");
+  // 64-channel sources (unet_bn level 0): the fp8 halo kernel (tap pairs / two concatenated sources per K step)
+  if (a.CAs == 64 && a.CBs % 64 == 0 && adp::launch_fwd_halop_f8(a, s)) {
+    adp::kernel_end();
+    return adp::check_launch("adp_conv_fwd");
+  }
   ADP_REQUIRE(a.CAs % 128 == 0 && a.CBs % 128 == 0,
               "adp_conv_fwd(fp8): source channel strides must be multiples of 128 (one 128-channel K step per tap)");
   if (!adp::launch_fwd_tap64(a, s)) {
@@ -1077,6 +1082,17 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   FwdArgs a;
   fill_fwd_args(d, io, a);
   ADP_REQUIRE(a.CAs % 8 == 0 && a.CBs % 8 == 0, "adp_conv_fwd: channel strides must be multiples of 8");
+  if (d->out_fp8) {   // a bf16 launch storing fp8: the input layer of the fp8 forward (UNetBN.forward_fp8) only
+    ADP_REQUIRE((std::is_same<T, bf16>::value), "adp_conv_fwd: out_fp8 needs a bf16 or fp8 launch");
+    a.out_f8 = 1;
+    if (!adp::launch_fwd_cin8(a, s)) {
+      adp::set_error("adp_conv_fwd: out_fp8 on a bf16 launch: input layers only (one 8-channel source, Nout == 64, "
+                     "no statistics)");
+      return -1;
+    }
+    adp::kernel_end();
+    return adp::check_launch("adp_conv_fwd");
+  }
   ADP_REQUIRE(a.M > 0 && a.Nout > 0, "adp_conv_fwd: empty problem");
   ADP_REQUIRE(d->out_mode != 1 || (d->shuffle_c > 0 && d->Nout % d->shuffle_c == 0), "adp_conv_fwd: bad shuffle_c");
   ADP_REQUIRE(d->out_mode != 2 || (io->out2 && d->split_c > 0), "adp_conv_fwd: split store needs out2/split_c");

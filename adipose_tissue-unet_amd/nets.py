@@ -822,11 +822,17 @@ class UNetBN(UNetEngine):
         return {"main_out": a["p"]}
 
     # ------------------------------------------------------------------ fp8 inference (configs[4])
+    fp8_level0 = True   # forward_fp8: level 0 in fp8 too (the 64-channel fp8 halo kernel; False: bf16 as in round 3)
+
     def _fp8_acts(self, B):
-        """fp8 e4m3 twins of every activation at levels >= 1 (channel strides >= 128): the operands of the
-        fp8 convs. Level 0 (64 channels) and pool0 stay bf16."""
+        """fp8 e4m3 twins of the activations the fp8 convs read: every level >= 1 (channel strides >= 128) and,
+        with fp8_level0, level 0 (64 channels: enc0_conv1's output, pool0, the decoder's concat halves and
+        dec0_conv1's output; dec0_conv2's output stays bf16 for the head)."""
         a = self.acts(B)
         q = {}
+        if self.fp8_level0 and self.levels > 1:
+            for k in ("az0_1", "az0_2", "pool0", "t0", "ay0_1"):
+                q[k] = self.buf("q/" + k, tuple(a[k].shape), ops.FP8_DTYPE)
         for i in range(1, self.levels):
             keys = [f"az{i}_1", f"az{i}_2"]
             if i < self.levels - 1:
@@ -837,10 +843,13 @@ class UNetBN(UNetEngine):
 
     def pack_fp8_weights(self):
         """fp8 forward weights + per-output-channel scales for every layer whose input channel strides are
-        multiples of 128 (one 128-channel K step per tap)."""
+        multiples of 128 (one 128-channel K step per tap) and every 3x3 layer over 64-channel sources (the fp8
+        halo kernel: tap pairs, or the two halves of a concat, per 128-deep K step)."""
         self._packed8 = {}
         for n, l in self.layers.items():
-            if isinstance(l, Dense) and all(c % 128 == 0 for c in l.cin_s) and l.K % 128 == 0:
+            wide = all(c % 128 == 0 for c in l.cin_s) and l.K % 128 == 0 if isinstance(l, Dense) else False
+            c64 = isinstance(l, Dense) and not l.transpose and l.k == 3 and all(c == 64 for c in l.cin_s)
+            if wide or c64:
                 dst = self.buf("w8/" + n, (l.Npad, l.Kpad), ops.FP8_DTYPE)
                 sc = self.buf("w8s/" + n, (l.Npad,), torch.float32)
                 ops.pack_weights_fp8(self.ps.view(n + "/W"), dst, sc)
@@ -863,7 +872,8 @@ class UNetBN(UNetEngine):
         rm, rv = self.running[name]
         ops.bn_finalize(-1.0, rm, rv, self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
                         self.bn_eps, 0.0, s[2], s[3], s[4], s[5], None, None)
-        if srcA.dtype != ops.FP8_DTYPE and act.dtype != ops.FP8_DTYPE and self.fuse_eval_bn:
+        if srcA.dtype != ops.FP8_DTYPE and self.fuse_eval_bn and (act.dtype != ops.FP8_DTYPE or l.Cin_s == 8):
+            # (bf16 operands; an fp8 act only from the input layer, whose kernel stores fp8 itself)
             self._conv_eval_folded(l, srcA, act, srcB=srcB)
             return
         if srcA.dtype == ops.FP8_DTYPE and self.fuse_eval_bn:

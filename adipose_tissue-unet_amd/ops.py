@@ -198,6 +198,9 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
                    "fp8 launch needs w_scale (f32, >= nout entries)")
             d.out_fp8 = 1 if out.dtype == FP8_DTYPE else 0
             io.w_scale = ptr(w_scale)
+        elif out.dtype == FP8_DTYPE:   # a bf16 input layer storing its fp8 operand (UNetBN.forward_fp8)
+            _check(srcA.dtype == torch.bfloat16, "fp8 output needs a bf16 (input layer) or fp8 launch")
+            d.out_fp8 = 1
         else:
             _check(out.dtype == srcA.dtype, "out dtype mismatch")
         if out_mode != 1:

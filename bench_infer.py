@@ -35,6 +35,7 @@ def parse():
     p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
     p.add_argument("--levels", type=int, default=5, help="unet_bn levels (mode fp8)")
     p.add_argument("--train-steps", type=int, default=60, help="mode fp8: bf16 training steps before the comparison")
+    p.add_argument("--fp8-level0", type=int, default=1, help="mode fp8: level 0 in fp8 too (0: bf16, as in round 3)")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--size", type=int, default=8192, help="WSI side (mode wsi)")
     p.add_argument("--tile", type=int, default=1024)
@@ -68,6 +69,7 @@ def fp8_main(args):
     torch.cuda.set_device(dev)
     B, S = args.batch, args.tile
     net = UNetBN(B, S, levels=args.levels, base=64, in_ch=3, dtype="bf16", device=dev, seed=865)
+    net.fp8_level0 = bool(args.fp8_level0)
     tr = Trainer(net, LossConfig(use_hard_mining=False), lr=1e-3)
     batches = []
     for k in range(2):
@@ -119,7 +121,7 @@ def fp8_main(args):
         "data": "synthetic (seeded histology-like tiles, resident in HBM)",
         "config": {"workload": f"unet_bn L{args.levels} base64 {S}x{S}x3 forward B={B} (BASELINE configs[4])",
                    "train_steps_before_eval": args.train_steps, "train_s": round(train_s, 2),
-                   "fp8_layers": sorted(net._packed8), "batch": B},
+                   "fp8_layers": sorted(net._packed8), "fp8_level0": net.fp8_level0, "batch": B},
         "bf16_tiles_per_s": round(steps * B / el16, 3), "fp8_speedup": round(el16 / el8, 4),
         "dice_bf16": round(float(np.mean(d16)), 5), "dice_fp8": round(float(np.mean(d8)), 5),
         "dice_delta": round(abs(float(np.mean(d8)) - float(np.mean(d16))), 6),

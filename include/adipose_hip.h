@@ -64,7 +64,8 @@ typedef struct adp_conv_desc {
   float mask2_scale;
   int accum_stride;         /* accum (f32) += stored value */
   int bnr_stride;           /* channel stride of io->bnr_z */
-  int out_fp8;              /* ADP_DTYPE_FP8 launches: 1 stores the output as fp8 e4m3 (else bf16) */
+  int out_fp8;              /* ADP_DTYPE_FP8 launches: 1 stores the output as fp8 e4m3 (else bf16); ADP_BF16
+                               launches: 1 on an input layer (one 8-channel source, Nout 64) stores fp8 */
   int bn_defer_fold;        /* 1: leave this launch's BatchNorm statistics in the library's accumulator
                                replicas instead of adding them into io->bn_sum / bn_sqsum; the next launch
                                on the stream must be adp_bn_finalize_fold for those two vectors */

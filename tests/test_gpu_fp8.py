@@ -204,18 +204,90 @@ def test_fp8_convtranspose_pixel_shuffle(cin, cout, H, out_fp8):
 
 
 def test_fp8_conv_rejects_unsupported_geometry():
-    x8 = torch.zeros(1, 8, 8, 64, dtype=F8, device=DEV)            # 64-channel stride: not a 128 K step
+    # 64-channel stride: not a 128 K step, and (dilation 2) not the 64-channel halo kernel's geometry either
+    x8 = torch.zeros(1, 8, 32, 64, dtype=F8, device=DEV)
     W8 = torch.zeros(64, 9 * 64, dtype=F8, device=DEV)
     sc = torch.ones(64, device=DEV)
-    out = torch.zeros(1, 8, 8, 64, dtype=torch.bfloat16, device=DEV)
+    out = torch.zeros(1, 8, 32, 64, dtype=torch.bfloat16, device=DEV)
     with pytest.raises(ops.AdpError):
-        ops.conv_fwd(x8, W8, 64, out=out, w_scale=sc)
+        ops.conv_fwd(x8, W8, 64, out=out, w_scale=sc, dil=2)
+    # a bf16 launch may store fp8 only as an input layer (one 8-channel source)
+    xb = torch.zeros(1, 8, 32, 64, dtype=torch.bfloat16, device=DEV)
+    Wb = torch.zeros(64, 9 * 64, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(ops.AdpError):
+        ops.conv_fwd(xb, Wb, 64, out=torch.zeros(1, 8, 32, 64, dtype=F8, device=DEV))
 
 
+@pytest.mark.parametrize("cinB,cout,H,W,out_fp8,relu", [
+    (0, 64, 16, 64, True, True),       # one 64-channel source: tap pairs (enc0_conv2), fp8 output
+    (0, 128, 8, 32, True, True),       # two 64-wide output blocks (enc1_conv1 over pool0)
+    (64, 64, 16, 32, True, True),      # two 64-channel sources: the decoder's concat (dec0_conv1)
+    (0, 64, 8, 64, False, True),       # bf16 output (dec0_conv2, read by the head)
+    (64, 128, 8, 32, False, False),
+])
+def test_fp8_halo64_vs_dequantised_reference(cinB, cout, H, W, out_fp8, relu):
+    """fp8 forward over 64-channel sources (conv_fwd_halo_f8.hip: one 128-deep K step = a tap pair of one source,
+    or one tap of two concatenated sources; resident weights, register-prefetched halo, permlane-transposed fp8
+    store) vs a float64 convolution of the same dequantised operands: only the f32 accumulation order and the
+    output rounding differ."""
+    from adipose_amd import _lib
+    g = torch.Generator().manual_seed(cinB + cout + H + W)
+    B = 2
+    xa8 = q8(torch.randn(B, H, W, 64, generator=g).clamp_min(0) * 2)
+    xb8 = q8(torch.randn(B, H, W, cinB, generator=g)) if cinB else None
+    cin = 64 + cinB
+    K = 9 * cin
+    Wf = torch.zeros(((cout + 63) // 64 * 64, K))
+    Wf[:cout] = torch.randn(cout, K, generator=g) * (2.0 / K) ** 0.5
+    bias = torch.randn(cout, generator=g) * 0.1
+    W8, sc = pack8(Wf)
+    out = torch.zeros(B, H, W, cout, dtype=F8 if out_fp8 else torch.bfloat16, device=DEV)
+    ops.conv_fwd(xa8.to(DEV), W8, cout, out=out, srcB=None if xb8 is None else xb8.to(DEV), bias=bias.to(DEV),
+                 kh=3, kw=3, relu=relu, w_scale=sc)
+    torch.cuda.synchronize()
+    kname = _lib.lib().adp_last_kernel().decode()
+    assert kname == "igemm_fwd_halop_f8_kernel<%d>" % (2 if cinB else 1), kname
+    x_cat = xa8 if xb8 is None else torch.cat([xa8.float(), xb8.float()], -1).to(F8)
+    ref = ref_conv(x_cat, W8, sc, cout, 3, 1, cin, bias=bias, relu=relu)
+    got = out.cpu().float().double()
+    rel = 2 ** -3 if out_fp8 else 2 ** -7
+    err = (got - ref).abs() - rel * ref.abs()
+    assert err.max().item() < 1e-3, err.max().item()
+
+
+@pytest.mark.parametrize("relu", [True, False])
+def test_input_layer_fp8_output(relu):
+    """The bf16 input layer (cin8 kernel) storing fp8 (forward_fp8's enc0_conv1: its consumer is the 64-channel fp8
+    halo kernel): the f32 result rounded once to e4m3 by the kernel's 4x4 lane transpose + 16-B stores, against
+    the bf16-stored result rounded to e4m3 on the host (double rounding: at most one e4m3 step, rarely)."""
+    from adipose_amd import _lib
+    g = torch.Generator().manual_seed(17)
+    B, H, W = 2, 32, 64
+    x = torch.zeros(B, H, W, 8)
+    x[..., :3] = torch.randn(B, H, W, 3, generator=g)
+    x = x.to(torch.bfloat16).to(DEV)
+    Wt = torch.zeros(64, 96)
+    Wt[:, :72] = torch.randn(64, 72, generator=g) * 0.3
+    Wt = Wt.to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    o16 = torch.zeros(B, H, W, 64, dtype=torch.bfloat16, device=DEV)
+    o8 = torch.zeros(B, H, W, 64, dtype=F8, device=DEV)
+    ops.conv_fwd(x, Wt, 64, out=o16, bias=bias, relu=relu)
+    ops.conv_fwd(x, Wt, 64, out=o8, bias=bias, relu=relu)
+    torch.cuda.synchronize()
+    assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_cin8_kernel"), _lib.lib().adp_last_kernel()
+    ref = q8(o16.cpu().float())
+    d = (o8.cpu().view(torch.uint8).int() - ref.view(torch.uint8).int()).abs()
+    # (sign-magnitude bytes: a one-step difference is a byte difference of 1 away from zero)
+    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 2e-2, (d.max().item(), (d > 0).float().mean().item())
+
+
+@pytest.mark.parametrize("level0", [True, False], ids=["fp8_level0", "bf16_level0"])
 @pytest.mark.parametrize("S", [64, 128])
-def test_unet_bn_fp8_forward_vs_bf16(S):
+def test_unet_bn_fp8_forward_vs_bf16(S, level0):
     B, L = 2, 3
     net = UNetBN(B, S, levels=L, base=64, in_ch=3, dtype="bf16", device=DEV, seed=11)
+    net.fp8_level0 = level0
     g = torch.Generator().manual_seed(3)
     x = torch.randn(B, S, S, 3, generator=g)
     ops.prep_input(x.to(DEV), net.acts(B)["x"], mean=0.0, std=1.0)

@@ -159,6 +159,12 @@ for s in $STEPS; do
     wlinespmc) bash tools/pmc_dom.sh "L2 256->256,L3 512->512,L4 1024->1024" fwd,fwd_stats "tap64p_wide=2" \
               > gpurun_out/pmc_dom.log 2>&1 ;;
     wab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_wide=1;tap64p_wide=2" > gpurun_out/wlines_ab.log 2>&1 ;;
+    f8l0) timeout -k 10 400 python -u -m pytest tests/test_gpu_fp8.py -v --timeout 200 --timeout-method thread \
+            > gpurun_out/f8l0_tests.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_l0.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode fp8 --fp8-level0 0 > gpurun_out/bench_fp8_l0off.log 2>&1 ;;
+    cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
+            -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     bndet) timeout -k 10 300 python -u tools/diag_bn_grads.py > gpurun_out/diag_bn_grads.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
