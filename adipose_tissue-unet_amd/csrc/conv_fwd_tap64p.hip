@@ -120,9 +120,11 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   constexpr bool ZALL = BNR && MIQ == 2;                     // (see load_zall)
   constexpr int EPI_OPS = 2 * MIQ * 4 * (BNR && !ZALL ? 2 : 1);   // vector-memory ops per thread per epilogue
   constexpr int EPI_OPS_W = 2 * MIQ * 2;                          // ... with 16-B stores (wide_st)
+  constexpr int EPI_OPS_Q = 2 * MIQ;                              // ... fp8 output, 16-B line stores (wide_st 3)
   // (vmcnt holds 0..63: a larger count is clamped, which only waits for more)
   constexpr int VM_EPI = (NST - 2) * LOPS + EPI_OPS < 63 ? (NST - 2) * LOPS + EPI_OPS : 63;
   constexpr int VM_EPI_W = (NST - 2) * LOPS + EPI_OPS_W < 63 ? (NST - 2) * LOPS + EPI_OPS_W : 63;
+  constexpr int VM_EPI_Q = (NST - 2) * LOPS + EPI_OPS_Q < 63 ? (NST - 2) * LOPS + EPI_OPS_Q : 63;
   constexpr int VM_Z = (NST - 2) * LOPS + 4 * 2 * MIQ < 63 ? (NST - 2) * LOPS + 4 * 2 * MIQ : 63;
   // ONE LDS object: with several, the compiler tags every LDS access with per-object alias scopes, and the
   // waitcnt pass then drains vmcnt(0) between the LDS-DMA prefetch of stage t+1 and the fragment reads of
@@ -829,7 +831,68 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       }
     }
   };
-  const bool wide = !BNR && !F32 && a.wide_st;   // (fp8: bf16 output only, the launcher checks)
+  // wide_st = 3 (fp8 output): the four 16-channel groups' quads of a lane (one e4m3 dword each) transposed over the
+  // lane rows -- v_permlane16_swap on the pairs (0, 1) and (2, 3), then v_permlane32_swap on (0, 2) and (1, 3) --
+  // leave lane row h4 with channels 16 h4 .. + 15 of its pixel: one 16-B store per pixel group instead of four
+  // 4-B stores (a 64-B fp8 pixel line per instruction and pixel; pixel-shuffle targets are whole 16-channel runs)
+  auto epilogue_q8 = [&](int m0) {
+    if constexpr (F8) {
+      int tidv = tid;
+      asm volatile("" : "+v"(tidv));
+      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+      // pass 1, group by group (8 constants live): each quad -> its e4m3 dword, kept in the accumulator's first
+      // register (no extra registers: the 256x256 forms have none to spare)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float4 b4 = p_lds_f4(&cst[0][wc * 64 + nt * 16 + 4 * h4]);
+        const float4 w4 = p_lds_f4(&cst[1][wc * 64 + nt * 16 + 4 * h4]);
+        const float bias[4] = {b4.x, b4.y, b4.z, b4.w}, wsc[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int mt = 0; mt < 2 * MIQ; ++mt) {
+          float c8[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = fmaf(acc[mt][nt][r], wsc[r], bias[r]);
+            if (a.relu) x = fmaxf(x, 0.f);
+            c8[r] = fminf(fmaxf(x, -FP8_MAX), FP8_MAX);
+          }
+          int q = __builtin_amdgcn_cvt_pk_fp8_f32(c8[0], c8[1], 0, false);
+          q = __builtin_amdgcn_cvt_pk_fp8_f32(c8[2], c8[3], q, true);
+          acc[mt][nt][0] = __builtin_bit_cast(float, q);
+        }
+      }
+      const int cw = n0 + wc * 64 + 16 * h4;   // this lane's 16 channels after the transpose
+      const bool cv = cw < a.Nout;
+      int sub = 0, cq = cw;
+      if (shuffle) { sub = cw / a.Cps; cq = cw - sub * a.Cps; }
+      const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, (int)out_bytes, P_RSRC3);
+      // pass 2, pixel group by pixel group: transpose and store
+#pragma unroll
+      for (int mt = 0; mt < 2 * MIQ; ++mt) {
+        const int m = pix(m0, wr * TM + (mt / MIQ) * HM + (mt % MIQ) * 16 + r16);
+        const bool mv = m < a.M;
+        unsigned d[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) d[nt] = __builtin_bit_cast(unsigned, acc[mt][nt][0]);
+        const auto p01 = __builtin_amdgcn_permlane16_swap(d[0], d[1], false, false);
+        const auto p23 = __builtin_amdgcn_permlane16_swap(d[2], d[3], false, false);
+        const auto q02 = __builtin_amdgcn_permlane32_swap(p01[0], p23[0], false, false);
+        const auto q13 = __builtin_amdgcn_permlane32_swap(p01[1], p23[1], false, false);
+        const v4u32_t st = {q02[0], q13[0], q02[1], q13[1]};
+        int pixo = m;
+        if (shuffle) {
+          const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
+          pixo = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
+        }
+        const unsigned off = mv && cv && !(a.debug_flags & 128) ? (unsigned)(pixo * a.out_stride + cq) : P_OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(st, rsO, off, 0, 0);
+      }
+    }
+  };
+  const bool q8l = F8 && a.wide_st == 3;   // (fp8 output, launcher: Nout % 16, Cps % 16, out_stride % 16)
+  // (fp8 forms: bf16 output through the narrow epilogue, fp8 output through epilogue_q8 -- the 16-B bf16 forms are not
+  //  compiled into them: with all three epilogues the 256x256 fp8 forms spill)
+  const bool wide = !BNR && !F32 && !F8 && a.wide_st && a.wide_st != 3;
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
@@ -912,7 +975,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         } else if (gs + NST - 2 >= lsteps) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (last_epi > gs - NST) {
-          if (wide) {
+          if (q8l) {
+            if (NST == 2 && hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_Q + 1 < 63 ? VM_EPI_Q + 1 : 63) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_Q) : "memory");
+          } else if (wide) {
             if (NST == 2 && hg_last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W + 1 < 63 ? VM_EPI_W + 1 : 63) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W) : "memory");
           } else if (NST == 2 && hg_last) {
@@ -930,6 +996,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         hdy = tp / 3;
         hdx = tp - 3 * hdy;
       } else if (gs + NST - 2 >= lsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (last_epi > gs - NST && q8l) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_Q) : "memory");
       else if (last_epi > gs - NST && wide) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI_W) : "memory");
       else if (last_epi > gs - NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_EPI) : "memory");
       else if (ZALL && zstep == gs - 1 && NST > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_Z) : "memory");
@@ -973,7 +1040,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       last_epi = -NST;   // (no epilogue ops were issued)
       continue;
     }
-    if (wide && a.wide_st == 2) epilogue_lines(m0c);
+    if (q8l) epilogue_q8(m0c);
+    else if (wide && a.wide_st == 2) epilogue_lines(m0c);
     else if (wide) epilogue_wide(m0c);
     else epilogue(m0c);
   }
@@ -1044,6 +1112,10 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
               a.Nout % 16 == 0 && (a.out_mode != 2 || a.split_c % 32 == 0)
                   ? (wide_opt == 2 ? 2 : 1)
                   : 0;
+  // fp8 output (option tap64p_f8_lines): the lane-transposed 16-B stores of epilogue_q8
+  if (a.f8 && a.out_f8 && option("tap64p_f8_lines", 1) && a.Nout % 16 == 0 && a.out_stride % 16 == 0 &&
+      (a.out_mode != 1 || a.Cps % 16 == 0))
+    a.wide_st = 3;
   int cfg = option("tap64p_cfg", 0);
   if (cfg < 1 || cfg > 3) {
     if (a.bnr_z && tile != 1 && option("tap64p_bnr", 1) < 2) return 0;

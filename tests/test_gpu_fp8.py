@@ -161,6 +161,43 @@ def test_fp8_persistent_halo_form(cinA, cinB, cout, H, W, relu, kern):
     assert ((outs[0] - outs[1]).abs() - 2 ** -7 * ref.abs()).max().item() < 1e-3
 
 
+@pytest.mark.parametrize("case", ["halo256", "halo128", "convt"])
+def test_fp8_output_line_stores_match_narrow(case):
+    """fp8-output launches of the persistent kernel store through epilogue_q8 (the four 16-channel quads of a lane
+    transposed over the lane rows by permlane16 / permlane32 swaps, one 16-B store per pixel group; option
+    tap64p_f8_lines): the same bytes as the 4-B quad stores (option off), on the 256x256 and 256x128 halo forms and the
+    pixel-shuffle ConvTranspose form."""
+    from adipose_amd import _lib
+    g = torch.Generator().manual_seed(41)
+    B = 2
+    if case == "convt":
+        cin, cout, H, W = 256, 128, 8, 16
+        x8 = q8(torch.randn(B, H, W, cin, generator=g).clamp_min(0))
+        W8, sc = pack8(torch.randn(4 * cout, cin, generator=g) * 0.05)
+        kw = dict(kh=1, kw=1, pad=0, out_mode=1, shuffle_c=cout)
+        nout, oshape = 4 * cout, (B, 2 * H, 2 * W, cout)
+    else:
+        cin, cout, H, W = (512, 512, 8, 32) if case == "halo256" else (256, 192, 16, 32)
+        x8 = q8(torch.randn(B, H, W, cin, generator=g).clamp_min(0))
+        W8, sc = pack8(torch.randn(cout, 9 * cin, generator=g) * (2.0 / (9 * cin)) ** 0.5)
+        kw = dict(kh=3, kw=3, relu=True)
+        nout, oshape = cout, (B, H, W, cout)
+    bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    outs, names = [], []
+    for lines in (1, 0):
+        out = torch.zeros(oshape, dtype=F8, device=DEV)
+        ops.set_option("tap64p_f8_lines", lines)
+        try:
+            ops.conv_fwd(x8.to(DEV), W8, nout, out=out, bias=bias, w_scale=sc, **kw)
+            torch.cuda.synchronize()
+            names.append(_lib.lib().adp_last_kernel().decode())
+        finally:
+            ops.set_option("tap64p_f8_lines", None)
+        outs.append(out.cpu().view(torch.uint8))
+    assert all(n.startswith("igemm_fwd_tap64p_kernel") for n in names), names
+    assert torch.equal(outs[0], outs[1]), (outs[0] != outs[1]).sum().item()
+
+
 @pytest.mark.parametrize("cin,cout,H,out_fp8", [(256, 128, 8, False), (128, 64, 16, True), (256, 128, 12, True),
                                                  (512, 256, 8, True), (1024, 512, 4, False)])
 def test_fp8_convtranspose_pixel_shuffle(cin, cout, H, out_fp8):
@@ -278,8 +315,9 @@ def test_input_layer_fp8_output(relu):
     assert _lib.lib().adp_last_kernel().decode().startswith("igemm_fwd_cin8_kernel"), _lib.lib().adp_last_kernel()
     ref = q8(o16.cpu().float())
     d = (o8.cpu().view(torch.uint8).int() - ref.view(torch.uint8).int()).abs()
-    # (sign-magnitude bytes: a one-step difference is a byte difference of 1 away from zero)
-    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 2e-2, (d.max().item(), (d > 0).float().mean().item())
+    # (sign-magnitude bytes: a one-step difference is a byte difference of 1 away from zero; the bf16 rounding moves a
+    # value across an e4m3 rounding midpoint for about 2^-5 of the values: 3.2 % measured without ReLU)
+    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 5e-2, (d.max().item(), (d > 0).float().mean().item())
 
 
 @pytest.mark.parametrize("level0", [True, False], ids=["fp8_level0", "bf16_level0"])

@@ -163,8 +163,16 @@ for s in $STEPS; do
             > gpurun_out/f8l0_tests.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_l0.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode fp8 --fp8-level0 0 > gpurun_out/bench_fp8_l0off.log 2>&1 ;;
+    f8q) timeout -k 10 400 python -u -m pytest tests/test_gpu_fp8.py -v --timeout 200 --timeout-method thread \
+            > gpurun_out/f8q_tests.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_q.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_f8_lines=0 > gpurun_out/bench_fp8_q0.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
+    f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+              SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE -f csv \
+              -d gpurun_out/f32pmc -o sq -- python3 bench.py --preset adipose_v3 --dtype f32 --size 1024 --batch 2 \
+              --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/f32pmc/sq.log 2>&1 ;;
     bndet) timeout -k 10 300 python -u tools/diag_bn_grads.py > gpurun_out/diag_bn_grads.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
