@@ -41,7 +41,7 @@ constexpr int halop_f8_lds() {
   return (NCH == 1 ? 5 : 9) * 64 * 128 + NCH * Q_HSTR + 2 * 64 * 4;
 }
 
-template <int NCH>
+template <int NCH, bool PIPE>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_f8_kernel(FwdArgs a) {
   constexpr int NTH = 512, BN = 64, NF = 4;
   constexpr int NSTEP = NCH == 1 ? 5 : 9;
@@ -161,17 +161,17 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_f8_kernel(FwdArgs a) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // (not unrolled: unrolled, the compiler hoists every step's LDS reads and runs out of registers)
-#pragma unroll 1
-    for (int p = 0; p < NSTEP; ++p) {
-      bf16x8 fb[NF][2], fa[2][2];
+    // K loop, software-pipelined by one step: the fragments of step p + 1 are read from LDS while step p multiplies
+    // (two named fragment sets, steps taken in pairs; a fully unrolled loop hoisted every step's reads and spilled)
+    struct Frag { bf16x8 fb[NF][2], fa[2][2]; };
+    auto load_frag = [&](int p, Frag& F) {
       const unsigned char* Wp = smem + p * BN * WROW;
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int q = nf * 16 + r16, c = 4 * s + h4;
-          fb[nf][s] = *reinterpret_cast<const bf16x8*>(Wp + q * WROW + ((c ^ swz(q)) << 4));
+          F.fb[nf][s] = *reinterpret_cast<const bf16x8*>(Wp + q * WROW + ((c ^ swz(q)) << 4));
         }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -183,15 +183,36 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_f8_kernel(FwdArgs a) {
 #pragma unroll
         for (int mf = 0; mf < 2; ++mf) {
           const int hr = (wave + dy) * Q_HW + mf * 16 + r16 + dx;
-          fa[mf][s] = *reinterpret_cast<const bf16x8*>(Hs_ + hr * Q_HROWB + ((h4 ^ q_hswz(hr)) << 4));
+          F.fa[mf][s] = *reinterpret_cast<const bf16x8*>(Hs_ + hr * Q_HROWB + ((h4 ^ q_hswz(hr)) << 4));
         }
       }
+    };
+    auto mma = [&](const Frag& F) {
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf)
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf)   // transposed: rows = output channels, columns = pixels
           acc[mf][nf] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-              __builtin_bit_cast(v8i32, fb[nf]), __builtin_bit_cast(v8i32, fa[mf]), acc[mf][nf], 0, 0, 0, 127, 0, 127);
+              __builtin_bit_cast(v8i32, F.fb[nf]), __builtin_bit_cast(v8i32, F.fa[mf]), acc[mf][nf], 0, 0, 0, 127, 0, 127);
+    };
+    Frag FA, FB;
+    if constexpr (PIPE) {   // (option halop_f8_pipe, default 1)
+      load_frag(0, FA);
+#pragma unroll 1
+      for (int p = 0; p < NSTEP; p += 2) {
+        if (p + 1 < NSTEP) load_frag(p + 1, FB);
+        mma(FA);
+        if (p + 1 < NSTEP) {
+          if (p + 2 < NSTEP) load_frag(p + 2, FA);
+          mma(FB);
+        }
+      }
+    } else {   // one step at a time: each step's reads, then its MFMAs
+#pragma unroll 1
+      for (int p = 0; p < NSTEP; ++p) {
+        load_frag(p, FA);
+        mma(FA);
+      }
     }
     // ---- epilogue: lane (r16, h4) holds channels 16 nf + 4 h4 .. + 3 of pixel mrow + 16 mf + r16
 #pragma unroll
@@ -280,17 +301,19 @@ int launch_fwd_halop_f8(FwdArgs& a, hipStream_t s) {
   const size_t lim = (size_t)1 << 31;
   if ((size_t)a.M * a.out_stride * (a.out_f8 ? 1 : 2) >= lim) return 0;
   a.ntile_n = a.Nout / 64;
+  const bool pipe = option("halop_f8_pipe", 1);   // K loop software-pipelined by one step
   const int tiles = a.Nimg * (a.Ho / Q_PH) * (a.Wo / Q_PW) * a.ntile_n;
   a.nblocks = tiles;
   int grid = std::max(1, std::min(tiles, option("halo_persist_grid", 256)));
   grid -= grid % a.ntile_n;
   if (grid == 0) grid = a.ntile_n;
+  adp::set_kernel("igemm_fwd_halop_f8_kernel<%d, %s>", a.CBs == 0 ? 1 : 2, pipe ? "true" : "false");
   if (a.CBs == 0) {
-    adp::set_kernel("igemm_fwd_halop_f8_kernel<1>");
-    hipLaunchKernelGGL((igemm_fwd_halop_f8_kernel<1>), dim3(grid), dim3(512), 0, s, a);
+    if (pipe) hipLaunchKernelGGL((igemm_fwd_halop_f8_kernel<1, true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_halop_f8_kernel<1, false>), dim3(grid), dim3(512), 0, s, a);
   } else {
-    adp::set_kernel("igemm_fwd_halop_f8_kernel<2>");
-    hipLaunchKernelGGL((igemm_fwd_halop_f8_kernel<2>), dim3(grid), dim3(512), 0, s, a);
+    if (pipe) hipLaunchKernelGGL((igemm_fwd_halop_f8_kernel<2, true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((igemm_fwd_halop_f8_kernel<2, false>), dim3(grid), dim3(512), 0, s, a);
   }
   return 1;
 }

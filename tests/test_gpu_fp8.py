@@ -283,7 +283,7 @@ def test_fp8_halo64_vs_dequantised_reference(cinB, cout, H, W, out_fp8, relu):
                  kh=3, kw=3, relu=relu, w_scale=sc)
     torch.cuda.synchronize()
     kname = _lib.lib().adp_last_kernel().decode()
-    assert kname == "igemm_fwd_halop_f8_kernel<%d>" % (2 if cinB else 1), kname
+    assert kname == "igemm_fwd_halop_f8_kernel<%d, true>" % (2 if cinB else 1), kname
     x_cat = xa8 if xb8 is None else torch.cat([xa8.float(), xb8.float()], -1).to(F8)
     ref = ref_conv(x_cat, W8, sc, cout, 3, 1, cin, bias=bias, relu=relu)
     got = out.cpu().float().double()

@@ -167,6 +167,10 @@ for s in $STEPS; do
             > gpurun_out/f8q_tests.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_q.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_f8_lines=0 > gpurun_out/bench_fp8_q0.log 2>&1 ;;
+    f8pipe) timeout -k 10 300 python -u -m pytest tests/test_gpu_fp8.py -v --timeout 200 --timeout-method thread \
+              -k "halo64 or line_stores" > gpurun_out/f8pipe_tests.log 2>&1 &&
+            timeout -k 10 300 python bench_infer.py --mode fp8 --opt halop_f8_pipe=0 > gpurun_out/bench_fp8_pipe0.log 2>&1 &&
+            timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_pipe1.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
