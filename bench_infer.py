@@ -65,6 +65,8 @@ def fp8_main(args):
     from adipose_amd.nets import UNetBN
     from adipose_amd.trainer import LossConfig, Trainer
 
+    for kv in args.opt:
+        ops.set_option(kv.split("=")[0], int(kv.split("=")[1]))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     B, S = args.batch, args.tile
