@@ -95,8 +95,14 @@ __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_ha
 // the e-th of half s taking element e -- lane group h4 then supplies k = 16 s + 4 h4 + e to it, and A and B share
 // that permutation, so every k of the step enters the dot product once. f32 epilogue: 16-B stores of a lane's
 // channel quad.
-template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false, bool F32 = false>
+// EPIC (bf16 forms): -1 = the epilogue chosen at run time from a.wide_st (narrow / pair-major 16-B / line-ordered
+// 16-B); 2 = only the line-ordered one compiled in -- the launcher's default store form, without the register
+// allocation of two epilogues it never runs (measured on the fp8 forms, whose ConvTranspose launch went from 0.215 to
+// 0.120 ms when the unused 16-B bf16 epilogues left it)
+template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false, bool F32 = false,
+          int EPIC = -1>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
+  static_assert(EPIC < 0 || (EPIC == 2 && !BNR && !F8 && !F32), "compile-time epilogue: the bf16 line-ordered form");
   static_assert(!F8 || !BNR, "fp8: no BN-backward reduction");
   static_assert(!WREG || (HALO && NST == 2 && !F8), "register-staged weights: the bf16 2-stage halo form");
   static_assert(!F32 || (HALO && !BNR && !F8 && !WREG), "f32: the halo form");
@@ -892,7 +898,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   const bool q8l = F8 && a.wide_st == 3;   // (fp8 output, launcher: Nout % 16, Cps % 16, out_stride % 16)
   // (fp8 forms: bf16 output through the narrow epilogue, fp8 output through epilogue_q8 -- the 16-B bf16 forms are not
   //  compiled into them: with all three epilogues the 256x256 fp8 forms spill)
-  const bool wide = !BNR && !F32 && !F8 && a.wide_st && a.wide_st != 3;
+  const bool wide = EPIC == 2 || (EPIC < 0 && !BNR && !F32 && !F8 && a.wide_st && a.wide_st != 3);
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
@@ -1040,7 +1046,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       last_epi = -NST;   // (no epilogue ops were issued)
       continue;
     }
-    if (q8l) epilogue_q8(m0c);
+    if constexpr (EPIC == 2) epilogue_lines(m0c);
+    else if (q8l) epilogue_q8(m0c);
     else if (wide && a.wide_st == 2) epilogue_lines(m0c);
     else if (wide) epilogue_wide(m0c);
     else epilogue(m0c);
@@ -1171,20 +1178,38 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
+  // (line-ordered stores, the default: the instance with only that epilogue compiled, option tap64p_epic)
+  const bool epic = a.wide_st == 2 && option("tap64p_epic", 1);
   if (halo_shape && cfg == 1) {
+    if (epic) {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>), dim3(grid), dim3(512), 0, s, a);
+      return 1;
+    }
     adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
   if (halo_shape && cfg == 2 && option("tap64p_halo128", 1)) {
+    if (epic) {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 2>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 2>), dim3(grid), dim3(512), 0, s, a);
+      return 1;
+    }
     adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
-  adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
+  if (epic && !bnr)
+    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, false, false, false, 2>", BM, BN, cfg == 1 ? 2 : 3);
+  else
+    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
 #define P_LAUNCH(BM_, BN_, NST_)                                                                           \
   do {                                                                                                     \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epic)                                                                                         \
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, false, false, false, false, false, 2>), dim3(grid), \
+                         dim3(512), 0, s, a);                                                             \
     else hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, false>), dim3(grid), dim3(512), 0, s, a);   \
   } while (0)
   if (cfg == 1) P_LAUNCH(256, 256, 2);

@@ -171,6 +171,14 @@ for s in $STEPS; do
               -k "halo64 or line_stores" > gpurun_out/f8pipe_tests.log 2>&1 &&
             timeout -k 10 300 python bench_infer.py --mode fp8 --opt halop_f8_pipe=0 > gpurun_out/bench_fp8_pipe0.log 2>&1 &&
             timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_pipe1.log 2>&1 ;;
+    epic) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
+              -k "tap64p_halo_matches or tap64_persistent_matches" > gpurun_out/epic_tests.log 2>&1 &&
+          timeout -k 10 400 python tools/bench_kernels.py --kinds fwd,fwd_stats --layers "L2 256->256,L3 512->512,L4 1024->1024" \
+              --variants "tap64p_epic=0;tap64p_epic=1" > gpurun_out/epic_kernels.log 2>&1 &&
+          timeout -k 10 300 python tools/ab_step.py --variant opt --opts "tap64p_epic=0;tap64p_epic=1" > gpurun_out/epic_ab.log 2>&1 ;;
+    f8ab) timeout -k 10 300 python bench_infer.py --mode fp8 --opt halop_f8_pipe=0 > gpurun_out/bench_fp8_pipe0.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_f8_lines=0 > gpurun_out/bench_fp8_q0.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_default.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
