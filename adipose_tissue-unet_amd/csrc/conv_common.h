@@ -43,6 +43,7 @@ struct FwdArgs {
   double* stat;          // BatchNorm accumulator replicas (f64) (adp::stat_scratch) for bn_sum / bnr_* launches
   int defer_fold;        // bn_sum launch whose replica sums adp_bn_finalize_fold adds in (adp_conv_desc)
   int f32;               // f32 launch on the LDS-DMA tap kernel (32-channel K steps, f32 MFMA)
+  int f32_skip;          // f32 256x128 tiles: 32-column groups past Nout skip their MFMAs (option f32_skip)
   int* claim;            // persistent kernels: dynamic tile claiming counters (adp::claim_slot), nullptr = static lists
   int claim_chunk;       // tiles per claim (halo forward: consecutive patches taken together)
   int claim_full;        // claiming: every tile claimed, none static (option claim_full; conv_common.h)

@@ -88,10 +88,16 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if constexpr (WM * WN == 8) prio_static<ADP_PRIO_T64>(wave);
-  const int wr = wave / WN, wc = wave % WN;
+  // f32 256x128 (as in the persistent kernel): waves w and w + 4 share a SIMD and take the two column halves
+  // (wc = w >> 2); a wave skips the MFMAs of a 32-column group wholly past Nout (option f32_skip)
+  constexpr bool SPLIT = F32 && WM == 4 && WN == 2;
+  const int wr = SPLIT ? (wave & 3) : wave / WN, wc = SPLIT ? (wave >> 2) : wave % WN;
   const int lin = xcd_remap(blockIdx.x, a.nblocks);
   const int tn = lin % a.ntile_n, tm = lin / a.ntile_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  const int wcu = SPLIT ? (__builtin_amdgcn_readfirstlane(wave) >> 2) : 0;
+  const bool skip0 = SPLIT && a.f32_skip && n0 + wcu * 64 >= a.Nout;        // (block- and wave-uniform)
+  const bool skip1 = SPLIT && a.f32_skip && n0 + wcu * 64 + 32 >= a.Nout;
   const int pos = lane & 7;
   const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
   const int Cin_s = a.CAs + a.CBs;
@@ -216,6 +222,8 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
+    if constexpr (F32)
+      if (hb ? skip1 : skip0) return;
     prio_hi<ADP_PRIO_T64>();
     if constexpr (F8) {
 #pragma unroll
@@ -414,12 +422,17 @@ constexpr int CFG_BN[4] = {256, 128, 64, 64};
 // 256x256 > 256x128 > 256x64 (two blocks per CU; the only one used at N = 64, +21-26 % over the
 // 4-wave kernel of conv_igemm.hip) ; 512x64 (one wave per SIMD) is never picked.
 constexpr double CFG_EFF[4] = {1.0, 0.85, 0.0, 0.6};
+// f32 (option f32_eff = 1): the f32 tiles spend 4x the MFMA time per K step, so the 256x64 tile's second
+// block per CU buys less than in bf16: 256x128 ran 123 TF per used column against 109 TF for 256x64 on the
+// adipose_v3 1024^2 step (profiles/r04c_f32_1024_bench.log: 92.7 TF at 3/4 column use, 109.3 TF at full use)
+constexpr double CFG_EFF_F32[4] = {0.0, 1.13, 0.0, 1.0};
 
 }  // namespace
 
 namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   a.stagger = option("tap64p_stagger", 1);
+  a.f32_skip = option("f32_skip", 1);
   int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
   // the fused BN-backward epilogue handles plain stores only (what the data-gradient launches use)
@@ -441,6 +454,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
     // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency
     // a configuration whose N tile is less than 3/4 used is not considered
     double best = 0.0;
+    const double* eff = a.f32 && option("f32_eff", 0) ? CFG_EFF_F32 : CFG_EFF;
     for (int c = 0; c < 4; ++c) {
       if (a.f8 && CFG_BM[c] * CFG_BN[c] > 256 * 128) continue;   // fp8: 256x128 / 256x64 tiles
       if (a.f32 && c == 0) continue;   // f32: the 256x256 tile spills in its f32 epilogue; 256x128 keeps 156 VGPRs
@@ -448,7 +462,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
       const long long blocks = tn * tmm, waves = (blocks + 255) / 256;
       const double colu = (double)a.Nout / (tn * CFG_BN[c]);
       if (colu < 0.75) continue;
-      const double sc = colu * (double)blocks / (waves * 256) * CFG_EFF[c];
+      const double sc = colu * (double)blocks / (waves * 256) * eff[c];
       if (sc > best) { best = sc; cfg = c; }
     }
     if (best <= 0.0) return 0;

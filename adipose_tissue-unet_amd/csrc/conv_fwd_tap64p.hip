@@ -142,8 +142,15 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   double (*sacc)[BN] = reinterpret_cast<double (*)[BN]>(smem + OC + 5 * BN * 4);   // block's BN sums (f64)
   int* ring = reinterpret_cast<int*>(smem + OC + 9 * BN * 4);   // dynamic claiming: tile ids of local tiles k & 3
 
+  // f32 (WN = 2): waves w and w + 4 share a SIMD and take the two column halves of the tile (wc = w >> 2), and a
+  // wave skips the MFMAs of a 32-column group that lies wholly past Nout (the 96- and 192-channel levels of
+  // adipose_v3's f32 path leave a quarter of a 128-wide tile column empty): the SIMD of such a pair then runs
+  // 3/4 of the MFMAs instead of idling through zero columns (option f32_skip)
+  constexpr bool SPLIT = F32 && WN == 2;
+  auto w_row = [](int w) { return SPLIT ? (w & 3) : w / WN; };
+  auto w_col = [](int w) { return SPLIT ? (w >> 2) : w % WN; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WN, wc = wave % WN;
+  const int wr = w_row(wave), wc = w_col(wave);
   const int G = gridDim.x;
   prio_static<ADP_PRIO_FWD>(wave);
   const int lin = xcd_remap(blockIdx.x, G);
@@ -159,6 +166,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   const int mine = dyn ? 0 : (lin < ntiles ? (ntiles - lin + G - 1) / G : 0);
   if (!dyn && mine == 0) return;   // uniform per block
   const int n0 = col * BN;
+  const int wcu = w_col(__builtin_amdgcn_readfirstlane(wave));
+  const bool skip0 = SPLIT && a.f32_skip && n0 + wcu * 64 >= a.Nout;        // (block- and wave-uniform)
+  const bool skip1 = SPLIT && a.f32_skip && n0 + wcu * 64 + 32 >= a.Nout;
   const int pos = lane & 7;
   const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
   const int Cin_s = a.CAs + a.CBs;
@@ -463,6 +473,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // column = pixel m0 + wr*TM + ha*HM + mi*16 + r16
   f32x4 acc[2 * MIQ][4];
   auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
+    if constexpr (F32)
+      if (hb ? skip1 : skip0) return;
     prio_hi<ADP_PRIO_FWD>();
     if constexpr (F8) {
 #pragma unroll
@@ -522,7 +534,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   auto load_zall = [&](int m0) {
     int tidv = tid;
     asm volatile("" : "+v"(tidv));
-    const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+    const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = w_row(tidv >> 6), wc = w_col(tidv >> 6);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int c = n0 + wc * 64 + nt * 16 + 4 * h4;
@@ -539,7 +551,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     // per-(mt, nt) offsets out of the tile loop (they would stay live across the K loop and spill)
     int tidv = tid;
     asm volatile("" : "+v"(tidv));
-    const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+    const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = w_row(tidv >> 6), wc = w_col(tidv >> 6);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int c = n0 + wc * 64 + nt * 16 + 4 * h4;   // first of this lane's 4 channels (GEMM column)
@@ -661,7 +673,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     if constexpr (!BNR && !F32) {
       int tidv = tid;
       asm volatile("" : "+v"(tidv));
-      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = w_row(tidv >> 6), wc = w_col(tidv >> 6);
 #pragma unroll
       for (int np = 0; np < 4; np += 2) {
         float bias[2][4], wsc[2][4];
@@ -749,7 +761,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     if constexpr (!BNR && !F32) {
       int tidv = tid;
       asm volatile("" : "+v"(tidv));
-      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = w_row(tidv >> 6), wc = w_col(tidv >> 6);
       float bias[4][4], wsc[4][4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
@@ -845,7 +857,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     if constexpr (F8) {
       int tidv = tid;
       asm volatile("" : "+v"(tidv));
-      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = (tidv >> 6) / WN, wc = (tidv >> 6) % WN;
+      const int r16 = tidv & 15, h4 = (tidv >> 4) & 3, wr = w_row(tidv >> 6), wc = w_col(tidv >> 6);
       // pass 1, group by group (8 constants live): each quad -> its e4m3 dword, kept in the accumulator's first
       // register (no extra registers: the 256x256 forms have none to spare)
 #pragma unroll

@@ -297,6 +297,41 @@ def test_tap64p_f32_halo(mode, grid, claim):
     torch.testing.assert_close(sp, stt, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("persist", [1, 0], ids=["tap64p", "tap64"])
+@pytest.mark.parametrize("nout", [96, 192, 352])
+def test_f32_column_skip_bit_identical(nout, persist):
+    """f32 256x128 tiles (option f32_skip, default on): the waves sharing a SIMD take the two column halves and a
+    wave skips the MFMAs of 32-column groups wholly past Nout. Every stored column keeps its K order, so the output
+    and the BatchNorm sums are bit-identical to the unskipped launch (f32_skip=0)."""
+    dt = torch.float32
+    g = torch.Generator().manual_seed(nout)
+    N, H, W_, cin = 2, 24, 64, 96
+    x = torch.randn(N, H, W_, cin, generator=g).to(DEV, dt)
+    Wt = (torch.randn(((nout + 63) // 64) * 64, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(nout, generator=g).to(DEV)
+    res = []
+    for skip in (1, 0):
+        out = torch.zeros(N, H, W_, nout, dtype=dt, device=DEV)
+        st = torch.zeros(2, nout, device=DEV)
+        for o_, v in (("f32_skip", skip), ("tap64p_f32", persist), ("fwd_tap64", 3)):
+            ops.set_option(o_, v)
+        try:
+            ops.conv_fwd(x, Wt, nout, out=out, bias=bias, relu=True, bn_stats=(st[0], st[1]))
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for o_ in ("f32_skip", "tap64p_f32", "fwd_tap64"):
+                ops.set_option(o_, None)
+        assert kname.startswith("igemm_fwd_tap64p_kernel<256, 128, 3" if persist else "igemm_fwd_tap64_kernel<4, 2, 64"), kname
+        res.append((out, st))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    xd = x.double().permute(0, 3, 1, 2)
+    ref = (F.conv2d(xd, Wt[:nout].double().view(nout, 3, 3, cin).permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+           + bias.double()).clamp_min(0.0)
+    assert (res[0][0].double() - ref).abs().max().item() < 1e-5 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("form", ["halo256", "halo128", "gather_dil2", "convt"])
 def test_tap64p_claim_counters_reset(form):
     """Dynamic tile claiming (option tap64p_claim): every launch takes its tiles from a counter slot of the

@@ -28,6 +28,9 @@ def main():
     p.add_argument("--opts", default="")
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--steps", type=int, default=8)
+    p.add_argument("--preset", default="unet_bn", choices=["unet_bn", "adipose_v3"],
+                   help="adipose_v3: the reference topology (1024^2, B=2; --variant opt only)")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     args = p.parse_args()
     import numpy as np
     import torch
@@ -39,9 +42,18 @@ def main():
     from adipose_amd.trainer import LossConfig, Trainer
 
     dev = torch.device("cuda", 0)
-    net = UNetBN(4, 1024, levels=5, base=64, in_ch=3, dtype="bf16", device=dev, seed=865)
-    tr = Trainer(net, LossConfig(use_hard_mining=False), lr=1e-4)
-    xs, ys = synthetic_batch(4, 1024, channels=3, seed=865)
+    if args.preset == "adipose_v3":
+        from adipose_amd.data import to_gray
+        from adipose_amd.nets import AdiposeV3Net
+        assert args.variant == "opt", "adipose_v3 runs the option A/B only"
+        net = AdiposeV3Net(2, 1024, dtype=args.dtype, device=dev, seed=865)
+        tr = Trainer(net, LossConfig(), lr=1e-4)
+        xs, ys = synthetic_batch(2, 1024, channels=3, seed=865)
+        xs = to_gray(xs.astype("float32"))
+    else:
+        net = UNetBN(4, 1024, levels=5, base=64, in_ch=3, dtype=args.dtype, device=dev, seed=865)
+        tr = Trainer(net, LossConfig(use_hard_mining=False), lr=1e-4)
+        xs, ys = synthetic_batch(4, 1024, channels=3, seed=865)
     x = torch.from_numpy(((xs - xs.mean()) / (xs.std() + 1e-10)).astype(np.float32)).to(dev)
     y = torch.from_numpy(ys).to(dev)
     if args.variant == "pack":

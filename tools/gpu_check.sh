@@ -179,6 +179,17 @@ for s in $STEPS; do
     f8ab) timeout -k 10 300 python bench_infer.py --mode fp8 --opt halop_f8_pipe=0 > gpurun_out/bench_fp8_pipe0.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode fp8 --opt tap64p_f8_lines=0 > gpurun_out/bench_fp8_q0.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_default.log 2>&1 ;;
+    f32map) timeout -k 10 300 python tools/launch_map.py --preset adipose_v3 --dtype f32 > gpurun_out/f32_map.log 2>&1 &&
+            mkdir -p gpurun_out/f32kt && timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d gpurun_out/f32kt -o kt -- \
+              python3 bench.py --no-cpu-baseline --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 3 --warmup 2 \
+              > gpurun_out/f32kt/kt.log 2>&1 &&
+            python3 tools/step_timeline.py gpurun_out/f32kt/kt_kernel_trace.csv > gpurun_out/f32_timeline.txt 2>&1 ;;
+    f32skip) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
+              -k "f32_column_skip or tap64p_f32_halo or f32_tap_kernel" > gpurun_out/f32skip_tests.log 2>&1 &&
+            timeout -k 10 400 python tools/ab_step.py --preset adipose_v3 --dtype f32 --variant opt --steps 4 \
+              --opts "f32_skip=0;f32_skip=1" > gpurun_out/f32skip_ab.log 2>&1 &&
+            timeout -k 10 400 python tools/ab_step.py --preset adipose_v3 --dtype f32 --variant opt --steps 4 \
+              --opts "f32_eff=0;f32_eff=1" > gpurun_out/f32eff_ab.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \

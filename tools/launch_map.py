@@ -14,6 +14,7 @@ def main():
     p.add_argument("--preset", default="adipose_v3", choices=["adipose_v3", "unet_bn"])
     p.add_argument("--batch", type=int, default=2)
     p.add_argument("--size", type=int, default=1024)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     args = p.parse_args()
     import torch
 
@@ -25,12 +26,12 @@ def main():
     dev = torch.device("cuda", 0)
     B, S = args.batch, args.size
     if args.preset == "unet_bn":
-        net = UNetBN(B, S, levels=5, base=64, in_ch=3, dtype="bf16", device=dev, seed=865)
+        net = UNetBN(B, S, levels=5, base=64, in_ch=3, dtype=args.dtype, device=dev, seed=865)
         tr = Trainer(net, LossConfig(use_hard_mining=False))
         xs, ys = synthetic_batch(B, S, channels=3, seed=865)
     else:
         from adipose_amd.data import to_gray
-        net = AdiposeV3Net(B, S, dtype="bf16", device=dev, seed=865)
+        net = AdiposeV3Net(B, S, dtype=args.dtype, device=dev, seed=865)
         tr = Trainer(net, LossConfig())
         xs, ys = synthetic_batch(B, S, channels=3, seed=865)
         xs = to_gray(xs.astype("float32"))
