@@ -90,14 +90,14 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   if constexpr (WM * WN == 8) prio_static<ADP_PRIO_T64>(wave);
   // f32 256x128 (as in the persistent kernel): waves w and w + 4 share a SIMD and take the two column halves
   // (wc = w >> 2); a wave skips the MFMAs of a 32-column group wholly past Nout (option f32_skip)
-  constexpr bool SPLIT = F32 && WM == 4 && WN == 2;
+  const bool SPLIT = F32 && WM == 4 && WN == 2 && a.f32_skip;   // (f32_skip = 0: the bf16 forms' wave layout)
   const int wr = SPLIT ? (wave & 3) : wave / WN, wc = SPLIT ? (wave >> 2) : wave % WN;
   const int lin = xcd_remap(blockIdx.x, a.nblocks);
   const int tn = lin % a.ntile_n, tm = lin / a.ntile_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int wcu = SPLIT ? (__builtin_amdgcn_readfirstlane(wave) >> 2) : 0;
-  const bool skip0 = SPLIT && a.f32_skip && n0 + wcu * 64 >= a.Nout;        // (block- and wave-uniform)
-  const bool skip1 = SPLIT && a.f32_skip && n0 + wcu * 64 + 32 >= a.Nout;
+  const bool skip0 = SPLIT && n0 + wcu * 64 >= a.Nout;        // (block- and wave-uniform)
+  const bool skip1 = SPLIT && n0 + wcu * 64 + 32 >= a.Nout;
   const int pos = lane & 7;
   const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
   const int Cin_s = a.CAs + a.CBs;

@@ -146,9 +146,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // wave skips the MFMAs of a 32-column group that lies wholly past Nout (the 96- and 192-channel levels of
   // adipose_v3's f32 path leave a quarter of a 128-wide tile column empty): the SIMD of such a pair then runs
   // 3/4 of the MFMAs instead of idling through zero columns (option f32_skip)
-  constexpr bool SPLIT = F32 && WN == 2;
-  auto w_row = [](int w) { return SPLIT ? (w & 3) : w / WN; };
-  auto w_col = [](int w) { return SPLIT ? (w >> 2) : w % WN; };
+  const bool SPLIT = F32 && WN == 2 && a.f32_skip;   // (f32_skip = 0: the bf16 forms' wave layout)
+  auto w_row = [&](int w) { return SPLIT ? (w & 3) : w / WN; };
+  auto w_col = [&](int w) { return SPLIT ? (w >> 2) : w % WN; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = w_row(wave), wc = w_col(wave);
   const int G = gridDim.x;
@@ -167,8 +167,8 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   if (!dyn && mine == 0) return;   // uniform per block
   const int n0 = col * BN;
   const int wcu = w_col(__builtin_amdgcn_readfirstlane(wave));
-  const bool skip0 = SPLIT && a.f32_skip && n0 + wcu * 64 >= a.Nout;        // (block- and wave-uniform)
-  const bool skip1 = SPLIT && a.f32_skip && n0 + wcu * 64 + 32 >= a.Nout;
+  const bool skip0 = SPLIT && n0 + wcu * 64 >= a.Nout;        // (block- and wave-uniform)
+  const bool skip1 = SPLIT && n0 + wcu * 64 + 32 >= a.Nout;
   const int pos = lane & 7;
   const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
   const int Cin_s = a.CAs + a.CBs;
