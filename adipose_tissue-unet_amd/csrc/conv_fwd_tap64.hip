@@ -432,7 +432,7 @@ constexpr double CFG_EFF_F32[4] = {0.0, 1.13, 0.0, 1.0};
 namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   a.stagger = option("tap64p_stagger", 1);
-  a.f32_skip = option("f32_skip", 1);
+  a.f32_skip = option("f32_skip", 0);
   int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
   // the fused BN-backward epilogue handles plain stores only (what the data-gradient launches use)

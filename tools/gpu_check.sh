@@ -171,7 +171,7 @@ for s in $STEPS; do
               -k "halo64 or line_stores" > gpurun_out/f8pipe_tests.log 2>&1 &&
             timeout -k 10 300 python bench_infer.py --mode fp8 --opt halop_f8_pipe=0 > gpurun_out/bench_fp8_pipe0.log 2>&1 &&
             timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_pipe1.log 2>&1 ;;
-    epic) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
+    epic) ADP_TEST_OPTS=tap64p_epic=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
               -k "tap64p_halo_matches or tap64_persistent_matches" > gpurun_out/epic_tests.log 2>&1 &&
           timeout -k 10 400 python tools/bench_kernels.py --kinds fwd,fwd_stats --layers "L2 256->256,L3 512->512,L4 1024->1024" \
               --variants "tap64p_epic=0;tap64p_epic=1" > gpurun_out/epic_kernels.log 2>&1 &&
@@ -184,7 +184,7 @@ for s in $STEPS; do
               python3 bench.py --no-cpu-baseline --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 3 --warmup 2 \
               > gpurun_out/f32kt/kt.log 2>&1 &&
             python3 tools/step_timeline.py gpurun_out/f32kt/kt_kernel_trace.csv > gpurun_out/f32_timeline.txt 2>&1 ;;
-    f32skip) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
+    f32skip) ADP_TEST_OPTS=f32_skip=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
               -k "f32_column_skip or tap64p_f32_halo or f32_tap_kernel" > gpurun_out/f32skip_tests.log 2>&1 &&
             timeout -k 10 400 python tools/ab_step.py --preset adipose_v3 --dtype f32 --variant opt --steps 4 \
               --opts "f32_skip=0;f32_skip=1" > gpurun_out/f32skip_ab.log 2>&1 &&
