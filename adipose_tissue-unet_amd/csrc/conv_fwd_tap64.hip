@@ -432,7 +432,7 @@ constexpr double CFG_EFF_F32[4] = {0.0, 1.13, 0.0, 1.0};
 namespace adp {
 int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   a.stagger = option("tap64p_stagger", 1);
-  a.f32_skip = option("f32_skip", 0);
+  a.f32_skip = option("f32_skip", 1);
   int mode = option("fwd_tap64", 1);   // 0 off, 1 auto, 2+c force configuration c
   if (mode == 0) return 0;
   // the fused BN-backward epilogue handles plain stores only (what the data-gradient launches use)
@@ -454,7 +454,7 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
     // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency
     // a configuration whose N tile is less than 3/4 used is not considered
     double best = 0.0;
-    const double* eff = a.f32 && option("f32_eff", 0) ? CFG_EFF_F32 : CFG_EFF;
+    const double* eff = a.f32 && option("f32_eff", 1) ? CFG_EFF_F32 : CFG_EFF;
     for (int c = 0; c < 4; ++c) {
       if (a.f8 && CFG_BM[c] * CFG_BN[c] > 256 * 128) continue;   // fp8: 256x128 / 256x64 tiles
       if (a.f32 && c == 0) continue;   // f32: the 256x256 tile spills in its f32 epilogue; 256x128 keeps 156 VGPRs

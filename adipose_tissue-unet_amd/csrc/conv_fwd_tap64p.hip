@@ -1191,7 +1191,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     return 1;
   }
   // (line-ordered stores, the default: the instance with only that epilogue compiled, option tap64p_epic)
-  const bool epic = a.wide_st == 2 && option("tap64p_epic", 0);
+  const bool epic = a.wide_st == 2 && option("tap64p_epic", 1);
   if (halo_shape && cfg == 1) {
     if (epic) {
       adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>");
