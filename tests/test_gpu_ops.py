@@ -415,7 +415,9 @@ def test_tap64p_wreg_matches_dma(mode, grid):
         finally:
             for k_ in opts:
                 ops.set_option(k_, None)
-        assert kname == "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, %s>" % ("true" if wreg else "false"), kname
+        # (the DMA arm: the default line-ordered-epilogue instance, EPIC = 2: "..., false, false, false, 2>")
+        assert kname == ("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true>" if wreg else
+                         "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>"), kname
         res.append((torch.cat(outs, -1), st.double()))
     (y1, s1), (y0, s0) = res
     assert torch.equal(y1, y0), (y1.double() - y0.double()).abs().max().item()
@@ -599,7 +601,7 @@ def test_upsample_gather_halo_forms(form, grid):
     cin, nout, kern = {"halop_1ch": (64, 64, "igemm_fwd_halop_kernel<false, 1, 64"),
                        "halop_2ch": (128, 64, "igemm_fwd_halop_kernel<false, 2, 32"),
                        "tap64p_256": (128, 256, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false"),
-                       "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false>"),
+                       "tap64p_128": (192, 128, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false"),
                        "w4_256": (128, 256, "igemm_fwd_w4_kernel<true")}[form]
     x = torch.randn(N, Hs, Ws, cin, generator=g).to(DEV, dt)
     Wt = (torch.randn(nout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
