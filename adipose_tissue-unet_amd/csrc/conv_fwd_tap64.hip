@@ -454,15 +454,20 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
     // score = column utilisation x last-wave utilisation of the 256-CU grid x per-block efficiency
     // a configuration whose N tile is less than 3/4 used is not considered
     double best = 0.0;
-    const double* eff = a.f32 && option("f32_eff", 1) ? CFG_EFF_F32 : CFG_EFF;
+    const int f32_eff = a.f32 ? option("f32_eff", 1) : 0;
+    const double* eff = f32_eff ? CFG_EFF_F32 : CFG_EFF;
     for (int c = 0; c < 4; ++c) {
       if (a.f8 && CFG_BM[c] * CFG_BN[c] > 256 * 128) continue;   // fp8: 256x128 / 256x64 tiles
       if (a.f32 && c == 0) continue;   // f32: the 256x256 tile spills in its f32 epilogue; 256x128 keeps 156 VGPRs
       const long long tn = (a.Nout + CFG_BN[c] - 1) / CFG_BN[c], tmm = (a.M + CFG_BM[c] - 1) / CFG_BM[c];
-      const long long blocks = tn * tmm, waves = (blocks + 255) / 256;
+      // resident blocks per wave of the grid: 256 CUs x 1 (f32_eff = 2: x 2 for the 256x64 tile, whose LDS
+      // (2 x 40 KB) and 4 waves leave room for a second block per CU -- the last-wave fill of the few-tile f32
+      // launches, e.g. 128^2 x 352 channels: 384 / 768 blocks)
+      const long long slots = (f32_eff >= 2 && c == 3) ? 512 : 256;
+      const long long blocks = tn * tmm, waves = (blocks + slots - 1) / slots;
       const double colu = (double)a.Nout / (tn * CFG_BN[c]);
       if (colu < 0.75) continue;
-      const double sc = colu * (double)blocks / (waves * 256) * eff[c];
+      const double sc = colu * (double)blocks / (waves * slots) * eff[c];
       if (sc > best) { best = sc; cfg = c; }
     }
     if (best <= 0.0) return 0;

@@ -1161,13 +1161,13 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   if (a.up != 1 && !(halo_shape && (cfg == 1 || (cfg == 2 && option("tap64p_halo128", 1))))) return 0;
   if (a.f32) {
     if (!halo_shape || cfg != 2) return 0;
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true, -1>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true>), dim3(grid), dim3(512), 0,
                        s, a);
     return 1;
   }
   if (a.f8 && !(halo_shape && (cfg == 1 || cfg == 2))) {   // gather form (ConvTranspose, fp8 output)
-    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, true, false>", BM, BN, cfg == 1 ? 2 : 3);
+    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, true, false, false, -1>", BM, BN, cfg == 1 ? 2 : 3);
     if (cfg == 1) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, false, true>), dim3(grid), dim3(512), 0, s, a);
     else if (cfg == 2) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, false, true>), dim3(grid), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<128, 256, 3, false, false, true>), dim3(grid), dim3(512), 0, s, a);
@@ -1175,10 +1175,10 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   }
   if (a.f8) {
     if (cfg == 1) {
-      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true, false>");
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true, false, false, -1>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true>), dim3(grid), dim3(512), 0, s, a);
     } else {
-      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true, false>");
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true, false, false, -1>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true>), dim3(grid), dim3(512), 0, s, a);
     }
     return 1;
@@ -1186,7 +1186,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   // the four-wave direct-weight form (conv_fwd_w4.hip) for the layers it covers
   if (halo_shape && cfg == 1 && launch_fwd_w4(a, s)) return 1;
   if (halo_shape && cfg == 1 && option("tap64p_wreg", 0)) {   // opt-in: 5-9 % slower (profiles/r03_wreg_ab.txt)
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true, false, -1>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
@@ -1198,7 +1198,7 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>), dim3(grid), dim3(512), 0, s, a);
       return 1;
     }
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, -1>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
@@ -1208,14 +1208,14 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 2>), dim3(grid), dim3(512), 0, s, a);
       return 1;
     }
-    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false>");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, -1>");
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
   if (epic && !bnr)
     adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, false, false, false, 2>", BM, BN, cfg == 1 ? 2 : 3);
   else
-    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false, false>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
+    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false, false, false, -1>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
 #define P_LAUNCH(BM_, BN_, NST_)                                                                           \
   do {                                                                                                     \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \

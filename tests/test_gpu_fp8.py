@@ -116,10 +116,10 @@ def test_fp8_conv_vs_dequantised_reference(cinA, cinB, cout, dil, H, out_fp8, re
 
 
 @pytest.mark.parametrize("cinA,cinB,cout,H,W,relu,kern", [
-    (128, 0, 128, 16, 64, False, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true, false>"),
-    (512, 0, 512, 8, 32, False, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true, false>"),
-    (256, 256, 256, 16, 32, True, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true, false>"),
-    (256, 0, 320, 8, 64, False, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true, false>"),   # ragged N tile
+    (128, 0, 128, 16, 64, False, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true, false, false, -1>"),
+    (512, 0, 512, 8, 32, False, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true, false, false, -1>"),
+    (256, 256, 256, 16, 32, True, "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, true, false, false, -1>"),
+    (256, 0, 320, 8, 64, False, "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, true, false, false, -1>"),   # ragged N tile
 ])
 def test_fp8_persistent_halo_form(cinA, cinB, cout, H, W, relu, kern):
     """fp8 halo form of the persistent forward kernel (128-channel K steps, one 32-B MFMA operand per

@@ -283,7 +283,7 @@ def test_tap64p_f32_halo(mode, grid, claim):
             for o_ in ("tap64p_f32", "tap64p_claim", "tap64_persist_grid", "fwd_tap64"):
                 ops.set_option(o_, None)
         if persist:
-            assert kname == "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true>", kname
+            assert kname == "igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, true, -1>", kname
         else:
             assert kname.startswith("igemm_fwd_tap64_kernel<4, 2, 64"), kname
         res.append((torch.cat(outs, -1).double(), st.double()))
@@ -416,7 +416,7 @@ def test_tap64p_wreg_matches_dma(mode, grid):
             for k_ in opts:
                 ops.set_option(k_, None)
         # (the DMA arm: the default line-ordered-epilogue instance, EPIC = 2: "..., false, false, false, 2>")
-        assert kname == ("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true>" if wreg else
+        assert kname == ("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true, false, -1>" if wreg else
                          "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>"), kname
         res.append((torch.cat(outs, -1), st.double()))
     (y1, s1), (y0, s0) = res

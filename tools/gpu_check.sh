@@ -196,6 +196,8 @@ for s in $STEPS; do
               --opts "f32_skip=0;f32_skip=1" > gpurun_out/f32combo_ab.log 2>&1 ;;
     namefix) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
               -k "tap64p_wreg_matches_dma or upsample_gather_halo_forms" > gpurun_out/namefix_tests.log 2>&1 ;;
+    f32eff2) timeout -k 10 400 python tools/ab_step.py --preset adipose_v3 --dtype f32 --variant opt --steps 4 \
+              --opts "f32_eff=1;f32_eff=2" > gpurun_out/f32eff2_ab.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
