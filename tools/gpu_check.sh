@@ -198,6 +198,8 @@ for s in $STEPS; do
               -k "tap64p_wreg_matches_dma or upsample_gather_halo_forms" > gpurun_out/namefix_tests.log 2>&1 ;;
     f32eff2) timeout -k 10 400 python tools/ab_step.py --preset adipose_v3 --dtype f32 --variant opt --steps 4 \
               --opts "f32_eff=1;f32_eff=2" > gpurun_out/f32eff2_ab.log 2>&1 ;;
+    names) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_fp8.py -v --timeout 200 \
+              --timeout-method thread -k "tap64p or fp8 or f32" > gpurun_out/names_tests.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
