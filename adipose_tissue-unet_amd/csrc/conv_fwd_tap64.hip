@@ -66,7 +66,10 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, u
 // holds 32 floats: staging, swizzle and barriers unchanged); each 16-B fragment is 4 k values of one row, fed to
 // four exact v_mfma_f32_16x16x4_f32 (lane group g supplies k = 4g + j to the j-th one: A and B share the
 // permutation, so every k of the step enters the dot product once); f32 epilogue stores.
-template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8, bool F32 = false>
+// KP: the K loop compiled in -- -1 either, chosen at run time by a.kpipe (the fp8 / f32 forms); 0 the plain double
+// buffer only; 1 the mid-step-barrier loop only (bf16 forms: one loop per instance leaves the register allocator
+// one schedule, as the persistent kernel's EPIC does for its epilogues)
+template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8, bool F32 = false, int KP = -1>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   static_assert(!(F8 && F32), "one operand dtype");
   using TO = typename std::conditional<F32, float, bf16>::type;   // output dtype
@@ -277,7 +280,8 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   // stage t + 1 (issued one step earlier), passes the barrier while that cluster's MFMAs run, refills stage t
   // with step t + 2, issues the fourth cluster and preloads stage t + 1's B half 0 behind it. The same
   // fragments and MFMA order: bit-identical.
-  if (a.kpipe) {
+  const bool kp = KP == 1 || (KP < 0 && a.kpipe);
+  if (kp) {
     auto issue_step = [&](int b_) {
       const Kt kk = kinfo();
       issueA(0, kk, b_); issueB(0, kk, b_); issueB(1, kk, b_); issueA(1, kk, b_);
@@ -376,13 +380,25 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
                    (size_t)((a.Nout + 63) / 64 * 64) * a.Kpad * es < lim;
 #define T64_LAUNCH(BUFV, BNRV, F8V)                                                                     \
   do {                                                                                                 \
-    adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, %s>", WM, WN, TM, BUFV ? "true" : "false", \
-                    BNRV ? "true" : "false", F8V ? "true" : "false");                                  \
+    adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, %s, false, -1>", WM, WN, TM,            \
+                    BUFV ? "true" : "false", BNRV ? "true" : "false", F8V ? "true" : "false");         \
     hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, F8V>), g, b, 0, s, a);           \
+  } while (0)
+#define T64_LAUNCH16(BUFV, BNRV)                                                                        \
+  do {                                                                                                 \
+    if (a.kpipe) {                                                                                     \
+      adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, false, 1>", WM, WN, TM,        \
+                      BUFV ? "true" : "false", BNRV ? "true" : "false");                               \
+      hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, false, 1>), g, b, 0, s, a); \
+    } else {                                                                                           \
+      adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, false, 0>", WM, WN, TM,        \
+                      BUFV ? "true" : "false", BNRV ? "true" : "false");                               \
+      hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, false, 0>), g, b, 0, s, a); \
+    }                                                                                                  \
   } while (0)
 #define T64_LAUNCH32(BUFV, BNRV)                                                                        \
   do {                                                                                                 \
-    adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, true>", WM, WN, TM,              \
+    adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, true, -1>", WM, WN, TM,          \
                     BUFV ? "true" : "false", BNRV ? "true" : "false");                                 \
     hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, true>), g, b, 0, s, a);   \
   } while (0)
@@ -404,13 +420,14 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
     }
   }
   if (a.bnr_z) {
-    if (buf) T64_LAUNCH(true, true, false);
-    else T64_LAUNCH(false, true, false);
+    if (buf) T64_LAUNCH16(true, true);
+    else T64_LAUNCH16(false, true);
   } else {
-    if (buf) T64_LAUNCH(true, false, false);
-    else T64_LAUNCH(false, false, false);
+    if (buf) T64_LAUNCH16(true, false);
+    else T64_LAUNCH16(false, false);
   }
 #undef T64_LAUNCH
+#undef T64_LAUNCH16
 #undef T64_LAUNCH32
 }
 

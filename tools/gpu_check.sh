@@ -200,6 +200,13 @@ for s in $STEPS; do
               --opts "f32_eff=1;f32_eff=2" > gpurun_out/f32eff2_ab.log 2>&1 ;;
     names) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_fp8.py -v --timeout 200 \
               --timeout-method thread -k "tap64p or fp8 or f32" > gpurun_out/names_tests.log 2>&1 ;;
+    kp) timeout -k 10 500 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
+              -k "tap64 and not tap64p" > gpurun_out/kp_tests.log 2>&1 &&
+          bash tools/ab_libs.sh "$(ls ab/libadipose_*.so | head -n 1)" adipose_tissue-unet_amd/libadipose_hip.so 2 \
+              tools/bench_kernels.py --kinds bnr --layers "L2 256->256,L3 512->512,L4 1024->1024" \
+              --variants "tap64_kpipe=0;tap64_kpipe=1" > gpurun_out/kp_kernels_ab.log 2>&1 &&
+          bash tools/ab_libs.sh "$(ls ab/libadipose_*.so | head -n 1)" adipose_tissue-unet_amd/libadipose_hip.so 3 \
+              bench.py --no-cpu-baseline --steps 10 > gpurun_out/kp_step_ab.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
