@@ -2019,7 +2019,7 @@ def test_f32_tap_kernel_matches_generic(case):
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
             ops.set_option("f32_tap", None)
-        assert kname.startswith("igemm_fwd_tap64_kernel") == bool(tap) and kname.endswith("true>") == bool(tap), kname
+        assert kname.startswith("igemm_fwd_tap64_kernel") == bool(tap) and kname.endswith("true, -1>") == bool(tap), kname
         res.append([out.clone()] + [e.clone() for e in extra])
     for a, b in zip(*res):
         assert relerr(a, b) < 1e-5, (name, relerr(a, b))
