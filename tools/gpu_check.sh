@@ -207,6 +207,8 @@ for s in $STEPS; do
               --variants "tap64_kpipe=0;tap64_kpipe=1" > gpurun_out/kp_kernels_ab.log 2>&1 &&
           bash tools/ab_libs.sh "$(ls ab/libadipose_*.so | head -n 1)" adipose_tissue-unet_amd/libadipose_hip.so 3 \
               bench.py --no-cpu-baseline --steps 10 > gpurun_out/kp_step_ab.log 2>&1 ;;
+    engprobe) timeout -k 10 300 python -u tools/engine_repeat_probe.py --reps 6 --comm 1 > gpurun_out/engprobe_comm.log 2>&1 &&
+              timeout -k 10 300 python -u tools/engine_repeat_probe.py --reps 6 --comm 0 > gpurun_out/engprobe_nocomm.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
