@@ -165,8 +165,14 @@ ADP_DEV void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[MI][NI], int mbase, int
       const int n = nbase + ni * 16 + col;
       if (lane < 16 && n < a.Nout) {
         int c = a.out_mode == 1 ? n % a.Cps : n;
-        atomicAdd(a.bn_sum + c, s);
-        atomicAdd(a.bn_sq + c, q);
+        if (a.stat) {   // the block's f64 replica (folded in a fixed order by the launcher: deterministic sums)
+          double* rep = a.stat + (size_t)((blockIdx.x + blockIdx.y * gridDim.x) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+          atomicAdd(rep + c, (double)s);
+          atomicAdd(rep + adp::STAT_CMAX + c, (double)q);
+        } else {
+          atomicAdd(a.bn_sum + c, s);
+          atomicAdd(a.bn_sq + c, q);
+        }
       }
     }
   }
@@ -1127,8 +1133,8 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   if (!a.bn_sum) a.stat = nullptr;
   const int rc = launch_fwd_plain<T>(a, s, fast);
   if (rc != 0) return rc;
-  // kernels with the LDS-staged epilogue added their statistics into the replicas (the register-staged
-  // generic kernels add into bn_sum directly and leave the replicas zero)
+  // every kernel added its statistics into the f64 replicas (since round 4 the register-staged generic kernels
+  // too: their f32 atomics into bn_sum made the f32 input layer's statistics run-dependent)
   if (a.stat && fold_stats(a, s) != 0) return -2;
   if (!bnr.bnr_z) return 0;
   return adp_bn_bwd_reduce(std::is_same<T, bf16>::value ? ADP_BF16 : ADP_F32, (size_t)bnr.M, bnr.out_stride, bnr.out,
