@@ -209,6 +209,8 @@ for s in $STEPS; do
               bench.py --no-cpu-baseline --steps 10 > gpurun_out/kp_step_ab.log 2>&1 ;;
     engprobe) timeout -k 10 300 python -u tools/engine_repeat_probe.py --reps 6 --comm 1 > gpurun_out/engprobe_comm.log 2>&1 &&
               timeout -k 10 300 python -u tools/engine_repeat_probe.py --reps 6 --comm 0 > gpurun_out/engprobe_nocomm.log 2>&1 ;;
+    dettests) timeout -k 10 600 python -u -m pytest tests/test_engine.py tests/test_gpu_network.py -v --timeout 200 \
+              --timeout-method thread > gpurun_out/dettests.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
