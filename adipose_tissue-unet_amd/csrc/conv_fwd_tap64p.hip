@@ -98,11 +98,12 @@ __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_ha
 // EPIC (bf16 forms): -1 = the epilogue chosen at run time from a.wide_st (narrow / pair-major 16-B / line-ordered
 // 16-B); 2 = only the line-ordered one compiled in -- the launcher's default store form, without the register
 // allocation of two epilogues it never runs (measured on the fp8 forms, whose ConvTranspose launch went from 0.215 to
-// 0.120 ms when the unused 16-B bf16 epilogues left it)
+// 0.120 ms when the unused 16-B bf16 epilogues left it); 3 = the same with static tile lists only (no claiming code:
+// the launches without a claim counter, i.e. every default launch; option tap64p_epic3)
 template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false, bool F32 = false,
           int EPIC = -1>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
-  static_assert(EPIC < 0 || (EPIC == 2 && !BNR && !F8 && !F32), "compile-time epilogue: the bf16 line-ordered form");
+  static_assert(EPIC < 0 || ((EPIC == 2 || EPIC == 3) && !BNR && !F8 && !F32), "compile-time epilogue: the bf16 line-ordered form");
   static_assert(!F8 || !BNR, "fp8: no BN-backward reduction");
   static_assert(!WREG || (HALO && NST == 2 && !F8), "register-staged weights: the bf16 2-stage halo form");
   static_assert(!F32 || (HALO && !BNR && !F8 && !WREG), "f32: the halo form");
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // tiles: static lists (lin, lin + G, ...: `mine` of them) or claimed one tile ahead from the counter of the
   // block's N column (dyn, conv_common.h); either way a block keeps one N column
   // (the fp8 eval forms and the opt-in register-staged form keep static lists: no spare registers there)
-  const bool dyn = !F8 && !WREG && a.claim != nullptr;
+  const bool dyn = EPIC != 3 && !F8 && !WREG && a.claim != nullptr;
   const bool full = dyn && a.claim_full;   // every tile claimed (tiles 0 and 1 by one claim at the start)
   int r2 = 0;
   if (full && tid == 0) r2 = claim_next2(a.claim + lin % a.ntile_n);   // (its wait lands at the cst stores)
@@ -910,7 +911,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   const bool q8l = F8 && a.wide_st == 3;   // (fp8 output, launcher: Nout % 16, Cps % 16, out_stride % 16)
   // (fp8 forms: bf16 output through the narrow epilogue, fp8 output through epilogue_q8 -- the 16-B bf16 forms are not
   //  compiled into them: with all three epilogues the 256x256 fp8 forms spill)
-  const bool wide = EPIC == 2 || (EPIC < 0 && !BNR && !F32 && !F8 && a.wide_st && a.wide_st != 3);
+  const bool wide = EPIC >= 2 || (EPIC < 0 && !BNR && !F32 && !F8 && a.wide_st && a.wide_st != 3);
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
@@ -1058,7 +1059,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       last_epi = -NST;   // (no epilogue ops were issued)
       continue;
     }
-    if constexpr (EPIC == 2) epilogue_lines(m0c);
+    if constexpr (EPIC >= 2) epilogue_lines(m0c);
     else if (q8l) epilogue_q8(m0c);
     else if (wide && a.wide_st == 2) epilogue_lines(m0c);
     else if (wide) epilogue_wide(m0c);
@@ -1192,7 +1193,13 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   }
   // (line-ordered stores, the default: the instance with only that epilogue compiled, option tap64p_epic)
   const bool epic = a.wide_st == 2 && option("tap64p_epic", 1);
+  const bool epic3 = epic && !a.claim && option("tap64p_epic3", 1);   // (static tile lists: no claiming code)
   if (halo_shape && cfg == 1) {
+    if (epic3) {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 3>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 3>), dim3(grid), dim3(512), 0, s, a);
+      return 1;
+    }
     if (epic) {
       adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>), dim3(grid), dim3(512), 0, s, a);
@@ -1203,6 +1210,11 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     return 1;
   }
   if (halo_shape && cfg == 2 && option("tap64p_halo128", 1)) {
+    if (epic3) {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 3>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 3>), dim3(grid), dim3(512), 0, s, a);
+      return 1;
+    }
     if (epic) {
       adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 2>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 2>), dim3(grid), dim3(512), 0, s, a);
