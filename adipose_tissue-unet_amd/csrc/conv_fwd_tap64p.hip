@@ -1225,12 +1225,16 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     return 1;
   }
   if (epic && !bnr)
-    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, false, false, false, 2>", BM, BN, cfg == 1 ? 2 : 3);
+    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, false, false, false, %d>", BM, BN, cfg == 1 ? 2 : 3,
+                    epic3 ? 3 : 2);
   else
     adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false, false, false, -1>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
 #define P_LAUNCH(BM_, BN_, NST_)                                                                           \
   do {                                                                                                     \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epic3)                                                                                        \
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, false, false, false, false, false, 3>), dim3(grid), \
+                         dim3(512), 0, s, a);                                                             \
     else if (epic)                                                                                         \
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, false, false, false, false, false, 2>), dim3(grid), \
                          dim3(512), 0, s, a);                                                             \

@@ -434,7 +434,9 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
 // thread's channel group is fixed, so its constants are 8 LDS words each) and -- blocks of input chunk 0
 // only -- stores dY for the data-gradient launch; the halo groups follow at rows BNA_ROW..7. No barrier
 // and no long-lived registers: every thread reads back only the LDS slots its own DMA wrote.
-template <int NW, bool BNA = false, int SPR = 8>
+// CLM: the patch-claiming code compiled in (false: static lists only, the instances of every launch without a claim
+// counter -- the register allocation without the claim ring and its waits, as the persistent forward's EPIC = 3)
+template <int NW, bool BNA = false, int SPR = 8, bool CLM = true>
 __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs a) {
   constexpr int NTH = NW * 64, RB = 128;
   constexpr int PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
@@ -464,7 +466,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   // 0 and 1 are the block's static ones, claim value c is super-patch 2 G + c; super-patch s + 2 is claimed at the
   // start of super-patch s (a compiler-visible atomic: this file is built without the atomic optimizer) and
   // published after the drain at the end of its first patch, before that patch's barrier
-  const bool dyn = a.claim != nullptr;
+  const bool dyn = CLM && a.claim != nullptr;
   const bool full = dyn && a.claim_full;   // every super-patch claimed (0 and 1 by one claim at the start)
   int* ring = reinterpret_cast<int*>(smem + 2 * STAGE + (BNA ? 6 * 64 * 4 : 0));
   const int nt = dyn ? 0 : (lin < T ? (T - lin + G - 1) / G : 0);
@@ -1169,26 +1171,33 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     // claim_full only with at least 4 super-patches per block (its first claim takes two at once)
     a.claim_full = option("claim_full", 0) && (tiles + a.claim_chunk - 1) / a.claim_chunk >= 4 * per;
     const int grid = per * combos;
+    const bool stat_inst = !a.claim && option("wgrad_halop_static", 1);   // (the CLM = false instances)
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8, true>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 8>), dim3(grid), dim3(512), 0, s, a);
+      } else if (stat_inst) {
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4, false>");
+        hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 4, false>), dim3(grid), dim3(512), 0, s, a);
       } else {   // halo groups two a row over rows 3-5
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4, true>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 4>), dim3(grid), dim3(512), 0, s, a);
       }
     } else if (option("wgrad_halop_waves", 8) == 9) {
-      adp::set_kernel("igemm_wgrad_halop_kernel<9, false>");
+      adp::set_kernel("igemm_wgrad_halop_kernel<9, false, 8, true>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
+    } else if (stat_inst && option("wgrad_halop_spread", 4) != 8) {
+      adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false>");
+      hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false>), dim3(grid), dim3(512), 0, s, a);
     } else {
       // the next patch's loads over rows 0-3 (3 groups a row) leave 4 rows of DMA slack before the patch
       // barrier: +1-3 % on every level but 0 64->64 against rows 0-7, step -0.3 %
       // (profiles/r02_wgrad_spread_ab.txt); option wgrad_halop_spread=8 keeps the all-rows schedule
       if (option("wgrad_halop_spread", 4) == 8) {
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 8>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 8, true>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 8>), dim3(grid), dim3(512), 0, s, a);
       } else {
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, true>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4>), dim3(grid), dim3(512), 0, s, a);
       }
     }

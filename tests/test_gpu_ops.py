@@ -1307,7 +1307,7 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.set_option("wgrad_halop_spread", 8)   # next patch's loads over all 8 patch rows
         dWs = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dWs, l.Nout, srcB=srcB)
-        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 8>"
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 8, true>"
         ops.set_option("wgrad_halop_waves", 9)   # one wave per tap
         dW9 = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dW9, l.Nout, srcB=srcB)
