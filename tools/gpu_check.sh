@@ -222,6 +222,9 @@ for s in $STEPS; do
               --variants "wgrad_halop_static=0;wgrad_halop_static=1" > gpurun_out/stat_kernels.log 2>&1 &&
           timeout -k 10 300 python tools/ab_step.py --variant opt --opts "wgrad_halop_static=0,tap64p_epic3=0;wgrad_halop_static=1,tap64p_epic3=1" > gpurun_out/stat_ab.log 2>&1 ;;
     statw) timeout -k 10 300 python tools/ab_step.py --variant opt --rounds 5 --opts "wgrad_halop_static=0;wgrad_halop_static=1" > gpurun_out/statw_ab.log 2>&1 ;;
+    finalinfer) timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/final_fp8.log 2>&1 &&
+          timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 > gpurun_out/final_infer_tiles.log 2>&1 &&
+          timeout -k 10 300 python bench.py --levels 4 --size 512 --batch 8 --no-cpu-baseline > gpurun_out/final_cfg2_bench.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
