@@ -103,9 +103,7 @@ __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_ha
 template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false, bool F32 = false,
           int EPIC = -1>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
-  static_assert(EPIC < 0 || (!F8 && !F32 && (EPIC == 3 || (EPIC == 2 && !BNR))),
-                "compile-time epilogue: the bf16 line-ordered form (EPIC 3 with BNR: static lists, the BNR epilogue)");
-  constexpr bool LINES = EPIC >= 2 && !BNR;   // only the line-ordered epilogue compiled in
+  static_assert(EPIC < 0 || ((EPIC == 2 || EPIC == 3) && !BNR && !F8 && !F32), "compile-time epilogue: the bf16 line-ordered form");
   static_assert(!F8 || !BNR, "fp8: no BN-backward reduction");
   static_assert(!WREG || (HALO && NST == 2 && !F8), "register-staged weights: the bf16 2-stage halo form");
   static_assert(!F32 || (HALO && !BNR && !F8 && !WREG), "f32: the halo form");
@@ -913,7 +911,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   const bool q8l = F8 && a.wide_st == 3;   // (fp8 output, launcher: Nout % 16, Cps % 16, out_stride % 16)
   // (fp8 forms: bf16 output through the narrow epilogue, fp8 output through epilogue_q8 -- the 16-B bf16 forms are not
   //  compiled into them: with all three epilogues the 256x256 fp8 forms spill)
-  const bool wide = LINES || (EPIC < 0 && !BNR && !F32 && !F8 && a.wide_st && a.wide_st != 3);
+  const bool wide = EPIC >= 2 || (EPIC < 0 && !BNR && !F32 && !F8 && a.wide_st && a.wide_st != 3);
 
   bf16x8 fa[MIQ][2], fb0[2][2], fb1[2][2];
   // staggered issue (option tap64p_stagger): waves 4-7 issue their LDS-DMA pieces after their first MFMA
@@ -1061,7 +1059,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       last_epi = -NST;   // (no epilogue ops were issued)
       continue;
     }
-    if constexpr (LINES) epilogue_lines(m0c);
+    if constexpr (EPIC >= 2) epilogue_lines(m0c);
     else if (q8l) epilogue_q8(m0c);
     else if (wide && a.wide_st == 2) epilogue_lines(m0c);
     else if (wide) epilogue_wide(m0c);
@@ -1226,21 +1224,14 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true>), dim3(grid), dim3(512), 0, s, a);
     return 1;
   }
-  // BNR launches without a claim counter: the static-list instance (option tap64p_bnr_static)
-  const bool bnr3 = bnr && !a.claim && option("tap64p_bnr_static", 1);
   if (epic && !bnr)
     adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, false, false, false, false, false, %d>", BM, BN, cfg == 1 ? 2 : 3,
                     epic3 ? 3 : 2);
-  else if (bnr3)
-    adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, true, false, false, false, false, 3>", BM, BN, cfg == 1 ? 2 : 3);
   else
     adp::set_kernel("igemm_fwd_tap64p_kernel<%d, %d, %d, %s, false, false, false, false, -1>", BM, BN, cfg == 1 ? 2 : 3, bnr ? "true" : "false");
 #define P_LAUNCH(BM_, BN_, NST_)                                                                           \
   do {                                                                                                     \
-    if (bnr3)                                                                                              \
-      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true, false, false, false, false, 3>), dim3(grid), \
-                         dim3(512), 0, s, a);                                                             \
-    else if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \
+    if (bnr) hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, true>), dim3(grid), dim3(512), 0, s, a); \
     else if (epic3)                                                                                        \
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<BM_, BN_, NST_, false, false, false, false, false, 3>), dim3(grid), \
                          dim3(512), 0, s, a);                                                             \
