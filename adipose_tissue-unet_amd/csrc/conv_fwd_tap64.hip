@@ -67,7 +67,8 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, u
 // four exact v_mfma_f32_16x16x4_f32 (lane group g supplies k = 4g + j to the j-th one: A and B share the
 // permutation, so every k of the step enters the dot product once); f32 epilogue stores.
 // KP: the K loop compiled in -- -1 either, chosen at run time by a.kpipe (the fp8 / f32 forms); 0 the plain double
-// buffer only; 1 the mid-step-barrier loop only (bf16 forms: one loop per instance leaves the register allocator
+// buffer only; 2 the same without the nearest-x2 upsample gather (launches with up == 1, option tap64_up1); 1 the
+// mid-step-barrier loop only (bf16 forms: one loop per instance leaves the register allocator
 // one schedule, as the persistent kernel's EPIC does for its epilogues)
 template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8, bool F32 = false, int KP = -1>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
@@ -102,7 +103,8 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   const bool skip0 = SPLIT && n0 + wcu * 64 >= a.Nout;        // (block- and wave-uniform)
   const bool skip1 = SPLIT && n0 + wcu * 64 + 32 >= a.Nout;
   const int pos = lane & 7;
-  const int HWo = a.Ho * a.Wo, Hv = a.Hs * a.up, Wv = a.Ws * a.up;
+  const int upv = KP == 2 ? 1 : a.up;   // (KP 2: up == 1 at compile time)
+  const int HWo = a.Ho * a.Wo, Hv = a.Hs * upv, Wv = a.Ws * upv;
   const int Cin_s = a.CAs + a.CBs;
   const int Wrows = (a.Nout + 63) / 64 * 64;
   const int nk = a.K / KSTEP;
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       int yi = ry[h][i] + k.oy, xi = rx[h][i] + k.ox;
       const bool v = rn[h][i] >= 0 && (unsigned)yi < (unsigned)Hv && (unsigned)xi < (unsigned)Wv;
       int pix;
-      if (a.up == 2) pix = (rn[h][i] + (yi >> 1)) * a.Ws + (xi >> 1);
+      if (upv == 2) pix = (rn[h][i] + (yi >> 1)) * a.Ws + (xi >> 1);
       else pix = pb[h][i] + k.dpix;
       if constexpr (BUF) {
         const unsigned off = v ? (unsigned)(pix * k.cs + k.cb + rc[h][i]) : T64_OOB;
@@ -390,6 +392,10 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
       adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, false, 1>", WM, WN, TM,        \
                       BUFV ? "true" : "false", BNRV ? "true" : "false");                               \
       hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, false, 1>), g, b, 0, s, a); \
+    } else if (a.up == 1 && adp::option("tap64_up1", 1)) {                                             \
+      adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, false, 2>", WM, WN, TM,        \
+                      BUFV ? "true" : "false", BNRV ? "true" : "false");                               \
+      hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, false, 2>), g, b, 0, s, a); \
     } else {                                                                                           \
       adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, %s, %s, false, false, 0>", WM, WN, TM,        \
                       BUFV ? "true" : "false", BNRV ? "true" : "false");                               \
