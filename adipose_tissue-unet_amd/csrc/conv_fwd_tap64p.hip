@@ -99,11 +99,13 @@ __device__ __forceinline__ int p_hswz(int r) { return r & 7; }   // (conv_fwd_ha
 // 16-B); 2 = only the line-ordered one compiled in -- the launcher's default store form, without the register
 // allocation of two epilogues it never runs (measured on the fp8 forms, whose ConvTranspose launch went from 0.215 to
 // 0.120 ms when the unused 16-B bf16 epilogues left it); 3 = the same with static tile lists only (no claiming code:
-// the launches without a claim counter, i.e. every default launch; option tap64p_epic3)
+// the launches without a claim counter, i.e. every default launch; option tap64p_epic3); 4 = 3 with plain stores only
+// (out_mode 0: no pixel-shuffle or split store paths; option tap64p_epic4)
 template <int BM, int BN, int NST, bool BNR, bool HALO = false, bool F8 = false, bool WREG = false, bool F32 = false,
           int EPIC = -1>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
-  static_assert(EPIC < 0 || ((EPIC == 2 || EPIC == 3) && !BNR && !F8 && !F32), "compile-time epilogue: the bf16 line-ordered form");
+  static_assert(EPIC < 0 || ((EPIC == 2 || EPIC == 3 || EPIC == 4) && !BNR && !F8 && !F32),
+                "compile-time epilogue: the bf16 line-ordered form");
   static_assert(!F8 || !BNR, "fp8: no BN-backward reduction");
   static_assert(!WREG || (HALO && NST == 2 && !F8), "register-staged weights: the bf16 2-stage halo form");
   static_assert(!F32 || (HALO && !BNR && !F8 && !WREG), "f32: the halo form");
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   // tiles: static lists (lin, lin + G, ...: `mine` of them) or claimed one tile ahead from the counter of the
   // block's N column (dyn, conv_common.h); either way a block keeps one N column
   // (the fp8 eval forms and the opt-in register-staged form keep static lists: no spare registers there)
-  const bool dyn = EPIC != 3 && !F8 && !WREG && a.claim != nullptr;
+  const bool dyn = EPIC < 3 && !F8 && !WREG && a.claim != nullptr;
   const bool full = dyn && a.claim_full;   // every tile claimed (tiles 0 and 1 by one claim at the start)
   int r2 = 0;
   if (full && tid == 0) r2 = claim_next2(a.claim + lin % a.ntile_n);   // (its wait lands at the cst stores)
@@ -515,7 +517,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
   };
 
   // ---- epilogue resources
-  const bool shuffle = a.out_mode == 1, split = a.out_mode == 2;
+  const bool shuffle = EPIC != 4 && a.out_mode == 1, split = EPIC != 4 && a.out_mode == 2;   // (EPIC 4: plain stores)
   const int Hq = 2 * a.Ho, Wq = 2 * a.Wo;
   const bool o8 = F8 && a.out_f8;   // fp8 output (the ConvTranspose forwards of UNetBN.forward_fp8)
   const int oes = o8 ? 1 : OES;
@@ -1195,6 +1197,11 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
   const bool epic = a.wide_st == 2 && option("tap64p_epic", 1);
   const bool epic3 = epic && !a.claim && option("tap64p_epic3", 1);   // (static tile lists: no claiming code)
   if (halo_shape && cfg == 1) {
+    if (epic3 && a.out_mode == 0 && option("tap64p_epic4", 1)) {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 4>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 4>), dim3(grid), dim3(512), 0, s, a);
+      return 1;
+    }
     if (epic3) {
       adp::set_kernel("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 3>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 3>), dim3(grid), dim3(512), 0, s, a);
@@ -1210,6 +1217,11 @@ int launch_fwd_tap64p(FwdArgs& a, hipStream_t s, int tile) {
     return 1;
   }
   if (halo_shape && cfg == 2 && option("tap64p_halo128", 1)) {
+    if (epic3 && a.out_mode == 0 && option("tap64p_epic4", 1)) {
+      adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 4>");
+      hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 4>), dim3(grid), dim3(512), 0, s, a);
+      return 1;
+    }
     if (epic3) {
       adp::set_kernel("igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 3>");
       hipLaunchKernelGGL((igemm_fwd_tap64p_kernel<256, 128, 3, false, true, false, false, false, 3>), dim3(grid), dim3(512), 0, s, a);

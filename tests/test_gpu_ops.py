@@ -417,7 +417,8 @@ def test_tap64p_wreg_matches_dma(mode, grid):
                 ops.set_option(k_, None)
         # (the DMA arm: the default line-ordered-epilogue instance, EPIC = 3 with static tile lists, 2 with claiming)
         assert kname in (("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, true, false, -1>",) if wreg else
-                         ("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 3>",
+                         ("igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 4>",
+                          "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 3>",
                           "igemm_fwd_tap64p_kernel<256, 256, 2, false, true, false, false, false, 2>")), kname
         res.append((torch.cat(outs, -1), st.double()))
     (y1, s1), (y0, s0) = res
