@@ -240,6 +240,9 @@ for s in $STEPS; do
           timeout -k 10 400 python tools/bench_kernels.py --kinds fwd,fwd_stats --layers "L1 128->128,L2 256->256,L3 512->512,L4 1024->1024" \
               --variants "tap64p_epic4=0;tap64p_epic4=1" > gpurun_out/epic4_kernels.log 2>&1 &&
           timeout -k 10 300 python tools/ab_step.py --variant opt --rounds 5 --opts "tap64p_epic4=0;tap64p_epic4=1" > gpurun_out/epic4_ab.log 2>&1 ;;
+    stat2) timeout -k 10 400 python tools/bench_kernels.py --kinds wgrad --layers "L0 64->64" \
+              --variants "wgrad_halop_static=1;wgrad_halop_static=2" > gpurun_out/stat2_kernels.log 2>&1 &&
+          timeout -k 10 300 python tools/ab_step.py --variant opt --rounds 5 --opts "wgrad_halop_static=1;wgrad_halop_static=2" > gpurun_out/stat2_ab.log 2>&1 ;;
     cfg5) timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -v -s --timeout 300 --timeout-method thread \
             -k "cfg5" > gpurun_out/cfg5_tests.log 2>&1 ;;
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
