@@ -1171,10 +1171,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     // claim_full only with at least 4 super-patches per block (its first claim takes two at once)
     a.claim_full = option("claim_full", 0) && (tiles + a.claim_chunk - 1) / a.claim_chunk >= 4 * per;
     const int grid = per * combos;
-    // (the CLM = false instances; option value 2: not for one-chunk 64-output layers, where the static instance
-    //  measured 7 % slower: profiles/r04e_wgrad_static_kernels.log)
-    const int stat_opt = option("wgrad_halop_static", 1);
-    const bool stat_inst = !a.claim && stat_opt && !(stat_opt == 2 && cin == 64 && a.Nout == 64);
+    const bool stat_inst = !a.claim && option("wgrad_halop_static", 1);   // (the CLM = false instances)
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {
         adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8, true>");
