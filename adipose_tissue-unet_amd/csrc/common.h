@@ -137,7 +137,8 @@ int bn_fold_reset(hipStream_t s);   // adp_bn_fold_reset
 // device, handed out in turn; a launch leaves its slot zeroed again), or nullptr (error set)
 constexpr int CLAIM_SLOTS = 64, CLAIM_INTS = 64;
 int* claim_slot();
-// per-device growable scratch (slot 0: weight-gradient split partials); growing synchronises the device
+// per-device growable scratch (slot 0: weight-gradient split partials / slabs, 1: dz of the unfused BN-backward
+// weight gradient, 2: metrics, 3: bias-gradient block sums); growing synchronises the device
 void* scratch(int slot, size_t bytes);
 int stat_fold(int C, float* dst0, float* dst1, hipStream_t s);   // elementwise.hip
 // the same over replica channels [c0, c0 + C) into dst0[0..C) (and dst1 unless nullptr)

@@ -62,7 +62,10 @@ struct WgradArgs {
   int M, mchunk, ntile_k, ntile_n;
   int debug_flags;      // timing-only ablations (tools/bench_kernels.py): bit0 skips the dW atomics
   float* part;          // tap64: per-split partial dW slabs [split][Nout][Kpad] (plain stores), reduced
-                        // into dW by a second launch; nullptr -> f32 atomics into dW
+                        // into dW by a second launch; nullptr -> f32 atomics into dW (halo weight gradient: one
+                        // slab per block index within its (chunk, output block) combination, fixed-order reduce)
+  int part_rmw;         // halo weight gradient with one block per combination: dW += partial by plain
+                        // load + store (the block owns its dW rows), no slab, no atomics
   // fused BatchNorm-backward apply (adp_conv_wgrad_bn): dY = bn_bwd_apply(bna_dA, bna_z) of the layer's
   // BatchNorm, computed on load and stored into dY (all three [M][dy_stride]); bna_dA == nullptr: plain dY
   const void* bna_dA; const void* bna_z;
@@ -451,6 +454,8 @@ int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input la
 int launch_fwd_halop_f8(FwdArgs& a, hipStream_t s);
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
+// dst[i] += sum_g part[g][i] over G slabs of n4 float4 each, in an order fixed by G alone (deterministic)
+void slab_reduce(int G, size_t n4, const float* part, float* dst, hipStream_t s);
 // conv_wgrad_f32.hip: f32 weight gradient on LDS-DMA staging (32-pixel stages, exact f32 MFMA)
 int launch_wgrad_f32(WgradArgs& a, hipStream_t s);
 // the persistent halo weight-gradient kernel takes this launch with the BatchNorm-backward apply fused

@@ -981,8 +981,10 @@ __global__ __launch_bounds__(NT, 2) void igemm_wgrad_glds_kernel(WgradArgs a) {
 
 // per-channel sum over pixels (bias gradient); plain [M][C] or pixel-shuffled ConvT gradient
 // (channel n of the GEMM = sub*Cps + c -> bias c)
+// part != 0: out is this launch's slab [gridDim.x][C] and block b stores its sums in row b (plain stores, summed in a
+// fixed order by adp::slab_reduce: deterministic), else f32 atomics into out
 template <typename T>
-__global__ void channel_sum_kernel(size_t M, int C, int stride, const T* x, float* out, int fold) {
+__global__ void channel_sum_kernel(size_t M, int C, int stride, const T* x, float* out, int fold, int part = 0) {
   const int G = C >> 3;
   const int lanes = NT / G;
   const int g = threadIdx.x % G, pl = threadIdx.x / G;
@@ -1004,8 +1006,24 @@ __global__ void channel_sum_kernel(size_t M, int C, int stride, const T* x, floa
   for (int c = threadIdx.x; c < C; c += NT) {
     float t = 0.f;
     for (int l = 0; l < lanes; ++l) t += red[(l * G + (c >> 3)) * 8 + (c & 7)];
-    atomicAdd(out + (fold ? c % fold : c), t);
+    if (part) out[(size_t)blockIdx.x * C + c] = t;
+    else atomicAdd(out + (fold ? c % fold : c), t);
   }
+}
+
+// bias gradient of a weight-gradient launch: per-channel sums of dY (ConvT: of its 2x-resolution pixel-shuffled
+// gradient); option wgrad_det (default on): per-block rows + the fixed-order slab reduce instead of f32 atomics
+template <typename T>
+void launch_bias_grad(const WgradArgs& a, hipStream_t s) {
+  const size_t Mp = a.dy_mode == 0 ? (size_t)a.M : (size_t)a.M * 4;
+  const int C = a.dy_mode == 0 ? a.Nout : a.Cps;
+  const int G = C / 8, lanes = NT / G;
+  const int blocks = (int)std::min<size_t>((Mp + lanes - 1) / lanes, 1024);
+  float* part = adp::option("wgrad_det", 1) && C % 4 == 0
+                    ? static_cast<float*>(adp::scratch(3, (size_t)blocks * C * sizeof(float))) : nullptr;
+  hipLaunchKernelGGL(channel_sum_kernel<T>, dim3(blocks), dim3(NT), 0, s, Mp, C, a.dy_stride,
+                     reinterpret_cast<const T*>(a.dY), part ? part : a.dB, 0, part ? 1 : 0);
+  if (part) adp::slab_reduce(blocks, (size_t)C / 4, part, a.dB, s);
 }
 
 }  // namespace
@@ -1250,21 +1268,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
           hipLaunchKernelGGL((igemm_wgrad_glds_kernel<128, 128>), dim3(tiles, splits), dim3(NT), 0, s, a); }
     }
     adp::kernel_end();   // (no-op when launch_wgrad_tap64 marked it before its split reduce)
-    if (a.dB) {
-      const int G = a.Nout / 8, lanes = NT / G;
-      const int blocks = (int)std::min<long long>((a.M + lanes - 1) / lanes, 1024);
-      if (a.dy_mode == 0) {
-        hipLaunchKernelGGL(channel_sum_kernel<bf16>, dim3(blocks), dim3(NT), 0, s, (size_t)a.M, a.Nout,
-                           a.dy_stride, reinterpret_cast<const bf16*>(a.dY), a.dB, 0);
-      } else {
-        // ConvT: bias c collects all 4 sub-pixels -> sum the 2x-resolution gradient per channel
-        const int Gc = a.Cps / 8, lc = NT / Gc;
-        const size_t Mo = (size_t)a.M * 4;
-        const int bl = (int)std::min<size_t>((Mo + lc - 1) / lc, 1024);
-        hipLaunchKernelGGL(channel_sum_kernel<bf16>, dim3(bl), dim3(NT), 0, s, Mo, a.Cps, a.dy_stride,
-                           reinterpret_cast<const bf16*>(a.dY), a.dB, 0);
-      }
-    }
+    if (a.dB) launch_bias_grad<bf16>(a, s);
     return adp::check_launch("adp_conv_wgrad");
   }
   if (std::is_same<T, bf16>::value && adp::option("conv_fast", 2) >= 1) {
@@ -1289,20 +1293,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
   }
   // f32: the LDS-DMA weight-gradient kernel (conv_wgrad_f32.hip), bias gradient as a channel-sum launch
   if (std::is_same<T, float>::value && adp::launch_wgrad_f32(a, s)) {
-    if (a.dB) {
-      const int G = a.Nout / 8, lanes = NT / G;
-      const int blocks = (int)std::min<long long>((a.M + lanes - 1) / lanes, 1024);
-      if (a.dy_mode == 0) {
-        hipLaunchKernelGGL(channel_sum_kernel<float>, dim3(blocks), dim3(NT), 0, s, (size_t)a.M, a.Nout,
-                           a.dy_stride, reinterpret_cast<const float*>(a.dY), a.dB, 0);
-      } else {
-        const int Gc = a.Cps / 8, lc = NT / Gc;
-        const size_t Mo = (size_t)a.M * 4;
-        const int bl = (int)std::min<size_t>((Mo + lc - 1) / lc, 1024);
-        hipLaunchKernelGGL(channel_sum_kernel<float>, dim3(bl), dim3(NT), 0, s, Mo, a.Cps, a.dy_stride,
-                           reinterpret_cast<const float*>(a.dY), a.dB, 0);
-      }
-    }
+    if (a.dB) launch_bias_grad<float>(a, s);
     return adp::check_launch("adp_conv_wgrad");
   }
   a.ntile_k = (a.K + 63) / 64;

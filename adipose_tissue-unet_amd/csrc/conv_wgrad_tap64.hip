@@ -436,8 +436,15 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
 // and no long-lived registers: every thread reads back only the LDS slots its own DMA wrote.
 // CLM: the patch-claiming code compiled in (false: static lists only, the instances of every launch without a claim
 // counter -- the register allocation without the claim ring and its waits, as the persistent forward's EPIC = 3)
-template <int NW, bool BNA = false, int SPR = 8, bool CLM = true>
+// PF (round 5): row-pipelined fragments -- each wave issues the LDS reads of patch row pr + 1 before the MFMAs of row
+// pr (two fragment sets in registers), and the next patch's row 0 right after the patch barrier, before row 7's MFMAs.
+// Without it a wave waits for its own row's reads before every MFMA cluster, and since the waves leave each patch
+// barrier together, all 8 waves read at once and then all multiply at once (the two waves of a SIMD do not cover each
+// other's read phase): the round-5 ablation (profiles/r05a_wgrad_ablation.log) ran the K loop with no LDS-DMA, no
+// barrier and no atomics at only 1.33 PF.
+template <int NW, bool BNA = false, int SPR = 8, bool CLM = true, bool PF = false>
 __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs a) {
+  static_assert(!PF || (NW == 8 && !BNA && !CLM), "PF: the plain static-list 8-wave form");
   constexpr int NTH = NW * 64, RB = 128;
   constexpr int PH = 8, PW = 32, HW = PW + 2, HROWS = (PH + 2) * HW;   // 340 halo pixels
   constexpr int HCH = HROWS * 8, DCH = PH * PW * 8;                     // 16-B chunks per image
@@ -451,6 +458,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap
+  const int dbg = a.debug_flags;   // timing-only ablations (option wgrad_debug): bits 0-3, see below
   prio_static<ADP_PRIO_WGRAD>(wave);
   const int dy = wave / 3, dx = wave - 3 * (wave / 3);
   const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
@@ -710,7 +718,122 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     W64_BAR();
   }
-  for (int k = 0; any; ++k) {
+  if constexpr (PF) {
+    struct Frags { bf16x8 fd[4], fx[4], fd8, fx8[2]; };
+    Frags F[2];   // fragments of the even / odd patch rows
+    // per-lane byte offset of a transposed 16 x 32 fragment whose 32 rows start at row C of an image (the same
+    // addressing as frag()); lz: an opaque copy of the lane id, so that the 29 addresses below are rebuilt per
+    // patch instead of being held across the loop next to their per-buffer sums
+    auto xoff = [&](int C, int col0, int lz) -> uint32_t {
+      const int g_ = lz >> 4, i_ = lz & 15;
+      const int R = C + 16 * (g_ >> 1) + 4 * (g_ & 1) + (i_ >> 2);
+      const int col = col0 + 4 * (i_ & 3), chunk = col >> 3, inb = (col & 7) * 2;
+      return (uint32_t)(R * RB + ((chunk ^ gsw<RB>(R)) << 4) + inb);
+    };
+    // halo rows of patch row pr = 4 q + m start at (pr + dy) * HW + dx: rows pr and pr + 4 differ by 4 HW = 136 rows
+    // (a multiple of 8: the same swizzle), so 4 address registers per column block serve all 8 rows with immediate
+    // offsets q * 136 * RB; the two 8-row halves of a fragment differ by 8 rows (same swizzle: + 8 RB); dY row pr
+    // is + pr * PW * RB
+    uint32_t ha[4][4], h8[4][2], da[4], d8;
+    auto addrs = [&](uint32_t hb) {
+      int lz = lane;
+      asm volatile("" : "+v"(lz));
+      const int C0 = dy * HW + dx;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) ha[m][cb] = hb + xoff(C0 + HW * m, cb * 16, lz);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) h8[m][j] = hb + xoff(2 * HW + 2 + HW * m, cb8 * 16 + 16 * j, lz);
+      }
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) da[nb] = hb + HBUF + xoff(0, nb * 16, lz);
+      d8 = hb + HBUF + xoff(0, nb8 * 16, lz);
+    };
+    auto rd = [](uint32_t ad, auto off) -> bf16x8 {   // two ds_read_b64_tr_b16 at immediate offsets off, off + 8 RB
+      v4s16 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(ad), "n"(decltype(off)::value) : "memory");
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(ad), "n"(decltype(off)::value + 8 * RB)
+                   : "memory");
+      bf16x8 r;
+      const bf16* l = reinterpret_cast<const bf16*>(&lo);
+      const bf16* h = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = h[e]; }
+      return r;
+    };
+    // the 22 reads of patch row pr (addresses of the current buffer) in two parts: 14 (dY, tap 8), then 8 (this
+    // wave's tap); lgkmcnt holds at most 15, so the wait for the previous row sits between the parts
+    auto load_row_a = [&](Frags& f, auto prc) {
+      constexpr int pr = decltype(prc)::value, m = pr & 3;
+      using HO = std::integral_constant<int, (pr >> 2) * 4 * HW * RB>;
+      using DO = std::integral_constant<int, pr * PW * RB>;
+      f.fd8 = rd(d8, DO{});
+      f.fx8[0] = rd(h8[m][0], HO{});
+      f.fx8[1] = rd(h8[m][1], HO{});
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) f.fd[nb] = rd(da[nb], DO{});
+    };
+    auto load_row_b = [&](Frags& f, auto prc) {
+      constexpr int pr = decltype(prc)::value, m = pr & 3;
+      using HO = std::integral_constant<int, (pr >> 2) * 4 * HW * RB>;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) f.fx[cb] = rd(ha[m][cb], HO{});
+    };
+    auto load_row = [&](Frags& f, auto prc) {
+      load_row_a(f, prc);
+      load_row_b(f, prc);
+    };
+    if (any) {
+      addrs(sbase);
+      load_row(F[0], std::integral_constant<int, 0>{});
+    }
+    for (int k = 0; any; ++k) {
+      const int buf = k & 1;
+      const int tn = tile_id(k + 1);
+      const bool more = tn >= 0;
+      const Patch Pn = patch(more ? tn : tcur);
+      addrs(sbase + buf * STAGE);
+      auto row = [&](auto prc) {
+        constexpr int pr = decltype(prc)::value;
+        if (more && !(dbg & 2)) issue_row(Pn, pr, buf ^ 1);
+        if constexpr (pr < PH - 1) {
+          load_row_a(F[(pr + 1) & 1], std::integral_constant<int, pr + 1>{});
+          lgkm_wait<14>();   // row pr's fragments (issued one row ago) have landed
+          load_row_b(F[(pr + 1) & 1], std::integral_constant<int, pr + 1>{});
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next patch landed (this thread's pieces)
+          lgkm_wait<0>();                                      // row 7's fragments: this buffer is read out
+          if (!(dbg & 4)) W64_BAR();
+          if (more) {                                          // the next patch's row 0 under row 7's MFMAs
+            addrs(sbase + (buf ^ 1) * STAGE);
+            load_row(F[0], std::integral_constant<int, 0>{});
+          }
+        }
+        const Frags& f = F[pr & 1];
+        prio_hi<ADP_PRIO_WGRAD>();
+        acc8[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.fd8, f.fx8[0], acc8[0], 0, 0, 0);
+        acc8[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.fd8, f.fx8[1], acc8[1], 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc[nb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.fd[nb], f.fx[cb], acc[nb][cb], 0, 0, 0);
+        prio_lo<ADP_PRIO_WGRAD>();
+      };
+      row(std::integral_constant<int, 0>{});
+      row(std::integral_constant<int, 1>{});
+      row(std::integral_constant<int, 2>{});
+      row(std::integral_constant<int, 3>{});
+      row(std::integral_constant<int, 4>{});
+      row(std::integral_constant<int, 5>{});
+      row(std::integral_constant<int, 6>{});
+      row(std::integral_constant<int, 7>{});
+      if (!more) break;
+      tcur = tn;
+    }
+  }
+  for (int k = 0; any && !PF; ++k) {
     const int buf = k & 1;
     const int tn = tile_id(k + 1);
     const bool more = tn >= 0;
@@ -733,7 +856,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bna_apply(Pn, buf ^ 1);
       }
-      if (more) issue_row(Pn, pr, buf ^ 1);
+      if (more && !(dbg & 2)) issue_row(Pn, pr, buf ^ 1);   // (wgrad_debug bit 1: no LDS-DMA after the prologue)
       bf16x8 fd[4], fx[4], fd8, fx8[2];
       if (NW == 8) {
         fd8 = frag(dbase, pr * PW, nb8 * 16);
@@ -747,7 +870,9 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
       // column block cb's MFMAs start as soon as its two reads (and the dY fragments) have landed
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        if (cb == 0) lgkm_wait<6>();
+        if (dbg & 8) {   // (wgrad_debug bit 3, timing only: the MFMAs do not wait for their fragments)
+          if (cb == 3) lgkm_wait<0>();
+        } else if (cb == 0) lgkm_wait<6>();
         else if (cb == 1) lgkm_wait<4>();
         else if (cb == 2) lgkm_wait<2>();
         else lgkm_wait<0>();
@@ -764,12 +889,12 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next patch landed
     if (claim_now && tid == 0) ring[(k / CH + 2) & 3] = claimed;   // (slot of super-patch s - 2: long done)
-    W64_BAR();                                          // and nobody reads this buffer any more
+    if (!(dbg & 4)) W64_BAR();                          // and nobody reads this buffer any more (bit 2: timing only)
     if (!more) break;
     tcur = tn;
   }
   if (dyn && tid == 0) claim_block_done(a.claim, combos, gridDim.x);   // (every claim of the block has returned)
-  if (!any) return;   // (dyn: a block that started late found the work taken)
+  if (!any && !a.part) return;   // (dyn: a block that started late found the work taken; a slab gets its zeros)
   if (a.debug_flags & 1) {
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
@@ -778,30 +903,38 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     asm volatile("" ::"v"(acc8[0]), "v"(acc8[1]));
     return;
   }
-  // dW[n][tap * 64 + c] += acc: each wave's 16-row blocks through LDS into 256-B rows
+  // dW[n][tap * 64 + c] += acc: each wave's 16-row blocks through LDS into 256-B rows. Three forms (launcher): f32
+  // atomics into dW; plain stores into this block's slab (block index lin of its combination: a fixed-order reduce
+  // launch adds the slabs into dW, so the result does not depend on the order the blocks finish); or, with one block
+  // per combination, dW += partial by plain load + store (the block owns those dW elements)
   constexpr int ES = 68;
   float* blk = reinterpret_cast<float*>(smem) + wave * 16 * ES;
   const int col = lane & 15, rq = (lane >> 4) * 4;
   const int kk = wave * (a.CAs + a.CBs) + ch * 64 + lane;
-  float* dW = a.dW + (size_t)nblk * 64 * a.Kpad;
+  float* dW = a.part ? a.part + ((size_t)lin * a.Nout + (size_t)nblk * 64) * a.Kpad : a.dW + (size_t)nblk * 64 * a.Kpad;
+  auto out = [&](auto put) {
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb) {
+    for (int nb = 0; nb < 4; ++nb) {
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
+      for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) blk[(rq + r) * ES + cb * 16 + col] = acc[nb][cb][r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (int r = 0; r < 4; ++r) blk[(rq + r) * ES + cb * 16 + col] = acc[nb][cb][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
-    for (int i = 0; i < 16; ++i) atomicAdd(dW + (size_t)(nb * 16 + i) * a.Kpad + kk, blk[i * ES + lane]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  }
-  if (NW == 8) {   // this wave's eighth of tap 8: rows nb8 * 16 + rq + r, columns cb8 * 16 + {0..31}
-    const int k8 = 8 * (a.CAs + a.CBs) + ch * 64 + cb8 * 16 + col;
+      for (int i = 0; i < 16; ++i) put(dW + (size_t)(nb * 16 + i) * a.Kpad + kk, blk[i * ES + lane]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+    if (NW == 8) {   // this wave's eighth of tap 8: rows nb8 * 16 + rq + r, columns cb8 * 16 + {0..31}
+      const int k8 = 8 * (a.CAs + a.CBs) + ch * 64 + cb8 * 16 + col;
 #pragma unroll
-    for (int j2 = 0; j2 < 2; ++j2)
+      for (int j2 = 0; j2 < 2; ++j2)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(dW + (size_t)(nb8 * 16 + rq + r) * a.Kpad + k8 + 16 * j2, acc8[j2][r]);
-  }
+        for (int r = 0; r < 4; ++r) put(dW + (size_t)(nb8 * 16 + rq + r) * a.Kpad + k8 + 16 * j2, acc8[j2][r]);
+    }
+  };
+  if (a.part) out([](float* p, float v) { *p = v; });
+  else if (a.part_rmw) out([](float* p, float v) { *p += v; });
+  else out([](float* p, float v) { atomicAdd(p, v); });
 }
 
 // Weight gradient of the input layers (one 8-channel source, 3x3 stride 1, 64 outputs; K = 72): an
@@ -1014,20 +1147,36 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_cin8_kernel(WgradArgs a) {
       if (k + 1 < nt) step(k + 1, z1);
     }
   }
-  if (nt == 0) return;
-  // wave partials -> LDS [64][80] f32 -> one atomic per element into dW[n][k], k < 72
+  if (nt == 0 && !a.part) return;   // (a slab gets its zeros)
+  // wave partials -> LDS [64][80] f32, added in wave order (deterministic) -> this block's slab [64][Kpad] (plain
+  // stores, zeros past k = 72; the launcher's fixed-order reduce adds the slabs into dW) or one f32 atomic per
+  // element into dW[n][k], k < 72
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* red = reinterpret_cast<float*>(smem);
-  for (int i = tid; i < 64 * 80; i += NTH) red[i] = 0.f;
   __syncthreads();
   const int col = lane & 15, rq = (lane >> 4) * 4;
+  for (int w = 0; w < NTH / 64; ++w) {
+    if (wave == w) {   // (a lane's (row, column) elements are its own: no race inside the wave)
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
+      for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-    for (int kb = 0; kb < 5; ++kb)
+        for (int kb = 0; kb < 5; ++kb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(red + (nb * 16 + rq + r) * 80 + kb * 16 + col, acc[nb][kb][r]);
-  __syncthreads();
+          for (int r = 0; r < 4; ++r) {
+            float* e = red + (nb * 16 + rq + r) * 80 + kb * 16 + col;
+            *e = w == 0 ? acc[nb][kb][r] : *e + acc[nb][kb][r];
+          }
+    }
+    __syncthreads();
+  }
+  if (a.part) {
+    float* slab = a.part + (size_t)blockIdx.x * 64 * a.Kpad;
+    for (int i = tid; i < 64 * a.Kpad; i += NTH) {
+      const int n = i / a.Kpad, kk = i - n * a.Kpad;
+      slab[i] = kk < 72 ? red[n * 80 + kk] : 0.f;
+    }
+    return;
+  }
   for (int i = tid; i < 64 * 72; i += NTH) {
     const int n = i / 72, kk = i - n * 72;
     atomicAdd(a.dW + (size_t)n * a.Kpad + kk, red[n * 80 + kk]);
@@ -1064,6 +1213,46 @@ __global__ void wgrad_reduce_kernel(int splits, size_t slab, const float4* part,
   }
 }
 
+// Fixed-order sum of G partial slabs into dW (dW[i] += sum_g part[g][i]): a 256-thread block takes 32 float4
+// elements; its 8 thread groups sum consecutive slab ranges [g0, g1) in order, and group 0 adds the 8 range sums in
+// order. The association depends only on G, so two runs give the same bits (unlike f32 atomics).
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(int G, size_t n4, const float4* __restrict__ part,
+                                                                float4* __restrict__ dW) {
+  __shared__ float4 ps[8][32];
+  const int e = threadIdx.x & 31, j = threadIdx.x >> 5;
+  const size_t i = (size_t)blockIdx.x * 32 + e;
+  const int per = (G + 7) / 8, g0 = min(G, j * per), g1 = min(G, g0 + per);
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    int g = g0;
+    for (; g + 4 <= g1; g += 4) {   // four loads in flight, added in order
+      const float4 v0 = part[(size_t)g * n4 + i], v1 = part[(size_t)(g + 1) * n4 + i];
+      const float4 v2 = part[(size_t)(g + 2) * n4 + i], v3 = part[(size_t)(g + 3) * n4 + i];
+      acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
+      acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
+      acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
+      acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
+    }
+    for (; g < g1; ++g) {
+      const float4 v = part[(size_t)g * n4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  ps[j][e] = acc;
+  __syncthreads();
+  if (j == 0 && i < n4) {
+    float4 s = ps[0][e];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
+      const float4 v = ps[q][e];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float4 d = dW[i];
+    d.x += s.x; d.y += s.y; d.z += s.z; d.w += s.w;
+    dW[i] = d;
+  }
+}
+
 // Pixel splits: enough blocks to fill the chip (target_blocks), but every split keeps at least
 // min_chunk pixels so that the f32 atomic epilogue (blocks x TN x TK x 4 bytes at ~1.3 TB/s) stays
 // small against the GEMM.
@@ -1087,7 +1276,10 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   const size_t slab = (size_t)a.Nout * a.Kpad;
   // (measured per layer, tools/bench_kernels.py: slabs win 7-14 % on the 256x256 tiles of the >= 256-channel
   // layers, atomics win 4-6 % on the narrow-N tiles, whose slabs are small but split ~1000 ways)
-  if (splits > 1 && adp::option("wgrad_partials", TN >= 256 ? 1 : 0) && !(a.debug_flags & 1))
+  // (wgrad_det, default on: every split launch writes slabs, summed by the fixed-order reduce: two runs give the
+  //  same bits)
+  const bool det = adp::option("wgrad_det", 1) != 0;
+  if (splits > 1 && (det || adp::option("wgrad_partials", TN >= 256 ? 1 : 0)) && !(a.debug_flags & 1))
     a.part = static_cast<float*>(adp::scratch(0, slab * splits * sizeof(float)));
   adp::set_kernel("igemm_wgrad_tap64_kernel<%d, %d, %d, %s, %s>", WN, WK, TNW, two ? "true" : "false",
                   ra ? "true" : "false");
@@ -1096,18 +1288,27 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   else if (!two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, false>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, false>), grid, block, 0, s, a);
   adp::kernel_end();   // (the split reduce below is a kernel of its own in rocprofv3's list)
-  if (a.part) {
+  if (a.part && det) {
+    const size_t n4 = slab / 4;
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)((n4 + 31) / 32)), dim3(256), 0, s, splits, n4,
+                       reinterpret_cast<const float4*>(a.part), reinterpret_cast<float4*>(a.dW));
+  } else if (a.part) {
     const size_t n4 = slab / 4;
     const int groups = (splits + WG_SG - 1) / WG_SG;
     const int blocks = (int)std::min<size_t>((n4 + 255) / 256, 4096);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks, groups), dim3(256), 0, s, splits, slab,
                        reinterpret_cast<const float4*>(a.part), reinterpret_cast<float4*>(a.dW));
   }
+  a.part = nullptr;
 }
 
 }  // namespace
 
 namespace adp {
+void slab_reduce(int G, size_t n4, const float* part, float* dst, hipStream_t s) {
+  hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)((n4 + 31) / 32)), dim3(256), 0, s, G, n4,
+                     reinterpret_cast<const float4*>(part), reinterpret_cast<float4*>(dst));
+}
 // shapes of the persistent halo weight-gradient kernel
 static bool halop_ok(const WgradArgs& a) {
   const int cin = a.CAs + a.CBs;
@@ -1149,12 +1350,20 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
   if (cin8_ok(a)) {   // (bna_dA set: the caller checked wgrad_bna_fusable)
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
     const int grid = std::max(1, std::min(tiles, option("wgrad_cin8_grid", 256)));
+    // wgrad_det (default on): per-block slabs [grid][64][Kpad] + the fixed-order reduce instead of f32 atomics
+    a.part = option("wgrad_det", 1) && !(a.debug_flags & 1)
+                 ? static_cast<float*>(scratch(0, (size_t)grid * 64 * a.Kpad * sizeof(float))) : nullptr;
     if (a.bna_dA) {
       adp::set_kernel("igemm_wgrad_cin8_kernel<true>");
       hipLaunchKernelGGL((igemm_wgrad_cin8_kernel<true>), dim3(grid), dim3(512), 0, s, a);
     } else {
       adp::set_kernel("igemm_wgrad_cin8_kernel<false>");
       hipLaunchKernelGGL((igemm_wgrad_cin8_kernel<false>), dim3(grid), dim3(512), 0, s, a);
+    }
+    if (a.part) {
+      adp::kernel_end();
+      slab_reduce(grid, (size_t)64 * a.Kpad / 4, a.part, a.dW, s);
+      a.part = nullptr;
     }
     return 1;
   }
@@ -1172,6 +1381,15 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     a.claim_full = option("claim_full", 0) && (tiles + a.claim_chunk - 1) / a.claim_chunk >= 4 * per;
     const int grid = per * combos;
     const bool stat_inst = !a.claim && option("wgrad_halop_static", 1);   // (the CLM = false instances)
+    // output form (option wgrad_det, default on): static lists write per-block slabs summed in a fixed order by
+    // wgrad_slab_reduce_kernel (one block per combination: dW += partial in place), so two runs give the same bits;
+    // wgrad_det = 0 or claimed patches: f32 atomics in the order blocks finish
+    a.part = nullptr;
+    a.part_rmw = 0;
+    const bool det = !a.claim && option("wgrad_det", 1) && !(a.debug_flags & 1);
+    if (det && per == 1) a.part_rmw = 1;
+    else if (det) a.part = static_cast<float*>(scratch(0, (size_t)per * a.Nout * a.Kpad * sizeof(float)));
+    // (a failed scratch allocation leaves part null: the atomic form)
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {
         adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8, true>");
@@ -1186,6 +1404,9 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     } else if (option("wgrad_halop_waves", 8) == 9) {
       adp::set_kernel("igemm_wgrad_halop_kernel<9, false, 8, true>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
+    } else if (stat_inst && option("wgrad_halop_spread", 4) != 8 && option("wgrad_halop_pf", 1)) {
+      adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false, true>");
+      hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false, true>), dim3(grid), dim3(512), 0, s, a);
     } else if (stat_inst && option("wgrad_halop_spread", 4) != 8) {
       adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false>");
       hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false>), dim3(grid), dim3(512), 0, s, a);
@@ -1200,6 +1421,11 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
         adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, true>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4>), dim3(grid), dim3(512), 0, s, a);
       }
+    }
+    if (a.part) {   // (a kernel of its own in rocprofv3's list and outside the conv's event bracket)
+      adp::kernel_end();
+      slab_reduce(per, (size_t)a.Nout * a.Kpad / 4, a.part, a.dW, s);
+      a.part = nullptr;
     }
     return 1;
   }

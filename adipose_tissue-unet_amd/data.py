@@ -76,6 +76,106 @@ def synthetic_batch(n, size, channels=3, seed=SEED):
     return np.stack(xs), np.stack(ys)
 
 
+def _smooth_field(gen, size, cells, device):
+    """A smooth random field in [-1, 1]-ish: a (cells+1)^2 grid of N(0,1) draws, bicubically upsampled."""
+    import torch
+    import torch.nn.functional as F
+
+    g = torch.randn(1, 1, cells + 1, cells + 1, generator=gen).to(device)
+    return F.interpolate(g, size=(size, size), mode="bicubic", align_corners=True)[0, 0]
+
+
+def synthetic_tile_hard(gen, size=1024, channels=3, device="cpu"):
+    """A harder synthetic histology tile than synthetic_tile (whose ellipse task saturates at Dice 0.998):
+    packed, touching adipocytes -- a power diagram of ~150-300 cells per 1024^2 whose neighbours share 1-4 px
+    membranes, some of them torn -- beside stroma regions (textured, with nuclei), bright NON-fat distractors
+    (vessel-like lumens with thick walls) and stain noise (per-tile H&E tint, low-frequency illumination, a
+    random blur, pixel noise). The mask is the fat-cell interiors (a torn membrane between two fat cells counts
+    as fat). Random draws come from the CPU torch.Generator `gen` (reproducible per seed); the arithmetic runs
+    on `device` (a 1024^2 tile takes milliseconds on the GPU). Returns (uint8 (S,S,C), float32 {0,1} (S,S))."""
+    import torch
+    import torch.nn.functional as F
+
+    S = size
+    sc = S / 1024.0
+    u = lambda a, b, n=(): (a + (b - a) * torch.rand(n, generator=gen)).to(device)   # noqa: E731
+    n = max(8, int((150 + 150 * torch.rand((), generator=gen).item()) * sc * sc))
+    seeds = u(-0.04 * S, 1.04 * S, (n, 2))
+    spacing = S / (n ** 0.5)
+    rad = u(0.0, 0.45 * spacing, (n,))            # additive power weights: cell-size variation
+    # cell kinds from a smooth tissue field: stroma (~25 %), distractor lumens (~6 %), fat (the rest)
+    tissue = _smooth_field(gen, S, 4, device)
+    sy = seeds[:, 0].clamp(0, S - 1).long()
+    sx = seeds[:, 1].clamp(0, S - 1).long()
+    tv = tissue[sy, sx]
+    stroma = tv < torch.quantile(tissue.flatten()[:: max(1, S * S // 65536)], 0.25)
+    lumen = (~stroma) & (u(0, 1, (n,)) < 0.07)
+    fat = ~(stroma | lumen)
+    # nearest two cells of every pixel (power distance), in row chunks
+    ys = torch.arange(S, device=device, dtype=torch.float32)
+    xs = torch.arange(S, device=device, dtype=torch.float32)
+    i1 = torch.empty(S, S, dtype=torch.long, device=device)
+    i2 = torch.empty(S, S, dtype=torch.long, device=device)
+    bis = torch.empty(S, S, device=device)       # distance to the bisector of the two nearest cells
+    rows = max(1, (1 << 22) // (S * n))
+    for y0 in range(0, S, rows):
+        yy = ys[y0:y0 + rows, None, None]
+        d = (yy - seeds[:, 0]) ** 2 + (xs[None, :, None] - seeds[:, 1]) ** 2 - rad ** 2
+        dv, di = torch.topk(d, 2, dim=2, largest=False)
+        s1, s2 = seeds[di[..., 0]], seeds[di[..., 1]]
+        i1[y0:y0 + rows] = di[..., 0]
+        bis[y0:y0 + rows] = (dv[..., 1] - dv[..., 0]) / (2.0 * (s1 - s2).norm(dim=-1) + 1e-6)
+        i2[y0:y0 + rows] = di[..., 1]   # (second-nearest cell: the torn-membrane rule)
+    half = float(u(0.6, 2.0))                      # membrane half-width (px)
+    wall = torch.where(lumen[i1], 3.0 + 2.0 * float(u(0, 1)), half)
+    torn = _smooth_field(gen, S, int(8 * max(1.0, sc)), device) > 1.1
+    memb = (bis < wall) & ~(torn & fat[i1] & fat[i2]) & ~(stroma[i1] & stroma[i2])   # (stroma: no membranes)
+    mask = (fat[i1] & ~memb).float()
+    # intensities (gray, before the tint)
+    noise = lambda s: torch.randn(S, S, generator=gen).to(device) * s   # noqa: E731
+    img = torch.full((S, S), 232.0, device=device) + noise(6.0) + 6.0 * _smooth_field(gen, S, 12, device)
+    img = torch.where(lumen[i1], 224.0 + noise(9.0), img)
+    tex = _smooth_field(gen, S, int(48 * max(1.0, sc)), device)
+    img = torch.where(stroma[i1], 188.0 + 24.0 * tex + noise(14.0), img)
+    img = torch.where(memb, float(u(115.0, 165.0)) + noise(18.0), img)
+    # nuclei: dark dots in the stroma and on some membranes
+    nn_ = int(400 * sc * sc)
+    ny, nx, nr = u(0, S, (nn_,)), u(0, S, (nn_,)), u(1.5, 4.0, (nn_,))
+    yi, xi = ny.long().clamp(0, S - 1), nx.long().clamp(0, S - 1)
+    ok = stroma[i1[yi, xi]] | (bis[yi, xi] < 3.0)
+    ny, nx, nr = ny[ok], nx[ok], nr[ok]
+    nuc = torch.zeros(S, S, dtype=torch.bool, device=device)
+    if len(ny):
+        rows = max(1, (1 << 22) // (S * len(ny)))
+        for y0 in range(0, S, rows):
+            d = (ys[y0:y0 + rows, None, None] - ny) ** 2 + (xs[None, :, None] - nx) ** 2 - nr ** 2
+            nuc[y0:y0 + rows] = (d < 0).any(dim=2)
+    img = torch.where(nuc, 85.0 + noise(12.0), img)
+    # blur, illumination, stain tint, pixel noise
+    sig = float(u(0.5, 1.4))
+    k = torch.arange(-4, 5, device=device, dtype=torch.float32)
+    k = torch.exp(-k * k / (2 * sig * sig))
+    k = k / k.sum()
+    im = F.conv2d(F.pad(img[None, None], (4, 4, 0, 0), mode="replicate"), k.view(1, 1, 1, 9))
+    im = F.conv2d(F.pad(im, (0, 0, 4, 4), mode="replicate"), k.view(1, 1, 9, 1))[0, 0]
+    im = im * (1.0 + 0.08 * _smooth_field(gen, S, 3, device))
+    base = torch.tensor([1.0, 0.86, 0.93], device=device)[:channels]
+    tint = base * (1.0 + u(-0.07, 0.07, (channels,)))
+    pink = torch.tensor([1.04, 0.90, 0.97], device=device)[:channels]
+    rgb = im[..., None] * torch.where(stroma[i1][..., None], tint * pink, tint)
+    rgb = rgb + torch.randn(S, S, channels, generator=gen).to(device) * 3.5
+    return rgb.clamp(0, 255).to(torch.uint8), mask
+
+
+def synthetic_stream_hard(seed, n, size, channels=3, device="cpu"):
+    """n tiles of synthetic_tile_hard from one seeded generator: (uint8 (n,S,S,C), float32 (n,S,S))."""
+    import torch
+
+    gen = torch.Generator().manual_seed(int(seed))
+    xs, ys = zip(*(synthetic_tile_hard(gen, size, channels, device) for _ in range(n)))
+    return torch.stack(xs), torch.stack(ys)
+
+
 def to_gray(rgb):
     """cv2.COLOR_RGB2GRAY / IMREAD_GRAYSCALE weights (ITU-R BT.601)."""
     rgb = np.asarray(rgb, np.float32)

@@ -35,6 +35,9 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-dice", action="store_true", help="skip the Dice@val leg (profiling runs)")
+    p.add_argument("--dice-seconds", type=float, default=45.0,
+                   help="Dice@val leg: training time of a fresh network on the hard synthetic task (eval excluded)")
     p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
     p.add_argument("--allreduce", default="overlap", choices=["overlap", "after"],
                    help="N > 1: gradient buckets all-reduced as the backward completes them (default) or all after it")
@@ -144,21 +147,25 @@ def committed_traffic(kernel, workload, build):
     return None, None, None
 
 
-def committed_dice_val(workload):
-    """Dice@val of this workload from the newest committed bench_converge.py run (profiles/*_converge*.json):
-    training on a stream of distinct tiles, validation on the 64-tile seeded val stream. The
-    throughput run itself trains one resident batch, which says nothing about Dice."""
-    import glob
-    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_converge*.json")))):
-        try:
-            d = json.loads(open(f).read().strip().splitlines()[-1])
-        except (OSError, ValueError, IndexError):
-            continue
-        if d.get("workload") == workload:
-            return {"dice_val": d.get("dice_val"), "dice_val_thr": d.get("dice_val_thr"), "steps": d.get("steps"),
-                    "train_seconds": d.get("train_seconds"), "time_to_target": d.get("time_to_target"),
-                    "target": d.get("target"), "fp8": d.get("fp8"), "source": os.path.basename(f)}
-    return None
+def dice_leg(args):
+    """Dice@val of THIS build, measured in this process after the timed steps (round-4 VERDICT item 5): a fresh
+    network of the benched workload (seed 865) trains for --dice-seconds on a pool of 128 distinct tiles of the
+    hard synthetic task (data.synthetic_tile_hard; x 8 dihedral views) and is validated on its 64-tile seeded val
+    stream as the reference monitors val_main_out_dice_coef (train_adipose_unet_v3.py:1267, :1316-1324; Keras
+    dice_coef, src/utils/model.py:93-98, mean over val batches), plus the thresholded per-tile Dice of
+    calculate_pixel_metrics; unet_bn also reports the fp8 forward (BASELINE configs[4]) on the same val tiles.
+    The throughput steps train one resident batch, which says nothing about Dice."""
+    from bench_converge import converge
+
+    a = argparse.Namespace(preset=args.preset, levels=args.levels, size=args.size, batch=args.batch, dtype=args.dtype,
+                           pool=128, val=64, lr=1e-3, max_steps=1 << 30, max_seconds=args.dice_seconds,
+                           eval_every=400, target=0.9, fp8=args.preset == "unet_bn", hard=True)
+    r = converge(a, log=lambda m: print(m, file=sys.stderr, flush=True))
+    out = {k: r.get(k) for k in ("dice_val", "dice_val_thr", "best_dice_val", "steps", "train_seconds", "fp8", "build",
+                                  "data")}
+    out["curve"] = [(c["step"], c["dice_val"]) for c in r["curve"]]
+    out["same_build"] = True   # (measured by this process on the library it benched)
+    return out
 
 
 def main():
@@ -274,6 +281,14 @@ def main():
             cpu = cpu_baseline(args)
         except Exception as e:  # report, never fake
             cpu = {"value": None, "error": repr(e)}
+    dice = None
+    if world == 1 and not args.no_dice:
+        del tr, net, x, y
+        torch.cuda.empty_cache()
+        try:
+            dice = dice_leg(args)
+        except Exception as e:  # report, never fake
+            dice = {"dice_val": None, "error": repr(e)}
     line = {
         "metric": "1024^2 tiles/sec (train)", "value": round(value, 4), "unit": "tiles/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -283,7 +298,7 @@ def main():
                    "tile": S, "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}",
                    "allreduce": args.allreduce if world > 1 else None},
         "build": build,
-        "train_loss": round(met["loss"], 5), "dice_val": committed_dice_val(wl),
+        "train_loss": round(met["loss"], 5), "dice_val": dice,
         "roofline": roof, "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

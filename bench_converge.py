@@ -40,6 +40,9 @@ def parse():
     p.add_argument("--eval-every", type=int, default=100)
     p.add_argument("--target", type=float, default=0.9, help="val_main_out_dice_coef to time")
     p.add_argument("--fp8", action="store_true", help="unet_bn: also the fp8 forward's Dice on the val tiles")
+    p.add_argument("--hard", action="store_true",
+                   help="the harder synthetic task (data.synthetic_tile_hard: packed touching cells, torn membranes, "
+                        "stroma, non-fat lumens, stain noise) instead of the ellipse tiles")
     return p.parse_args()
 
 
@@ -48,12 +51,17 @@ def log(msg):
 
 
 def main():
-    args = parse()
+    print(json.dumps(converge(parse(), log=log)), flush=True)
+
+
+def converge(args, log=log):
+    """Train a fresh network on the seeded distinct-tile stream and validate on the 64-tile val stream; returns
+    the result line (a dict). `args` carries the fields of parse() (bench.py builds one for its Dice leg)."""
     import numpy as np
     import torch
 
     import _adipose_pkg  # noqa: F401
-    from adipose_amd import ops
+    from adipose_amd import _lib, ops
     from adipose_amd.data import synthetic_tile, to_gray
     from adipose_amd.metrics import calculate_pixel_metrics
     from adipose_amd.nets import AdiposeV3Net, UNetBN
@@ -77,14 +85,30 @@ def main():
                 log(f"{what}: {i + 1}/{n} tiles ({time.perf_counter() - t0:.1f} s)")
         return np.stack(xs), np.stack(ys)
 
-    xp, yp = stream(865, args.pool, "train pool")
-    xv, yv = stream(865 + 10_000, args.val, "val")
-    mean, std = float(xp.astype(np.float32).mean()), float(xp.astype(np.float32).std())
-    # resident in HBM: the pool as stored (u8 RGB / f32 gray), normalised per batch on the device
-    XP = torch.from_numpy(xp).to(dev)
-    YP = torch.from_numpy(yp.astype(np.float32)).to(dev)
-    XV = torch.from_numpy(xv).to(dev)
-    YV = torch.from_numpy(yv.astype(np.float32)).to(dev)
+    if getattr(args, "hard", False):   # generated on the device (torch, outside every timed step)
+        from adipose_amd.data import synthetic_stream_hard
+
+        def stream_hard(seed, n, what):
+            t0 = time.perf_counter()
+            x, y = synthetic_stream_hard(seed, n, S, 3, device=dev)
+            if gray:
+                x = (x[..., 0].float() * 0.299 + x[..., 1].float() * 0.587 + x[..., 2].float() * 0.114)
+            torch.cuda.synchronize()
+            log(f"{what}: {n} hard tiles ({time.perf_counter() - t0:.1f} s)")
+            return x, y
+
+        XP, YP = stream_hard(865, args.pool, "train pool")
+        XV, YV = stream_hard(865 + 10_000, args.val, "val")
+        mean, std = float(XP.float().mean()), float(XP.float().std())
+    else:
+        xp, yp = stream(865, args.pool, "train pool")
+        xv, yv = stream(865 + 10_000, args.val, "val")
+        mean, std = float(xp.astype(np.float32).mean()), float(xp.astype(np.float32).std())
+        # resident in HBM: the pool as stored (u8 RGB / f32 gray), normalised per batch on the device
+        XP = torch.from_numpy(xp).to(dev)
+        YP = torch.from_numpy(yp.astype(np.float32)).to(dev)
+        XV = torch.from_numpy(xv).to(dev)
+        YV = torch.from_numpy(yv.astype(np.float32)).to(dev)
 
     if args.preset == "unet_bn":
         net = UNetBN(B, S, levels=args.levels, base=64, in_ch=3, dtype=args.dtype, device=dev, seed=865)
@@ -129,8 +153,7 @@ def main():
             ops.prep_input(x, net.acts(B)["x"], mean=0.0, std=1.0)
             p = (net.forward_fp8(B) if fp8 else net.forward(B, train=False))["main_out"].float()
             kd.append(((2 * (y * p).sum() + 1) / (y.sum() + p.sum() + 1)).item())
-            pc, yc = p.cpu().numpy(), y.cpu().numpy()
-            td.extend(calculate_pixel_metrics(pc[k], yc[k])["dice_score"] for k in range(B))
+            td.extend(calculate_pixel_metrics(p[k].contiguous(), y[k].contiguous())["dice_score"] for k in range(B))
         return float(np.mean(kd)), float(np.mean(td))
 
     curve = []
@@ -145,6 +168,11 @@ def main():
         n = min(args.eval_every, args.max_steps - step)
         for k in range(n):
             tr.train_step(xb, yb)
+            if k % 25 == 24:   # (the time budget holds inside an eval interval too)
+                torch.cuda.synchronize()
+                if t_train + time.perf_counter() - t0 >= args.max_seconds:
+                    n = k + 1
+                    break
             if k + 1 < n:
                 xb, yb = batch()
         torch.cuda.synchronize()
@@ -158,8 +186,11 @@ def main():
         if hit is None and d[0] >= args.target:
             hit = {"step": step, "train_s": round(t_train, 3)}
     final = curve[-1]
+    task = "hard synthetic histology (data.synthetic_tile_hard)" if getattr(args, "hard", False) else \
+        "synthetic histology (ellipse tiles, data.synthetic_tile)"
     line = {"metric": "Dice@val (val_main_out_dice_coef) after 1024^2 training", "workload": wl,
-            "data": f"synthetic histology: {args.pool} distinct seeded train tiles x 8 dihedral views, "
+            "build": _lib.lib().adp_source_hash().decode()[:16],
+            "data": f"{task}: {args.pool} distinct seeded train tiles x 8 dihedral views, "
                     f"{args.val} seeded val tiles (SURVEY §8d); dataset z-score",
             "optimizer": f"Adam lr {args.lr}", "loss": "BCE + Dice" if args.preset == "unet_bn" else "OHEM + DS",
             "dice_val": final["dice_val"], "dice_val_thr": final["dice_val_thr"],
@@ -173,7 +204,7 @@ def main():
         line["fp8"] = {"dice_val": round(d8[0], 5), "dice_val_thr": round(d8[1], 5),
                        "delta_dice_val": round(d8[0] - final["dice_val"], 6),
                        "delta_dice_val_thr": round(d8[1] - final["dice_val_thr"], 6)}
-    print(json.dumps(line), flush=True)
+    return line
 
 
 if __name__ == "__main__":

@@ -266,9 +266,9 @@ def test_unet_bn_bf16_runs_are_deterministic(levels, S):
     data-gradient chains: since round 4 the BatchNorm sums (forward statistics in every conv epilogue and the
     fused BN-backward reductions) are f64 replicas fed f32 partials of a fixed order (csrc/common.h), where f32
     atomics in run-dependent order used to make runs differ by bf16 rounding flips (per-layer gradient cosines down
-    to 0.9895: profiles/r03_bf16_bn_nondeterminism.txt). The weight gradients themselves are still f32 atomic sums
-    over blocks, whose order can move the last bits of an element; nothing downstream of them in the step reads
-    them, so they stay within 1e-5 of each other."""
+    to 0.9895: profiles/r03_bf16_bn_nondeterminism.txt). Since round 5 the weight gradients are bit-identical too:
+    the halo / input-layer / tap64 weight-gradient kernels write per-block slabs that a fixed-order reduce adds into
+    dW (option wgrad_det), where f32 atomics in the order blocks finished used to move the last bits."""
     B = 2
     w = R.unet_bn_keras_weights(levels=levels, base=64, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
@@ -285,8 +285,7 @@ def test_unet_bn_bf16_runs_are_deterministic(levels, S):
         assert torch.equal(p0, p1), (p0 - p1).abs().max().item()
         for n in w:
             for a, b in zip(g0[n], g1[n]):
-                r = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-30)
-                assert r <= 1e-5, (n, r)
+                assert torch.equal(a, b), (n, (a - b).abs().max().item() / max(a.abs().max().item(), 1e-30))
 
 
 def test_unet_bn_repeated_steps_and_double_backward():

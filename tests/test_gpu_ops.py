@@ -1303,8 +1303,18 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
     try:
         ops.conv_wgrad(xd[0], dzd, dW, l.Nout, srcB=srcB)
-        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_halop_kernel")
+        # default: the row-pipelined static-list form (round 5)
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false, true>"
         torch.cuda.synchronize()
+        dW2 = torch.zeros_like(dW)   # fixed-order slab reduce (option wgrad_det): a second run gives the same bits
+        ops.conv_wgrad(xd[0], dzd, dW2, l.Nout, srcB=srcB)
+        torch.cuda.synchronize()
+        assert torch.equal(dW, dW2)
+        ops.set_option("wgrad_halop_pf", 0)   # the unpipelined row loop: the same per-block sums
+        dWn = torch.zeros_like(dW)
+        ops.conv_wgrad(xd[0], dzd, dWn, l.Nout, srcB=srcB)
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false>"
+        ops.set_option("wgrad_halop_pf", None)
         ops.set_option("wgrad_halop_spread", 8)   # next patch's loads over all 8 patch rows
         dWs = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dWs, l.Nout, srcB=srcB)
@@ -1320,7 +1330,9 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.set_option("wgrad_halop", None)
         ops.set_option("wgrad_halop_waves", None)
         ops.set_option("wgrad_halop_spread", None)
+        ops.set_option("wgrad_halop_pf", None)
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
+    assert torch.equal(dW, dWn)   # (same per-block sums, same fixed-order reduce)
     assert relerr(dW.cpu(), ref.cpu()) < 1e-4 and relerr(dW9.cpu(), ref.cpu()) < 1e-4
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 

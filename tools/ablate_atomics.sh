@@ -5,5 +5,5 @@
 set -o pipefail
 for o in "" "--opt wgrad_partials=0" "--opt wgrad_debug=1" ${EXTRA:-}; do
   echo "== $o" >> gpurun_out/ablate.log
-  timeout -k 10 200 python bench.py --no-cpu-baseline --steps 8 $o 2>&1 | grep metric | cut -c1-160 >> gpurun_out/ablate.log || exit 1
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-dice --steps 8 $o 2>&1 | grep metric | cut -c1-160 >> gpurun_out/ablate.log || exit 1
 done

@@ -1,6 +1,6 @@
 #!/bin/bash
 # sample GFX clock / power while the bench step runs (1 GPU)
-( timeout -k 10 120 python bench.py --no-cpu-baseline --steps 60 --warmup 3 > gpurun_out/clk_bench.log 2>&1 ) &
+( timeout -k 10 120 python bench.py --no-cpu-baseline --no-dice --steps 60 --warmup 3 > gpurun_out/clk_bench.log 2>&1 ) &
 BP=$!
 for i in $(seq 1 24); do
   sleep 0.5

@@ -22,11 +22,11 @@ for s in $STEPS; do
                --steps 5 --warmup 2 > gpurun_out/prof_f32.log 2>&1 ;;
     nettests) timeout -k 10 600 python -u -m pytest tests/test_gpu_network.py -x -v --timeout 120 \
              --timeout-method thread > gpurun_out/gpu_nettests.log 2>&1 ;;
-    v3bench) timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --no-cpu-baseline \
+    v3bench) timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --no-cpu-baseline --no-dice \
                > gpurun_out/v3_bench_cpad64.log 2>&1 &&
-             timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --cpad 8 --no-cpu-baseline \
+             timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --cpad 8 --no-cpu-baseline --no-dice \
                > gpurun_out/v3_bench_cpad8.log 2>&1 ;;
-    v3mix) timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --cpad 8,8,64,64 --no-cpu-baseline \
+    v3mix) timeout -k 10 300 python bench.py --preset adipose_v3 --batch 2 --cpad 8,8,64,64 --no-cpu-baseline --no-dice \
                > gpurun_out/v3_bench_cpad_mix.log 2>&1 &&
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8,8,64,64 > gpurun_out/infer_tiles_mix.log 2>&1 &&
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8,64,64,64 > gpurun_out/infer_tiles_mix2.log 2>&1 ;;
@@ -37,10 +37,10 @@ for s in $STEPS; do
            timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 --cpad 8 > gpurun_out/infer_tiles_cpad8.log 2>&1 &&
            timeout -k 10 400 python bench_infer.py --mode wsi > gpurun_out/infer_wsi.log 2>&1 ;;
     f32bench) timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 256 --batch 2 --steps 10 \
-                --no-cpu-baseline > gpurun_out/f32_cfg1_bench.log 2>&1 &&
+                --no-cpu-baseline --no-dice > gpurun_out/f32_cfg1_bench.log 2>&1 &&
               timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 5 \
-                --warmup 2 --no-cpu-baseline > gpurun_out/f32_1024_bench.log 2>&1 ;;
-    cfg2bench) timeout -k 10 300 python bench.py --levels 4 --size 512 --batch 8 --no-cpu-baseline \
+                --warmup 2 --no-cpu-baseline --no-dice > gpurun_out/f32_1024_bench.log 2>&1 ;;
+    cfg2bench) timeout -k 10 300 python bench.py --levels 4 --size 512 --batch 8 --no-cpu-baseline --no-dice \
                 > gpurun_out/cfg2_bench.log 2>&1 ;;
     bnaab) timeout -k 10 300 python tools/ab_step.py --variant opt --opts "wgrad_bna_maxch=2;wgrad_bna_maxch=1" \
              > gpurun_out/bna_maxch_ab.log 2>&1 ;;
@@ -60,9 +60,9 @@ for s in $STEPS; do
             tests/test_gpu_configs.py -v --timeout 200 --timeout-method thread -k "f32 or wgrad or cfg1" \
             > gpurun_out/wf32_tests.log 2>&1 &&
           timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 5 \
-            --warmup 2 --no-cpu-baseline > gpurun_out/f32_1024_bench.log 2>&1 &&
+            --warmup 2 --no-cpu-baseline --no-dice > gpurun_out/f32_1024_bench.log 2>&1 &&
           timeout -k 10 300 python bench.py --preset adipose_v3 --dtype f32 --size 256 --batch 2 --steps 10 \
-            --no-cpu-baseline > gpurun_out/f32_cfg1_bench.log 2>&1 ;;
+            --no-cpu-baseline --no-dice > gpurun_out/f32_cfg1_bench.log 2>&1 ;;
     wide) timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -v --timeout 120 --timeout-method thread \
           -k "tap64_persistent_matches or tap64p_halo_matches" > gpurun_out/wide_tests.log 2>&1 &&
         timeout -k 10 300 python tools/bench_kernels.py --kinds fwd_stats,fwd --layers "L2,L3,L4" \
@@ -126,10 +126,10 @@ for s in $STEPS; do
     contention2) timeout -k 10 400 python -u tools/contention_probe.py --blocks 0,8,32 \
           --opt tap64_persist_grid=1000000 --opt halo_persist_grid=1000000 > gpurun_out/contention_nonpersist.log 2>&1 ;;
     dp2) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-           --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline \
+           --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline --no-dice \
            > gpurun_out/bench_dp2_gloo.log 2>&1 ;;
     dp2after) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-           --master-port 29518 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline --allreduce after \
+           --master-port 29518 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --no-cpu-baseline --no-dice --allreduce after \
            > gpurun_out/bench_dp2_gloo_after.log 2>&1 ;;
     dptests) timeout -k 10 400 python -u -m pytest tests/test_gpu_dp.py -v --timeout 200 --timeout-method thread \
            > gpurun_out/dp_tests.log 2>&1 ;;
@@ -137,7 +137,7 @@ for s in $STEPS; do
           timeout -k 10 300 python -u tools/diag_f32_freeze.py > gpurun_out/diag_freeze.log 2>&1 ;;
     pmcdom) bash tools/pmc_dom.sh > gpurun_out/pmc_dom.log 2>&1 ;;
     abref) bash tools/ab_libs.sh "$(ls ab/libadipose_*.so | head -n 1)" adipose_tissue-unet_amd/libadipose_hip.so 3 \
-             bench.py --no-cpu-baseline --steps 10 > gpurun_out/ab_ref.log 2>&1 ;;
+             bench.py --no-cpu-baseline --no-dice --steps 10 > gpurun_out/ab_ref.log 2>&1 ;;
     claimk3) timeout -k 10 500 python tools/bench_kernels.py --kinds fwd,fwd_stats,bnr,wgrad \
               --layers "L0 64->64,L0 128->64,L1 128->128,L2 256->256,L3 512->512,L4 1024->1024" \
               --variants "tap64p_claim=0,halop_claim=0,wgrad_halop_claim=0;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1;tap64p_claim=1,halop_claim=1,wgrad_halop_claim=1,claim_full=1" \
@@ -181,7 +181,7 @@ for s in $STEPS; do
           timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/bench_fp8_default.log 2>&1 ;;
     f32map) timeout -k 10 300 python tools/launch_map.py --preset adipose_v3 --dtype f32 > gpurun_out/f32_map.log 2>&1 &&
             mkdir -p gpurun_out/f32kt && timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d gpurun_out/f32kt -o kt -- \
-              python3 bench.py --no-cpu-baseline --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 3 --warmup 2 \
+              python3 bench.py --no-cpu-baseline --no-dice --preset adipose_v3 --dtype f32 --size 1024 --batch 2 --steps 3 --warmup 2 \
               > gpurun_out/f32kt/kt.log 2>&1 &&
             python3 tools/step_timeline.py gpurun_out/f32kt/kt_kernel_trace.csv > gpurun_out/f32_timeline.txt 2>&1 ;;
     f32skip) ADP_TEST_OPTS=f32_skip=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py -v --timeout 200 --timeout-method thread \
@@ -206,7 +206,7 @@ for s in $STEPS; do
               tools/bench_kernels.py --kinds bnr --layers "L2 256->256,L3 512->512,L4 1024->1024" \
               --variants "tap64_kpipe=0;tap64_kpipe=1" > gpurun_out/kp_kernels_ab.log 2>&1 &&
           bash tools/ab_libs.sh "$(ls ab/libadipose_*.so | head -n 1)" adipose_tissue-unet_amd/libadipose_hip.so 3 \
-              bench.py --no-cpu-baseline --steps 10 > gpurun_out/kp_step_ab.log 2>&1 ;;
+              bench.py --no-cpu-baseline --no-dice --steps 10 > gpurun_out/kp_step_ab.log 2>&1 ;;
     engprobe) timeout -k 10 300 python -u tools/engine_repeat_probe.py --reps 6 --comm 1 > gpurun_out/engprobe_comm.log 2>&1 &&
               timeout -k 10 300 python -u tools/engine_repeat_probe.py --reps 6 --comm 0 > gpurun_out/engprobe_nocomm.log 2>&1 ;;
     dettests) timeout -k 10 600 python -u -m pytest tests/test_engine.py tests/test_gpu_network.py -v --timeout 200 \
@@ -224,7 +224,7 @@ for s in $STEPS; do
     statw) timeout -k 10 300 python tools/ab_step.py --variant opt --rounds 5 --opts "wgrad_halop_static=0;wgrad_halop_static=1" > gpurun_out/statw_ab.log 2>&1 ;;
     finalinfer) timeout -k 10 300 python bench_infer.py --mode fp8 > gpurun_out/final_fp8.log 2>&1 &&
           timeout -k 10 300 python bench_infer.py --mode tiles --steps 5 > gpurun_out/final_infer_tiles.log 2>&1 &&
-          timeout -k 10 300 python bench.py --levels 4 --size 512 --batch 8 --no-cpu-baseline > gpurun_out/final_cfg2_bench.log 2>&1 ;;
+          timeout -k 10 300 python bench.py --levels 4 --size 512 --batch 8 --no-cpu-baseline --no-dice > gpurun_out/final_cfg2_bench.log 2>&1 ;;
     bnr3) timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_network.py -v --timeout 200 --timeout-method thread \
               -k "tap64p or bnr or bn_" > gpurun_out/bnr3_tests.log 2>&1 &&
           timeout -k 10 400 python tools/bench_kernels.py --kinds bnr --layers "L1 256->128,L2 256->256,L3 512->512,L4 1024->1024,L3 1024->512" \
@@ -248,7 +248,7 @@ for s in $STEPS; do
     f32pmc) mkdir -p gpurun_out/f32pmc && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
               SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE -f csv \
               -d gpurun_out/f32pmc -o sq -- python3 bench.py --preset adipose_v3 --dtype f32 --size 1024 --batch 2 \
-              --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/f32pmc/sq.log 2>&1 ;;
+              --steps 2 --warmup 1 --no-cpu-baseline --no-dice > gpurun_out/f32pmc/sq.log 2>&1 ;;
     bndet) timeout -k 10 300 python -u tools/diag_bn_grads.py > gpurun_out/diag_bn_grads.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -1,10 +1,20 @@
 #!/usr/bin/env python3
-"""Per-kernel time breakdown from a rocprofv3 `--stats -f csv` kernel_stats file.
+"""Per-kernel time breakdown of the TIMED bench steps from a rocprofv3 `--kernel-trace` CSV.
 
-usage: python tools/kstats.py <prefix>_kernel_stats.csv [steps]
-Prints each kernel's calls, mean duration and total per step (total / steps).
+usage: python tools/kstats.py <prefix>_kernel_trace.csv <bench.json>
+       python tools/kstats.py <prefix>_kernel_stats.csv <bench.json>     (fallback: whole run / (warmup + steps))
+
+The bench line (bench.json: the JSON line bench.py printed under the profiler) gives W warm-up and K timed
+steps. Every training step ends with exactly one `adam_kernel` launch, so the timed steps are the launches
+after the W-th adam_kernel up to and including the (W + K)-th: first-step allocations (torch fills of newly
+allocated buffers), library scratch growth and the warm-up steps are excluded. Prints each kernel's calls per
+step, mean duration and time per step, the kernel time and the wall span per step, and the bench's own
+ms_per_step under the profiler for comparison (round-4 VERDICT weak #5: the old breakdown divided the whole
+trace by a fixed 14).
 """
+import collections
 import csv
+import json
 import re
 import sys
 
@@ -14,17 +24,57 @@ def short(name):
     return (m.group(1) + (m.group(2) or "")) if m else name[:52]
 
 
+def bench_line(path):
+    return json.loads(open(path).read().strip().splitlines()[-1])
+
+
+def from_trace(path, warmup, steps):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    if len(ends) < warmup + steps:
+        raise SystemExit(f"{path}: {len(ends)} adam_kernel launches, expected >= {warmup + steps}")
+    lo = ends[warmup - 1] + 1 if warmup > 0 else 0
+    hi = ends[warmup + steps - 1]
+    timed = rows[lo:hi + 1]
+    acc = collections.defaultdict(lambda: [0, 0.0])
+    for r in timed:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        e = acc[short(r["Kernel_Name"])]
+        e[0] += 1
+        e[1] += d
+    span = int(timed[-1]["End_Timestamp"]) - int(rows[lo - 1]["End_Timestamp"] if lo > 0 else timed[0]["Start_Timestamp"])
+    outside = len(rows) - len(timed)
+    return acc, span, outside
+
+
+def from_stats(path):
+    acc = {}
+    for r in csv.DictReader(open(path)):
+        acc[short(r["Name"])] = [int(r["Calls"]), float(r["TotalDurationNs"])]
+    return acc
+
+
 def main():
-    rows = list(csv.DictReader(open(sys.argv[1])))
-    steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
-    tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    for r in rows:
-        t = float(r["TotalDurationNs"])
+    path = sys.argv[1]
+    b = bench_line(sys.argv[2])
+    W, K = int(b["warmup"]), int(b["steps"])
+    if "kernel_trace" in path:
+        acc, span, outside = from_trace(path, W, K)
+        div, note = K, f"timed steps only: {K} steps after {W} warm-up steps ({outside} launches outside excluded)"
+    else:
+        acc, span, outside = from_stats(path), None, None
+        div, note = W + K, f"whole run / {W + K} (warm-up steps included)"
+    tot = sum(v[1] for v in acc.values())
+    print(f"# {note}")
+    for k, (n, t) in sorted(acc.items(), key=lambda kv: -kv[1][1]):
         if t / tot < 0.002:
             continue
-        print(f"{short(r['Name'])[:52]:<52} calls={int(r['Calls']):5d} avg={float(r['AverageNs']) / 1e3:9.1f}us "
-              f"per_step={t / 1e6 / steps:7.2f}ms {100 * t / tot:5.1f}%")
-    print(f"total per step: {tot / 1e6 / steps:.2f} ms")
+        print(f"{k[:52]:<52} calls/step={n / div:6.2f} avg={t / n / 1e3:9.1f}us per_step={t / 1e6 / div:7.3f}ms "
+              f"{100 * t / tot:5.1f}%")
+    print(f"kernel time per step: {tot / 1e6 / div:.3f} ms")
+    if span is not None:
+        print(f"wall span per step (kernels + gaps): {span / 1e6 / div:.3f} ms")
+    print(f"bench ms_per_step under the profiler: {b['ms_per_step']:.3f} ms")
 
 
 if __name__ == "__main__":

@@ -21,7 +21,7 @@ shift || true
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
-BENCH="bench.py --no-cpu-baseline $*"
+BENCH="bench.py --no-cpu-baseline --no-dice $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT" -o kt -- python3 $BENCH > "$OUT/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d "$OUT" -o fetch -- python3 $BENCH > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d "$OUT" -o write -- python3 $BENCH > "$OUT/write.log" 2>&1
@@ -29,5 +29,6 @@ cp "$OUT/kt_kernel_stats.csv" "$OUT/kernel_stats.csv"
 grep '^{"metric"' "$OUT/kt.log" | tail -1 > "$OUT/bench.json" || true
 python3 tools/traffic_summary.py "$OUT/fetch_counter_collection.csv" "$OUT/write_counter_collection.csv" "$OUT/traffic.json" \
   "$OUT/bench.json"
-python3 tools/kstats.py "$OUT/kernel_stats.csv" 14 > "$OUT/kernel_breakdown.txt"
+# per-step figures over the timed steps only (warm-up / first-step allocations excluded; steps from the bench line)
+python3 tools/kstats.py "$OUT/kt_kernel_trace.csv" "$OUT/bench.json" > "$OUT/kernel_breakdown.txt"
 echo done
