@@ -87,10 +87,10 @@ def _smooth_field(gen, size, cells, device):
 
 def synthetic_tile_hard(gen, size=1024, channels=3, device="cpu"):
     """A harder synthetic histology tile than synthetic_tile (whose ellipse task saturates at Dice 0.998):
-    packed, touching adipocytes -- a power diagram of ~150-300 cells per 1024^2 whose neighbours share 1-4 px
-    membranes, some of them torn -- beside stroma regions (textured, with nuclei), bright NON-fat distractors
-    (vessel-like lumens with thick walls) and stain noise (per-tile H&E tint, low-frequency illumination, a
-    random blur, pixel noise). The mask is the fat-cell interiors (a torn membrane between two fat cells counts
+    packed, touching adipocytes -- a power diagram of ~300-900 cells per 1024^2 whose neighbours share 1-3 px
+    membranes, many of them torn -- beside stroma regions (textured, with nuclei), bright NON-fat distractors
+    (vessel-like lumens, a fifth of the non-stroma cells, whose walls are only ~1 px thicker than a membrane) and
+    stain noise (per-tile H&E tint, low-frequency illumination, a sigma 0.8-2 blur, pixel noise). The mask is the fat-cell interiors (a torn membrane between two fat cells counts
     as fat). Random draws come from the CPU torch.Generator `gen` (reproducible per seed); the arithmetic runs
     on `device` (a 1024^2 tile takes milliseconds on the GPU). Returns (uint8 (S,S,C), float32 {0,1} (S,S))."""
     import torch
@@ -99,7 +99,7 @@ def synthetic_tile_hard(gen, size=1024, channels=3, device="cpu"):
     S = size
     sc = S / 1024.0
     u = lambda a, b, n=(): (a + (b - a) * torch.rand(n, generator=gen)).to(device)   # noqa: E731
-    n = max(8, int((150 + 150 * torch.rand((), generator=gen).item()) * sc * sc))
+    n = max(8, int((300 + 600 * torch.rand((), generator=gen).item()) * sc * sc))
     seeds = u(-0.04 * S, 1.04 * S, (n, 2))
     spacing = S / (n ** 0.5)
     rad = u(0.0, 0.45 * spacing, (n,))            # additive power weights: cell-size variation
@@ -108,8 +108,8 @@ def synthetic_tile_hard(gen, size=1024, channels=3, device="cpu"):
     sy = seeds[:, 0].clamp(0, S - 1).long()
     sx = seeds[:, 1].clamp(0, S - 1).long()
     tv = tissue[sy, sx]
-    stroma = tv < torch.quantile(tissue.flatten()[:: max(1, S * S // 65536)], 0.25)
-    lumen = (~stroma) & (u(0, 1, (n,)) < 0.07)
+    stroma = tv < torch.quantile(tissue.flatten()[:: max(1, S * S // 65536)], 0.3)
+    lumen = (~stroma) & (u(0, 1, (n,)) < 0.2)
     fat = ~(stroma | lumen)
     # nearest two cells of every pixel (power distance), in row chunks
     ys = torch.arange(S, device=device, dtype=torch.float32)
@@ -126,18 +126,18 @@ def synthetic_tile_hard(gen, size=1024, channels=3, device="cpu"):
         i1[y0:y0 + rows] = di[..., 0]
         bis[y0:y0 + rows] = (dv[..., 1] - dv[..., 0]) / (2.0 * (s1 - s2).norm(dim=-1) + 1e-6)
         i2[y0:y0 + rows] = di[..., 1]   # (second-nearest cell: the torn-membrane rule)
-    half = float(u(0.6, 2.0))                      # membrane half-width (px)
-    wall = torch.where(lumen[i1], 3.0 + 2.0 * float(u(0, 1)), half)
-    torn = _smooth_field(gen, S, int(8 * max(1.0, sc)), device) > 1.1
+    half = float(u(0.5, 1.5))                      # membrane half-width (px)
+    wall = torch.where(lumen[i1], 2.0 + float(u(0, 1)), half)   # (lumen walls: only ~1 px thicker)
+    torn = _smooth_field(gen, S, int(8 * max(1.0, sc)), device) > 0.7
     memb = (bis < wall) & ~(torn & fat[i1] & fat[i2]) & ~(stroma[i1] & stroma[i2])   # (stroma: no membranes)
     mask = (fat[i1] & ~memb).float()
     # intensities (gray, before the tint)
     noise = lambda s: torch.randn(S, S, generator=gen).to(device) * s   # noqa: E731
     img = torch.full((S, S), 232.0, device=device) + noise(6.0) + 6.0 * _smooth_field(gen, S, 12, device)
-    img = torch.where(lumen[i1], 224.0 + noise(9.0), img)
+    img = torch.where(lumen[i1], 228.0 + noise(8.0), img)
     tex = _smooth_field(gen, S, int(48 * max(1.0, sc)), device)
     img = torch.where(stroma[i1], 188.0 + 24.0 * tex + noise(14.0), img)
-    img = torch.where(memb, float(u(115.0, 165.0)) + noise(18.0), img)
+    img = torch.where(memb, float(u(140.0, 190.0)) + noise(18.0), img)
     # nuclei: dark dots in the stroma and on some membranes
     nn_ = int(400 * sc * sc)
     ny, nx, nr = u(0, S, (nn_,)), u(0, S, (nn_,)), u(1.5, 4.0, (nn_,))
@@ -152,7 +152,7 @@ def synthetic_tile_hard(gen, size=1024, channels=3, device="cpu"):
             nuc[y0:y0 + rows] = (d < 0).any(dim=2)
     img = torch.where(nuc, 85.0 + noise(12.0), img)
     # blur, illumination, stain tint, pixel noise
-    sig = float(u(0.5, 1.4))
+    sig = float(u(0.8, 2.0))
     k = torch.arange(-4, 5, device=device, dtype=torch.float32)
     k = torch.exp(-k * k / (2 * sig * sig))
     k = k / k.sum()
@@ -163,7 +163,7 @@ def synthetic_tile_hard(gen, size=1024, channels=3, device="cpu"):
     tint = base * (1.0 + u(-0.07, 0.07, (channels,)))
     pink = torch.tensor([1.04, 0.90, 0.97], device=device)[:channels]
     rgb = im[..., None] * torch.where(stroma[i1][..., None], tint * pink, tint)
-    rgb = rgb + torch.randn(S, S, channels, generator=gen).to(device) * 3.5
+    rgb = rgb + torch.randn(S, S, channels, generator=gen).to(device) * 7.0
     return rgb.clamp(0, 255).to(torch.uint8), mask
 
 

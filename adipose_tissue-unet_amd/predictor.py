@@ -12,8 +12,10 @@ MI355X-first differences (same results): all TTA views of a tile run as ONE batc
 view transform is folded into adp_prep_input's load, the inverse transform + mean into adp_tta_merge),
 sliding-window tiles are read in place from the HBM-resident image, several tiles x views are batched
 per forward, and blending accumulates on the GPU (adp_blend_accum). With a torch.distributed process
-group, sliding-window positions are sharded by contiguous tile rows across ranks and the blend
-accumulators are SUM-reduced over RCCL (BASELINE.json config 4).
+group, sliding-window positions are sharded by contiguous tile rows across ranks; each rank blends its tiles
+into a ROW BAND of the frame (its tiles' rows plus the tile overlap) and the bands are added into rank 0's frame
+by point-to-point transfers in rank order (BandCanvas; SURVEY.md §8e: a reduce of row-band buffers to rank 0, RCCL
+having no gather), so no rank but 0 holds a full-frame canvas (BASELINE.json config 4).
 """
 from __future__ import annotations
 
@@ -202,6 +204,72 @@ class LinearBlender:
         return _gpu_reconstruct(self, tiles, positions, output_shape)
 
 
+def band_rows(positions, tile):
+    """Rows [y0, y1) the tiles at `positions` (top-left corners) cover; (0, 0) for none."""
+    if not positions:
+        return 0, 0
+    return min(y for y, _ in positions), max(y for y, _ in positions) + tile
+
+
+def _p2p_cpu(group):
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"   # (gloo's send / recv take host tensors)
+
+
+class BandCanvas:
+    """Blend accumulators (acc, wsum) of one (H, W) output plane, held for rows [y0, y1) only.
+
+    Sharded sliding-window inference (the path it shards is full_evaluation_enhanced.py:286-329):
+    every rank but 0 allocates just the band its tiles cover (their rows plus the tile overlap) and blends into it at
+    row offset y0; rank 0 holds the whole frame (band (0, H)). reduce_to_root() adds the other ranks' bands into
+    rank 0's frame in rank order -- one send of the 2 x band buffer per rank, received and added by rank 0 -- so the
+    sum's association depends only on the sharding (deterministic), and the result equals the one-rank canvas up to
+    f32 rounding of the different association. Full-frame worst case per rank before: 2 x H x W f32 (512 MiB at
+    8192^2); now 2 x band x W on ranks > 0."""
+
+    def __init__(self, shape, rows, device):
+        H, W = int(shape[0]), int(shape[1])
+        self.H, self.W = H, W
+        self.y0, self.y1 = int(rows[0]), int(max(rows[0], rows[1]))
+        self.buf = torch.zeros((2, self.y1 - self.y0, W), dtype=torch.float32, device=device)
+        self.acc, self.ws = self.buf[0], self.buf[1]
+
+    def add(self, tile, weight, y, x):
+        ops.blend_accum(tile, weight, self.acc, self.ws, y - self.y0, x)
+
+    def reduce_to_root(self, group, bands):
+        """bands[q]: rows (y0, y1) of rank q's band (rank 0: its frame). Returns True on rank 0, whose (acc, ws)
+        then hold the sums over all ranks; the other ranks send their band and return False."""
+        import torch.distributed as dist
+        r, n = dist.get_rank(group), dist.get_world_size(group)
+        host = _p2p_cpu(group)
+        if r != 0:
+            if self.y1 > self.y0:
+                dist.send(self.buf.cpu() if host else self.buf, dist.get_global_rank(group, 0), group=group)
+            return False
+        if (self.y0, self.y1) != (0, self.H):
+            raise ValueError("rank 0's canvas must cover the whole frame")
+        for q in range(1, n):
+            y0, y1 = int(bands[q][0]), int(bands[q][1])
+            if y1 <= y0:
+                continue
+            tmp = torch.empty((2, y1 - y0, self.W), dtype=torch.float32, device="cpu" if host else self.buf.device)
+            dist.recv(tmp, dist.get_global_rank(group, q), group=group)
+            tmp = tmp.to(self.buf.device)
+            for k in range(2):
+                dst = self.buf[k, y0:y1]
+                if dst.is_cuda and dst.numel() % 8 == 0:
+                    ops.add_mask(dst, dst, b=tmp[k])
+                else:
+                    dst.add_(tmp[k])
+        return True
+
+    def finalize(self, floor_):
+        out = torch.empty_like(self.acc)
+        ops.blend_finalize(self.acc, self.ws, out, floor_)
+        return out
+
+
 def _gpu_reconstruct(blender, tiles, positions, output_shape):
     dev = torch.device("cuda", torch.cuda.current_device())
     h, w = output_shape
@@ -252,12 +320,12 @@ class SlidingWindowInference:
         T = self.tile_size
         return [image[y:y + T, x:x + T] for y, x in pos], pos
 
-    def shard(self, positions):
+    def shard(self, positions, rank=None):
         """Contiguous runs of tile positions per rank (tile rows stay together)."""
         if self.group is None:
             return positions
         import torch.distributed as dist
-        r, n = dist.get_rank(self.group), dist.get_world_size(self.group)
+        r, n = dist.get_rank(self.group) if rank is None else rank, dist.get_world_size(self.group)
         per = math.ceil(len(positions) / n)
         return positions[r * per:(r + 1) * per]
 
@@ -272,8 +340,14 @@ class SlidingWindowInference:
         positions = self.extract_tile_positions((h, w))
         mine = self.shard(positions)
         views = TTA_VIEWS[(tta_mode or "basic").lower()] if use_tta else [0]
-        acc = torch.zeros((h, w), dtype=torch.float32, device=dev)
-        ws = torch.zeros((h, w), dtype=torch.float32, device=dev)
+        bands = None
+        if self.group is None:
+            canvas = BandCanvas((h, w), (0, h), dev)
+        else:   # rank 0: the frame; others: the row band of their tiles
+            import torch.distributed as dist
+            n = dist.get_world_size(self.group)
+            bands = [(0, h)] + [band_rows(self.shard(positions, q), T) for q in range(1, n)]
+            canvas = BandCanvas((h, w), bands[dist.get_rank(self.group)], dev)
         wmap = self.blender.device_weights(dev, T, T)
         per = max(1, getattr(model, "max_batch", 8) // len(views))
         for i0 in range(0, len(mine), per):
@@ -281,11 +355,8 @@ class SlidingWindowInference:
             tiles = [img[y:y + T, x:x + T] for y, x in chunk]
             probs = model.predict_views(tiles, mean, std, views)
             for (y, x), p in zip(chunk, probs):
-                ops.blend_accum(p, wmap, acc, ws, y, x)
-        if self.group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(acc, group=self.group)
-            dist.all_reduce(ws, group=self.group)
-        out = torch.empty_like(acc)
-        ops.blend_finalize(acc, ws, out, self.blender.floor)
+                canvas.add(p, wmap, y, x)
+        if self.group is not None and not canvas.reduce_to_root(self.group, bands):
+            return None   # (the blended frame lives on rank 0 only)
+        out = canvas.finalize(self.blender.floor)
         return out if return_device else out.cpu().numpy()

@@ -35,7 +35,8 @@ import torch
 from . import ops
 from .evaluation import (BoundaryRefiner, _add_weighted, calculate_pixel_metrics, load_training_stats,
                          set_deterministic_seeds)
-from .predictor import TTA_VIEWS, AdiposeUNet, GaussianBlender, LinearBlender, TestTimeAugmentation
+from .predictor import (TTA_VIEWS, AdiposeUNet, BandCanvas, GaussianBlender, LinearBlender, TestTimeAugmentation,
+                        band_rows)
 
 __all__ = ["parse_tile_filename", "group_tiles_by_slide", "get_source_image_dimensions",
            "infer_full_image_dimensions", "get_full_image_dimensions", "find_missing_tiles",
@@ -149,34 +150,32 @@ def _read_gt(path):
 
 
 class _Canvas:
-    """Device blend accumulators of one output plane (GaussianBlender / LinearBlender.reconstruct)."""
+    """Device blend accumulators of one output plane (GaussianBlender / LinearBlender.reconstruct), held as a row
+    band (predictor.BandCanvas): with a process group, rank 0 holds the frame and the other ranks the band of their
+    tiles, added into rank 0's frame by result()."""
 
-    def __init__(self, blender, shape, dev):
-        self.blender, self.dev = blender, dev
-        self.acc = torch.zeros(shape, dtype=torch.float32, device=dev)
-        self.ws = torch.zeros(shape, dtype=torch.float32, device=dev)
+    def __init__(self, blender, shape, dev, bands=None, rank=0):
+        self.blender, self.dev, self.bands = blender, dev, bands
+        self.c = BandCanvas(shape, (0, shape[0]) if bands is None else bands[rank], dev)
 
     def add(self, tile, y, x):
         T = tile.shape[-1]
         if tile.shape[-2] != T:
             raise ValueError("blend tiles must be square")
-        ops.blend_accum(tile, self.blender.device_weights(self.dev, T, T), self.acc, self.ws, y, x)
+        self.c.add(tile, self.blender.device_weights(self.dev, T, T), y, x)
 
     def result(self, group=None):
-        if group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(self.acc, group=group)
-            dist.all_reduce(self.ws, group=group)
-        out = torch.empty_like(self.acc)
-        ops.blend_finalize(self.acc, self.ws, out, self.blender.floor)
-        return out
+        """The blended plane (on rank 0 with a process group; None on the other ranks)."""
+        if group is not None and not self.c.reduce_to_root(group, self.bands):
+            return None
+        return self.c.finalize(self.blender.floor)
 
 
-def _shard(items, group):
+def _shard(items, group, rank=None):
     if group is None:
         return 0, len(items)
     import torch.distributed as dist
-    r, n = dist.get_rank(group), dist.get_world_size(group)
+    r, n = dist.get_rank(group) if rank is None else rank, dist.get_world_size(group)
     per = math.ceil(len(items) / n)
     return min(r * per, len(items)), min((r + 1) * per, len(items))
 
@@ -197,15 +196,26 @@ def reconstruct_slide(model, tiles_info: List[Tuple], full_shape: Tuple[int, int
     views = TTA_VIEWS[(tta_mode or "basic").lower() if (tta_mode or "basic").lower() in TTA_VIEWS else "basic"] \
         if use_tta else [0]
     lo, hi = _shard(tiles_info, process_group)
-    pred_c = _Canvas(blender, (H, W), dev)
-    rgb_c = [_Canvas(blender, (H, W), dev) for _ in range(3)]
-    gt_c = _Canvas(blender, (H, W), dev)
     # GT tiles pair with positions in order of appearance (zip over the GT list)
     gt_rank = []
     n_gt = 0
     for _, _, _, m in tiles_info:
         gt_rank.append(n_gt if m is not None else -1)
         n_gt += m is not None
+    # row bands of every rank (rank 0: the frame): its tiles' rows, and the rows of the positions its GT tiles go to
+    bands = gt_bands = None
+    rank = 0
+    if process_group is not None:
+        import torch.distributed as dist
+        rank, n = dist.get_rank(process_group), dist.get_world_size(process_group)
+        bands, gt_bands = [(0, H)], [(0, H)]
+        for q in range(1, n):
+            a, b = _shard(tiles_info, process_group, q)
+            bands.append(band_rows(positions[a:b], tile_size))
+            gt_bands.append(band_rows([positions[gt_rank[i]] for i in range(a, b) if gt_rank[i] >= 0], tile_size))
+    pred_c = _Canvas(blender, (H, W), dev, bands, rank)
+    rgb_c = [_Canvas(blender, (H, W), dev, bands, rank) for _ in range(3)]
+    gt_c = _Canvas(blender, (H, W), dev, gt_bands, rank)
     batched = hasattr(model, "predict_views")
     per = max(1, getattr(model, "max_batch", 8) // len(views)) if batched else 1
     for i0 in range(lo, hi, per):
@@ -235,8 +245,11 @@ def reconstruct_slide(model, tiles_info: List[Tuple], full_shape: Tuple[int, int
                 gy, gx = positions[gt_rank[i]]
                 gt_c.add(torch.from_numpy(np.ascontiguousarray(_read_gt(m), dtype=np.float32)).to(dev), gy, gx)
     full_pred = pred_c.result(process_group)
-    full_rgb = torch.stack([c.result(process_group) for c in rgb_c], dim=-1)
+    rgbs_ = [c.result(process_group) for c in rgb_c]
     full_gt = gt_c.result(process_group) if n_gt else None
+    if full_pred is None:   # (a rank > 0: the planes live on rank 0)
+        return None, None, None
+    full_rgb = torch.stack(rgbs_, dim=-1)
     if return_device:
         return full_rgb, full_pred, full_gt
     return (full_rgb.cpu().numpy(), full_pred.cpu().numpy(), None if full_gt is None else full_gt.cpu().numpy())

@@ -235,10 +235,17 @@ def main():
     t1 = time.perf_counter()
     ops.set_launch_timer(None)
     elapsed = t1 - t0
-    if world > 1:
+    comm = None
+    if world > 1:   # max over ranks; the per-rank times and the communicator's own rank count go into the line
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        per_rank = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(per_rank, t)
+        ones = torch.ones(1, device=dev)
+        dist.all_reduce(ones)   # (a live check: the sum over the communicator's ranks)
+        comm = {"backend": dist.get_backend(), "ranks": dist.get_world_size(), "allreduce_check": int(ones.item()),
+                "per_rank_ms_per_step": [round(v.item() / args.steps * 1e3, 3) for v in per_rank]}
+        elapsed = max(v.item() for v in per_rank)
+        world = dist.get_world_size()
     met = tr.read_metrics()
 
     summ = timer.summary()
@@ -297,6 +304,7 @@ def main():
         "config": {"workload": wl, "preset": args.preset, "levels": args.levels if args.preset == "unet_bn" else 4,
                    "tile": S, "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}",
                    "allreduce": args.allreduce if world > 1 else None},
+        "comm": comm,
         "build": build,
         "train_loss": round(met["loss"], 5), "dice_val": dice,
         "roofline": roof, "cpu_baseline": cpu,

@@ -223,7 +223,7 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    checksum = float(out.double().sum().item())
+    checksum = float(out.double().sum().item()) if out is not None else None   # (wsi: the frame is on rank 0)
     summ = timer.summary()
     if rank == 0:
         dom = max(summ.items(), key=lambda kv: kv[1][2])

@@ -165,3 +165,54 @@ def test_sliding_window_shards_cover_positions():
     got = [p for r in range(WORLD) for p in res[r]["mine"]]
     assert got == list(allpos)                         # disjoint, contiguous, complete, in order
     assert all(len(res[r]["mine"]) > 0 for r in range(WORLD))
+
+
+# ------------------------------------------------------------------------------- row-band reduce to rank 0
+def _tile(y, x, T):
+    g = torch.Generator().manual_seed(1000 * y + x)
+    return torch.rand(T, T, generator=g)
+
+
+def _accum(c, tile, w, y, x):
+    """blend_accum's arithmetic (acc += w * p, wsum += w) on a CPU BandCanvas (the kernel needs a GPU)."""
+    T = tile.shape[-1]
+    c.acc[y - c.y0:y - c.y0 + T, x:x + T] += w * tile
+    c.ws[y - c.y0:y - c.y0 + T, x:x + T] += w
+
+
+def _band_fn(rank, world):
+    import _adipose_pkg  # noqa: F401
+    from adipose_amd.predictor import BandCanvas, GaussianBlender, SlidingWindowInference, band_rows
+
+    H, W, T = 320, 288, 64
+    sw = SlidingWindowInference(tile_size=T, overlap=0.5, process_group=dist.group.WORLD, verbose=False)
+    pos = sw.extract_tile_positions((H, W))
+    bands = [(0, H)] + [band_rows(sw.shard(pos, q), T) for q in range(1, world)]
+    c = BandCanvas((H, W), bands[rank], "cpu")
+    w = torch.from_numpy(GaussianBlender(T).weight_map)
+    for y, x in sw.shard(pos):
+        _accum(c, _tile(y, x, T), w, y, x)
+    root = c.reduce_to_root(dist.group.WORLD, bands)
+    return {"root": root, "rows": c.y1 - c.y0, "acc": c.acc.clone() if root else None,
+            "ws": c.ws.clone() if root else None}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_band_reduce_to_root_matches_one_canvas(world):
+    """predictor.BandCanvas: ranks > 0 hold only the rows of their tiles; rank 0 adds their bands in rank order and
+    gets the one-canvas blend sums (full_evaluation_enhanced.py:286-329) within f32 rounding of the association."""
+    import _adipose_pkg  # noqa: F401
+    from adipose_amd.predictor import BandCanvas, GaussianBlender, SlidingWindowInference
+
+    res = run_ranks(_band_fn, world)
+    H, W, T = 320, 288, 64
+    sw = SlidingWindowInference(tile_size=T, overlap=0.5, verbose=False)
+    ref = BandCanvas((H, W), (0, H), "cpu")
+    w = torch.from_numpy(GaussianBlender(T).weight_map)
+    for y, x in sw.extract_tile_positions((H, W)):
+        _accum(ref, _tile(y, x, T), w, y, x)
+    assert res[0]["root"] and res[0]["rows"] == H
+    np.testing.assert_allclose(res[0]["acc"], ref.acc.numpy(), rtol=0, atol=2e-6)
+    np.testing.assert_allclose(res[0]["ws"], ref.ws.numpy(), rtol=0, atol=2e-6)
+    for r in range(1, world):
+        assert not res[r]["root"] and 0 < res[r]["rows"] < H

@@ -9,8 +9,9 @@ process group (the collectives run on CUDA tensors through gloo; RCCL is the sam
   ready hooks (trainer.GradBuckets). Per-layer gradients must match the single-device ones to f32 tolerance
   and the post-Adam weights to Adam's sign tolerance (dropout off: its stateless mask is keyed by the
   rank-local element index).
-* SlidingWindowInference(process_group=...) on a small image: tile rows sharded over the ranks, the blend
-  canvases SUM-all-reduced, equal to the one-process output (full_evaluation_enhanced.py:286-329)."""
+* SlidingWindowInference(process_group=...) on a small image at world 2 and 4: tile rows sharded over the ranks,
+  each rank > 0 blending into a row band of the frame only, the bands added into rank 0's frame (BandCanvas),
+  equal to the one-process output (full_evaluation_enhanced.py:286-329)."""
 import os
 import socket
 import sys
@@ -156,19 +157,34 @@ def _sw_predictor():
 def _sw_fn(rank, world):
     import torch.distributed as dist
 
-    from adipose_amd.predictor import SlidingWindowInference
-    sw = SlidingWindowInference(64, 0.5, "gaussian", process_group=dist.group.WORLD, verbose=False)
+    from adipose_amd import predictor as P
+    sw = P.SlidingWindowInference(64, 0.5, "gaussian", process_group=dist.group.WORLD, verbose=False)
     pos = sw.extract_tile_positions((320, 288))
-    out = sw.predict_with_sliding_window(_sw_image(), _sw_predictor(), 127.0, 50.0, use_tta=True, tta_mode="basic")
-    return {"out": out, "mine": len(sw.shard(pos)), "all": len(pos)}
+    rows = []   # the canvas rows this rank allocates (BandCanvas.__init__)
+    orig = P.BandCanvas.__init__
+
+    def spy(self, shape, band, device):
+        orig(self, shape, band, device)
+        rows.append(self.y1 - self.y0)
+    P.BandCanvas.__init__ = spy
+    try:
+        out = sw.predict_with_sliding_window(_sw_image(), _sw_predictor(), 127.0, 50.0, use_tta=True,
+                                             tta_mode="basic")
+    finally:
+        P.BandCanvas.__init__ = orig
+    return {"out": out, "mine": len(sw.shard(pos)), "all": len(pos), "rows": rows}
 
 
-def test_dp_sliding_window_world2_matches_one_rank():
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_sliding_window_bands_match_one_rank(world):
     from adipose_amd.predictor import SlidingWindowInference
-    res = run_ranks(_sw_fn)
+    res = run_ranks(_sw_fn, world)
     sw = SlidingWindowInference(64, 0.5, "gaussian", verbose=False)
     ref = sw.predict_with_sliding_window(_sw_image(), _sw_predictor(), 127.0, 50.0, use_tta=True, tta_mode="basic")
-    assert res[0]["mine"] + res[1]["mine"] == res[0]["all"] and min(res[0]["mine"], res[1]["mine"]) > 0
-    for r in range(WORLD):
-        # the canvases are summed in a different order (rank partial sums), so allow f32 rounding
-        np.testing.assert_allclose(res[r]["out"], ref, rtol=0, atol=2e-6)
+    assert sum(res[r]["mine"] for r in range(world)) == res[0]["all"] and min(res[r]["mine"] for r in range(world)) > 0
+    # the bands are summed in a different association (rank partial sums), so allow f32 rounding
+    np.testing.assert_allclose(res[0]["out"], ref, rtol=0, atol=2e-6)
+    assert res[0]["rows"] == [320]
+    for r in range(1, world):
+        assert res[r]["out"] is None   # (the frame lives on rank 0)
+        assert len(res[r]["rows"]) == 1 and res[r]["rows"][0] < 320, res[r]["rows"]   # a band, not the frame
