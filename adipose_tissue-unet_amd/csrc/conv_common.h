@@ -165,26 +165,22 @@ ADP_DEV int claim_ring_read(const int* p) {
 ADP_DEV int claim_next2(int* cnt) {
   return __hip_atomic_fetch_add(cnt, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// In the K loop the claim must not stall: a compiler-visible atomic gets an immediate s_waitcnt vmcnt(0) (the
-// atomic optimizer broadcasts its result at once, and loop-carried copies of a pending result wait too), which
-// drains the LDS-DMA prefetch. claim_issue is the atomic as inline asm (one lane), and claim_publish waits for
-// it with the count of the vector-memory ops issued after it (NYOUNG, exact: a larger count could pass while
-// the atomic is still in flight) and stores the raw value into the LDS ring, all in ONE asm block, in the same
-// loop iteration (no copy of the pending register can exist in between)
+// In the K loop the claim must not stall. The atomic is compiler-visible (so every use of its result is ordered
+// after its return by the compiler's own vmcnt accounting), in files built without the atomic optimizer
+// (-amdgpu-atomic-optimizer-strategy=None, Makefile NOATOMOPT), whose wave form would broadcast the result at once
+// and put an s_waitcnt vmcnt(0) right behind the atomic, draining the LDS-DMA prefetch. claim_publish stores the
+// value into the LDS ring a step later; the compiler waits for the atomic in front of it (round 4 kept the atomic
+// in inline asm with a hand-counted vmcnt, which the compiler could not see: a copy of the pending register in
+// between would have read a stale tile id -- round-4 ADVICE; tests/test_isa.py walks the code for such reads)
 ADP_DEV int claim_issue(int* cnt) {
-  int r;
-  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(r) : "v"(cnt), "v"(1) : "memory");
-  return r;
+  return __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// (NYOUNG < 0: the caller's own wait already covers the atomic -- no vmcnt wait here)
+// (NYOUNG: kept for the call sites' documentation of how many vector-memory ops follow the atomic; the wait is the
+// compiler's)
 template <int NYOUNG>
 ADP_DEV void claim_publish(int* lds, int r) {
   const unsigned addr = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
-  if constexpr (NYOUNG < 0)
-    asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(%2)\n\tds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r),
-                 "n"(NYOUNG < 63 ? NYOUNG : 0) : "memory");
+  asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(addr), "v"(r) : "memory");
 }
 // claim_full (option claim_full): a block's first two tiles are claimed too -- one synchronous claim of two at
 // the start (claim_next2) -- instead of being its static ones. With static first tiles a block whose CU is

@@ -265,7 +265,19 @@ void igemm_fwd_halo_kernel(FwdArgs a) {
 // tap64p_wide); needs the store limit (Nout, or split_c for the first part) on an 8-channel boundary
 // DYN: tiles claimed from a counter (a.claim) instead of the static list -- a compile-time form, since the
 // claimed tile id and the pending claim cost registers the tightest forms do not have
-template <bool BNR, int NCH, int BN, bool PIPE, int EPI, bool WIDE = false, bool DYN = false>
+// SWP (round 5): software-pipelined fragment reads -- the LDS reads of K step s + 1 are issued before the MFMAs of step
+// s (two fragment sets in registers), so a wave no longer waits for its own step's reads before every MFMA cluster.
+// Without it each step is "6 reads, wait, 8 MFMAs" and the waves, which leave each tile's barriers together, read
+// and multiply in phase: with the halo loads removed (timing ablation, profiles/r05g_halop_ablation.log) the L0
+// 64 -> 64 forward still ran at only 1.16 PF.
+template <int I, int N, typename F>
+__device__ __forceinline__ void halop_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    halop_static_for<I + 1, N>(f);
+  }
+}
+template <bool BNR, int NCH, int BN, bool PIPE, int EPI, bool WIDE = false, bool DYN = false, bool SWP = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   static_assert(!BNR || EPI == 0, "the BN-backward reduction launch stores the plain product");
   static_assert(EPI < 4 || !PIPE, "mask / addend quads, the dropout hash and two accumulator sets: registers");
@@ -538,7 +550,18 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   // previous tile's epilogue units run between this tile's taps -- or (!PIPE) this tile's epilogue.
   // tk = tile_id(k); returns tile_id(k + 1) (dyn: each is an LDS read of the claim ring with its own lgkmcnt
   // wait, so the ids are read once per tile and carried)
-  auto run_tile = [&](int k, int tk, auto with_prev) -> int {
+  auto load_halo = [&](int t, uint4 (&hr)[GH]) {   // registers <- the halo of patch t
+    int img1, y01, x01;
+    tile_origin(t, img1, y01, x01);
+    const bool nohalo = (a.debug_flags & 1024) != 0;   // timing-only ablation (fwd_debug bit 10): no halo loads
+#pragma unroll
+    for (int i = 0; i < GH; ++i) {
+      const uint4* p = nohalo ? nullptr : halo_src(img1, y01, x01, i);
+      hr[i] = p ? *p : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // hreg: the next tile's halo, loaded at the start of this tile and written to LDS at its end
+  auto run_tile = [&](int k, int tk, auto with_prev, uint4 (&hreg)[GH]) -> int {
     constexpr bool EPI_PREV = decltype(with_prev)::value;
     if constexpr (!DYN) tk = tile_id(k);   // (static lists: arithmetic -- nothing carried across the taps)
     const int tn = tile_id(k + 1);
@@ -557,22 +580,71 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       if (has_mask) load_q(rsM, mstr, ocol0, mrow, zreg);
       if (has_add) load_q(rsD, a.addend_stride, ocol0, mrow, dreg);
     }
-    uint4 hreg[GH];
-    if (more) {
-      int img1, y01, x01;
-      tile_origin(DYN ? tn : tile_id(k + 1), img1, y01, x01);
-#pragma unroll
-      for (int i = 0; i < GH; ++i) {
-        const uint4* p = halo_src(img1, y01, x01, i);
-        hreg[i] = p ? *p : make_uint4(0, 0, 0, 0);
-      }
-    }
+    if (more) load_halo(DYN ? tn : tile_id(k + 1), hreg);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (SWP) {
+      constexpr int NS = 18 * NCH;   // K steps of a tile: (tap, input chunk, 32-deep half)
+      bf16x8 FB[2][NF], FA[2][2];
+      auto ldf = [&](auto sc, bf16x8 (&fb)[NF], bf16x8 (&fa)[2]) {
+        constexpr int st = decltype(sc)::value, t = st / (2 * NCH), cc = (st >> 1) % NCH, kq = st & 1;
+        constexpr int dy = t / 3, dx = t - 3 * dy;
+        const unsigned char* Wt = smem + OFF_W + t * WTAP + cc * BN * ROWB;
+        const unsigned char* Hc = smem + cc * HROWS * ROWB;
+        const int ck = 4 * kq + h4;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
+        for (int nf = 0; nf < NF; ++nf) {
+          const int q = nf * 16 + r16;
+          fb[nf] = *reinterpret_cast<const bf16x8*>(Wt + q * ROWB + ((ck ^ swz(q)) << 4));
+        }
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf) {
+          const int hr = (wave + dy) * HW + mf * 16 + r16 + dx;
+          fa[mf] = *reinterpret_cast<const bf16x8*>(Hc + hr * ROWB + ((ck ^ hswz(hr)) << 4));
+        }
+      };
+      ldf(std::integral_constant<int, 0>{}, FB[0], FA[0]);
+      halop_static_for<0, NS>([&](auto sc) {
+        constexpr int st = decltype(sc)::value, t = st / (2 * NCH), cc = (st >> 1) % NCH, kq = st & 1;
+        if constexpr (st + 1 < NS) ldf(std::integral_constant<int, st + 1>{}, FB[(st + 1) & 1], FA[(st + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);   // (the next step's reads stay ahead of this step's MFMAs)
+        const bf16x8(&fb)[NF] = FB[st & 1];
+        const bf16x8(&fa)[2] = FA[st & 1];
+        constexpr bool with_unit = EPI_PREV && cc == 0 && kq == 0 && t >= 1 && t - 1 < 2 * NF;
+        if constexpr (with_unit) {
+          constexpr int u = t - 1;
+          if constexpr (WIDE) {
+            constexpr int p = u >> 1, mf = p & 1, nf = 2 * (p >> 1);
+            if constexpr ((u & 1) == 0) {
+              pend = __builtin_bit_cast(v2u32_h, epi_vals(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp));
+            } else {
+              epi_join(mf, nf, pend, __builtin_bit_cast(v2u32_h, epi_vals(mf, nf + 1, accp[mf][nf + 1],
+                                                                          zreg[mf][nf + 1], mrowp)), mrowp);
+            }
+          } else {
+            epi_unit(u & 1, u >> 1, accp[u & 1][u >> 1], zreg[u & 1][u >> 1], mrowp);
+          }
+        }
+        if constexpr (!with_unit) prio_hi<ADP_PRIO_FWD>();
+#pragma unroll
+        for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf)
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nf], fa[mf], acc[mf][nf], 0, 0, 0);
+        if constexpr (!with_unit) prio_lo<ADP_PRIO_FWD>();
+        if constexpr (with_unit) {
+#pragma unroll
+          for (int i = 0; i < 2 * NF; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, HALOP_VALU_PER_MFMA, 0);
+          }
+        }
+      });
+    }
+#pragma unroll
+    for (int t = 0; t < (SWP ? 0 : 9); ++t) {
       const int dy = t / 3, dx = t - 3 * dy;
 #pragma unroll
       for (int cc = 0; cc < NCH; ++cc) {
@@ -650,8 +722,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     }
     return DYN ? tn : tile_id(k + 1);
   };
-  int tnext = run_tile(0, tile_id(0), std::false_type{});
-  for (int k = 1; tnext >= 0; ++k) tnext = run_tile(k, tnext, std::integral_constant<bool, PIPE>{});
+  uint4 hA[GH];
+  int tnext = run_tile(0, tile_id(0), std::false_type{}, hA);
+  for (int k = 1; tnext >= 0; ++k) tnext = run_tile(k, tnext, std::integral_constant<bool, PIPE>{}, hA);
   if constexpr (PIPE) {   // the last tile's epilogue
     if constexpr (BNR) load_z(mrowp, zreg);
     epi_all(accp, zreg, mrowp, dreg);
@@ -738,7 +811,9 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     // (one-chunk launches only by default: +8 % on the 64 -> 64 forward; the two-chunk form has twice the
     // MFMA work per epilogue and lost 2-5 % to the extra registers -- profiles/r02_halop_pipe_ab.txt)
     const int pm = option("halop_pipe", 1);
-    const bool pipe = !bnr && !maskepi && !dropepi && (pm == 2 || (pm == 1 && one_chunk));
+    // SWP (option halop_swp) replaces the pipelined epilogue: with both, the forms spill
+    const bool swp_req = !bnr && !dropepi && option("halop_swp", 0) != 0;   // (the dropout form spills with it)
+    const bool pipe = !swp_req && !bnr && !maskepi && !dropepi && (pm == 2 || (pm == 1 && one_chunk));
     const int epi = bnr ? 0 : dropepi ? 5 : maskepi ? 4 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
     // WIDE (option halop_wide: 0 off, 1 the tile-serial forms, 2 every form, 3 every form but the pipelined
     // ones with statistics): 16-B stores of channel-quad pairs when every 8-channel run of the store is wholly
@@ -762,29 +837,40 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
       a.claim_full = option("claim_full", 0) && nsup >= 4 * (grid / nt_n);
     }
     const bool dyn = a.claim != nullptr;
-    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
-                    pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false");
-#define HALOP_LAUNCH_WD(NCH_, BN_, W_, D_)                                                                       \
+    // SWP (option halop_swp, static lists only): the software-pipelined K loop of the kernel comment
+    const bool swp = !dyn && swp_req;
+    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s%s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
+                    pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false", swp ? ", true" : "");
+#define HALOP_LAUNCH_WD(NCH_, BN_, W_, D_, P_)                                                                   \
   do {                                                                                                      \
-    if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0, false, D_>), dim3(grid), dim3(512), 0, s, a); \
-    else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
-    else if (epi == 5) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 5, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+    if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0, false, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 5) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 5, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
     else if (pipe) {                                                                                        \
-      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 3, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 0, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 1, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 2, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 3, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, true, 0, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
     } else {                                                                                                \
-      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
-      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
-      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0, W_, D_>), dim3(grid), dim3(512), 0, s, a); \
+      if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+      else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
+      else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0, W_, D_, P_>), dim3(grid), dim3(512), 0, s, a); \
     }                                                                                                       \
   } while (0)
-#define HALOP_LAUNCH_W(NCH_, BN_, W_)                   \
-  do {                                                  \
-    if (dyn) HALOP_LAUNCH_WD(NCH_, BN_, W_, true);      \
-    else HALOP_LAUNCH_WD(NCH_, BN_, W_, false);         \
+#define HALOP_LAUNCH_SWP(NCH_, BN_, W_)                                                                         \
+  do {                                                                                                      \
+    if (epi == 4) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 4, W_, false, true>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 1) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 1, W_, false, true>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 2) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 2, W_, false, true>), dim3(grid), dim3(512), 0, s, a); \
+    else if (epi == 3) hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 3, W_, false, true>), dim3(grid), dim3(512), 0, s, a); \
+    else hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, NCH_, BN_, false, 0, W_, false, true>), dim3(grid), dim3(512), 0, s, a); \
+  } while (0)
+#define HALOP_LAUNCH_W(NCH_, BN_, W_)                          \
+  do {                                                         \
+    if (dyn) HALOP_LAUNCH_WD(NCH_, BN_, W_, true, false);      \
+    else if (swp) HALOP_LAUNCH_SWP(NCH_, BN_, W_);              \
+    else HALOP_LAUNCH_WD(NCH_, BN_, W_, false, false);         \
   } while (0)
 #define HALOP_LAUNCH(NCH_, BN_)                  \
   do {                                           \
@@ -795,6 +881,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     else HALOP_LAUNCH(2, 32);
 #undef HALOP_LAUNCH_W
 #undef HALOP_LAUNCH_WD
+#undef HALOP_LAUNCH_SWP
 #undef HALOP_LAUNCH
     return 1;
   }

@@ -902,6 +902,57 @@ def test_halop_pipelined_epilogue_matches(parts, cout, split, grid, epi):
         assert relerr(res[1][1], res[0][1]) < 1e-5
 
 
+@pytest.mark.parametrize("epi", ["stats", "relu", "plain", "mask"])
+@pytest.mark.parametrize("grid", [None, 3], ids=["chip_grid", "3_blocks"])
+@pytest.mark.parametrize("parts,cout,split,S", [([64], 64, False, 64), ([64], 128, True, 64), ([64], 64, False, 96),
+                                                ([64, 64], 128, False, 64), ([128], 64, False, 64)])
+def test_halop_swp_matches(parts, cout, split, S, grid, epi):
+    """Persistent halo kernel with the software-pipelined K loop (halop_swp=1: the LDS fragments of step s + 1 read
+    before the MFMAs of step s) vs the default forms (the pipelined epilogue on the one-chunk layers): the same K
+    order, so outputs are bit-identical and the BatchNorm sums equal; one and two input chunks, plain / split stores,
+    statistics, ReLU, the mask epilogue."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16
+    N = 2
+    g = torch.Generator().manual_seed(57)
+    xs = [torch.randn(N, S, S, c, generator=g).to(DEV, dt) for c in parts]
+    cin = sum(parts)
+    W = (torch.randn(cout, 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    bias = torch.randn(cout, generator=g).to(DEV)
+    mask = (torch.rand(N, S, S, cout, generator=g) > 0.3).to(DEV, dt) if epi == "mask" else None
+    res = []
+    for swp in (0, 1):
+        ops.set_option("halop_swp", swp)
+        if grid:
+            ops.set_option("halo_persist_grid", grid)
+        try:
+            st = torch.zeros(2, cout, device=DEV)
+            kw = dict(srcB=xs[1] if len(xs) > 1 else None, bias=bias, relu=epi == "relu",
+                      bn_stats=(st[0], st[1]) if epi == "stats" else None)
+            if mask is not None:
+                kw.update(mask=mask, mask_scale=2.0)
+            if split:
+                o1 = torch.zeros(N, S, S, 64, dtype=dt, device=DEV)
+                o2 = torch.zeros(N, S, S, cout - 64, dtype=dt, device=DEV)
+                ops.conv_fwd(xs[0], W, cout, out=o1, out_mode=2, out2=o2, split_c=64, **kw)
+                outs = [o1, o2]
+            else:
+                o = torch.zeros(N, S, S, cout, dtype=dt, device=DEV)
+                ops.conv_fwd(xs[0], W, cout, out=o, **kw)
+                outs = [o]
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            for o_ in ("halop_swp", "halo_persist_grid"):
+                ops.set_option(o_, None)
+        assert kname.startswith("igemm_fwd_halop_kernel") and kname.endswith(", true>") == bool(swp), kname
+        res.append((outs, st))
+    for a_, b_ in zip(res[0][0], res[1][0]):
+        assert torch.equal(a_, b_)
+    if epi == "stats":
+        assert relerr(res[1][1], res[0][1]) < 1e-6
+
+
 HALOP_WIDE_CASES = [
     # name, source channels, Nout, epilogue, split, up
     ("1ch_stats", [64], 64, "stats", False, 1),
