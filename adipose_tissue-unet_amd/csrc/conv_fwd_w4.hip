@@ -46,10 +46,12 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
   constexpr int NTH = 256, ROWB = 128;
   constexpr int OBS = 2 * W4_HBUF, BSTAGE = 256 * ROWB;            // weight stages (LB)
   constexpr int OCST = OBS + (LB ? 2 * BSTAGE : 0);
-  constexpr int ODUM = OCST + 3 * 256 * 4;
+  constexpr int ODUM = OCST + 256 * 4 + 2 * 256 * 8;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[ODUM + 256 * 16];
   float* cst = reinterpret_cast<float*>(smem + OCST);   // bias [256]
-  float* sacc = cst + 256;                              // block's BN sums [2][256]
+  // block's BN sums [2][256] in f64: the waves' f32 row partials added in any order give the same f64 sum up to
+  // ~1e-16 relative (deterministic after the fold's single rounding to f32, as the other producers' sums)
+  double* sacc = reinterpret_cast<double*>(cst + 256);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -68,8 +70,8 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
   if (tid < 256) {
     const int n = n0 + tid;
     cst[tid] = (a.bias && n < a.Nout) ? a.bias[n] : 0.f;
-    sacc[tid] = 0.f;
-    sacc[256 + tid] = 0.f;
+    sacc[tid] = 0.0;
+    sacc[256 + tid] = 0.0;
   }
 
   const int npix = a.Nimg * a.Hs * a.Ws;
@@ -204,8 +206,8 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
         if (r16 == 0) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            atomicAdd(&sacc[cl + r], s1[r]);
-            atomicAdd(&sacc[256 + cl + r], s2[r]);
+            atomicAdd(&sacc[cl + r], (double)s1[r]);
+            atomicAdd(&sacc[256 + cl + r], (double)s2[r]);
           }
         }
       }
@@ -354,8 +356,8 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
     double* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
     const int n = n0 + tid;
     if (n < a.Nout) {
-      atomicAdd(rep + n, (double)sacc[tid]);
-      atomicAdd(rep + adp::STAT_CMAX + n, (double)sacc[256 + tid]);
+      atomicAdd(rep + n, sacc[tid]);
+      atomicAdd(rep + adp::STAT_CMAX + n, sacc[256 + tid]);
     }
   }
 }

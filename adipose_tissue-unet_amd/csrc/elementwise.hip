@@ -882,14 +882,16 @@ static double* stat_scratch_impl(bool fold, int C, const float* sum, hipStream_t
 }
 double* stat_scratch() { return stat_scratch_impl(false, 0, nullptr, nullptr); }
 // drop a deferred fold that never reached its adp_bn_finalize_fold (an error or exception between the two) and
-// re-zero the replicas it left its sums in, stream-ordered on s; a no-op when nothing is pending
+// re-zero the replicas it left its sums in, stream-ordered on s; a no-op when nothing is pending -- and when the
+// pending fold was left on another stream: that one belongs to another caller (engine handle, thread) whose launch
+// may still be in flight, and a memset on s would neither be ordered after it nor be ours to make (round-4 ADVICE)
 int bn_fold_reset(hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) { set_error("adp_bn_fold_reset: hipGetDevice failed"); return -2; }
   {
     std::lock_guard<std::mutex> lk(g_fold_mu);
     PendingFold& pf = pending_folds()[dev];
-    if (!pf.on) return 0;
+    if (!pf.on || pf.s != s) return 0;
     pf.on = false;
   }
   double* p = stat_scratch();

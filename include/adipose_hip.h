@@ -224,7 +224,8 @@ int adp_bn_finalize_fold(int C, float count, float* sum, float* sqsum, const flo
                          float eps, float momentum, float* scale, float* shift, float* mean, float* invstd,
                          float* running_mean, float* running_var, adp_stream_t s);
 /* Drops a bn_defer_fold record that never reached its adp_bn_finalize_fold (an error or exception between the
- * two) and re-zeroes the replicas, stream-ordered on s; a no-op when nothing is pending. Trainer steps and
+ * two) and re-zeroes the replicas, stream-ordered on s; a no-op when nothing is pending, and when the pending
+ * record was made on another stream (another caller's fold, possibly still in flight). Trainer steps and
  * adp_train_step call it first, so a failed step cannot poison the replicas for the rest of the process. */
 int adp_bn_fold_reset(adp_stream_t s);
 /* a = relu(z*scale + shift), the post-BatchNorm activation, materialised once per layer */

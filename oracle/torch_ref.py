@@ -64,7 +64,8 @@ ADIPOSE_LAYERS = (
 
 
 def adipose_v3_keras_weights(seed=865, init_nb=44, deep_supervision=True):
-    """Glorot-uniform kernels / zero biases with Keras shapes, keyed by Keras layer name."""
+    """Glorot-uniform kernels and N(0, 0.01) biases (Keras would start biases at zero; non-zero biases exercise
+    the bias paths) with Keras shapes, keyed by Keras layer name."""
     rng = np.random.default_rng(seed)
     nb = init_nb
     shapes = {

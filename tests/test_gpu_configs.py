@@ -156,11 +156,12 @@ def unet_bn_slice_vs_oracle(L, S, B, seed):
               f"{(outs['main_out'].cpu() - p).abs().mean().item():.3e}")
         # (bf16: storage rounding through 8 BatchNorm layers, at a logit near the 0.5 boundary. Since round 4 the
         # BatchNorm sums are deterministic, so this is one fixed value per build rather than a run-dependent spread:
-        # 4.06e-2 max / 2.71e-3 mean measured (profiles/r04c_gates.log); round 3 allowed 6e-2 / 5e-3 for the spread)
-        assert err < (1e-4 if dtype == "f32" else 5e-2), (dtype, err)
+        # 4.06e-2 max / 2.71e-3 mean measured (profiles/r04c_gates.log); round 3 allowed 6e-2 / 5e-3 for the spread,
+        # round 4 5e-2)
+        assert err < (1e-4 if dtype == "f32" else 4.5e-2), (dtype, err)
         assert (outs["main_out"].cpu() - p).abs().mean().item() < (1e-5 if dtype == "f32" else 3.5e-3)
         bad = []
-        worst_c = 1.0
+        worst_c, worst_r = 1.0, 0.0
         for name, ts in W.items():
             for si, (gi, t) in enumerate(zip(net.get_layer_grads(name), ts)):
                 c = cos(torch.as_tensor(gi), t.grad)
@@ -168,9 +169,10 @@ def unet_bn_slice_vs_oracle(L, S, B, seed):
                     # f32 vs f32 at 512^2: the BatchNorm backward's mean subtractions cancel digits on both sides
                     # (dz = s (dA - mean dA - xhat mean(dA xhat)) over 2 x 64^2 .. 2 x 512^2 pixels), so the largest
                     # element error of a deep layer reaches a few 1e-2 of its largest gradient (2.4e-2 measured on
-                    # enc3_conv2's kernel); the direction is exact to 1e-5
+                    # enc3_conv2's kernel); the direction is exact to 1e-5. Gate 3.5e-2 (5e-2 until round 4)
                     r = rel_err(gi, t.grad)
-                    if r >= 5e-2 or c < 0.9999:
+                    worst_r = max(worst_r, r)
+                    if r >= 3.5e-2 or c < 0.9999:
                         bad.append((name, si, r, c))
                 elif c <= 0.965:   # (bf16 vs the f32 oracle: 0.974 lowest measured, profiles/r04c_gates.log)
                     bad.append((name, si, c))
@@ -178,6 +180,8 @@ def unet_bn_slice_vs_oracle(L, S, B, seed):
                     worst_c = min(worst_c, c)
         if dtype == "bf16":
             print(f"[gate] unet_bn slice L{L} S{S} B{B} bf16: lowest gradient cosine vs the f32 oracle {worst_c:.5f}")
+        else:
+            print(f"[gate] unet_bn slice L{L} S{S} B{B} f32: largest gradient element error {worst_r:.3e}")
         assert not bad, (dtype, bad)
         del net, tr
         torch.cuda.empty_cache()

@@ -164,7 +164,9 @@ def test_dilated_bottleneck_taps_inside(case, dt):
 @pytest.fixture(scope="module")
 def native_case():
     """One 1024^2 reference training tile: synthetic histology (seed 865), BT.601 gray, z-scored, the
-    reference's own Keras-initialised weights (glorot-uniform, zero bias), oracle forward + OHEM/DS loss
+    reference topology's weights as oracle/torch_ref.adipose_v3_keras_weights draws them (glorot-uniform kernels,
+    N(0, 0.01) biases -- non-zero, so the bias paths are exercised, where Keras would start from zeros), oracle
+    forward + OHEM/DS loss
     gradients on the CPU in f32."""
     B, S = 1, 1024
     xs, ys = synthetic_batch(B, S, channels=3, seed=865)

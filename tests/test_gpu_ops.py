@@ -2008,6 +2008,11 @@ def test_deferred_bn_fold_is_guarded():
     ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()), defer_fold=True)
     with pytest.raises(ops.AdpError):
         ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()))
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):   # a reset on another stream leaves the pending fold alone (not its caller's)
+        ops.bn_fold_reset()
+    with pytest.raises(ops.AdpError):
+        ops.conv_fwd(x, W, C, out=out, bn_stats=(vec(), vec()))
     ops.bn_fold_reset()
     ops.bn_fold_reset()   # nothing pending: a no-op
     s1, q1 = vec(), vec()
