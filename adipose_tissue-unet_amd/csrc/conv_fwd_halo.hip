@@ -811,8 +811,11 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
     // (one-chunk launches only by default: +8 % on the 64 -> 64 forward; the two-chunk form has twice the
     // MFMA work per epilogue and lost 2-5 % to the extra registers -- profiles/r02_halop_pipe_ab.txt)
     const int pm = option("halop_pipe", 1);
-    // SWP (option halop_swp) replaces the pipelined epilogue: with both, the forms spill
-    const bool swp_req = !bnr && !dropepi && option("halop_swp", 0) != 0;   // (the dropout form spills with it)
+    // SWP (option halop_swp: 0 off, 1 every non-BNR form, 2 the two-chunk ones -- default) replaces the pipelined
+    // epilogue (with both the forms spill). Measured (profiles/r05i_swp_ab.log): two-chunk forward +4-6 % (L0 128->64,
+    // L1 128->128), the one-chunk forward 1 % behind its pipelined epilogue, L1 256->128 (tap64p) untouched
+    const int swm = option("halop_swp", 2);
+    const bool swp_req = !bnr && !dropepi && (swm == 1 || (swm == 2 && !one_chunk));   // (the dropout form spills)
     const bool pipe = !swp_req && !bnr && !maskepi && !dropepi && (pm == 2 || (pm == 1 && one_chunk));
     const int epi = bnr ? 0 : dropepi ? 5 : maskepi ? 4 : (a.bn_sum ? 1 : 0) + (a.relu ? 2 : 0);
     // WIDE (option halop_wide: 0 off, 1 the tile-serial forms, 2 every form, 3 every form but the pipelined
