@@ -1404,9 +1404,16 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     } else if (option("wgrad_halop_waves", 8) == 9) {
       adp::set_kernel("igemm_wgrad_halop_kernel<9, false, 8, true>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
-    } else if (stat_inst && option("wgrad_halop_spread", 4) != 8 && option("wgrad_halop_pf", 1)) {
-      adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false, true>");
-      hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false, true>), dim3(grid), dim3(512), 0, s, a);
+    } else if (stat_inst && option("wgrad_halop_pf", 1)) {
+      // (option wgrad_halop_spread: the next patch's LDS-DMA over patch rows 0-3 (4, default) or 0-7 (8))
+      const int spr = option("wgrad_halop_spread", 4);
+      if (spr == 8) {
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 8, false, true>");
+        hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 8, false, true>), dim3(grid), dim3(512), 0, s, a);
+      } else {   // (rows 0-1 / row 0 only: -1..-16 % / -2..-4 % at L0-L4, profiles/r05k_spread*_ab.log)
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false, true>");
+        hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false, true>), dim3(grid), dim3(512), 0, s, a);
+      }
     } else if (stat_inst && option("wgrad_halop_spread", 4) != 8) {
       adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false>");
       hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false>), dim3(grid), dim3(512), 0, s, a);

@@ -873,6 +873,7 @@ def test_halop_pipelined_epilogue_matches(parts, cout, split, grid, epi):
     res = []
     for pipe in (0, 1):
         ops.set_option("halop_pipe", 2 * pipe)   # 2: every (non-BNR) form pipelined
+        ops.set_option("halop_swp", 0)           # (the two-chunk forms' default software-pipelined loop replaces it)
         if grid:
             ops.set_option("halo_persist_grid", grid)
         try:
@@ -892,6 +893,7 @@ def test_halop_pipelined_epilogue_matches(parts, cout, split, grid, epi):
             kname = _lib.lib().adp_last_kernel().decode()
         finally:
             ops.set_option("halop_pipe", None)
+            ops.set_option("halop_swp", None)
             ops.set_option("halo_persist_grid", None)
         # igemm_fwd_halop_kernel<BNR, NCH, BN, PIPE, EPI>
         assert kname.startswith("igemm_fwd_halop_kernel") and kname.split(", ")[3] == ("true" if pipe else "false"), kname
@@ -1369,9 +1371,14 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false>"
         ops.set_option("wgrad_halop_pf", None)
         ops.set_option("wgrad_halop_spread", 8)   # next patch's loads over all 8 patch rows
+        dWp8 = torch.zeros_like(dW)
+        ops.conv_wgrad(xd[0], dzd, dWp8, l.Nout, srcB=srcB)
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 8, false, true>"
+        ops.set_option("wgrad_halop_pf", 0)
         dWs = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dWs, l.Nout, srcB=srcB)
         assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 8, true>"
+        ops.set_option("wgrad_halop_pf", None)
         ops.set_option("wgrad_halop_waves", 9)   # one wave per tap
         dW9 = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dW9, l.Nout, srcB=srcB)
@@ -1385,7 +1392,7 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.set_option("wgrad_halop_spread", None)
         ops.set_option("wgrad_halop_pf", None)
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
-    assert torch.equal(dW, dWn)   # (same per-block sums, same fixed-order reduce)
+    assert torch.equal(dW, dWn) and torch.equal(dW, dWp8)   # (same per-block sums, same fixed-order reduce)
     assert relerr(dW.cpu(), ref.cpu()) < 1e-4 and relerr(dW9.cpu(), ref.cpu()) < 1e-4
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
