@@ -450,8 +450,11 @@ int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input la
 int launch_fwd_halop_f8(FwdArgs& a, hipStream_t s);
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.
 int launch_wgrad_tap64(WgradArgs& a, hipStream_t s);
-// dst[i] += sum_g part[g][i] over G slabs of n4 float4 each, in an order fixed by G alone (deterministic)
+// dst[i] += sum_g part[g][i] over G slabs of n4 float4 each, in an order fixed by G alone (deterministic); recorded
+// instead of launched while the stream defers (adp_wgrad_defer), launched batched by adp_wgrad_flush
 void slab_reduce(int G, size_t n4, const float* part, float* dst, hipStream_t s);
+// the slabs of one such reduction: library scratch `slot`, or (deferring stream) the stream's arena
+float* reduce_part(int slot, size_t bytes, hipStream_t s);
 // conv_wgrad_f32.hip: f32 weight gradient on LDS-DMA staging (32-pixel stages, exact f32 MFMA)
 int launch_wgrad_f32(WgradArgs& a, hipStream_t s);
 // the persistent halo weight-gradient kernel takes this launch with the BatchNorm-backward apply fused

@@ -1019,8 +1019,8 @@ void launch_bias_grad(const WgradArgs& a, hipStream_t s) {
   const int C = a.dy_mode == 0 ? a.Nout : a.Cps;
   const int G = C / 8, lanes = NT / G;
   const int blocks = (int)std::min<size_t>((Mp + lanes - 1) / lanes, 1024);
-  float* part = adp::option("wgrad_det", 1) && C % 4 == 0
-                    ? static_cast<float*>(adp::scratch(3, (size_t)blocks * C * sizeof(float))) : nullptr;
+  float* part = adp::option("wgrad_det", 1) && C % 4 == 0 ? adp::reduce_part(3, (size_t)blocks * C * sizeof(float), s)
+                                                           : nullptr;
   hipLaunchKernelGGL(channel_sum_kernel<T>, dim3(blocks), dim3(NT), 0, s, Mp, C, a.dy_stride,
                      reinterpret_cast<const T*>(a.dY), part ? part : a.dB, 0, part ? 1 : 0);
   if (part) adp::slab_reduce(blocks, (size_t)C / 4, part, a.dB, s);

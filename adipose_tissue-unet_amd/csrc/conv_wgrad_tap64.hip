@@ -17,7 +17,10 @@
 // pixel rows advance by 64 per stage with incremental (image, y, x) coordinates — no divisions in
 // the loop.
 #include "conv_common.h"
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 namespace {
 
@@ -1216,11 +1219,10 @@ __global__ void wgrad_reduce_kernel(int splits, size_t slab, const float4* part,
 // Fixed-order sum of G partial slabs into dW (dW[i] += sum_g part[g][i]): a 256-thread block takes 32 float4
 // elements; its 8 thread groups sum consecutive slab ranges [g0, g1) in order, and group 0 adds the 8 range sums in
 // order. The association depends only on G, so two runs give the same bits (unlike f32 atomics).
-__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(int G, size_t n4, const float4* __restrict__ part,
-                                                                float4* __restrict__ dW) {
-  __shared__ float4 ps[8][32];
+__device__ __forceinline__ void slab_reduce_block(int G, size_t n4, const float4* __restrict__ part,
+                                                  float4* __restrict__ dW, int blk, float4 (&ps)[8][32]) {
   const int e = threadIdx.x & 31, j = threadIdx.x >> 5;
-  const size_t i = (size_t)blockIdx.x * 32 + e;
+  const size_t i = (size_t)blk * 32 + e;
   const int per = (G + 7) / 8, g0 = min(G, j * per), g1 = min(G, g0 + per);
   float4 acc = {0.f, 0.f, 0.f, 0.f};
   if (i < n4) {
@@ -1252,6 +1254,29 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(int G, size_t n4
     dW[i] = d;
   }
 }
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(int G, size_t n4, const float4* __restrict__ part,
+                                                                float4* __restrict__ dW) {
+  __shared__ float4 ps[8][32];
+  slab_reduce_block(G, n4, part, dW, blockIdx.x, ps);
+}
+// the deferred reductions of a backward in one launch (adp_wgrad_defer / adp_wgrad_flush): segment j takes blocks
+// [blk0[j], blk0[j + 1]), each block the same arithmetic as wgrad_slab_reduce_kernel (bit-identical sums)
+constexpr int SEG_MAX = 32;
+struct SegTable {
+  int n;
+  int blk0[SEG_MAX + 1];
+  int G[SEG_MAX];
+  unsigned long long n4[SEG_MAX];
+  const float4* part[SEG_MAX];
+  float4* dst[SEG_MAX];
+};
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_batched_kernel(SegTable t) {
+  __shared__ float4 ps[8][32];
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < t.n && b >= t.blk0[j + 1]) ++j;
+  slab_reduce_block(t.G[j], (size_t)t.n4[j], t.part[j], t.dst[j], b - t.blk0[j], ps);
+}
 
 // Pixel splits: enough blocks to fill the chip (target_blocks), but every split keeps at least
 // min_chunk pixels so that the f32 atomic epilogue (blocks x TN x TK x 4 bytes at ~1.3 TB/s) stays
@@ -1280,7 +1305,8 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   //  same bits)
   const bool det = adp::option("wgrad_det", 1) != 0;
   if (splits > 1 && (det || adp::option("wgrad_partials", TN >= 256 ? 1 : 0)) && !(a.debug_flags & 1))
-    a.part = static_cast<float*>(adp::scratch(0, slab * splits * sizeof(float)));
+    a.part = det ? adp::reduce_part(0, slab * splits * sizeof(float), s)
+                 : static_cast<float*>(adp::scratch(0, slab * splits * sizeof(float)));
   adp::set_kernel("igemm_wgrad_tap64_kernel<%d, %d, %d, %s, %s>", WN, WK, TNW, two ? "true" : "false",
                   ra ? "true" : "false");
   if (ra && !two) hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, false, true>), grid, block, 0, s, a);
@@ -1289,9 +1315,7 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   else hipLaunchKernelGGL((igemm_wgrad_tap64_kernel<WN, WK, TNW, true, false>), grid, block, 0, s, a);
   adp::kernel_end();   // (the split reduce below is a kernel of its own in rocprofv3's list)
   if (a.part && det) {
-    const size_t n4 = slab / 4;
-    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)((n4 + 31) / 32)), dim3(256), 0, s, splits, n4,
-                       reinterpret_cast<const float4*>(a.part), reinterpret_cast<float4*>(a.dW));
+    adp::slab_reduce(splits, slab / 4, a.part, a.dW, s);
   } else if (a.part) {
     const size_t n4 = slab / 4;
     const int groups = (splits + WG_SG - 1) / WG_SG;
@@ -1305,9 +1329,98 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
 }  // namespace
 
 namespace adp {
+// ---- deferred slab reductions (adp_wgrad_defer / adp_wgrad_flush). Every deterministic weight / bias gradient launch
+// is followed by a small reduce launch (~10 us) and, like every launch, a ~5.8 us dependency gap: 21 per training
+// step, ~0.34 ms (profiles/r05a: tools/kstats.py, gap analysis in DESIGN.md §3 (30)). Deferred, the slabs go to a
+// per-stream arena (chunks kept across steps) and the reductions are recorded; adp_wgrad_flush launches them all as one
+// kernel (up to SEG_MAX segments per launch), in the same fixed order: bit-identical gradients.
+struct Deferred {
+  bool on = false;
+  std::vector<std::pair<char*, size_t>> chunks;   // (base, bytes), reused across steps
+  size_t ci = 0, used = 0;                          // current chunk, bytes used in it
+  std::vector<SegTable> tables;                     // (built as the segments are recorded)
+};
+static std::mutex g_def_mu;
+static std::map<hipStream_t, Deferred>& deferred_map() {
+  static std::map<hipStream_t, Deferred> m;
+  return m;
+}
+float* reduce_part(int slot, size_t bytes, hipStream_t s) {
+  {
+    std::lock_guard<std::mutex> lk(g_def_mu);
+    auto it = deferred_map().find(s);
+    if (it != deferred_map().end() && it->second.on) {
+      Deferred& d = it->second;
+      bytes = (bytes + 255) / 256 * 256;
+      while (d.ci < d.chunks.size() && d.used + bytes > d.chunks[d.ci].second) { ++d.ci; d.used = 0; }
+      if (d.ci == d.chunks.size()) {   // (first steps only: a new chunk, never freed while the process runs)
+        const size_t sz = std::max(bytes, (size_t)256 << 20);
+        void* p = nullptr;
+        if (hipMalloc(&p, sz) != hipSuccess) { set_error("adp_wgrad_defer: arena allocation failed"); return nullptr; }
+        d.chunks.push_back({static_cast<char*>(p), sz});
+        d.used = 0;
+      }
+      float* r = reinterpret_cast<float*>(d.chunks[d.ci].first + d.used);
+      d.used += bytes;
+      return r;
+    }
+  }
+  return static_cast<float*>(scratch(slot, bytes));
+}
 void slab_reduce(int G, size_t n4, const float* part, float* dst, hipStream_t s) {
+  {
+    std::lock_guard<std::mutex> lk(g_def_mu);
+    auto it = deferred_map().find(s);
+    if (it != deferred_map().end() && it->second.on) {
+      Deferred& d = it->second;
+      // segments of one launch run concurrently: a destination already in the open table (the same gradient
+      // accumulated twice) starts a new table, launched after it
+      bool clash = false;
+      if (!d.tables.empty()) {
+        const SegTable& o = d.tables.back();
+        const float4* lo = reinterpret_cast<const float4*>(dst);
+        for (int j = 0; j < o.n && !clash; ++j) clash = lo < o.dst[j] + o.n4[j] && o.dst[j] < lo + n4;
+      }
+      if (d.tables.empty() || d.tables.back().n == SEG_MAX || clash) {
+        d.tables.emplace_back();
+        d.tables.back().n = 0;
+        d.tables.back().blk0[0] = 0;
+      }
+      SegTable& t = d.tables.back();
+      const int j = t.n++;
+      t.G[j] = G;
+      t.n4[j] = n4;
+      t.part[j] = reinterpret_cast<const float4*>(part);
+      t.dst[j] = reinterpret_cast<float4*>(dst);
+      t.blk0[j + 1] = t.blk0[j] + (int)((n4 + 31) / 32);
+      return;
+    }
+  }
   hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)((n4 + 31) / 32)), dim3(256), 0, s, G, n4,
                      reinterpret_cast<const float4*>(part), reinterpret_cast<float4*>(dst));
+}
+int wgrad_defer(hipStream_t s, int on) {
+  std::lock_guard<std::mutex> lk(g_def_mu);
+  Deferred& d = deferred_map()[s];
+  if (!on && !d.tables.empty()) { set_error("adp_wgrad_defer: reductions pending (adp_wgrad_flush first)"); return -1; }
+  d.on = on != 0 && option("wgrad_defer", 1);   // (option wgrad_defer = 0: every reduction launched at once)
+  return 0;
+}
+// launch the pending reductions of stream s (stream-ordered after the launches that wrote their slabs) and end the
+// deferral; the arena is reused by the next deferred launches, which are ordered after these reductions
+int wgrad_flush(hipStream_t s) {
+  std::vector<SegTable> tables;
+  {
+    std::lock_guard<std::mutex> lk(g_def_mu);
+    Deferred& d = deferred_map()[s];
+    tables.swap(d.tables);
+    d.on = false;
+    d.ci = 0;
+    d.used = 0;
+  }
+  for (const SegTable& t : tables)
+    if (t.n > 0) hipLaunchKernelGGL(wgrad_slab_reduce_batched_kernel, dim3((unsigned)t.blk0[t.n]), dim3(256), 0, s, t);
+  return 0;
 }
 // shapes of the persistent halo weight-gradient kernel
 static bool halop_ok(const WgradArgs& a) {
@@ -1352,7 +1465,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     const int grid = std::max(1, std::min(tiles, option("wgrad_cin8_grid", 256)));
     // wgrad_det (default on): per-block slabs [grid][64][Kpad] + the fixed-order reduce instead of f32 atomics
     a.part = option("wgrad_det", 1) && !(a.debug_flags & 1)
-                 ? static_cast<float*>(scratch(0, (size_t)grid * 64 * a.Kpad * sizeof(float))) : nullptr;
+                 ? reduce_part(0, (size_t)grid * 64 * a.Kpad * sizeof(float), s) : nullptr;
     if (a.bna_dA) {
       adp::set_kernel("igemm_wgrad_cin8_kernel<true>");
       hipLaunchKernelGGL((igemm_wgrad_cin8_kernel<true>), dim3(grid), dim3(512), 0, s, a);
@@ -1388,7 +1501,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     a.part_rmw = 0;
     const bool det = !a.claim && option("wgrad_det", 1) && !(a.debug_flags & 1);
     if (det && per == 1) a.part_rmw = 1;
-    else if (det) a.part = static_cast<float*>(scratch(0, (size_t)per * a.Nout * a.Kpad * sizeof(float)));
+    else if (det) a.part = reduce_part(0, (size_t)per * a.Nout * a.Kpad * sizeof(float), s);
     // (a failed scratch allocation leaves part null: the atomic form)
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {

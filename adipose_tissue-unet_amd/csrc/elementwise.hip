@@ -1115,6 +1115,11 @@ extern "C" int adp_bn_finalize(int C, float count, const float* sum, const float
 }
 
 extern "C" int adp_bn_fold_reset(adp_stream_t st) { return adp::bn_fold_reset((hipStream_t)st) ? -2 : 0; }
+extern "C" int adp_wgrad_defer(int on, adp_stream_t st) { return adp::wgrad_defer((hipStream_t)st, on) ? -1 : 0; }
+extern "C" int adp_wgrad_flush(adp_stream_t st) {
+  adp::wgrad_flush((hipStream_t)st);
+  return adp::check_launch("adp_wgrad_flush");
+}
 
 extern "C" int adp_bn_finalize_fold(int C, float count, float* sum, float* sq, const float* gamma, const float* beta,
                                     float eps, float momentum, float* scale, float* shift, float* mean, float* invstd,

@@ -181,6 +181,7 @@ struct adp_handle {
   hipEvent_t comm_done = nullptr;
   bool dp_active = false;
   float* Gsnap = nullptr;             // adp_debug_grad_flat(which = 1): G as each bucket's all-reduce was issued
+  bool deferring = false;             // inside a train step's backward: weight-gradient reductions deferred
   std::string comm_err;
 
   ~adp_handle() {
@@ -759,6 +760,10 @@ struct adp_handle {
   int dp_launch(int bi, hipStream_t s) {
     Bucket& bk = buckets[bi];
     bk.launched = true;
+    if (deferring) {   // the bucket's gradients are final only after the recorded reductions ran
+      CL(adp_wgrad_flush(s));
+      CL(adp_wgrad_defer(1, s));
+    }
     CK(hipEventRecord(bev[bi], s));
     CK(hipStreamWaitEvent(cstream, bev[bi], 0));
     if (adp::option("dp_snapshot", 0)) {   // test hook: what the all-reduce is about to read
@@ -1784,10 +1789,16 @@ extern "C" int adp_train_step(adp_handle* h, const float* x, const float* y, int
     for (const char* e : {"down1_conv1", "down1_conv2", "down2_conv1", "down2_conv2", "down3_conv1", "down3_conv2"})
       frozen.insert(h->dense_id(e));
   CL(h->dp_begin(frozen));
+  // the deterministic weight-gradient reductions of the backward are recorded and launched together (adp_wgrad_defer:
+  // one launch instead of ~21 with their dependency gaps); a bucket's all-reduce flushes first (dp_launch)
+  CL(adp_wgrad_defer(1, s));
+  h->deferring = true;
   const int brc = bn ? h->bn_backward(N, s) : h->backward(N, keep, full, s);
-  if (brc) {
+  h->deferring = false;
+  const int frc = adp_wgrad_flush(s);
+  if (brc || frc) {
     h->dp_abort(s);
-    return brc;
+    return brc ? brc : frc;
   }
   CL(h->dp_finish(s));
   const size_t lo = full ? 0 : h->enc_end;

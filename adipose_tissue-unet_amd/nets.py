@@ -546,6 +546,17 @@ class AdiposeV3Net(UNetEngine):
     frozen_encoder = False
 
     def backward(self, grads_out):
+        """The backward pass; its deterministic weight-gradient reductions are deferred (ops.wgrad_defer) and launched
+        together at its end (one launch instead of one per layer); every gradient is final when it returns."""
+        ops.wgrad_defer(True)
+        self._deferring = True
+        try:
+            return self._backward(grads_out)
+        finally:
+            self._deferring = False
+            ops.wgrad_flush()
+
+    def _backward(self, grads_out):
         """grads_out: {'main_out': dL/dp (B,S,S) f32, 'aux_out1': ..., 'aux_out2': ...}.
         Accumulates parameter gradients into self.ps.grad (caller zeroes)."""
         a, L = self.a, self.layers
@@ -952,6 +963,17 @@ class UNetBN(UNetEngine):
         ops.bn_bwd_apply(dA, z, s[2], s[3], s[4], s[5], self.ps.view(name + "/gamma"), dg, db, count, dz)
 
     def backward(self, grads_out):
+        """The backward pass; its deterministic weight-gradient reductions are deferred (ops.wgrad_defer) and launched
+        together at its end (one launch instead of one per layer); every gradient is final when it returns."""
+        ops.wgrad_defer(True)
+        self._deferring = True
+        try:
+            return self._backward(grads_out)
+        finally:
+            self._deferring = False
+            ops.wgrad_flush()
+
+    def _backward(self, grads_out):
         a, L = self.a, self.layers
         Lv = self.levels
         self.pack_dgrad_weights([n for n, l in L.items() if isinstance(l, Dense) and n != "enc0_conv1"])

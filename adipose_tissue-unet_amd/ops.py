@@ -474,6 +474,17 @@ def fill(dst, value):
     call("adp_fill_f32", dst.numel(), float(value), ptr(dst), stream_ptr())
 
 
+def wgrad_defer(on=True):
+    """adp_wgrad_defer on the current stream: the deterministic weight / bias gradient reductions of the following
+    conv_wgrad launches are recorded, not launched; dW / dB are final only after wgrad_flush()."""
+    call("adp_wgrad_defer", 1 if on else 0, stream_ptr())
+
+
+def wgrad_flush():
+    """adp_wgrad_flush: every recorded reduction of the current stream in one launch; ends the deferral."""
+    call("adp_wgrad_flush", stream_ptr())
+
+
 def bn_fold_reset():
     """Drop a deferred BatchNorm fold left pending by a failed step and re-zero the accumulator replicas
     (adp_bn_fold_reset, stream-ordered; a no-op when nothing is pending)."""

@@ -93,6 +93,7 @@ class GradBuckets:
         self.world = dist.get_world_size(group)
         self.buckets = plan_buckets(net.ps, bucket_bytes)
         self.ps = net.ps
+        self.net = net
         self.works = []
 
     def begin(self, frozen=()):
@@ -112,6 +113,9 @@ class GradBuckets:
     def _launch(self, i):
         _, lo, hi = self.buckets[i]
         self.launched[i] = True
+        if getattr(self.net, "_deferring", False):   # the bucket's gradients are final after the recorded reductions
+            ops.wgrad_flush()
+            ops.wgrad_defer(True)
         self.works.append(dist.all_reduce(self.ps.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                           async_op=True))
 

@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 16 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 17 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
@@ -39,7 +39,8 @@ extern "C" {
                               v13: adp_vec_mul (eval BatchNorm folded into the fp8 dequantisation scale);
                               v14: adp_scale_rows (eval BatchNorm folded into bf16 / f32 forward weights);
                               v15: adp_conv_wgrad_bn with dY = NULL (dz not stored), input-layer fused form;
-                              v16: adp_bn_fold_reset, adp_debug_grad_flat */
+                              v16: adp_bn_fold_reset, adp_debug_grad_flat;
+                              v17: adp_wgrad_defer / adp_wgrad_flush */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -228,6 +229,14 @@ int adp_bn_finalize_fold(int C, float count, float* sum, float* sqsum, const flo
  * record was made on another stream (another caller's fold, possibly still in flight). Trainer steps and
  * adp_train_step call it first, so a failed step cannot poison the replicas for the rest of the process. */
 int adp_bn_fold_reset(adp_stream_t s);
+/* Deferred weight-gradient reductions (round 5). The weight / bias gradient launches (adp_conv_wgrad, _bn) sum per-block
+ * partial slabs in a fixed order (deterministic) with a small reduce launch each. Between adp_wgrad_defer(1, s) and
+ * adp_wgrad_flush(s), launches on stream s write their slabs to a per-stream arena and only record the reduction;
+ * adp_wgrad_flush launches every recorded reduction as one kernel (same arithmetic: bit-identical gradients) and ends
+ * the deferral. Until the flush the dW / dB buffers of those launches are NOT final: call it before anything reads
+ * them (the optimizer, a gradient all-reduce). adp_wgrad_defer(0, s) with reductions pending is an error. */
+int adp_wgrad_defer(int on, adp_stream_t s);
+int adp_wgrad_flush(adp_stream_t s);
 /* a = relu(z*scale + shift), the post-BatchNorm activation, materialised once per layer */
 int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* scale, const float* shift,
                  void* out, adp_stream_t s);

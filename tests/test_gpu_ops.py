@@ -1397,6 +1397,64 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
 
+def test_wgrad_deferred_reductions():
+    """adp_wgrad_defer / adp_wgrad_flush: between them the slab reductions of the deterministic weight-gradient
+    launches are only recorded (dW untouched), the flush runs them all in one batched launch with the arithmetic of
+    the per-launch reduce (bit-identical dW), a gradient accumulated twice into one buffer keeps both terms (the
+    second segment goes to a table launched after the first), and ending a deferral with reductions pending is an
+    error. Covers the halo kernel's slabs, the tap64 kernel's split slabs (wgrad_halop = 0) and bias sums."""
+    from adipose_amd import _lib
+    N, H, W, cout = 2, 64, 64, 64
+    _, kern, bias, l = make_case(N, H, [64], cout, 1, False, seed=23)
+    g = torch.Generator().manual_seed(24)
+    x = torch.randn(N, H, W, 64, generator=g).to(DEV, torch.bfloat16)
+    dz = nhwc_pad(rb(torch.randn(N, H, W, cout, generator=g), torch.bfloat16), l.cout_s, torch.bfloat16)
+    z = lambda: torch.zeros((l.Npad, l.Kpad), device=DEV)   # noqa: E731
+
+    def run(dst, opt=None, dB=None):
+        if opt:
+            ops.set_option(opt, 0)
+        try:
+            ops.conv_wgrad(x, dz, dst, l.Nout, dB=dB)
+        finally:
+            if opt:
+                ops.set_option(opt, None)
+    # immediate: halo slabs, twice into one buffer; tap64 split slabs; bias sums
+    ref_h, ref_h2, ref_t = z(), z(), z()
+    ref_b = torch.zeros(l.Npad, device=DEV)
+    run(ref_h)
+    run(ref_h2)
+    run(ref_h2)
+    run(ref_t, "wgrad_halop", dB=ref_b)
+    torch.cuda.synchronize()
+    d_h, d_h2, d_t = z(), z(), z()
+    d_b = torch.zeros(l.Npad, device=DEV)
+    ops.wgrad_defer(True)
+    try:
+        run(d_h)
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false, true>"
+        run(d_h2)
+        run(d_h2)
+        run(d_t, "wgrad_halop", dB=d_b)
+        assert _lib.lib().adp_last_kernel().decode().startswith("igemm_wgrad_tap64_kernel")
+        torch.cuda.synchronize()
+        untouched = [bool((t == 0).all()) for t in (d_h, d_h2, d_t, d_b)]
+        with pytest.raises(ops.AdpError):
+            ops.wgrad_defer(False)   # reductions pending
+    finally:
+        ops.wgrad_flush()
+    torch.cuda.synchronize()
+    assert untouched == [True] * 4
+    assert torch.equal(d_h, ref_h) and torch.equal(d_h2, ref_h2) and torch.equal(d_t, ref_t)
+    assert torch.equal(d_b, ref_b)
+    assert relerr(ref_h2.cpu(), 2 * ref_h.cpu()) < 1e-6 and relerr(ref_t.cpu(), ref_h.cpu()) < 1e-4
+    # after the flush the stream launches its reductions at once again
+    d = z()
+    run(d)
+    torch.cuda.synchronize()
+    assert torch.equal(d, ref_h)
+
+
 F32_HALO_WGRAD_CASES = [
     # name, N, H, W (output grid), source channel strides, Nout, up
     ("c64_64", 2, 32, 64, [64], 64, False),
