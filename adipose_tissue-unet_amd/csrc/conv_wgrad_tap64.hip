@@ -1338,8 +1338,14 @@ struct Deferred {
   bool on = false;
   std::vector<std::pair<char*, size_t>> chunks;   // (base, bytes), reused across steps
   size_t ci = 0, used = 0;                          // current chunk, bytes used in it
+  size_t pending = 0;                               // slab bytes recorded since the last launch of the tables
   std::vector<SegTable> tables;                     // (built as the segments are recorded)
 };
+static void launch_tables(std::vector<SegTable>& tables, hipStream_t s) {
+  for (const SegTable& t : tables)
+    if (t.n > 0) hipLaunchKernelGGL(wgrad_slab_reduce_batched_kernel, dim3((unsigned)t.blk0[t.n]), dim3(256), 0, s, t);
+  tables.clear();
+}
 static std::mutex g_def_mu;
 static std::map<hipStream_t, Deferred>& deferred_map() {
   static std::map<hipStream_t, Deferred> m;
@@ -1352,6 +1358,17 @@ float* reduce_part(int slot, size_t bytes, hipStream_t s) {
     if (it != deferred_map().end() && it->second.on) {
       Deferred& d = it->second;
       bytes = (bytes + 255) / 256 * 256;
+      // (option wgrad_defer_mb: once the recorded slabs would pass this many MB, the recorded reductions are
+      //  launched first and the arena starts over: the slabs are re-read while they still sit in the MALL, and the
+      //  arena's first chunk stays resident)
+      const size_t lim = (size_t)std::max(0, option("wgrad_defer_mb", 64)) << 20;
+      if (lim && d.pending + bytes > lim && !d.tables.empty()) {
+        launch_tables(d.tables, s);
+        d.ci = 0;
+        d.used = 0;
+        d.pending = 0;
+      }
+      d.pending += bytes;
       while (d.ci < d.chunks.size() && d.used + bytes > d.chunks[d.ci].second) { ++d.ci; d.used = 0; }
       if (d.ci == d.chunks.size()) {   // (first steps only: a new chunk, never freed while the process runs)
         const size_t sz = std::max(bytes, (size_t)256 << 20);
@@ -1417,9 +1434,9 @@ int wgrad_flush(hipStream_t s) {
     d.on = false;
     d.ci = 0;
     d.used = 0;
+    d.pending = 0;
   }
-  for (const SegTable& t : tables)
-    if (t.n > 0) hipLaunchKernelGGL(wgrad_slab_reduce_batched_kernel, dim3((unsigned)t.blk0[t.n]), dim3(256), 0, s, t);
+  launch_tables(tables, s);
   return 0;
 }
 // shapes of the persistent halo weight-gradient kernel

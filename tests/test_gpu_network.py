@@ -269,7 +269,8 @@ def test_unet_bn_bf16_runs_are_deterministic(levels, S):
     to 0.9895: profiles/r03_bf16_bn_nondeterminism.txt). Since round 5 the weight gradients are bit-identical too:
     the halo / input-layer / tap64 weight-gradient kernels write per-block slabs that a fixed-order reduce adds into
     dW (option wgrad_det), where f32 atomics in the order blocks finished used to move the last bits. The third run launches every
-    reduction at once (option wgrad_defer = 0) instead of batched at the end of the backward: the same bits."""
+    reduction at once (option wgrad_defer = 0) instead of batched at the end of the backward, the fourth keeps the
+    off-critical-path weight gradients on the backward's own stream (UNetBN.wgrad_side = False): the same bits."""
     B = 2
     w = R.unet_bn_keras_weights(levels=levels, base=64, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
@@ -277,12 +278,14 @@ def test_unet_bn_bf16_runs_are_deterministic(levels, S):
     net.set_weights(w)
     tr = Trainer(net, LossConfig(use_hard_mining=False))
     runs = []
-    for i in range(3):
+    for i in range(4):
         ops.set_option("wgrad_defer", 0 if i == 2 else None)
+        net.wgrad_side = i != 3
         try:
             outs, _ = _unet_bn_step(net, tr, x, y, B)
         finally:
             ops.set_option("wgrad_defer", None)
+            net.wgrad_side = True
         runs.append((outs["main_out"].clone(), {n: [torch.as_tensor(g).clone() for g in net.get_layer_grads(n)]
                                                 for n in w}))
     p0, g0 = runs[0]

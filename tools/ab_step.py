@@ -10,6 +10,8 @@ alternating timed blocks so that clock drift and device variance hit both arms a
   --variant headdA: head backward storing dA (old) vs dA recomputed by adp_bn_bwd_apply_head
                   (UNetBN.head_recompute_dA)
   --variant bnwgrad: adp_bn_bwd_apply + weight gradient (old) vs adp_conv_wgrad_bn (UNetBN.fuse_bn_wgrad)
+  --variant side: every weight gradient on the backward's stream (old) vs the off-critical-path ones on a second
+                  stream (UNetBN.wgrad_side)
   --variant opt --opts "a=1;a=0": two native option settings (';'-separated, each ','-separated name=value)
 (the round-1 "stat" arm, per-layer statistic fills vs one arena fill, measured neutral:
 profiles/r01i_ab_stat_arena.txt; only the arena path remains)"""
@@ -24,8 +26,9 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head", "fold", "headdA", "bnwgrad", "opt"])
+    p.add_argument("--variant", default="pack", choices=["pack", "pool", "head", "fold", "headdA", "bnwgrad", "side", "opt"])
     p.add_argument("--opts", default="")
+    p.add_argument("--side", action="store_true", help="UNetBN.wgrad_side in both arms (default: off in both)")
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--steps", type=int, default=8)
     p.add_argument("--preset", default="unet_bn", choices=["unet_bn", "adipose_v3"],
@@ -42,6 +45,7 @@ def main():
     from adipose_amd.trainer import LossConfig, Trainer
 
     dev = torch.device("cuda", 0)
+    UNetBN.wgrad_side = args.side   # (both arms; --variant side overrides per arm)
     if args.preset == "adipose_v3":
         from adipose_amd.data import to_gray
         from adipose_amd.nets import AdiposeV3Net
@@ -74,6 +78,8 @@ def main():
         owner, attr, old, new = UNetBN, "head_recompute_dA", False, True
     elif args.variant == "bnwgrad":
         owner, attr, old, new = UNetBN, "fuse_bn_wgrad", False, True
+    elif args.variant == "side":
+        owner, attr, old, new = UNetBN, "wgrad_side", False, True   # (default True since round 5)
     elif args.variant == "opt":
         class _Opts:   # setattr(owner, attr, settings) applies a native option setting
             def __setattr__(self, _, st):
