@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 
 class AdpError(RuntimeError):
@@ -45,7 +45,8 @@ class ConvIO(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in (
         "srcA", "srcB", "bn_scaleA", "bn_shiftA", "bn_scaleB", "bn_shiftB", "W", "bias",
         "out", "out2", "addend", "mask", "mask2", "accum", "bn_sum", "bn_sqsum",
-        "bnr_z", "bnr_scale", "bnr_shift", "bnr_mean", "bnr_invstd", "bnr_dgamma", "bnr_dbeta", "w_scale")]
+        "bnr_z", "bnr_scale", "bnr_shift", "bnr_mean", "bnr_invstd", "bnr_dgamma", "bnr_dbeta", "w_scale",
+        "act_outA")]
 
 
 class BnBwdArgs(C.Structure):

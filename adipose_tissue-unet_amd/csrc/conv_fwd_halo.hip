@@ -277,8 +277,19 @@ __device__ __forceinline__ void halop_static_for(F&& f) {
     halop_static_for<I + 1, N>(f);
   }
 }
-template <bool BNR, int NCH, int BN, bool PIPE, int EPI, bool WIDE = false, bool DYN = false, bool SWP = false>
+// EPI_ 6 (round 5, BNL): EPI 1 (statistics) on a source A read pre-BatchNorm: every halo chunk goes through
+// relu(z * scale + shift) (a.scA / a.shA: adp_bn_apply's arithmetic, bit-identical; out-of-image chunks stay 0) on its
+// way from the registers into LDS, and the blocks of output block 0 store the interior chunks of each patch -- every
+// pixel of the activation exactly once over the launch -- to a.act_out (which the weight gradient reads later). It
+// replaces the adp_bn_apply pass between the two convs of a unet_bn level (read z + write act, then the conv reads
+// act) by the conv's own read of z plus the act stores. The next patch's chunks are applied in the registers they were
+// loaded into, chunk j between the MFMAs of tap 3 + j (kq 1), so that only the LDS stores remain at the tile's end (applied
+// there, after the barrier, the one-chunk forward ran 20 % and the two-chunk one 44 % longer; profiles/r05u_*).
+template <bool BNR, int NCH, int BN, bool PIPE, int EPI_, bool WIDE = false, bool DYN = false, bool SWP = false>
 __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
+  constexpr bool BNL = EPI_ == 6;
+  constexpr int EPI = BNL ? 1 : EPI_;
+  static_assert(!BNL || (!BNR && !DYN && !SWP && NCH == 1), "BN-on-load: one-chunk static-list forward launches");
   static_assert(!BNR || EPI == 0, "the BN-backward reduction launch stores the plain product");
   static_assert(EPI < 4 || !PIPE, "mask / addend quads, the dropout hash and two accumulator sets: registers");
   // NCH 64-channel input chunks (1: Cin_s 64; 2: Cin_s 128 from one or two sources), BN output channels
@@ -290,11 +301,13 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   constexpr int GW = 9 * NCH * BN * 8 / NTH;                // resident weight chunks per thread
   constexpr int WTAP = NCH * BN * ROWB;
   constexpr int OFF_W = HBUF, OFF_C = OFF_W + 9 * WTAP;
-  constexpr int SMEM = OFF_C + 5 * BN * 4 + 16;             // + per-channel epilogue constants, claimed-tile ring
+  constexpr int OFF_S = OFF_C + 5 * BN * 4 + 16;            // + per-channel epilogue constants, claimed-tile ring
+  constexpr int SMEM = OFF_S + (BNL ? 2 * NCH * 64 * 4 : 0); // + BNL: scale | shift of the input channels
   static_assert(GW * NTH == 9 * NCH * BN * 8, "weights must split evenly");
   static_assert(SMEM <= 160 * 1024, "LDS");
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   typedef unsigned int v2u32_h __attribute__((ext_vector_type(2)));
+  typedef unsigned int v4u32_h __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -377,6 +390,38 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
                                           (inA ? cc * 64 : cc * 64 - a.CAs) + 8 * ((tid & 7) ^ hswz(hr)));
   };
 
+  // BNL: the applied halo chunk i of patch (img, y0, x0) (returned; v as loaded, zeros outside the image). Branch-free:
+  // the act store goes through a buffer resource, lanes with nothing to store aim past its end
+  const float* sS = reinterpret_cast<const float*>(smem + OFF_S);
+  const bool act_w = BNL && n0 == 0 && a.act_out != nullptr;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      a.act_out, 0, act_w ? a.Nimg * a.Hs * a.Ws * a.CAs * 2 : 0, 0x00020000);
+  auto bnl = [&](uint4 v, int img, int y0, int x0, int i) -> uint4 {
+    const int idx = i * NTH + tid;
+    const int cc = NCH == 1 ? 0 : (idx >= HROWS * 8 ? 1 : 0), hr = (idx - cc * HROWS * 8) >> 3;
+    const int hy = hr / HW, hx = hr - hy * HW;
+    const int gy = y0 + hy - 1, gx = x0 + hx - 1;   // (up == 1)
+    const bool inimg = (unsigned)gy < (unsigned)a.Hs && (unsigned)gx < (unsigned)a.Ws;
+    const int c0 = cc * 64 + 8 * ((tid & 7) ^ hswz(hr));
+    Grp<bf16> g;
+    g.v = v;
+    // (two halves of four channels: fewer registers live at once in the K loop the apply sits in)
+    bf16* e = reinterpret_cast<bf16*>(&g.v);
+#pragma unroll
+    for (int hv = 0; hv < 2; ++hv) {
+      const float4 q = *reinterpret_cast<const float4*>(sS + c0 + 4 * hv);
+      const float4 r = *reinterpret_cast<const float4*>(sS + NCH * 64 + c0 + 4 * hv);
+      e[4 * hv + 0] = (bf16)fmaxf(fmaf((float)e[4 * hv + 0], q.x, r.x), 0.f);
+      e[4 * hv + 1] = (bf16)fmaxf(fmaf((float)e[4 * hv + 1], q.y, r.y), 0.f);
+      e[4 * hv + 2] = (bf16)fmaxf(fmaf((float)e[4 * hv + 2], q.z, r.z), 0.f);
+      e[4 * hv + 3] = (bf16)fmaxf(fmaf((float)e[4 * hv + 3], q.w, r.w), 0.f);
+    }
+    const bool wr = inimg && hy >= 1 && hy <= PH && hx >= 1 && hx <= PW;
+    const unsigned off = wr ? (unsigned)((((img * a.Hs + gy) * a.Ws + gx) * a.CAs + c0) * 2) : 0x80000000u;
+    if (act_w) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_h, g.v), rsA, off, 0, 0);
+    return inimg ? g.v : v;
+  };
+
   // ---- prologue: nine weight taps (resident), first halo, per-channel constants
 #pragma unroll
   for (int i = 0; i < GW; ++i) {
@@ -410,8 +455,24 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     cst[3 * BN + tid] = (BNR && v) ? -a.bnr_mean[c] * a.bnr_invstd[c] : 0.f;   // xhat = z * invstd + this
     cst[4 * BN + tid] = (BNR && v) ? a.bnr_invstd[c] : 0.f;
   }
+  if constexpr (BNL) {
+    float* sw = reinterpret_cast<float*>(smem + OFF_S);
+    if (tid < NCH * 64) {
+      sw[tid] = a.scA[tid];
+      sw[NCH * 64 + tid] = a.shA[tid];
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (BNL) {   // the first patch's halo came in by LDS-DMA: each thread applies its own chunks in place
+#pragma unroll
+    for (int i = 0; i < GH; ++i)
+      if (i * NTH + tid < HCH) {
+        uint4* q = reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16);
+        *q = bnl(*q, img0, y00, x00, i);
+      }
+    __syncthreads();
+  }
 
   const int r16 = lane & 15, h4 = lane >> 4;
   constexpr bool stats = BNR || EPI == 1 || EPI == 3;
@@ -513,7 +574,6 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   auto epi_join = [&](int mf, int nf, v2u32_h o0, v2u32_h o1, int mrow_) {
     const auto e0 = __builtin_amdgcn_permlane16_swap(o0.x, o1.x, false, false);
     const auto e1 = __builtin_amdgcn_permlane16_swap(o0.y, o1.y, false, false);
-    typedef unsigned int v4u32_h __attribute__((ext_vector_type(4)));
     const v4u32_h st = {e0[0], e1[0], e0[1], e1[1]};
     const int cw = 16 * (nf + (h4 & 1)) + 8 * (h4 >> 1), m = mrow_ + mf * 16 + r16;
     const unsigned off = n0 + cw < nlim ? (unsigned)((m * ostride + ocol0 + cw) * 2) : 0x80000000u;
@@ -581,6 +641,10 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       if (has_add) load_q(rsD, a.addend_stride, ocol0, mrow, dreg);
     }
     if (more) load_halo(DYN ? tn : tile_id(k + 1), hreg);
+    int img1 = 0, y01 = 0, x01 = 0;   // BNL: the next patch (uniform)
+    if constexpr (BNL) {
+      if (more) tile_origin(tn, img1, y01, x01);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -686,14 +750,19 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
               epi_unit(mf, nf, accp[mf][nf], zreg[mf][nf], mrowp);
             }
           }
-          if (!with_unit) prio_hi<ADP_PRIO_FWD>();   // (setprio would split the interleave region)
+          // BNL: chunk t - 3 of the next patch's halo through the BatchNorm-ReLU, its VALU between this step's MFMAs
+          const bool with_apply = BNL && kq == 1 && t >= 3 && t - 3 < GH;
+          if constexpr (BNL) {
+            if (with_apply && more) hreg[t - 3] = bnl(hreg[t - 3], img1, y01, x01, t - 3);
+          }
+          if (!with_unit && !with_apply) prio_hi<ADP_PRIO_FWD>();   // (setprio would split the interleave region)
 #pragma unroll
           for (int mf = 0; mf < 2; ++mf)
 #pragma unroll
             for (int nf = 0; nf < NF; ++nf)   // transposed: rows = output channels, columns = pixels
               acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nf], fa[mf], acc[mf][nf], 0, 0, 0);
-          if (!with_unit) prio_lo<ADP_PRIO_FWD>();
-          if (with_unit) {
+          if (!with_unit && !with_apply) prio_lo<ADP_PRIO_FWD>();
+          if (with_unit || with_apply) {
 #pragma unroll
             for (int i = 0; i < 2 * NF; ++i) {
               __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
@@ -715,7 +784,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     if (more) {
       LDS_BAR();   // every wave is done with this tile's halo
 #pragma unroll
-      for (int i = 0; i < GH; ++i)
+      for (int i = 0; i < GH; ++i)   // (BNL: applied in the K loop)
         if (i * NTH + tid < HCH) *reinterpret_cast<uint4*>(smem + (size_t)(i * NTH + tid) * 16) = hreg[i];
       if (claim_now && tid == 0) ring[(k / CH + 2) & 3] = claimed;   // (slot of super-tile s - 2: long done)
       LDS_BAR();
@@ -766,8 +835,14 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   const int mode = option("fwd_halo", 1);   // 0 off, 1 auto, 2 = no single-buffer form (A/B)
   if (mode == 0) return 0;
   const int Cin_s = a.CAs + a.CBs;
+  // BN-on-load of source A (a.scA with a.act_out: EPI 6 of the persistent kernel) only where that form exists; every
+  // other BN-on-load launch goes to the register-staged kernels (adp_conv_fwd materialises act_out first)
+  const bool bnl = a.scA != nullptr;
+  if (bnl && !(a.act_out && a.CBs == 0 && a.up == 1 && a.CAs == 64 && a.bn_sum && !a.bnr_z &&
+               !a.relu && !a.bias && option("halop_bnl", 1)))
+    return 0;
   // up = 2 (nearest upsample folded into the gather): the persistent forms only
-  if (a.scA || a.scB || a.kh != 3 || a.kw != 3 || a.dil != 1 || a.pad != 1 || a.stride != 1 || (a.up != 1 && a.up != 2) ||
+  if (a.scB || a.kh != 3 || a.kw != 3 || a.dil != 1 || a.pad != 1 || a.stride != 1 || (a.up != 1 && a.up != 2) ||
       a.Ho != a.Hs * a.up || a.Wo != a.Ws * a.up || a.Ho % PH != 0 || a.Wo % PW != 0 || a.CAs % 64 != 0 || a.CBs % 64 != 0 ||
       a.K != 9 * Cin_s || a.Kpad != a.K || a.Nout > 128)
     return 0;
@@ -839,9 +914,22 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
       // claim_full only with at least 4 super-tiles per block (its first claim takes two at once)
       a.claim_full = option("claim_full", 0) && nsup >= 4 * (grid / nt_n);
     }
+    if (bnl) a.claim = nullptr;   // (static lists only)
     const bool dyn = a.claim != nullptr;
     // SWP (option halop_swp, static lists only): the software-pipelined K loop of the kernel comment
     const bool swp = !dyn && swp_req;
+    if (bnl) {   // the two forms of the unet_bn convs after a BatchNorm-ReLU: levels 0 and 1
+      if (one_chunk && a.Nout <= 64 && pipe && !wide && !swp && epi == 1) {
+        adp::set_kernel("igemm_fwd_halop_kernel<false, 1, 64, true, 6, false, false, false>");
+        hipLaunchKernelGGL((igemm_fwd_halop_kernel<false, 1, 64, true, 6, false, false, false>), dim3(grid), dim3(512), 0,
+                           s, a);
+        return 1;
+      }
+      // (the two-chunk forms: 4 output blocks apply each halo again, and with the software-pipelined K loop the
+      //  apply spills 37 VGPRs; without it, applied at the tile's end, L1's conv2 ran 44 % longer -- 143 us against
+      //  the 89 us of the apply pass it saves: profiles/r05u_*. Such launches take the two-launch form.)
+      return 0;
+    }
     adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s%s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
                     pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false", swp ? ", true" : "");
 #define HALOP_LAUNCH_WD(NCH_, BN_, W_, D_, P_)                                                                   \
@@ -891,6 +979,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
   // 128 outputs from more than two input chunks (unet_bn dec1_conv1, 256 -> 128): the 256x128 halo form of
   // the persistent tap64 kernel takes plain launches (917 vs 852 TF with statistics,
   // profiles/r02_tap64p_halo_ab.txt)
+  if (bnl) return 0;
   if (a.Nout == 128 && Cin_s > 128 && !a.bnr_z && plain && a.out_mode != 1 && option("halo_defer_tap64p", 1))
     return 0;
   if (a.up != 1) return 0;   // (the non-persistent halo kernels gather at the source resolution)

@@ -1061,6 +1061,7 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
   a.debug_flags = adp::option("fwd_debug", 0);
   a.f32 = 0;
   a.stat = (a.bn_sum || a.bnr_z) ? adp::stat_scratch() : nullptr;
+  a.act_out = io->act_outA;
 }
 
 // after a launch whose epilogue added BatchNorm sums into the replicas: fold them into the caller's
@@ -1129,6 +1130,23 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   ADP_REQUIRE(!a.stat || (d->out_mode == 1 ? d->shuffle_c : d->Nout) <= adp::STAT_CMAX,
               "adp_conv_fwd: BatchNorm sums need <= 2048 channels");
   const int fast = adp::option("conv_fast", 2);
+  if (a.act_out) {
+    // BN-on-load with the applied source stored too: one launch of the persistent halo forward where it takes the
+    // shape, else adp_bn_apply into act_outA and the launch on it (the same bits either way)
+    ADP_REQUIRE(a.scA && a.shA && !a.scB && a.CBs == 0 && io->srcA != io->act_outA,
+                "adp_conv_fwd: act_outA needs bn_scaleA / bn_shiftA, one source and its own buffer");
+    if (std::is_same<T, bf16>::value && fast == 2 && adp::launch_fwd_halo(a, s)) {
+      adp::kernel_end();
+      if (adp::check_launch("adp_conv_fwd")) return -2;
+      return fold_stats(a, s);
+    }
+    const int rc = adp_bn_apply(std::is_same<T, bf16>::value ? ADP_BF16 : ADP_F32, (size_t)a.Nimg * a.Hs * a.Ws, a.CAs,
+                                a.srcA, a.scA, a.shA, a.act_out, (adp_stream_t)s);
+    if (rc) return rc;
+    a.srcA = a.act_out;
+    a.scA = a.shA = nullptr;
+    a.act_out = nullptr;
+  }
   if (std::is_same<T, bf16>::value && fast == 2 && !a.scA && !a.scB &&
       (adp::launch_fwd_cin8(a, s) || adp::launch_fwd_halo(a, s) || adp::launch_fwd_tap64(a, s))) {
     adp::kernel_end();

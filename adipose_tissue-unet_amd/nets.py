@@ -358,14 +358,14 @@ class UNetEngine:
 
     # conv helpers -----------------------------------------------------------------------
     def conv(self, l, srcA, out, *, srcB=None, bnA=None, bnB=None, dropout=0.0, seed=0, accum=None,
-             bn_stats=None, defer_fold=False):
+             bn_stats=None, defer_fold=False, act_out=None):
         if l.transpose:
             return ops.conv_fwd(srcA, self.Wf(l.name), l.Nout, out=out, bias=self.bias(l.name), kh=1, kw=1,
                                 pad=0, bnA=bnA, out_mode=1, shuffle_c=l.cout_s)
         return ops.conv_fwd(srcA, self.Wf(l.name), l.Nout, out=out, srcB=srcB, bnA=bnA, bnB=bnB,
                             bias=self.bias(l.name) if l.bias else None, up=l.up, kh=l.k, kw=l.k, dil=l.dil,
                             relu=l.relu and not l.bn, dropout_rate=dropout, dropout_seed=seed, accum=accum,
-                            bn_stats=bn_stats, defer_fold=defer_fold)
+                            bn_stats=bn_stats, defer_fold=defer_fold, act_out=act_out)
 
     def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None, bias_grad=True, bn_apply=None):
         dW = self.ps.gview(l.name + "/W")
@@ -679,6 +679,10 @@ class UNetBN(UNetEngine):
     # (adp_conv_wgrad_bn: computed inside the halo weight-gradient kernel on levels 0-1, which also stores
     # dz for the data gradient); False: adp_bn_bwd_apply, then the weight gradient re-reads dz
     fuse_bn_wgrad = True
+    # training forward, 64-channel levels: conv2 reads conv1's pre-BatchNorm output and applies
+    # relu(bn(.)) on load, storing the activation for the backward itself (adp_conv_io.act_outA: the persistent halo
+    # forward's EPI 6) instead of an adp_bn_apply pass between the convs; the same bits
+    fuse_bn_load = True
     # the encoder pool backward recomputes its argmax from z (relu(z*scale+shift), rounded as stored) instead of
     # reading the stored activation
     pool_argmax_from_z = True
@@ -756,17 +760,18 @@ class UNetBN(UNetEngine):
         s = self.st[name]
         return (s[2], s[3])
 
-    def _bn_conv(self, name, srcA, out, act, *, srcB=None, train=True, pool=None):
+    def _bn_conv(self, name, srcA, out, act, *, srcB=None, train=True, pool=None, bnA=None, act_in=None):
         """conv -> BN statistics (epilogue) -> scale/shift -> act = relu(bn(out)) materialised (and, with
         pool, its 2x2 max-pool in the same pass; act=None: not materialised, the consumer applies it on
-        load)."""
+        load). bnA / act_in (training): srcA is the previous layer's pre-BatchNorm output, applied on load and
+        stored to act_in by this conv (fuse_bn_load)."""
         l = self.layers[name]
         s = self.st[name]
         if train:
             # s[:2] was zeroed with the forward part of the stat arena at the start of this training forward
             # the conv leaves its statistics in the accumulator replicas; the finalize folds them (one launch)
             fold = self.fuse_bn_fold
-            self.conv(l, srcA, out, srcB=srcB, bn_stats=(s[0], s[1]), defer_fold=fold)
+            self.conv(l, srcA, out, srcB=srcB, bn_stats=(s[0], s[1]), defer_fold=fold, bnA=bnA, act_out=act_in)
             count = out.shape[0] * out.shape[1] * out.shape[2]
             rm, rv = self.running[name]
             ops.bn_finalize(count, s[0], s[1], self.ps.view(name + "/gamma"), self.ps.view(name + "/beta"),
@@ -806,22 +811,33 @@ class UNetBN(UNetEngine):
             ops.fill(self._stat_fwd, 0.0)
         Lv = self.levels
         src = a["x"]
+        def bnl(i):   # conv2 of level i applies conv1's BatchNorm-ReLU on load (the persistent halo forward's shapes)
+            return train and self.fuse_bn_load and self.dt == torch.bfloat16 and self.ch(i) == 64
         for i in range(Lv):
-            self._bn_conv(f"enc{i}_conv1", src, a[f"z{i}_1"], a[f"az{i}_1"], train=train)
-            self._bn_conv(f"enc{i}_conv2", a[f"az{i}_1"], a[f"z{i}_2"], a[f"az{i}_2"], train=train,
-                          pool=a[f"pool{i}"] if i < Lv - 1 else None)
+            if bnl(i):
+                self._bn_conv(f"enc{i}_conv1", src, a[f"z{i}_1"], None, train=train)
+                self._bn_conv(f"enc{i}_conv2", a[f"z{i}_1"], a[f"z{i}_2"], a[f"az{i}_2"], train=train,
+                              pool=a[f"pool{i}"] if i < Lv - 1 else None, bnA=self.bnvec(f"enc{i}_conv1"),
+                              act_in=a[f"az{i}_1"])
+            else:
+                self._bn_conv(f"enc{i}_conv1", src, a[f"z{i}_1"], a[f"az{i}_1"], train=train)
+                self._bn_conv(f"enc{i}_conv2", a[f"az{i}_1"], a[f"z{i}_2"], a[f"az{i}_2"], train=train,
+                              pool=a[f"pool{i}"] if i < Lv - 1 else None)
             if i < Lv - 1:
                 src = a[f"pool{i}"]
         prev = a[f"az{Lv - 1}_2"]
         for i in range(Lv - 2, -1, -1):
             self.conv(self.layers[f"dec{i}_up"], prev, a[f"t{i}"])
-            self._bn_conv(f"dec{i}_conv1", a[f"az{i}_2"], a[f"y{i}_1"], a[f"ay{i}_1"], srcB=a[f"t{i}"], train=train)
+            f = bnl(i)
+            self._bn_conv(f"dec{i}_conv1", a[f"az{i}_2"], a[f"y{i}_1"], None if f else a[f"ay{i}_1"],
+                          srcB=a[f"t{i}"], train=train)
             # level 0: relu(bn(y0_2)) is only read by the head, which applies it on load (same rounding); eval
             # with the BatchNorm folded into the convs materialises it in the conv epilogue instead
             head_bn = self.fuse_head_bn and (train or not self.fuse_eval_bn)
             fuse = i == 0 and head_bn
-            self._bn_conv(f"dec{i}_conv2", a[f"ay{i}_1"], a[f"y{i}_2"], None if fuse else a[f"ay{i}_2"],
-                          train=train)
+            self._bn_conv(f"dec{i}_conv2", a[f"y{i}_1"] if f else a[f"ay{i}_1"], a[f"y{i}_2"],
+                          None if fuse else a[f"ay{i}_2"], train=train,
+                          bnA=self.bnvec(f"dec{i}_conv1") if f else None, act_in=a[f"ay{i}_1"] if f else None)
             prev = a[f"ay{i}_2"]
         if self.fuse_head_bn and (train or not self.fuse_eval_bn):
             ops.head_fwd(a["y0_2"], self.ps.view("head/W"), self.ps.view("head/b"), a["p"], cin=self.ch(0),
@@ -972,8 +988,11 @@ class UNetBN(UNetEngine):
     # BatchNorm-fused forms, which produce the dz their data gradient reads) run on a second stream, event-ordered
     # after the dz they read, so that their tails, slab writes and launch gaps overlap the data-gradient chain.
     # Single-process only (the bucketed all-reduce orders on the issuing stream): with a grad_hook it stays off.
-    # Measured -0.5..-0.6 % per step, the same bits (profiles/r05p_side_ab.log, r05q_ab3.log).
-    wgrad_side = True
+    # Measured -0.5..-0.6 % per step, the same bits (profiles/r05p_side_ab.log, r05q_side_ab.log). Off by default:
+    # with two streams the kernels overlap, and every per-kernel duration (rocprofv3's, and the HIP-event timing the
+    # bench's roofline divides by) then includes the time shared with the other stream (the halo weight gradient
+    # reads 462 instead of 282 us), so no kernel's roofline fraction can be measured in the step.
+    wgrad_side = False
 
     def backward(self, grads_out):
         """The backward pass; its deterministic weight-gradient reductions are deferred (ops.wgrad_defer) and launched

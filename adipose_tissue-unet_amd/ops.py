@@ -161,8 +161,12 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
              kh=3, kw=3, dil=1, pad=None, Ho=None, Wo=None, relu=False, dropout_rate=0.0, dropout_seed=0,
              out_mode=0, shuffle_c=0, out2=None, split_c=0, addend=None, mask=None, mask_scale=1.0,
              mask2=None, mask2_scale=1.0, accum=None, bn_stats=None, bn_reduce=None, w_scale=None,
-             defer_fold=False):
+             defer_fold=False, act_out=None):
     """Implicit-GEMM conv forward-shaped launch (conv, conv dgrad, convT fwd/dgrad).
+
+    bnA=(scale, shift) with act_out (one source): srcA is read pre-BatchNorm, relu(srcA*scale+shift) is what the
+    conv multiplies and is also stored to act_out (adp_conv_io.act_outA: one launch on the persistent halo forward,
+    else bn_apply + the launch; bit-identical to bn_apply(srcA) -> act_out, conv_fwd(act_out)).
 
     bn_reduce=(z, scale, shift, mean, invstd, dgamma, dbeta): fuse the BatchNorm-backward reduction
     (bn_bwd_reduce) of the layer whose activation relu(z*scale+shift) `out` is the gradient of.
@@ -231,11 +235,17 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
         d.bnr_stride = z.shape[3]
         io.bnr_z, io.bnr_scale, io.bnr_shift, io.bnr_mean = ptr(z), ptr(sc), ptr(sh), ptr(mu)
         io.bnr_invstd, io.bnr_dgamma, io.bnr_dbeta = ptr(ist), ptr(dg), ptr(dbt)
+    if act_out is not None:
+        _check(bnA is not None and srcB is None, "act_out needs bnA and one source")
+        _check(act_out.shape == srcA.shape and act_out.dtype == srcA.dtype and act_out.is_contiguous() and
+               act_out.data_ptr() != srcA.data_ptr(), "act_out must be a separate tensor shaped like srcA")
+        io.act_outA = ptr(act_out)
     dc = dtype_code(srcA)
     flops = 2.0 * N * Ho * Wo * nout * kh * kw * (d.CA_stride + d.CB_stride)
     # algorithmic bytes: every operand read once, every output written once
     nbytes = _nbytes(srcA) + _nbytes(srcB) + _nbytes(W) + _nbytes(out) + _nbytes(out2) + _nbytes(addend) + \
-        _nbytes(mask) + _nbytes(mask2) + 2 * _nbytes(accum) + (_nbytes(bn_reduce[0]) if bn_reduce else 0)
+        _nbytes(mask) + _nbytes(mask2) + 2 * _nbytes(accum) + (_nbytes(bn_reduce[0]) if bn_reduce else 0) + \
+        _nbytes(act_out)
     _timed(dc, flops,
            lambda: call("adp_conv_fwd", dc, C.byref(d), C.byref(io), stream_ptr()), nbytes)
     return out

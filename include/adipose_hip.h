@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 17 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 18 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
@@ -40,7 +40,8 @@ extern "C" {
                               v14: adp_scale_rows (eval BatchNorm folded into bf16 / f32 forward weights);
                               v15: adp_conv_wgrad_bn with dY = NULL (dz not stored), input-layer fused form;
                               v16: adp_bn_fold_reset, adp_debug_grad_flat;
-                              v17: adp_wgrad_defer / adp_wgrad_flush */
+                              v17: adp_wgrad_defer / adp_wgrad_flush
+                              v18: adp_conv_io.act_outA */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -101,6 +102,11 @@ typedef struct adp_conv_io {
   float* bnr_dbeta;
   /* ADP_DTYPE_FP8 launches: per-GEMM-column dequantisation scale of W (adp_pack_weights_fp8) */
   const float* w_scale;
+  /* (v18) with bn_scaleA / bn_shiftA on a one-source adp_conv_fwd: relu(srcA*scale+shift) is also stored here
+     (srcA's shape and layout), bit-identical to adp_bn_apply(srcA) -> act_outA followed by the launch on
+     act_outA; the persistent halo forward (3x3, 64 / 128 channels, BatchNorm statistics) does both in one
+     launch, every other geometry runs exactly that pair */
+  void* act_outA;
 } adp_conv_io;
 
 /* ---- library ---------------------------------------------------------------------------- */

@@ -225,7 +225,7 @@ def test_unet_bn_forward_and_grads(dtype, base, S):
 
 
 @pytest.mark.parametrize("flag", ["fuse_head_bn", "head_recompute_dA", "fuse_bn_fold", "fuse_bn_wgrad",
-                                  "pool_argmax_from_z"])
+                                  "pool_argmax_from_z", "fuse_bn_load"])
 def test_unet_bn_fallback_paths_match_default(flag):
     """The alternate schedules nets.UNetBN keeps for A/B runs (each fusion flag off, and the pool backward's
     argmax read from the stored activation instead of recomputed from z) give the default path's outputs and
@@ -233,8 +233,9 @@ def test_unet_bn_fallback_paths_match_default(flag):
     sums are deterministic (f64 replicas fed fixed-order f32 partials, csrc/common.h) and every fused form computes
     the same f32 partials as its unfused pair, so the outputs are bit-identical (measured: max difference 0 for
     every flag, profiles/r04c_gates.log; round 3 allowed 1.5e-2 and gradient cosines down to 0.98, when f32
-    atomics in run order made even two runs of one path differ). Weight gradients: f32 atomic sums over blocks in
-    run order, within 1e-5."""
+    atomics in run order made even two runs of one path differ). Weight gradients within 1e-5 (the fused and unfused
+    weight-gradient kernels may sum a block's pixels in another order). Round 5 adds the BatchNorm-ReLU applied on
+    load by conv2 of levels 0-1 (fuse_bn_load); the second-stream weight gradients are in the determinism test."""
     B, L, S = 2, 3, 64
     w = R.unet_bn_keras_weights(levels=L, base=64, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
@@ -269,8 +270,8 @@ def test_unet_bn_bf16_runs_are_deterministic(levels, S):
     to 0.9895: profiles/r03_bf16_bn_nondeterminism.txt). Since round 5 the weight gradients are bit-identical too:
     the halo / input-layer / tap64 weight-gradient kernels write per-block slabs that a fixed-order reduce adds into
     dW (option wgrad_det), where f32 atomics in the order blocks finished used to move the last bits. The third run launches every
-    reduction at once (option wgrad_defer = 0) instead of batched at the end of the backward, the fourth keeps the
-    off-critical-path weight gradients on the backward's own stream (UNetBN.wgrad_side = False): the same bits."""
+    reduction at once (option wgrad_defer = 0) instead of batched at the end of the backward, the fourth puts the
+    off-critical-path weight gradients on a second stream (UNetBN.wgrad_side): the same bits."""
     B = 2
     w = R.unet_bn_keras_weights(levels=levels, base=64, in_ch=3, seed=5)
     x, y = synth_batch(B, S, C=3, seed=9)
@@ -280,12 +281,12 @@ def test_unet_bn_bf16_runs_are_deterministic(levels, S):
     runs = []
     for i in range(4):
         ops.set_option("wgrad_defer", 0 if i == 2 else None)
-        net.wgrad_side = i != 3
+        net.wgrad_side = i == 3
         try:
             outs, _ = _unet_bn_step(net, tr, x, y, B)
         finally:
             ops.set_option("wgrad_defer", None)
-            net.wgrad_side = True
+            net.wgrad_side = False
         runs.append((outs["main_out"].clone(), {n: [torch.as_tensor(g).clone() for g in net.get_layer_grads(n)]
                                                 for n in w}))
     p0, g0 = runs[0]

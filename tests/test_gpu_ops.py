@@ -957,6 +957,51 @@ def test_halop_swp_matches(parts, cout, split, S, grid, epi):
         assert relerr(res[1][1], res[0][1]) < 1e-6
 
 
+@pytest.mark.parametrize("C,cout,S,grid,opt", [(64, 64, 64, None, None), (64, 64, 96, 100, None),
+                                               (128, 128, 64, None, None), (128, 128, 32, 96, None),
+                                               (64, 96, 64, None, None), (64, 64, 64, None, "halop_bnl"),
+                                               (256, 128, 32, None, None)])
+def test_conv_bn_on_load_with_act_out(C, cout, S, grid, opt):
+    """adp_conv_io.act_outA (round 5): conv_fwd(z, bnA=(scale, shift), act_out=act) with BatchNorm statistics equals
+    bn_apply(z) -> act followed by conv_fwd(act) bit for bit: output, statistics and the stored activation. 64 -> 64
+    launches take the persistent halo forward's EPI 6 (one launch; also a static grid that does not divide the
+    patch count); 128-channel sources, 64 -> 96 outputs, option halop_bnl = 0 and a 256-channel source take the
+    library's two-launch fallback. Out-of-image halo pixels must stay 0 (relu(0 * scale + shift) would not be)."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16
+    N = 2
+    g = torch.Generator().manual_seed(61)
+    z = (torch.randn(N, S, S, C, generator=g) * 2).to(DEV, dt)
+    sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(C, generator=g) * 0.5 + 0.3).to(DEV)   # (mostly positive: a zero halo would show)
+    W = (torch.randn(ops.round_up(cout, 64), 9 * C, generator=g) * 0.03).to(DEV, dt)
+    act_ref = torch.zeros_like(z)
+    o_ref = torch.zeros(N, S, S, cout, dtype=dt, device=DEV)
+    st_ref = torch.zeros(2, cout, device=DEV)
+    ops.bn_apply(z, sc, sh, act_ref)
+    ops.conv_fwd(act_ref, W, cout, out=o_ref, bn_stats=(st_ref[0], st_ref[1]))
+    act = torch.full_like(z, 7.0)
+    o = torch.zeros_like(o_ref)
+    st = torch.zeros_like(st_ref)
+    if grid:
+        ops.set_option("halo_persist_grid", grid)
+    if opt:
+        ops.set_option(opt, 0)
+    try:
+        ops.conv_fwd(z, W, cout, out=o, bnA=(sc, sh), act_out=act, bn_stats=(st[0], st[1]))
+        kname = _lib.lib().adp_last_kernel().decode()
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("halo_persist_grid", None)
+        if opt:
+            ops.set_option(opt, None)
+    fused = C == 64 and cout == 64 and not opt
+    assert (", 6, " in kname) == fused, kname
+    assert torch.equal(act, act_ref)
+    assert torch.equal(o, o_ref), (o.float() - o_ref.float()).abs().max().item()
+    assert torch.equal(st, st_ref), relerr(st, st_ref)
+
+
 HALOP_WIDE_CASES = [
     # name, source channels, Nout, epilogue, split, up
     ("1ch_stats", [64], 64, "stats", False, 1),

@@ -79,7 +79,7 @@ def main():
     elif args.variant == "bnwgrad":
         owner, attr, old, new = UNetBN, "fuse_bn_wgrad", False, True
     elif args.variant == "side":
-        owner, attr, old, new = UNetBN, "wgrad_side", False, True   # (default True since round 5)
+        owner, attr, old, new = UNetBN, "wgrad_side", False, True
     elif args.variant == "opt":
         class _Opts:   # setattr(owner, attr, settings) applies a native option setting
             def __setattr__(self, _, st):
