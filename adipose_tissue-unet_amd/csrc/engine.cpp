@@ -974,8 +974,10 @@ struct adp_handle {
   float* stv(const BnLayer& l, int k) const { return l.st + (size_t)k * l.cout_s; }
   // conv -> BatchNorm statistics (epilogue, folded by the finalize) -> scale / shift -> relu(bn) materialised
   // (with its 2x2 max-pool when pool != nullptr; act == nullptr: the consumer applies it on load)
+  // bnA (training): srcA is layer bnA's pre-BatchNorm output, applied on load; its activation is stored to act_in by
+  // this launch (adp_conv_io.act_outA; nets.UNetBN.fuse_bn_load)
   int bn_conv(const std::string& name, int N, const void* srcA, const void* srcB, void* out, void* act, void* pool,
-              bool train, hipStream_t s) {
+              bool train, hipStream_t s, const BnLayer* bnA = nullptr, void* act_in = nullptr) {
     BnLayer& l = L(name);
     const int H = side(l.level), C = l.cout_s;
     adp_conv_desc d = desc3(N, H, l);
@@ -984,6 +986,11 @@ struct adp_handle {
     io.srcB = srcB;
     io.W = wfwd(l);
     io.out = out;
+    if (bnA) {
+      io.bn_scaleA = stv(*bnA, 2);
+      io.bn_shiftA = stv(*bnA, 3);
+      io.act_outA = act_in;
+    }
     if (!train && act) {
       // eval (nets.UNetBN._conv_eval_folded): the running-statistics BatchNorm is affine, so its scale goes into
       // the weights (f32 master rows x scale -> compute dtype) and its shift + ReLU into the conv epilogue, which
@@ -1043,24 +1050,31 @@ struct adp_handle {
     if (train) CL(adp_fill_f32(n_stat_fwd, 0.f, stat_fwd, s));
     const int Lv = levels;
     const void* src = b("x");
+    // training, bf16, 64-channel levels: conv2 applies conv1's BatchNorm-ReLU on load and stores the activation
+    // (nets.UNetBN.fuse_bn_load)
+    auto bnl = [&](int i) { return train && cfg.dtype == ADP_DTYPE_BF16 && L("enc" + std::to_string(i) + "_conv1").cout_s == 64; };
     for (int i = 0; i < Lv; ++i) {
       const std::string k = std::to_string(i);
-      CL(bn_conv("enc" + k + "_conv1", N, src, nullptr, b(("z" + k + "_1").c_str()), b(("az" + k + "_1").c_str()),
-                 nullptr, train, s));
-      CL(bn_conv("enc" + k + "_conv2", N, b(("az" + k + "_1").c_str()), nullptr, b(("z" + k + "_2").c_str()),
-                 b(("az" + k + "_2").c_str()), i < Lv - 1 ? b(("pool" + k).c_str()) : nullptr, train, s));
+      const bool f = bnl(i);
+      CL(bn_conv("enc" + k + "_conv1", N, src, nullptr, b(("z" + k + "_1").c_str()),
+                 f ? nullptr : b(("az" + k + "_1").c_str()), nullptr, train, s));
+      CL(bn_conv("enc" + k + "_conv2", N, b((f ? "z" + k + "_1" : "az" + k + "_1").c_str()), nullptr,
+                 b(("z" + k + "_2").c_str()), b(("az" + k + "_2").c_str()), i < Lv - 1 ? b(("pool" + k).c_str()) : nullptr,
+                 train, s, f ? &L("enc" + k + "_conv1") : nullptr, f ? b(("az" + k + "_1").c_str()) : nullptr));
       if (i < Lv - 1) src = b(("pool" + k).c_str());
     }
     const void* prev = b(("az" + std::to_string(Lv - 1) + "_2").c_str());
     for (int i = Lv - 2; i >= 0; --i) {
       const std::string k = std::to_string(i);
       CL(convt_fwd("dec" + k + "_up", N, prev, b(("t" + k).c_str()), s));
+      const bool f = bnl(i);
       CL(bn_conv("dec" + k + "_conv1", N, b(("az" + k + "_2").c_str()), b(("t" + k).c_str()),
-                 b(("y" + k + "_1").c_str()), b(("ay" + k + "_1").c_str()), nullptr, train, s));
+                 b(("y" + k + "_1").c_str()), f ? nullptr : b(("ay" + k + "_1").c_str()), nullptr, train, s));
       // level 0 in training: relu(bn(y0_2)) is only read by the head, which applies it on load; in eval the
       // folded conv writes it (nets.UNetBN.forward: head_bn only when training)
-      CL(bn_conv("dec" + k + "_conv2", N, b(("ay" + k + "_1").c_str()), nullptr, b(("y" + k + "_2").c_str()),
-                 i == 0 && train ? nullptr : b(("ay" + k + "_2").c_str()), nullptr, train, s));
+      CL(bn_conv("dec" + k + "_conv2", N, b((f ? "y" + k + "_1" : "ay" + k + "_1").c_str()), nullptr,
+                 b(("y" + k + "_2").c_str()), i == 0 && train ? nullptr : b(("ay" + k + "_2").c_str()), nullptr, train, s,
+                 f ? &L("dec" + k + "_conv1") : nullptr, f ? b(("ay" + k + "_1").c_str()) : nullptr));
       prev = b(("ay" + k + "_2").c_str());
     }
     const BnLayer& h = L("head");
