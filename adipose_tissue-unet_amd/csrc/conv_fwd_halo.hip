@@ -393,7 +393,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   // BNL: the applied halo chunk i of patch (img, y0, x0) (returned; v as loaded, zeros outside the image). Branch-free:
   // the act store goes through a buffer resource, lanes with nothing to store aim past its end
   const float* sS = reinterpret_cast<const float*>(smem + OFF_S);
-  const bool act_w = BNL && n0 == 0 && a.act_out != nullptr;
+  const bool act_w = BNL && n0 == 0 && a.act_out != nullptr && !(a.debug_flags & 4096);   // (fwd_debug bit 12: timing)
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       a.act_out, 0, act_w ? a.Nimg * a.Hs * a.Ws * a.CAs * 2 : 0, 0x00020000);
   auto bnl = [&](uint4 v, int img, int y0, int x0, int i) -> uint4 {
