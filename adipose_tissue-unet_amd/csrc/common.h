@@ -8,6 +8,16 @@
 //   * f32 is the parity dtype (exact f32 MFMA), bf16 the throughput dtype (f32 accumulate).
 #pragma once
 #include <hip/hip_runtime.h>
+
+// Timing-only ablation switches (options fwd_debug / wgrad_debug) are read by the kernels only in a library built
+// with -DADP_ABLATION (make ABLATION=1: tools that measure ablations build that variant into ab/). In the product build
+// ADP_DBG is the constant 0 and every ablation branch compiles away: as run-time branches inside the K loops they cost
+// the halo weight gradient 8 % (its waits were selected per column block at run time; profiles/r05_bisect.log).
+#ifdef ADP_ABLATION
+#define ADP_DBG(a) ((a).debug_flags)
+#else
+#define ADP_DBG(a) 0
+#endif
 #include <stdint.h>
 #include <algorithm>
 #include <cmath>

@@ -411,7 +411,7 @@ template <int NTH, int BN>
 ADP_DEV void epi_bn_flush(const FwdArgs& a, float* red, int n0, int tid, const float (&bs)[8],
                           const float (&bq)[8]) {
   constexpr int GPR = BN / 8;
-  if (a.debug_flags & 2) return;
+  if (ADP_DBG(a) & 2) return;
   ADP_LDS_BARRIER();
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = bs[j]; red[tid * 16 + 8 + j] = bq[j]; }

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8_kernel(FwdArgs a) {
       }
     }
   }
-  if (!a.bn_sum || (a.debug_flags & 2)) return;
+  if (!a.bn_sum || (ADP_DBG(a) & 2)) return;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void igemm_fwd_cin8p_kernel(FwdArgs a) {
     gather(g0 + 2 * step, xa);
     pass(g0 + step, xb);
   }
-  if (!a.bn_sum || (a.debug_flags & 2)) return;
+  if (!a.bn_sum || (ADP_DBG(a) & 2)) return;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll

@@ -393,7 +393,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   // BNL: the applied halo chunk i of patch (img, y0, x0) (returned; v as loaded, zeros outside the image). Branch-free:
   // the act store goes through a buffer resource, lanes with nothing to store aim past its end
   const float* sS = reinterpret_cast<const float*>(smem + OFF_S);
-  const bool act_w = BNL && n0 == 0 && a.act_out != nullptr && !(a.debug_flags & 4096);   // (fwd_debug bit 12: timing)
+  const bool act_w = BNL && n0 == 0 && a.act_out != nullptr && !(ADP_DBG(a) & 4096);   // (fwd_debug bit 12: timing)
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       a.act_out, 0, act_w ? a.Nimg * a.Hs * a.Ws * a.CAs * 2 : 0, 0x00020000);
   auto bnl = [&](uint4 v, int img, int y0, int x0, int i) -> uint4 {
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   auto load_halo = [&](int t, uint4 (&hr)[GH]) {   // registers <- the halo of patch t
     int img1, y01, x01;
     tile_origin(t, img1, y01, x01);
-    const bool nohalo = (a.debug_flags & 1024) != 0;   // timing-only ablation (fwd_debug bit 10): no halo loads
+    const bool nohalo = (ADP_DBG(a) & 1024) != 0;   // timing-only ablation (fwd_debug bit 10): no halo loads
 #pragma unroll
     for (int i = 0; i < GH; ++i) {
       const uint4* p = nohalo ? nullptr : halo_src(img1, y01, x01, i);
@@ -799,7 +799,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
     epi_all(accp, zreg, mrowp, dreg);
   }
   if (dyn && tid == 0) claim_block_done(a.claim, NT, G);   // (every claim of the block has returned)
-  if (!stats || (a.debug_flags & 2)) return;   // (uniform)
+  if (!stats || (ADP_DBG(a) & 2)) return;   // (uniform)
   double* d0 = a.stat + (size_t)((blockIdx.x * 8 + wave) & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
 #pragma unroll
   for (int nf = 0; nf < NF; ++nf)

@@ -335,7 +335,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   }
   T64_BAR();   // the epilogue reuses the stages
 
-  if (a.debug_flags & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue at all
+  if (ADP_DBG(a) & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue at all
 #pragma unroll
     for (int i = 0; i < 2 * MIQ; ++i)
 #pragma unroll

@@ -243,7 +243,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     }
     return r;
   };
-  const bool l2_only = (a.debug_flags & 256) != 0;   // (fwd_debug bit 8)
+  const bool l2_only = (ADP_DBG(a) & 256) != 0;   // (fwd_debug bit 8)
   auto issue = [&](const Kt& k, int buf) {
     // A0 B0 B1 A1
 #pragma unroll
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
     return t * BM;
   };
   auto pix = [&](int m0, int p) { return HALO ? m0 + (p >> 5) * a.Wo + (p & 31) : m0 + p; };
-  const bool no_dma = (a.debug_flags & 32) != 0;   // timing-only ablation (fwd_debug bit 5): the K loop
+  const bool no_dma = (ADP_DBG(a) & 32) != 0;   // timing-only ablation (fwd_debug bit 5): the K loop
                                                     // multiplies whatever the prologue loaded
   int nissued = 0;
   // HALO: one 16-B group g of the halo of chunk c of tile k into slot `slot`; returns whether this wave
@@ -623,7 +623,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           pix = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
         }
         // (timing-only ablation, fwd_debug bit 7: every store to an out-of-range offset, dropped)
-        const unsigned off = v && !(a.debug_flags & 128) ? (unsigned)((pix * ostr + cq) * oes) : P_OOB;
+        const unsigned off = v && !(ADP_DBG(a) & 128) ? (unsigned)((pix * ostr + cq) * oes) : P_OOB;
         if constexpr (F32) {
           const f32x4 o4 = {x[0], x[1], x[2], x[3]};
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32_t, o4), rsO, off, 0, 0);
@@ -730,7 +730,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
             const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
             pixo = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
           }
-          const unsigned off = mv && cv && !(a.debug_flags & 128) ? (unsigned)((pixo * ostr + cq) * OES) : P_OOB;
+          const unsigned off = mv && cv && !(ADP_DBG(a) & 128) ? (unsigned)((pixo * ostr + cq) * OES) : P_OOB;
           __builtin_amdgcn_raw_buffer_store_b128(st, rsO, off, 0, 0);
         }
         if (stats) {
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
             pixo = (img * Hq + 2 * yo + (subp[pi] >> 1)) * Wq + 2 * xo + (subp[pi] & 1);
           }
           const unsigned off =
-              mv && cvp[pi] && !(a.debug_flags & 128) ? (unsigned)((pixo * ostrp[pi] + cqp[pi]) * OES) : P_OOB;
+              mv && cvp[pi] && !(ADP_DBG(a) & 128) ? (unsigned)((pixo * ostrp[pi] + cqp[pi]) * OES) : P_OOB;
           __builtin_amdgcn_raw_buffer_store_b128(st, rsOp[pi], off, 0, 0);
         }
       }
@@ -905,7 +905,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
           const int img = m / HWo, rem = m - img * HWo, yo = rem / a.Wo, xo = rem - yo * a.Wo;
           pixo = (img * Hq + 2 * yo + (sub >> 1)) * Wq + 2 * xo + (sub & 1);
         }
-        const unsigned off = mv && cv && !(a.debug_flags & 128) ? (unsigned)(pixo * a.out_stride + cq) : P_OOB;
+        const unsigned off = mv && cv && !(ADP_DBG(a) & 128) ? (unsigned)(pixo * a.out_stride + cq) : P_OOB;
         __builtin_amdgcn_raw_buffer_store_b128(st, rsO, off, 0, 0);
       }
     }
@@ -992,7 +992,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
         if constexpr (WREG) {
           // the stage and the halo groups were written by every wave's ds_write at earlier steps
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        } else if (a.debug_flags & 64) {   // timing-only ablation (fwd_debug bit 6): LDS-DMA issued, never waited for
+        } else if (ADP_DBG(a) & 64) {   // timing-only ablation (fwd_debug bit 6): LDS-DMA issued, never waited for
         } else if (gs + NST - 2 >= lsteps) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (last_epi > gs - NST) {
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * LOPS) : "memory");
       if (dyn && !full && gs == 0 && tid == 0) claim_publish<-1>(ring + 1, c1val);   // tile 1 (claimed in the prologue)
       // (timing-only ablation, fwd_debug bit 9: no barrier -- the stages race, the values are garbage)
-      if (!(a.debug_flags & 512)) P_BAR();   // stage cs landed for every wave, nobody reads the stage being refilled
+      if (!(ADP_DBG(a) & 512)) P_BAR();   // stage cs landed for every wave, nobody reads the stage being refilled
       if constexpr (ZALL) {
         if (!zissued && lk > k) {   // the loader is past this tile: z before the next tile's first stage
           load_zall(m0c);
@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
       cs = cs == NST - 1 ? 0 : cs + 1;
     }
     last_epi = gs - 1;
-    if (a.debug_flags & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue
+    if (ADP_DBG(a) & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue
 #pragma unroll
       for (int i = 0; i < 2 * MIQ; ++i)
 #pragma unroll
@@ -1070,7 +1070,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_tap64p_kernel(FwdArgs a) {
 
   if (dyn && tid == 0) claim_block_done(a.claim, ntn, G);   // (every claim of the block has returned)
   // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
-  if (!stats || (a.debug_flags & 2)) return;
+  if (!stats || (ADP_DBG(a) & 2)) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
   double* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;

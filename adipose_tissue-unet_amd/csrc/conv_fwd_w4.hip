@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256, 1) void igemm_fwd_w4_kernel(FwdArgs a) {
 
   // ---- BatchNorm sums of the block -> its replica of the accumulators (folded by the launcher)
   if constexpr (STATS) {
-    if (a.debug_flags & 2) return;
+    if (ADP_DBG(a) & 2) return;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     double* rep = a.stat + (size_t)(blockIdx.x & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;

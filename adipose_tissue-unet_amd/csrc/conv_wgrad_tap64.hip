@@ -374,7 +374,7 @@ __global__ __launch_bounds__(WN * WK * 64, (wg64_occ<WN, WK, TNW>())) void igemm
   }
 
   const int col = lane & 15, rq = (lane >> 4) * 4;
-  if (a.debug_flags & 1) {   // timing-only ablation: keep the accumulators live, skip the atomics
+  if (ADP_DBG(a) & 1) {   // timing-only ablation: keep the accumulators live, skip the atomics
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // = tap
-  const int dbg = a.debug_flags;   // timing-only ablations (option wgrad_debug): bits 0-3, see below
+  const int dbg = ADP_DBG(a);   // timing-only ablations (option wgrad_debug): bits 0-3, see below
   prio_static<ADP_PRIO_WGRAD>(wave);
   const int dy = wave / 3, dx = wave - 3 * (wave / 3);
   const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
@@ -898,7 +898,7 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   }
   if (dyn && tid == 0) claim_block_done(a.claim, combos, gridDim.x);   // (every claim of the block has returned)
   if (!any && !a.part) return;   // (dyn: a block that started late found the work taken; a slab gets its zeros)
-  if (a.debug_flags & 1) {
+  if (ADP_DBG(a) & 1) {
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
@@ -1304,7 +1304,7 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   // (wgrad_det, default on: every split launch writes slabs, summed by the fixed-order reduce: two runs give the
   //  same bits)
   const bool det = adp::option("wgrad_det", 1) != 0;
-  if (splits > 1 && (det || adp::option("wgrad_partials", TN >= 256 ? 1 : 0)) && !(a.debug_flags & 1))
+  if (splits > 1 && (det || adp::option("wgrad_partials", TN >= 256 ? 1 : 0)) && !(ADP_DBG(a) & 1))
     a.part = det ? adp::reduce_part(0, slab * splits * sizeof(float), s)
                  : static_cast<float*>(adp::scratch(0, slab * splits * sizeof(float)));
   adp::set_kernel("igemm_wgrad_tap64_kernel<%d, %d, %d, %s, %s>", WN, WK, TNW, two ? "true" : "false",
@@ -1481,7 +1481,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     const int tiles = a.Nimg * (a.Ho / 8) * (a.Wo / 32);
     const int grid = std::max(1, std::min(tiles, option("wgrad_cin8_grid", 256)));
     // wgrad_det (default on): per-block slabs [grid][64][Kpad] + the fixed-order reduce instead of f32 atomics
-    a.part = option("wgrad_det", 1) && !(a.debug_flags & 1)
+    a.part = option("wgrad_det", 1) && !(ADP_DBG(a) & 1)
                  ? reduce_part(0, (size_t)grid * 64 * a.Kpad * sizeof(float), s) : nullptr;
     if (a.bna_dA) {
       adp::set_kernel("igemm_wgrad_cin8_kernel<true>");
@@ -1516,7 +1516,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     // wgrad_det = 0 or claimed patches: f32 atomics in the order blocks finish
     a.part = nullptr;
     a.part_rmw = 0;
-    const bool det = !a.claim && option("wgrad_det", 1) && !(a.debug_flags & 1);
+    const bool det = !a.claim && option("wgrad_det", 1) && !(ADP_DBG(a) & 1);
     if (det && per == 1) a.part_rmw = 1;
     else if (det) a.part = reduce_part(0, (size_t)per * a.Nout * a.Kpad * sizeof(float), s);
     // (a failed scratch allocation leaves part null: the atomic form)

@@ -2,8 +2,9 @@
 """Timing probe of the level-0 conv2 with the BatchNorm-ReLU applied on load (halo forward EPI 6) against the plain
 launch and the bn_apply pass it replaces (unet_bn L0: 4 x 1024^2 x 64 -> 64, statistics). Arms: plain conv on the
 activation; bn_apply alone; the fused launch; the fused launch without its activation stores (fwd_debug bit 12,
-timing only); the fused launch without the halo apply VALU is not separable. Prints ms per launch (20 launches,
-median of 5 repeats)."""
+timing only: run with ADP_LIB_PATH=ab/libadipose_ablation.so from tools/build_ablation_lib.sh, the product library
+ignores the option); the fused launch without the halo apply VALU is not separable. Prints ms per launch (20 launches,
+median of 5 repeats).""" 
 import os
 import sys
 
