@@ -383,8 +383,10 @@ ADP_DEV void epi_rows_bnr(const FwdArgs& a, const float* tile, int rows, int m0,
     grp_from_f(gr, v);
     grp_store(gr, reinterpret_cast<TO*>(a.out) + (size_t)m * a.out_stride + n);
     grp_to_f(gr, v);   // the stored (rounded) gradient
-    grp_load(gr, reinterpret_cast<const TO*>(a.bnr_z) + (size_t)m * a.bnr_zs + n);
+    if (ADP_DBG(a) & 8192) grp_zero(gr);   // (timing-only ablation, fwd_debug bit 13: no z loads)
+    else grp_load(gr, reinterpret_cast<const TO*>(a.bnr_z) + (size_t)m * a.bnr_zs + n);
     grp_to_f(gr, f);
+    if (ADP_DBG(a) & 16384) continue;   // (fwd_debug bit 14: no sums)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const float4 sc = *reinterpret_cast<const float4*>(a.bnr_sc + n + 4 * h);
