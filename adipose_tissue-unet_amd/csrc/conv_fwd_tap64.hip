@@ -87,7 +87,10 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int OA1 = QA * ROWB, OB0 = BM * ROWB, OB1 = (BM + QB) * ROWB;
   constexpr int EPI = TM * (BN + 4) * 4;
-  constexpr int SMEM = cmax(cmax(2 * STAGE, EPI), NTH * 16 * 4);
+  constexpr int SMEM0 = cmax(cmax(2 * STAGE, EPI), NTH * 16 * 4);
+  // BNL (BN-backward reduction, bf16, buffer resources): + the per-channel parameters of the LDS-staged epilogue
+  constexpr bool BNRL = BNR && BUF && !F32 && !F8;
+  constexpr int SMEM = SMEM0 + (BNRL ? 4 * BN * 4 : 0);
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -342,6 +345,90 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
+  // ---- BN-backward-reduction epilogue through LDS only (option tap64_bnr_lds, round 5): per wave row group the z rows
+  // come in by LDS-DMA while the group's accumulators are staged as bf16 (the values the launch stores, rounded once as
+  // grp_from_f rounds them), and the row loop reads dA, z and the per-channel parameters from LDS: no row waits on a
+  // global load (epi_rows_bnr issues each row's z load behind that row's store; at level 2 the z reads were two thirds
+  // of an epilogue that took 29 % of the launch). Same values and sums, same order: bit-identical.
+  if constexpr (BNRL) {
+    if (a.bnr_lds && !a.addend && !a.mask) {
+      constexpr int LTB = BN + 8;                         // bf16 per staged row (+16 B: rows start on other banks)
+      constexpr int ZOFF = TM * LTB * 2;                  // z rows of the group: 16-B chunks, row-major
+      constexpr int GPR = BN / 8, RSTEP = NTH / GPR;
+      constexpr int ZCH = TM * GPR, GZ = ZCH / NTH;
+      static_assert(ZOFF + TM * BN * 2 <= SMEM0 && GZ * NTH == ZCH, "LDS-staged BNR epilogue layout");
+      bf16* t16 = reinterpret_cast<bf16*>(smem);
+      float* prm = reinterpret_cast<float*>(smem + SMEM0);   // scale | shift | mean | invstd, BN each
+      if (tid < BN) {
+        const int c = n0 + tid;
+        const bool v = c < a.Nout;
+        prm[tid] = v ? a.bnr_sc[c] : 0.f;
+        prm[BN + tid] = v ? a.bnr_sh[c] : 0.f;
+        prm[2 * BN + tid] = v ? a.bnr_mean[c] : 0.f;
+        prm[3 * BN + tid] = v ? a.bnr_invstd[c] : 0.f;
+      }
+      const __amdgpu_buffer_rsrc_t rsZ =
+          __builtin_amdgcn_make_buffer_rsrc((void*)a.bnr_z, 0, a.M * a.bnr_zs * 2, T64_RSRC3);
+      const int col = lane & 15, rq = (lane >> 4) * 4;
+      const int cg = tid % GPR, n = n0 + cg * 8;
+      float bs[8], bq[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { bs[j] = 0.f; bq[j] = 0.f; }
+      for (int p = 0; p < WM; ++p) {
+        const int mb = m0 + p * TM;
+#pragma unroll
+        for (int i = 0; i < GZ; ++i) {
+          const int idx = i * NTH + tid, row = idx / GPR, cc = idx - row * GPR, m = mb + row;
+          const unsigned off =
+              m < a.M && n0 + cc * 8 < a.Nout ? (unsigned)(((size_t)m * a.bnr_zs + n0 + cc * 8) * 2) : T64_OOB;
+          buf_lds16(rsZ, smem + ZOFF + (size_t)(i * NTH + wave * 64) * 16, off);
+        }
+        if (wr == p) {
+#pragma unroll
+          for (int mt = 0; mt < 2 * MIQ; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                t16[((mt / MIQ) * HM + (mt % MIQ) * 16 + rq + r) * LTB + wc * 64 + nt * 16 + col] = (bf16)acc[mt][nt][r];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's z chunks landed
+        ADP_LDS_BARRIER();                                  // every thread's, and the staging
+        if (n < a.Nout) {
+          for (int row = tid / GPR; row < TM; row += RSTEP) {
+            const int m = mb + row;
+            if (m >= a.M) break;
+            Grp<bf16> gd, gz;
+            gd.v = *reinterpret_cast<const uint4*>(t16 + row * LTB + cg * 8);
+            gz.v = *reinterpret_cast<const uint4*>(smem + ZOFF + (size_t)(row * GPR + cg) * 16);
+            grp_store(gd, reinterpret_cast<bf16*>(a.out) + (size_t)m * a.out_stride + n);
+            float v[8], f[8];
+            grp_to_f(gd, v);
+            grp_to_f(gz, f);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const float4 sc = *reinterpret_cast<const float4*>(prm + cg * 8 + 4 * h);
+              const float4 sh = *reinterpret_cast<const float4*>(prm + BN + cg * 8 + 4 * h);
+              const float4 mu = *reinterpret_cast<const float4*>(prm + 2 * BN + cg * 8 + 4 * h);
+              const float4 is = *reinterpret_cast<const float4*>(prm + 3 * BN + cg * 8 + 4 * h);
+              const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+              const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int jj = 4 * h + j;
+                const float db = fmaf(f[jj], scv[j], shv[j]) > 0.f ? v[jj] : 0.f;
+                bs[jj] += db;
+                bq[jj] += db * (f[jj] - muv[j]) * isv[j];
+              }
+            }
+          }
+        }
+        ADP_LDS_BARRIER();   // the group's rows are read out: the next group's DMA and staging may overwrite them
+      }
+      epi_bn_flush<NTH, BN>(a, reinterpret_cast<float*>(smem), n0, tid, bs, bq);
+      return;
+    }
+  }
   // ---- epilogue: one wave row group (TM rows x BN) at a time through LDS
   float* tile = reinterpret_cast<float*>(smem);
   constexpr int LT = BN + 4;
@@ -501,6 +588,9 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   // f32: the persistent halo form for the 256x128 choice (3x3 stride-1 layers; falls through otherwise)
   if (cfg == 1 && a.f32 && launch_fwd_tap64p(a, s, 1)) return 1;
   a.kpipe = option("tap64_kpipe", 0);   // (opt-in: +1-1.5 % on the BN-backward data gradients, profiles/r03_kpipe_ab.txt)
+  // (LDS-staged BN-backward epilogue: level 2 256 -> 256 -9 %, level 3 1024 -> 512 -3 %, others within 1 %;
+  //  profiles/r05_bnrlds_kernels.log)
+  a.bnr_lds = option("tap64_bnr_lds", 1) && (size_t)a.M * a.bnr_zs * 2 < ((size_t)1 << 31);
   if (a.f32 && cfg == 0) cfg = 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);

@@ -1002,6 +1002,42 @@ def test_conv_bn_on_load_with_act_out(C, cout, S, grid, opt):
     assert torch.equal(st, st_ref), relerr(st, st_ref)
 
 
+@pytest.mark.parametrize("N,H,W,cin,cout,cfg", [(2, 32, 32, 256, 256, 2), (1, 24, 40, 256, 192, 2),
+                                                (2, 16, 64, 128, 128, 5), (1, 32, 32, 512, 256, 2)])
+def test_tap64_bnr_lds_epilogue(N, H, W, cin, cout, cfg):
+    """The tap64 data gradient's LDS-staged BN-backward-reduction epilogue (option tap64_bnr_lds: z by LDS-DMA, dA
+    staged as bf16) against the row-serial epilogue: the stored gradient bit for bit and the same dgamma / dbeta sums
+    (same values, same order); ragged pixel counts (M not a multiple of the 256-row tile) and a 192-wide N tile."""
+    from adipose_amd import _lib
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(71)
+    x = torch.randn(N, H, W, cin, generator=g).to(DEV, dt)
+    z = (torch.randn(N, H, W, cout, generator=g) * 2).to(DEV, dt)
+    W_ = (torch.randn(ops.round_up(cout, 64), 9 * cin, generator=g) * 0.03).to(DEV, dt)
+    vec = lambda: (torch.rand(cout, generator=g) + 0.5).to(DEV)   # noqa: E731
+    sc, sh, mu, ist = vec(), vec() - 1.0, vec() - 1.0, vec()
+    res = []
+    for lds in (0, 1):
+        o = torch.zeros(N, H, W, cout, dtype=dt, device=DEV)
+        dg, db = torch.zeros(cout, device=DEV), torch.zeros(cout, device=DEV)
+        ops.set_option("tap64_bnr_lds", lds)
+        ops.set_option("fwd_tap64", cfg)
+        ops.set_option("fwd_halo", 0)
+        try:
+            ops.conv_fwd(x, W_, cout, out=o, bn_reduce=(z, sc, sh, mu, ist, dg, db))
+            kname = _lib.lib().adp_last_kernel().decode()
+            torch.cuda.synchronize()
+        finally:
+            for k in ("tap64_bnr_lds", "fwd_tap64", "fwd_halo"):
+                ops.set_option(k, None)
+        assert kname.startswith("igemm_fwd_tap64_kernel<") and ", true, true," in kname, kname
+        res.append((o, dg, db))
+    (o0, g0, b0), (o1, g1, b1) = res
+    assert torch.equal(o0, o1)
+    assert torch.equal(g0, g1) and torch.equal(b0, b1), (relerr(g1, g0), relerr(b1, b0))
+    assert g0.abs().sum().item() > 0
+
+
 HALOP_WIDE_CASES = [
     # name, source channels, Nout, epilogue, split, up
     ("1ch_stats", [64], 64, "stats", False, 1),
