@@ -1534,10 +1534,12 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     } else if (option("wgrad_halop_waves", 8) == 9) {
       adp::set_kernel("igemm_wgrad_halop_kernel<9, false, 8, true>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
-    } else if (stat_inst && (option("wgrad_halop_pf", 1) == 2 ||
-                             (option("wgrad_halop_pf", 1) == 1 && a.M <= option("wgrad_halop_pf_maxm", 1 << 19)))) {
-      // (row-pipelined form: levels 2-4 of the bench, M <= 2^19 pixels; at levels 0-1 the plain loop is 1-4 % ahead,
-      //  profiles/r05_wgrad_variants.log: option wgrad_halop_pf 0 never, 1 by M, 2 always)
+    } else if (stat_inst && (option("wgrad_halop_pf", 2) == 2 ||
+                             (option("wgrad_halop_pf", 2) == 1 && a.M <= option("wgrad_halop_pf_maxm", 1 << 19)))) {
+      // (row-pipelined form; option wgrad_halop_pf 0 never, 1 only where M <= 2^19 pixels, 2 always -- the default:
+      //  at levels 0-1 the plain loop is 1-4 % ahead per launch (profiles/r05_wgrad_variants.log) but the step does not
+      //  move (22.627 vs 22.632 ms, r05_pfauto_ab.log), and one instance for every launch keeps the step's dominant
+      //  kernel the same instantiation round to round)
       // (option wgrad_halop_spread: the next patch's LDS-DMA over patch rows 0-3 (4, default) or 0-7 (8))
       const int spr = option("wgrad_halop_spread", 4);
       if (spr == 8) {
