@@ -49,6 +49,7 @@ struct FwdArgs {
   int claim_full;        // claiming: every tile claimed, none static (option claim_full; conv_common.h)
   void* act_out;         // with scA / shA: relu(srcA * scA + shA) stored here too (adp_conv_io.act_outA)
   int bnr_lds;           // tap64 BN-backward-reduction launches: the LDS-staged epilogue (option tap64_bnr_lds)
+  int mask_lds;          // tap64 mask / addend launches: mask and addend rows by LDS-DMA (option tap64_mask_lds)
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]

@@ -429,6 +429,100 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       return;
     }
   }
+  // ---- mask / addend epilogue through LDS (option tap64_mask_lds, round 5: the adipose_v3 data gradients). Per half
+  // row group the mask and addend rows come in by LDS-DMA while the half's f32 accumulators are staged, so no row
+  // waits on a global load (epi_rows loads each row's addend and mask behind that row's store: at level 2 of the bf16
+  // adipose_v3 step that epilogue was 36 % of the launch, profiles/r05_mask_epi_probe.log). Plain stores with bias,
+  // addend, mask and BatchNorm statistics only (the host checks); epi_rows' arithmetic in its order: bit-identical.
+  {
+    constexpr int ESZ = F32 ? 4 : 2;
+    constexpr int H2 = TM / 2;
+    constexpr int MOFF = H2 * (BN + 4) * 4;            // f32 staging of half a row group, then the mask and addend rows
+    constexpr int AOFF = MOFF + H2 * BN * ESZ;
+    constexpr int CPR = BN * ESZ / 16;                 // 16-B chunks per row
+    constexpr bool MAL = BUF && !F8 && !BNR && AOFF + H2 * BN * ESZ <= SMEM0 && (H2 * CPR) % NTH == 0;
+    if constexpr (MAL) {
+      if (a.mask_lds && (a.mask || a.addend)) {
+        constexpr int GQ = H2 * CPR / NTH, GPR = BN / 8, RSTEP = NTH / GPR, LT = BN + 4;
+        float* st = reinterpret_cast<float*>(smem);
+        const TO* mk = reinterpret_cast<const TO*>(smem + MOFF);
+        const TO* ad = reinterpret_cast<const TO*>(smem + AOFF);
+        const __amdgpu_buffer_rsrc_t rsM = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)a.mask, 0, a.mask ? a.M * a.mask_stride * ESZ : 0, T64_RSRC3);
+        const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)a.addend, 0, a.addend ? a.M * a.addend_stride * ESZ : 0, T64_RSRC3);
+        const int col = lane & 15, rq = (lane >> 4) * 4;
+        const int cg = tid % GPR, n = n0 + cg * 8;
+        float bias[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bias[j] = a.bias && n + j < a.Nout ? a.bias[n + j] : 0.f;
+        float bs[8], bq[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { bs[j] = 0.f; bq[j] = 0.f; }
+        for (int p = 0; p < WM; ++p) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int mb = m0 + p * TM + h * H2;
+#pragma unroll
+            for (int i = 0; i < GQ; ++i) {
+              const int idx = i * NTH + tid, row = idx / CPR, cq = idx - row * CPR, m = mb + row;
+              const int c = n0 + cq * (16 / ESZ);
+              const bool ok = m < a.M && c < a.Nout;
+              const size_t lo = (size_t)(i * NTH + wave * 64) * 16;
+              if (a.mask) buf_lds16(rsM, smem + MOFF + lo, ok ? (unsigned)(((size_t)m * a.mask_stride + c) * ESZ) : T64_OOB);
+              if (a.addend)
+                buf_lds16(rsD, smem + AOFF + lo, ok ? (unsigned)(((size_t)m * a.addend_stride + c) * ESZ) : T64_OOB);
+            }
+            if (wr == p) {
+#pragma unroll
+              for (int mi = 0; mi < MIQ; ++mi)
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                  for (int r = 0; r < 4; ++r)
+                    st[(mi * 16 + rq + r) * LT + wc * 64 + nt * 16 + col] = acc[h * MIQ + mi][nt][r];
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's mask / addend chunks landed
+            ADP_LDS_BARRIER();
+            if (n < a.Nout) {
+              for (int row = tid / GPR; row < H2; row += RSTEP) {
+                const int m = mb + row;
+                if (m >= a.M) break;
+                float v[8], f[8];
+                const float4* tp = reinterpret_cast<const float4*>(st + row * LT + cg * 8);
+                const float4 t0 = tp[0], t1 = tp[1];
+                v[0] = t0.x; v[1] = t0.y; v[2] = t0.z; v[3] = t0.w; v[4] = t1.x; v[5] = t1.y; v[6] = t1.z; v[7] = t1.w;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] += bias[j];
+                Grp<TO> gr;
+                if (a.addend) {
+                  grp_load(gr, ad + row * BN + cg * 8);
+                  grp_to_f(gr, f);
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) v[j] += f[j];
+                }
+                if (a.mask) {
+                  grp_load(gr, mk + row * BN + cg * 8);
+                  grp_to_f(gr, f);
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) v[j] = f[j] > 0.f ? v[j] * a.mask_scale : 0.f;
+                }
+                grp_from_f(gr, v);
+                grp_store(gr, reinterpret_cast<TO*>(a.out) + (size_t)m * a.out_stride + n);
+                if (a.bn_sum) {
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) { bs[j] += v[j]; bq[j] += v[j] * v[j]; }
+                }
+              }
+            }
+            ADP_LDS_BARRIER();   // the half is read out: the next half's DMA and staging may overwrite it
+          }
+        }
+        if (a.bn_sum) epi_bn_flush<NTH, BN>(a, reinterpret_cast<float*>(smem), n0, tid, bs, bq);
+        return;
+      }
+    }
+  }
   // ---- epilogue: one wave row group (TM rows x BN) at a time through LDS
   float* tile = reinterpret_cast<float*>(smem);
   constexpr int LT = BN + 4;
@@ -591,6 +685,13 @@ int launch_fwd_tap64(FwdArgs& a, hipStream_t s) {
   // (LDS-staged BN-backward epilogue: level 2 256 -> 256 -9 %, level 3 1024 -> 512 -3 %, others within 1 %;
   //  profiles/r05_bnrlds_kernels.log)
   a.bnr_lds = option("tap64_bnr_lds", 1) && (size_t)a.M * a.bnr_zs * 2 < ((size_t)1 << 31);
+  {
+    const size_t es = a.f32 ? 4 : 2, lim = (size_t)1 << 31;
+    a.mask_lds = option("tap64_mask_lds", 1) && !a.f8 && !a.bnr_z && a.out && a.out_mode == 0 && !a.relu &&
+                 a.drop_rate == 0.f && !a.accum && a.out_stride % 8 == 0 &&
+                 (!a.mask || ((size_t)a.mask_stride * es % 16 == 0 && (size_t)a.M * a.mask_stride * es < lim)) &&
+                 (!a.addend || ((size_t)a.addend_stride * es % 16 == 0 && (size_t)a.M * a.addend_stride * es < lim));
+  }
   if (a.f32 && cfg == 0) cfg = 1;
   if (cfg == 0) launch_cfg<2, 4, 128>(a, s);
   else if (cfg == 1) launch_cfg<4, 2, 64>(a, s);

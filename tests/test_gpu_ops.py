@@ -1038,6 +1038,42 @@ def test_tap64_bnr_lds_epilogue(N, H, W, cin, cout, cfg):
     assert g0.abs().sum().item() > 0
 
 
+@pytest.mark.parametrize("dt,N,H,W,cin,cout,mask,add,stats", [
+    ("bf16", 2, 32, 32, 192, 192, True, True, False), ("bf16", 1, 24, 40, 128, 96, True, False, True),
+    ("bf16", 2, 16, 32, 256, 256, False, True, False), ("f32", 2, 32, 32, 64, 64, True, False, False),
+    ("f32", 1, 24, 40, 96, 96, True, True, True)])
+def test_tap64_mask_lds_epilogue(dt, N, H, W, cin, cout, mask, add, stats):
+    """The tap64 kernel's LDS-staged mask / addend epilogue (option tap64_mask_lds: the rows come in by LDS-DMA) against
+    the row-serial epilogue, bf16 and f32: the stored output bit for bit and the same BatchNorm sums; ragged pixel
+    counts and N tiles wider than Nout."""
+    from adipose_amd import _lib
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    g = torch.Generator().manual_seed(73)
+    x = torch.randn(N, H, W, cin, generator=g).to(DEV, tdt)
+    W_ = (torch.randn(ops.round_up(cout, 64), ops.round_up(9 * cin, 32), generator=g) * 0.03).to(DEV, tdt)
+    mk = (torch.rand(N, H, W, cout, generator=g) > 0.4).to(DEV, tdt) if mask else None
+    ad = torch.randn(N, H, W, cout, generator=g).to(DEV, tdt) if add else None
+    res = []
+    for lds in (0, 1):
+        o = torch.zeros(N, H, W, cout, dtype=tdt, device=DEV)
+        st = torch.zeros(2, cout, device=DEV)
+        ops.set_option("tap64_mask_lds", lds)
+        ops.set_option("fwd_halo", 0)
+        ops.set_option("tap64_persist", 0)
+        try:
+            ops.conv_fwd(x, W_, cout, out=o, mask=mk, mask_scale=2.0, addend=ad,
+                         bn_stats=(st[0], st[1]) if stats else None)
+            kname = _lib.lib().adp_last_kernel().decode()
+            torch.cuda.synchronize()
+        finally:
+            for k in ("tap64_mask_lds", "fwd_halo", "tap64_persist"):
+                ops.set_option(k, None)
+        assert kname.startswith("igemm_fwd_tap64_kernel<"), kname
+        res.append((o, st))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 HALOP_WIDE_CASES = [
     # name, source channels, Nout, epilogue, split, up
     ("1ch_stats", [64], 64, "stats", False, 1),
