@@ -930,8 +930,8 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s) {
       //  the 89 us of the apply pass it saves: profiles/r05u_*. Such launches take the two-launch form.)
       return 0;
     }
-    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s%s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
-                    pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false", swp ? ", true" : "");
+    adp::set_kernel("igemm_fwd_halop_kernel<%s, %d, %d, %s, %d, %s, %s, %s>", bnr ? "true" : "false", one_chunk ? 1 : 2, bn,
+                    pipe ? "true" : "false", epi, wide ? "true" : "false", dyn ? "true" : "false", swp ? "true" : "false");
 #define HALOP_LAUNCH_WD(NCH_, BN_, W_, D_, P_)                                                                   \
   do {                                                                                                      \
     if (bnr) hipLaunchKernelGGL((igemm_fwd_halop_kernel<true, NCH_, BN_, false, 0, false, D_, P_>), dim3(grid), dim3(512), 0, s, a); \

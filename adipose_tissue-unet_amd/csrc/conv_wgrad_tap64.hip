@@ -1522,17 +1522,17 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     // (a failed scratch allocation leaves part null: the atomic form)
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
       if (option("wgrad_halop_spread", 4) == 8) {
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8, true>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 8, true, false>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 8>), dim3(grid), dim3(512), 0, s, a);
       } else if (stat_inst) {
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4, false>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4, false, false>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 4, false>), dim3(grid), dim3(512), 0, s, a);
       } else {   // halo groups two a row over rows 3-5
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4, true>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4, true, false>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 4>), dim3(grid), dim3(512), 0, s, a);
       }
     } else if (option("wgrad_halop_waves", 8) == 9) {
-      adp::set_kernel("igemm_wgrad_halop_kernel<9, false, 8, true>");
+      adp::set_kernel("igemm_wgrad_halop_kernel<9, false, 8, true, false>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);
     } else if (stat_inst && (option("wgrad_halop_pf", 2) == 2 ||
                              (option("wgrad_halop_pf", 2) == 1 && a.M <= option("wgrad_halop_pf_maxm", 1 << 19)))) {
@@ -1550,17 +1550,17 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false, true>), dim3(grid), dim3(512), 0, s, a);
       }
     } else if (stat_inst && option("wgrad_halop_spread", 4) != 8) {
-      adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false>");
+      adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, false, false>");
       hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4, false>), dim3(grid), dim3(512), 0, s, a);
     } else {
       // the next patch's loads over rows 0-3 (3 groups a row) leave 4 rows of DMA slack before the patch
       // barrier: +1-3 % on every level but 0 64->64 against rows 0-7, step -0.3 %
       // (profiles/r02_wgrad_spread_ab.txt); option wgrad_halop_spread=8 keeps the all-rows schedule
       if (option("wgrad_halop_spread", 4) == 8) {
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 8, true>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 8, true, false>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 8>), dim3(grid), dim3(512), 0, s, a);
       } else {
-        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, true>");
+        adp::set_kernel("igemm_wgrad_halop_kernel<8, false, 4, true, false>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, false, 4>), dim3(grid), dim3(512), 0, s, a);
       }
     }

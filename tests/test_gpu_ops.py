@@ -1485,7 +1485,7 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.set_option("wgrad_halop_pf", 0)   # the unpipelined row loop: the same per-block sums
         dWn = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dWn, l.Nout, srcB=srcB)
-        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false>"
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false, false>"
         ops.set_option("wgrad_halop_pf", None)
         ops.set_option("wgrad_halop_spread", 8)   # next patch's loads over all 8 patch rows
         dWp8 = torch.zeros_like(dW)
@@ -1494,7 +1494,7 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.set_option("wgrad_halop_pf", 0)
         dWs = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dWs, l.Nout, srcB=srcB)
-        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 8, true>"
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 8, true, false>"
         ops.set_option("wgrad_halop_pf", None)
         ops.set_option("wgrad_halop_waves", 9)   # one wave per tap
         dW9 = torch.zeros_like(dW)

@@ -173,3 +173,30 @@ def test_claim_atomic_result_retired_before_use(code_objects):
                     bad.append((_demangle([fn])[0], hex(addr), p[:3]))
     assert checked > 0, "no claim atomic found in the persistent forward's code object"
     assert not bad, bad
+
+
+def test_reported_kernel_names_exist(code_objects):
+    """Every name the library reports for a launch (adp::set_kernel, read back by adp_last_kernel and used as the bench's
+    roofline key) is the full demangled name of a kernel in the code objects, as rocprofv3 prints it: the per-kernel
+    timing and the committed kernel-trace summaries must name the same instantiation (round 5: several names had
+    dropped defaulted template arguments)."""
+    src_dir = os.path.join(ROOT, "adipose_tissue-unet_amd", "csrc")
+    pats = []
+    for f in sorted(os.listdir(src_dir)):
+        if f.endswith((".hip", ".cpp", ".h")):
+            text = open(os.path.join(src_dir, f)).read()
+            for m in re.finditer(r'set_kernel\(\s*"([A-Za-z0-9_]+_kernel<[^"]*>)"', text):
+                pats.append((f, m.group(1)))
+    assert len(pats) > 20
+    names = set()
+    for co in code_objects.values():
+        notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], capture_output=True,
+                               text=True).stdout
+        for d in _demangle(re.findall(r"\.name:\s+(\S+)", notes)):
+            names.add(d.split("(")[0])
+    missing = []
+    for f, p in pats:
+        rx = re.escape(p).replace("%d", r"-?\d+").replace("%s", "(true|false)")
+        if not any(re.fullmatch(rx, n) for n in names):
+            missing.append((f, p))
+    assert not missing, missing
