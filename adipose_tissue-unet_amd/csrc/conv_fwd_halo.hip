@@ -509,7 +509,16 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
         zr[mf][nf] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
       }
   };
-  auto load_z = [&](int mrow_, uint2 (&zr)[2][NF]) { load_q(rsZ, a.bnr_zs, n0, mrow_, zr); };
+  auto load_z = [&](int mrow_, uint2 (&zr)[2][NF]) {
+    if (ADP_DBG(a) & 8192) {   // (timing-only ablation, fwd_debug bit 13: no z loads)
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) zr[mf][nf] = uint2{0u, 0u};
+      return;
+    }
+    load_q(rsZ, a.bnr_zs, n0, mrow_, zr);
+  };
   // epilogue of accumulator tile (mf, nf): lane = pixel mrow_ + mf*16 + r16, channels nf*16 + 4*h4 .. +3;
   // returns the stored quad (the BatchNorm sums are taken here), epi_unit / epi_pair store it
   auto epi_vals = [&](int mf, int nf, const f32x4& av, uint2 zv, int mrow_, uint2 dv = uint2{0u, 0u}) -> bf16x4 {
@@ -540,6 +549,7 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
       o[i] = (bf16)v[i];
     }
     if constexpr (BNR) {
+      if (ADP_DBG(a) & 16384) return o;   // (timing-only ablation, fwd_debug bit 14: no BN-backward sums)
       const float4 sc = *reinterpret_cast<const float4*>(cst + BN + c0);
       const float4 sh = *reinterpret_cast<const float4*>(cst + 2 * BN + c0);
       const float4 nm = *reinterpret_cast<const float4*>(cst + 3 * BN + c0);
