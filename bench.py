@@ -133,6 +133,7 @@ def committed_traffic(kernel, workload, build):
     never used. The third value says whether the profiled library build is the one running now."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    hits = []
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -143,8 +144,12 @@ def committed_traffic(kernel, workload, build):
             continue
         e = d.get(kernel)
         if e and e.get("traffic_bytes") is not None:
-            return int(e["traffic_bytes"]), os.path.basename(f), meta.get("build") == build
-    return None, None, None
+            hits.append((int(e["traffic_bytes"]), os.path.basename(f), meta.get("build") == build))
+    # a summary of the running build first (file names sort by round, not by time within a round), else the last
+    for h in hits:
+        if h[2]:
+            return h
+    return hits[0] if hits else (None, None, None)
 
 
 def dice_leg(args):
