@@ -906,15 +906,19 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
     asm volatile("" ::"v"(acc8[0]), "v"(acc8[1]));
     return;
   }
-  // dW[n][tap * 64 + c] += acc: each wave's 16-row blocks through LDS into 256-B rows. Three forms (launcher): f32
-  // atomics into dW; plain stores into this block's slab (block index lin of its combination: a fixed-order reduce
-  // launch adds the slabs into dW, so the result does not depend on the order the blocks finish); or, with one block
-  // per combination, dW += partial by plain load + store (the block owns those dW elements)
+  // dW[n][tap * 64 + c] += acc: each wave's 16-row blocks through LDS, out as 16-B pieces (16 lanes per 256-B row,
+  // four rows per instruction; round 5: a quarter of the row form's store instructions, which all blocks issue at
+  // once at the end of the launch). Three forms (launcher): f32 atomics into dW; plain stores into this block's slab
+  // (block index lin of its combination: a fixed-order reduce launch adds the slabs into dW, so the result does not
+  // depend on the order the blocks finish); or, with one block per combination, dW += partial by plain load + store
+  // (the block owns those dW elements)
   constexpr int ES = 68;
   float* blk = reinterpret_cast<float*>(smem) + wave * 16 * ES;
   const int col = lane & 15, rq = (lane >> 4) * 4;
-  const int kk = wave * (a.CAs + a.CBs) + ch * 64 + lane;
   float* dW = a.part ? a.part + ((size_t)lin * a.Nout + (size_t)nblk * 64) * a.Kpad : a.dW + (size_t)nblk * 64 * a.Kpad;
+  // (the per-lane part of an address is a 32-bit offset, the row part wave-uniform)
+  const int voff = wave * (a.CAs + a.CBs) + ch * 64 + col * 4 + (lane >> 4) * a.Kpad;
+  const int lrd = (lane >> 4) * ES + col * 4;
   auto out = [&](auto put) {
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
@@ -924,20 +928,35 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
         for (int r = 0; r < 4; ++r) blk[(rq + r) * ES + cb * 16 + col] = acc[nb][cb][r];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
-      for (int i = 0; i < 16; ++i) put(dW + (size_t)(nb * 16 + i) * a.Kpad + kk, blk[i * ES + lane]);
+      for (int j = 0; j < 4; ++j)
+        put(dW + (size_t)(nb * 16 + j * 4) * a.Kpad + voff, *reinterpret_cast<const float4*>(blk + j * 4 * ES + lrd));
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    if (NW == 8) {   // this wave's eighth of tap 8: rows nb8 * 16 + rq + r, columns cb8 * 16 + {0..31}
+  };
+  // this wave's eighth of tap 8: rows nb8 * 16 + rq + r, columns cb8 * 16 + {0..31}
+  auto out8 = [&](auto put1) {
+    if constexpr (NW == 8) {
       const int k8 = 8 * (a.CAs + a.CBs) + ch * 64 + cb8 * 16 + col;
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) put(dW + (size_t)(nb8 * 16 + rq + r) * a.Kpad + k8 + 16 * j2, acc8[j2][r]);
+        for (int r = 0; r < 4; ++r) put1(dW + (size_t)(nb8 * 16 + rq + r) * a.Kpad + k8 + 16 * j2, acc8[j2][r]);
     }
   };
-  if (a.part) out([](float* p, float v) { *p = v; });
-  else if (a.part_rmw) out([](float* p, float v) { *p += v; });
-  else out([](float* p, float v) { atomicAdd(p, v); });
+  if (a.part) {
+    out([](float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; });
+    out8([](float* p, float v) { *p = v; });
+  } else if (a.part_rmw) {
+    out([](float* p, float4 v) {
+      float4 o = *reinterpret_cast<float4*>(p);
+      o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+      *reinterpret_cast<float4*>(p) = o;
+    });
+    out8([](float* p, float v) { *p += v; });
+  } else {
+    out([](float* p, float4 v) { atomicAdd(p, v.x); atomicAdd(p + 1, v.y); atomicAdd(p + 2, v.z); atomicAdd(p + 3, v.w); });
+    out8([](float* p, float v) { atomicAdd(p, v); });
+  }
 }
 
 // Weight gradient of the input layers (one 8-channel source, 3x3 stride 1, 64 outputs; K = 72): an
@@ -1517,7 +1536,7 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     a.part = nullptr;
     a.part_rmw = 0;
     const bool det = !a.claim && option("wgrad_det", 1) && !(ADP_DBG(a) & 1);
-    if (det && per == 1) a.part_rmw = 1;
+    if (det && per == 1 && ((uintptr_t)a.dW & 15) == 0) a.part_rmw = 1;   // (16-B pieces of dW: aligned dW only)
     else if (det) a.part = reduce_part(0, (size_t)per * a.Nout * a.Kpad * sizeof(float), s);
     // (a failed scratch allocation leaves part null: the atomic form)
     if (a.bna_dA) {   // the caller checked wgrad_bna_fusable
