@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 
 class AdpError(RuntimeError):
@@ -38,7 +38,8 @@ class ConvDesc(C.Structure):
         ("out2_stride", C.c_int), ("split_c", C.c_int),
         ("mask_stride", C.c_int), ("mask_scale", C.c_float),
         ("mask2_stride", C.c_int), ("mask2_scale", C.c_float),
-        ("accum_stride", C.c_int), ("bnr_stride", C.c_int), ("out_fp8", C.c_int), ("bn_defer_fold", C.c_int)]
+        ("accum_stride", C.c_int), ("bnr_stride", C.c_int), ("out_fp8", C.c_int), ("bn_defer_fold", C.c_int),
+        ("CA_real", C.c_int), ("CB_real", C.c_int), ("Nout_real", C.c_int)]
 
 
 class ConvIO(C.Structure):

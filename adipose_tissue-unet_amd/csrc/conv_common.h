@@ -50,6 +50,8 @@ struct FwdArgs {
   void* act_out;         // with scA / shA: relu(srcA * scA + shA) stored here too (adp_conv_io.act_outA)
   int bnr_lds;           // tap64 BN-backward-reduction launches: the LDS-staged epilogue (option tap64_bnr_lds)
   int mask_lds;          // tap64 mask / addend launches: mask and addend rows by LDS-DMA (option tap64_mask_lds)
+  int ztail;             // zero tails of the weights (adp_conv_desc CA_real / CB_real / Nout_real): bit 0 every source a
+                         // 64-channel stride with <= 48 real channels, bit 1 Nout == 64 with <= 48 real columns
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]

@@ -69,10 +69,17 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, u
 // KP: the K loop compiled in -- -1 either, chosen at run time by a.kpipe (the fp8 / f32 forms); 0 the plain double
 // buffer only; 2 the same without the nearest-x2 upsample gather (launches with up == 1, option tap64_up1); 1 the
 // mid-step-barrier loop only (bf16 forms: one loop per instance leaves the register allocator
-// one schedule, as the persistent kernel's EPIC does for its epilogues)
+// one schedule, as the persistent kernel's EPIC does for its epilogues); 4-6 (F32, WN == 1, round 5) the plain
+// loop with the zero tails ZT = KP - 3 of FwdArgs::ztail skipped: bit 0 -- every source is a 64-channel stride whose
+// weight columns [48, 64) are zeros (44-channel f32 layers), so the upper 16 channels of every odd K step (the
+// source's channels 48-63) are neither read from LDS nor multiplied (the loop runs two steps per trip, so the step
+// parity is known at compile time); bit 1 -- Nout == 64 with zero weight rows [48, 64): the 16-column MFMA group
+// 48-63 is skipped and its accumulators stay 0. The skipped products are exact zeros: the same values.
 template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8, bool F32 = false, int KP = -1>
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   static_assert(!(F8 && F32), "one operand dtype");
+  constexpr int ZT = KP >= 4 ? KP - 3 : 0;
+  static_assert(ZT == 0 || (F32 && WN == 1 && !BNR), "zero-tail forms: f32, 64-column tiles");
   using TO = typename std::conditional<F32, float, bf16>::type;   // output dtype
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
@@ -203,12 +210,13 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   };
 
   const int r16 = lane & 15, h4 = lane >> 4;
-  auto readA = [&](int buf, int h, bf16x8 (&fa)[MIQ][2]) {
+  auto readA = [&](int buf, int h, bf16x8 (&fa)[MIQ][2], bool ktail = false) {
     const unsigned char* base = smem + buf * STAGE + h * OA1;
 #pragma unroll
     for (int mi = 0; mi < MIQ; ++mi)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        if ((ZT & 1) && ktail && s == 1) continue;
         const int q = wr * HM + mi * 16 + r16, c = 4 * s + h4;
         fa[mi][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
       }
@@ -219,6 +227,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        if ((ZT & 2) && h == 1 && ni == 1) continue;
         const int q = wc * 32 + ni * 16 + r16, c = 4 * s + h4;
         fb[ni][s] = *reinterpret_cast<const bf16x8*>(base + q * ROWB + ((c ^ swz(q)) << 4));
       }
@@ -229,7 +238,7 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   for (int i = 0; i < 2 * MIQ; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb) {
+  auto mma = [&](const bf16x8 (&fa)[MIQ][2], const bf16x8 (&fb)[2][2], int ha, int hb, bool ktail = false) {
     if constexpr (F32)
       if (hb ? skip1 : skip0) return;
     prio_hi<ADP_PRIO_T64>();
@@ -248,6 +257,8 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
         for (int mi = 0; mi < MIQ; ++mi)
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni) {
+            if ((ZT & 1) && ktail && s == 1) continue;
+            if ((ZT & 2) && hb == 1 && ni == 1) continue;
             const f32x4 av = __builtin_bit_cast(f32x4, fa[mi][s]), bv = __builtin_bit_cast(f32x4, fb[ni][s]);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -314,6 +325,32 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
         if (late && t + 2 < nk) issue_step(buf);
       }
     }
+  } else if constexpr (ZT != 0) {
+    // (the plain loop below, two K steps per trip: the second is the odd one; nk is even, the launcher checks)
+    auto step = [&](int t, auto odd) {
+      constexpr bool kt = decltype(odd)::value && (ZT & 1);
+      const int buf = t & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      T64_BAR();
+      if (t + 1 < nk) {
+        const Kt k1 = kinfo();
+        issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
+      }
+      readA(buf, 0, fa, kt);
+      readB(buf, 0, fb0);
+      mma(fa, fb0, 0, 0, kt);
+      readB(buf, 1, fb1);
+      mma(fa, fb1, 0, 1, kt);
+      readA(buf, 1, fa, kt);
+      mma(fa, fb1, 1, 1, kt);
+      mma(fa, fb0, 1, 0, kt);
+    };
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+      step(t, std::false_type{});
+      step(t + 1, std::true_type{});
+    }
+    if (t < nk) step(t, std::false_type{});   // (an odd nk: bit 1 only)
   } else
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
@@ -590,6 +627,17 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, true>), g, b, 0, s, a);   \
   } while (0)
   if (a.f32) {
+    // zero tails (FwdArgs::ztail, option f32_ztail): the KP 4-6 instances of the 64-column tile
+    if constexpr (WN == 1 && TM == 64) {
+      const int zt = adp::option("f32_ztail", 1) && buf && !a.bnr_z && !a.kpipe ? a.ztail & 3 : 0;
+      if (zt) {
+        adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, true, false, false, true, %d>", WM, WN, TM, zt + 3);
+        if (zt == 1) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false, true, 4>), g, b, 0, s, a);
+        else if (zt == 2) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false, true, 5>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false, true, 6>), g, b, 0, s, a);
+        return;
+      }
+    }
     if (a.bnr_z) {
       if (buf) T64_LAUNCH32(true, true);
       else T64_LAUNCH32(false, true);

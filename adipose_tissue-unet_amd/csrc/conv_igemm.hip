@@ -1062,6 +1062,11 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
   a.f32 = 0;
   a.stat = (a.bn_sum || a.bnr_z) ? adp::stat_scratch() : nullptr;
   a.act_out = io->act_outA;
+  // zero tails of the weights (the caller's real channel counts, adp_conv_desc v19): products with zero weight
+  // columns / rows that a kernel may skip exactly
+  auto tail48 = [](int stride, int real) { return stride == 64 && real > 0 && real <= 48; };
+  a.ztail = (tail48(d->CA_stride, d->CA_real) && (d->CB_stride == 0 || tail48(d->CB_stride, d->CB_real)) ? 1 : 0) |
+            (tail48(d->Nout, d->Nout_real) && d->out_mode == 0 ? 2 : 0);
 }
 
 // after a launch whose epilogue added BatchNorm sums into the replicas: fold them into the caller's

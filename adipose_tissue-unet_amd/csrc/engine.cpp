@@ -460,6 +460,10 @@ struct adp_handle {
     d.dil = l.dil;
     d.pad = l.dil;
     d.Nout = l.cout_s;
+    // real channel counts: the pad weight columns / rows are zeros (adp_conv_desc v19 hints, nets.Dense.real_fwd)
+    d.CA_real = l.cin[0];
+    d.CB_real = l.cin.size() > 1 ? l.cin[1] : 0;
+    d.Nout_real = l.cout;
     d.relu = 1;
     d.out_stride = l.cout_s;
     d.mask_scale = d.mask2_scale = 1.f;
@@ -519,6 +523,8 @@ struct adp_handle {
     d.dil = l.dil;
     d.pad = l.dil;
     d.Nout = l.Cin_s;
+    d.CA_real = l.cout;   // (hints as in conv(): nets.Dense.real_dgrad)
+    d.Nout_real = l.cin.size() == 1 ? l.cin[0] : 0;
     d.mask_scale = mscale;
     d.mask2_scale = 1.f;
     io.srcA = dZ;
@@ -527,6 +533,7 @@ struct adp_handle {
     if (skip_first) {
       io.W = static_cast<const char*>(l.Wd) + (size_t)l.cin_s[0] * l.dKpad * es;
       d.Nout = l.cin_s[1];
+      d.Nout_real = l.cin[1];
       ostride = l.cin_s[1];
       out = out2;
       mask = mask2;

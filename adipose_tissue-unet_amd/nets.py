@@ -98,6 +98,10 @@ class Dense:
         self.dtaps = 4 if transpose else self.taps
         self.dK = self.dtaps * self.cout_s
         self.dKpad = round_up(self.dK, 32)
+        # real channel counts of the forward / data-gradient launches (ops.conv_fwd real=: the pad weight columns and
+        # rows are zeros, which the f32 tap kernel may skip)
+        self.real_fwd = (cin_parts[0], cin_parts[1] if len(cin_parts) > 1 else 0, cout)
+        self.real_dgrad = (cout, 0, cin_parts[0] if len(cin_parts) == 1 else 0)
         # (+64 rows for concat inputs so the decoder-only row slice of a split data-gradient stays
         #  a valid [Npad][Kpad] operand)
         self.dNpad = round_up(self.Cin_s, 64) + (64 if len(self.cin_parts) > 1 else 0)
@@ -365,7 +369,7 @@ class UNetEngine:
         return ops.conv_fwd(srcA, self.Wf(l.name), l.Nout, out=out, srcB=srcB, bnA=bnA, bnB=bnB,
                             bias=self.bias(l.name) if l.bias else None, up=l.up, kh=l.k, kw=l.k, dil=l.dil,
                             relu=l.relu and not l.bn, dropout_rate=dropout, dropout_seed=seed, accum=accum,
-                            bn_stats=bn_stats, defer_fold=defer_fold, act_out=act_out)
+                            bn_stats=bn_stats, defer_fold=defer_fold, act_out=act_out, real=l.real_fwd)
 
     def wgrad(self, l, srcA, dZ, *, srcB=None, bnA=None, bnB=None, bias_grad=True, bn_apply=None):
         dW = self.ps.gview(l.name + "/W")
@@ -393,13 +397,13 @@ class UNetEngine:
             # only the second (decoder) part of a concat input is needed: offset the weight rows
             Wsub = Wd[l.cin_s[0]:]
             return ops.conv_fwd(dZ, Wsub, l.cin_s[1], out=out2, kh=l.k, kw=l.k, dil=l.dil, mask=mask2,
-                                mask_scale=mask2_scale)
+                                mask_scale=mask2_scale, real=(l.cout, 0, l.cin_parts[1]))
         if split:
             return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=l.k, kw=l.k, dil=l.dil, out_mode=2, out2=out2,
                                 split_c=l.cin_s[0], addend=addend, mask=mask, mask_scale=mask_scale,
-                                mask2=mask2, mask2_scale=mask2_scale, bn_stats=bn_stats)
+                                mask2=mask2, mask2_scale=mask2_scale, bn_stats=bn_stats, real=(l.cout, 0, 0))
         return ops.conv_fwd(dZ, Wd, l.Cin_s, out=out, kh=l.k, kw=l.k, dil=l.dil, addend=addend, mask=mask,
-                            mask_scale=mask_scale, bn_reduce=bn_reduce)
+                            mask_scale=mask_scale, bn_reduce=bn_reduce, real=l.real_dgrad)
 
 
 # --------------------------------------------------------------------------------- adipose_v3

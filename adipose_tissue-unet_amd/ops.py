@@ -161,8 +161,12 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
              kh=3, kw=3, dil=1, pad=None, Ho=None, Wo=None, relu=False, dropout_rate=0.0, dropout_seed=0,
              out_mode=0, shuffle_c=0, out2=None, split_c=0, addend=None, mask=None, mask_scale=1.0,
              mask2=None, mask2_scale=1.0, accum=None, bn_stats=None, bn_reduce=None, w_scale=None,
-             defer_fold=False, act_out=None):
+             defer_fold=False, act_out=None, real=None):
     """Implicit-GEMM conv forward-shaped launch (conv, conv dgrad, convT fwd/dgrad).
+
+    real=(CA_real, CB_real, Nout_real) (optional hints, adp_conv_desc v19): the unpadded channel counts of the
+    sources and of the GEMM columns whose pad weight columns / rows are zeros (every packed layer's are); the
+    f32 tap kernel then skips the products with those zero weights (44-channel layers in 64-channel strides).
 
     bnA=(scale, shift) with act_out (one source): srcA is read pre-BatchNorm, relu(srcA*scale+shift) is what the
     conv multiplies and is also stored to act_out (adp_conv_io.act_outA: one launch on the persistent halo forward,
@@ -176,6 +180,10 @@ def conv_fwd(srcA, W, nout, *, out=None, srcB=None, bnA=None, bnB=None, bias=Non
     on the stream must be bn_finalize(..., fold=True) on the same two vectors."""
     d, io, N, Ho, Wo = _desc_io(srcA, W, srcB, bnA, bnB, bias, up, stride, kh, kw, dil, pad, Ho, Wo, nout)
     d.relu = 1 if relu else 0
+    if real is not None:
+        ca, cb, nr = (int(v) for v in real)
+        _check(0 <= ca <= d.CA_stride and 0 <= cb <= d.CB_stride and 0 <= nr <= nout, "real channel counts out of range")
+        d.CA_real, d.CB_real, d.Nout_real = ca, cb, nr
     d.dropout_rate = float(dropout_rate)
     d.dropout_seed = int(dropout_seed) & 0xFFFFFFFF
     d.out_mode = out_mode

@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 18 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 19 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
@@ -41,7 +41,8 @@ extern "C" {
                               v15: adp_conv_wgrad_bn with dY = NULL (dz not stored), input-layer fused form;
                               v16: adp_bn_fold_reset, adp_debug_grad_flat;
                               v17: adp_wgrad_defer / adp_wgrad_flush
-                              v18: adp_conv_io.act_outA */
+                              v18: adp_conv_io.act_outA;
+                              v19: adp_conv_desc.CA_real / CB_real / Nout_real (zero-weight hints) */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -71,6 +72,11 @@ typedef struct adp_conv_desc {
   int bn_defer_fold;        /* 1: leave this launch's BatchNorm statistics in the library's accumulator
                                replicas instead of adding them into io->bn_sum / bn_sqsum; the next launch
                                on the stream must be adp_bn_finalize_fold for those two vectors */
+  int CA_real, CB_real;     /* v19, optional (0 = unknown): real channels of source A / B when the weight
+                               columns of the pad channels [real, stride) are zeros (packed layers) */
+  int Nout_real;            /* v19, optional (0 = unknown): real GEMM columns when weight rows [real, Nout)
+                               are zeros. With these hints a kernel may skip products with zero weights
+                               (f32 44-channel layers in 64-channel strides); results are unchanged */
 } adp_conv_desc;
 
 typedef struct adp_conv_io {

@@ -26,14 +26,14 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_error_plumbing():
     lib = _lib.lib()
-    assert lib.adp_abi_version() == _lib.ABI_VERSION == 18
+    assert lib.adp_abi_version() == _lib.ABI_VERSION == 19
     assert isinstance(lib.adp_last_error(), bytes)
 
 
 def test_conv_desc_layout_matches_header():
     # 15 ints, float, uint, 6 ints, float, int, float, int, int, int (out_fp8), int (bn_defer_fold)
     # -> 30 4-byte fields
-    assert ctypes.sizeof(_lib.ConvDesc) == 30 * 4
+    assert ctypes.sizeof(_lib.ConvDesc) == 33 * 4
     # 16 operand pointers + 7 fused BatchNorm-backward reduction pointers + fp8 weight scales + act_outA (v18)
     assert ctypes.sizeof(_lib.ConvIO) == 25 * 8
 

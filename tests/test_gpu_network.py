@@ -108,6 +108,43 @@ def test_adipose_grads(dtype, cpad, S, hard_mining, adipose_weights):
             assert cos(torch.as_tensor(gk), k.grad) > 0.99, name
 
 
+def test_adipose_f32_zero_tail_skip_is_exact(adipose_weights):
+    """f32 adipose_v3 (44-channel level-0 layers in 64-channel strides): the tap kernel's zero-tail forms (option
+    f32_ztail, default on; the real channel counts passed by nets.py) skip the products with the zero pad weights --
+    forward probabilities bit-identical to the launches that multiply them, parameter gradients to the f32 weight-
+    gradient atomics' run-to-run order (each zero-tail launch is bit-exact: test_gpu_ops.py::test_f32_zero_tail_forms)."""
+    from adipose_amd import _lib
+    B, S = 2, 64
+    x, y = synth_batch(B, S, seed=4)
+    res = []
+    for zt in (0, 1):
+        ops.set_option("f32_ztail", zt)
+        try:
+            net = build_adipose("f32", adipose_weights, B, S)
+            tr = Trainer(net, LossConfig(use_hard_mining=True))
+            a = net.acts(B)
+            ops.prep_input(x.to(DEV), a["x"], mean=0.0, std=1.0)
+            outs = net.forward(B, train=False)
+            grads = tr.loss_and_grads(outs, y.to(DEV))
+            ops.fill(net.ps.grad, 0.0)
+            net.backward(grads)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_option("f32_ztail", None)
+        o = outs if isinstance(outs, dict) else dict(enumerate(outs))
+        res.append(({k: v.clone() for k, v in o.items() if torch.is_tensor(v)},
+                    {n: net.get_layer_grads(n) for n in adipose_weights}))
+    assert res[0][0].keys() == res[1][0].keys() and res[0][0]
+    for k in res[0][0]:
+        assert torch.equal(res[0][0][k], res[1][0][k]), k
+    # the f32 weight gradients add per-block partials with f32 atomics in the order blocks finish (4-7e-7 between
+    # identical runs, profiles/r04e_f32_step_determinism.txt): gradients to 1e-5 of each layer's largest element
+    for n in adipose_weights:
+        for g0, g1 in zip(res[0][1][n], res[1][1][n]):
+            g0, g1 = torch.as_tensor(g0), torch.as_tensor(g1)
+            assert (g0 - g1).abs().max().item() <= 1e-5 * max(g0.abs().max().item(), 1e-12), n
+
+
 def test_adipose_frozen_encoder_grads(adipose_weights):
     """Phase 1: encoder frozen -> encoder grads exactly zero, decoder grads unchanged."""
     B, S = 2, 64

@@ -1074,6 +1074,72 @@ def test_tap64_mask_lds_epilogue(dt, N, H, W, cin, cout, mask, add, stats):
     assert torch.equal(res[0][1], res[1][1])
 
 
+ZTAIL_CASES = [
+    # name, real channels of the sources (stride 64 each), Nout (stride), real Nout, up, epilogue, expected ZT
+    ("1src_both", [44], 64, 44, False, "relu_stats", 3),
+    ("2src_both_mask_add", [44, 44], 64, 44, False, "mask_add", 3),
+    ("1src_ntail", [64], 64, 44, False, "relu_stats", 2),
+    ("1src_ktail", [44], 64, 64, False, "relu_stats", 1),
+    ("1src_up2_both", [44], 64, 44, True, "relu_stats", 3),
+    ("1src_n40_k8", [8], 64, 40, False, "relu_stats", 3),
+]
+
+
+@pytest.mark.parametrize("case", ZTAIL_CASES, ids=[c[0] for c in ZTAIL_CASES])
+def test_f32_zero_tail_forms(case):
+    """f32 tap kernel, zero-tail forms (KP 4-6; adp_conv_desc CA_real / CB_real / Nout_real, ABI v19): sources of
+    64-channel stride with <= 48 real channels skip the upper 16 channels of every odd K step, Nout 64 with <= 48 real
+    columns the MFMA group 48-63 -- the skipped weights are the pad zeros of every packed layer. Output and BatchNorm
+    sums bit-identical to the launch without the hints (ragged pixel count, bias, ReLU, mask, addend, upsample)."""
+    from adipose_amd import _lib
+    name, reals, nout, nreal, up, epi, zt = case
+    g = torch.Generator().manual_seed(97)
+    N, H, W = 2, 24, 40
+    Hs, Ws = (H // 2, W // 2) if up else (H, W)
+    xs = []
+    for r in reals:
+        x = torch.zeros(N, Hs, Ws, 64)
+        x[..., :r] = torch.randn(N, Hs, Ws, r, generator=g)
+        xs.append(x.to(DEV))
+    cin_s = 64 * len(reals)
+    Wt = torch.zeros(64, ops.round_up(9 * cin_s, 32))
+    for t in range(9):
+        for p, r in enumerate(reals):
+            Wt[:nreal, t * cin_s + 64 * p: t * cin_s + 64 * p + r] = torch.randn(nreal, r, generator=g) * 0.05
+    Wt = Wt.to(DEV)
+    bias = torch.zeros(64)
+    bias[:nreal] = torch.randn(nreal, generator=g) * 0.1
+    bias = bias.to(DEV)
+    mk = (torch.rand(N, H, W, 64, generator=g) > 0.4).float().to(DEV) if epi == "mask_add" else None
+    ad = torch.randn(N, H, W, 64, generator=g).to(DEV) if epi == "mask_add" else None
+    res = []
+    for hint in (False, True):
+        o = torch.zeros(N, H, W, 64, device=DEV)
+        st = torch.zeros(2, 64, device=DEV)
+        ops.set_option("fwd_halo", 0)
+        ops.set_option("tap64_persist", 0)
+        try:
+            real = (reals[0], reals[1] if len(reals) > 1 else 0, nreal) if hint else None
+            if epi == "mask_add":
+                ops.conv_fwd(xs[0], Wt, nout, out=o, srcB=xs[1] if len(xs) > 1 else None, up=up, mask=mk,
+                             mask_scale=2.0, addend=ad, real=real)
+            else:
+                ops.conv_fwd(xs[0], Wt, nout, out=o, srcB=xs[1] if len(xs) > 1 else None, up=up, bias=bias,
+                             relu=True, bn_stats=(st[0], st[1]), real=real)
+            kname = _lib.lib().adp_last_kernel().decode()
+            torch.cuda.synchronize()
+        finally:
+            for k in ("fwd_halo", "tap64_persist"):
+                ops.set_option(k, None)
+        assert kname.startswith("igemm_fwd_tap64_kernel<4, 1, 64,"), kname
+        assert kname.endswith(f", {zt + 3}>" if hint else ", -1>"), kname
+        res.append((o, st))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    if epi != "mask_add" and nreal < 64:   # (the zero weight rows: zero pad channels; an addend's pad channels pass through)
+        assert res[1][0][..., nreal:].abs().max().item() == 0
+
+
 HALOP_WIDE_CASES = [
     # name, source channels, Nout, epilogue, split, up
     ("1ch_stats", [64], 64, "stats", False, 1),
