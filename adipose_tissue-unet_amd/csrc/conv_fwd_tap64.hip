@@ -70,7 +70,7 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, u
 // buffer only; 2 the same without the nearest-x2 upsample gather (launches with up == 1, option tap64_up1); 1 the
 // mid-step-barrier loop only (bf16 forms: one loop per instance leaves the register allocator
 // one schedule, as the persistent kernel's EPIC does for its epilogues); 4-6 (F32, WN == 1, round 5) the plain
-// loop with the zero tails ZT = KP - 3 of FwdArgs::ztail skipped: bit 0 -- every source is a 64-channel stride whose
+// loop with the zero tails ZT = KP - 3 of FwdArgs::ztail skipped (bit 1: WN == 1 only): bit 0 -- every source is a 64-channel stride whose
 // weight columns [48, 64) are zeros (44-channel f32 layers), so the upper 16 channels of every odd K step (the
 // source's channels 48-63) are neither read from LDS nor multiplied (the loop runs two steps per trip, so the step
 // parity is known at compile time); bit 1 -- Nout == 64 with zero weight rows [48, 64): the 16-column MFMA group
@@ -79,7 +79,7 @@ template <int WM, int WN, int TM, bool BUF, bool BNR, bool F8, bool F32 = false,
 __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm_fwd_tap64_kernel(FwdArgs a) {
   static_assert(!(F8 && F32), "one operand dtype");
   constexpr int ZT = KP >= 4 ? KP - 3 : 0;
-  static_assert(ZT == 0 || (F32 && WN == 1 && !BNR), "zero-tail forms: f32, 64-column tiles");
+  static_assert(ZT == 0 || (F32 && !BNR && (WN == 1 || ZT == 1)), "zero-tail forms: f32; the N tail on 64-column tiles");
   using TO = typename std::conditional<F32, float, bf16>::type;   // output dtype
   constexpr int NTH = WM * WN * 64;
   constexpr int BM = WM * TM, BN = WN * 64;
@@ -332,13 +332,17 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
       const int buf = t & 1;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       T64_BAR();
-      if (t + 1 < nk) {
-        const Kt k1 = kinfo();
-        issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
-      }
+      auto issue_next = [&]() {
+        if (t + 1 < nk) {
+          const Kt k1 = kinfo();
+          issueA(0, k1, buf ^ 1); issueB(0, k1, buf ^ 1); issueB(1, k1, buf ^ 1); issueA(1, k1, buf ^ 1);
+        }
+      };
+      if (!late) issue_next();
       readA(buf, 0, fa, kt);
       readB(buf, 0, fb0);
       mma(fa, fb0, 0, 0, kt);
+      if (late) issue_next();
       readB(buf, 1, fb1);
       mma(fa, fb1, 0, 1, kt);
       readA(buf, 1, fa, kt);
@@ -627,10 +631,17 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, BUFV, BNRV, false, true>), g, b, 0, s, a);   \
   } while (0)
   if (a.f32) {
-    // zero tails (FwdArgs::ztail, option f32_ztail): the KP 4-6 instances of the 64-column tile
-    if constexpr (WN == 1 && TM == 64) {
-      const int zt = adp::option("f32_ztail", 1) && buf && !a.bnr_z && !a.kpipe ? a.ztail & 3 : 0;
-      if (zt) {
+    // zero tails (FwdArgs::ztail, option f32_ztail): the KP 4-6 instances of the 64-column tile, KP 4 (K tail) of
+    // the 256x128 one
+    if constexpr ((WN == 1 || WN == 2) && TM == 64) {
+      const int zt = adp::option("f32_ztail", 1) && buf && !a.bnr_z && !a.kpipe ? a.ztail & (WN == 1 ? 3 : 1) : 0;
+      if constexpr (WN == 2) {
+        if (zt) {
+          adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, true, false, false, true, 4>", WM, WN, TM);
+          hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false, true, 4>), g, b, 0, s, a);
+          return;
+        }
+      } else if (zt) {
         adp::set_kernel("igemm_fwd_tap64_kernel<%d, %d, %d, true, false, false, true, %d>", WM, WN, TM, zt + 3);
         if (zt == 1) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false, true, 4>), g, b, 0, s, a);
         else if (zt == 2) hipLaunchKernelGGL((igemm_fwd_tap64_kernel<WM, WN, TM, true, false, false, true, 5>), g, b, 0, s, a);

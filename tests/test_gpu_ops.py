@@ -1082,6 +1082,8 @@ ZTAIL_CASES = [
     ("1src_ktail", [44], 64, 64, False, "relu_stats", 1),
     ("1src_up2_both", [44], 64, 44, True, "relu_stats", 3),
     ("1src_n40_k8", [8], 64, 40, False, "relu_stats", 3),
+    ("1src_ktail_n128", [44], 128, 0, False, "relu_stats", 1),       # (256x128 tile: the K tail only)
+    ("2src_ktail_n128_mask", [44, 40], 128, 0, False, "mask_add", 1),
 ]
 
 
@@ -1102,22 +1104,25 @@ def test_f32_zero_tail_forms(case):
         x[..., :r] = torch.randn(N, Hs, Ws, r, generator=g)
         xs.append(x.to(DEV))
     cin_s = 64 * len(reals)
-    Wt = torch.zeros(64, ops.round_up(9 * cin_s, 32))
+    nr = nreal or nout
+    Wt = torch.zeros(nout, ops.round_up(9 * cin_s, 32))
     for t in range(9):
         for p, r in enumerate(reals):
-            Wt[:nreal, t * cin_s + 64 * p: t * cin_s + 64 * p + r] = torch.randn(nreal, r, generator=g) * 0.05
+            Wt[:nr, t * cin_s + 64 * p: t * cin_s + 64 * p + r] = torch.randn(nr, r, generator=g) * 0.05
     Wt = Wt.to(DEV)
-    bias = torch.zeros(64)
-    bias[:nreal] = torch.randn(nreal, generator=g) * 0.1
+    bias = torch.zeros(nout)
+    bias[:nr] = torch.randn(nr, generator=g) * 0.1
     bias = bias.to(DEV)
-    mk = (torch.rand(N, H, W, 64, generator=g) > 0.4).float().to(DEV) if epi == "mask_add" else None
-    ad = torch.randn(N, H, W, 64, generator=g).to(DEV) if epi == "mask_add" else None
+    mk = (torch.rand(N, H, W, nout, generator=g) > 0.4).float().to(DEV) if epi == "mask_add" else None
+    ad = torch.randn(N, H, W, nout, generator=g).to(DEV) if epi == "mask_add" else None
     res = []
     for hint in (False, True):
-        o = torch.zeros(N, H, W, 64, device=DEV)
-        st = torch.zeros(2, 64, device=DEV)
+        o = torch.zeros(N, H, W, nout, device=DEV)
+        st = torch.zeros(2, nout, device=DEV)
         ops.set_option("fwd_halo", 0)
         ops.set_option("tap64_persist", 0)
+        ops.set_option("tap64p_f32", 0)
+        ops.set_option("fwd_tap64", 3 if nout == 128 else 1)   # (Nout 128: the 256x128 tile, not two 64-wide ones)
         try:
             real = (reals[0], reals[1] if len(reals) > 1 else 0, nreal) if hint else None
             if epi == "mask_add":
@@ -1129,15 +1134,15 @@ def test_f32_zero_tail_forms(case):
             kname = _lib.lib().adp_last_kernel().decode()
             torch.cuda.synchronize()
         finally:
-            for k in ("fwd_halo", "tap64_persist"):
+            for k in ("fwd_halo", "tap64_persist", "tap64p_f32", "fwd_tap64"):
                 ops.set_option(k, None)
-        assert kname.startswith("igemm_fwd_tap64_kernel<4, 1, 64,"), kname
+        assert kname.startswith(f"igemm_fwd_tap64_kernel<4, {nout // 64}, 64,"), kname
         assert kname.endswith(f", {zt + 3}>" if hint else ", -1>"), kname
         res.append((o, st))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
-    if epi != "mask_add" and nreal < 64:   # (the zero weight rows: zero pad channels; an addend's pad channels pass through)
-        assert res[1][0][..., nreal:].abs().max().item() == 0
+    if epi != "mask_add" and nr < nout:   # (the zero weight rows: zero pad channels; an addend's pad channels pass through)
+        assert res[1][0][..., nr:].abs().max().item() == 0
 
 
 HALOP_WIDE_CASES = [
