@@ -50,6 +50,7 @@ struct FwdArgs {
   void* act_out;         // with scA / shA: relu(srcA * scA + shA) stored here too (adp_conv_io.act_outA)
   int bnr_lds;           // tap64 BN-backward-reduction launches: the LDS-staged epilogue (option tap64_bnr_lds)
   int mask_lds;          // tap64 mask / addend launches: mask and addend rows by LDS-DMA (option tap64_mask_lds)
+  int ca_real;           // adp_conv_desc.CA_real (0 = unknown)
   int ztail;             // zero tails of the weights (adp_conv_desc CA_real / CB_real / Nout_real): bit 0 every source a
                          // 64-channel stride with <= 48 real channels, bit 1 Nout == 64 with <= 48 real columns
 };
@@ -453,6 +454,7 @@ int launch_fwd_halo(FwdArgs& a, hipStream_t s);
 // layers with Nout % 256 == 0; called by launch_fwd_tap64p for its 256x256 halo shapes.
 int launch_fwd_w4(FwdArgs& a, hipStream_t s);
 int launch_fwd_cin8(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: input layers (one 8-channel source)
+int launch_fwd_cin8_f32(FwdArgs& a, hipStream_t s);   // conv_fwd_cin8.hip: f32 3x3 input layers
 // conv_fwd_halo_f8.hip: fp8 forward of 3x3 layers with 64-channel sources (one, or two concatenated)
 int launch_fwd_halop_f8(FwdArgs& a, hipStream_t s);
 // conv_wgrad_tap64.hip: phase-pipelined LDS-DMA weight-gradient kernel for the same layers.

@@ -330,6 +330,106 @@ void launch_cin8(FwdArgs& a, hipStream_t s) {
   else launch_cin8_u<KS, 2>(a, s);
 }
 
+// f32 form (round 5; the drop-in CLIs' default dtype, adipose_v3 down1_conv1 at the reference's precision): the same
+// product on exact v_mfma_f32_16x16x4_f32 -- a 4-deep k step is one channel quad of one tap: lane l supplies
+// W[16 mb + (l & 15)][8 t + 4 q + (l >> 4)] (registers for the whole launch) and X[pixel l & 15][tap t][channel
+// 4 q + (l >> 4)] (one 4-B gather), so C^T = W X^T lands as in the bf16 form: lane l holds channels 16 mb + 4 (l >> 4)
+// + i of pixel l & 15, one 16-B store per 16-channel block. Q = 1 when the caller's CA_real <= 4 (adp_conv_desc v19:
+// the weight columns of channels 4-7 are zeros, e.g. the gray input): one quad per tap. 3x3 taps. The generic
+// register-staged kernel it replaces ran this layer at ~1 TB/s (0.59 ms of the 1024^2 B=2 f32 step).
+template <int Q, int UNR>
+__global__ __launch_bounds__(256) void igemm_fwd_cin8_f32_kernel(FwdArgs a) {
+  constexpr int T = 9;
+  const int lane = threadIdx.x & 63;
+  const int r16 = lane & 15, h4 = lane >> 4;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+  const float* W = reinterpret_cast<const float*>(a.W);
+  const float* src = reinterpret_cast<const float*>(a.srcA);
+  float* out = reinterpret_cast<float*>(a.out);
+  float wf[4][T][Q];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) wf[mb][t][q] = W[(size_t)(16 * mb + r16) * a.Kpad + 8 * t + 4 * q + h4];
+  float bias[4][4], s1[4][4], s2[4][4];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = 16 * mb + 4 * h4 + i;
+      bias[mb][i] = (a.bias && co < a.Nout) ? a.bias[co] : 0.f;
+      s1[mb][i] = 0.f;
+      s2[mb][i] = 0.f;
+    }
+  const int HWo = a.Ho * a.Wo;
+  const int groups = (a.M + 15) / 16;
+  for (int g0 = wave * UNR; g0 < groups; g0 += nwaves * UNR) {
+    float xb[UNR][T][Q];
+    int mm[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int m = (g0 + u) * 16 + r16;
+      mm[u] = m;
+      const bool mv = g0 + u < groups && m < a.M;
+      const int mc = mv ? m : 0;
+      const int n = mc / HWo, rem = mc - n * HWo, y = rem / a.Wo, x = rem - y * a.Wo;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int yi = y + (t / 3) * a.dil - a.pad, xi = x + (t % 3) * a.dil - a.pad;
+        const bool ok = mv && (unsigned)yi < (unsigned)a.Hs && (unsigned)xi < (unsigned)a.Ws;
+        const float* p = src + ((size_t)(n * a.Hs + yi) * a.Ws + xi) * 8 + h4;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) xb[u][t][q] = ok ? p[4 * q] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb)
+            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[mb][t][q], xb[u][t][q], acc[mb], 0, 0, 0);
+      const int m = mm[u];
+      if (g0 + u >= groups || m >= a.M) continue;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int co0 = 16 * mb + 4 * h4;
+        if (co0 >= a.Nout) continue;
+        f32x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float x = acc[mb][i] + bias[mb][i];
+          if (a.relu) x = fmaxf(x, 0.f);
+          s1[mb][i] += x;
+          s2[mb][i] += x * x;
+          v[i] = x;
+        }
+        *reinterpret_cast<f32x4*>(out + (size_t)m * a.out_stride + co0) = v;
+      }
+    }
+  }
+  if (!a.bn_sum) return;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = row16_sum(s1[mb][i]), y = row16_sum(s2[mb][i]);
+      const int co = 16 * mb + 4 * h4 + i;
+      if (r16 == 0 && co < a.Nout) {   // this wave's replica; the launcher folds them into bn_sum / bn_sq
+        double* rep = a.stat + (size_t)(wave & (adp::STAT_REPL - 1)) * 2 * adp::STAT_CMAX;
+        atomicAdd(rep + co, (double)x);
+        atomicAdd(rep + adp::STAT_CMAX + co, (double)y);
+      }
+    }
+}
+
 }  // namespace
 
 namespace adp {
@@ -350,6 +450,26 @@ int launch_fwd_cin8(FwdArgs& a, hipStream_t s) {
   if (ks == 1) launch_cin8<1>(a, s);
   else if (ks == 2) launch_cin8<2>(a, s);
   else launch_cin8<3>(a, s);
+  return 1;
+}
+
+// f32 forward of a 3x3 input layer (igemm_fwd_cin8_f32_kernel): one 8-channel source, Nout <= 64, plain store with
+// bias / ReLU / BN statistics; 16-B aligned output rows
+int launch_fwd_cin8_f32(FwdArgs& a, hipStream_t s) {
+  if (option("fwd_cin8_f32", 1) == 0) return 0;
+  if (a.CAs != 8 || a.CBs != 0 || a.scA || a.up != 1 || a.stride != 1 || a.kh != 3 || a.kw != 3 || a.K != 72 ||
+      a.Kpad < 72 || a.Nout > 64 || a.Nout % 4 != 0 || a.out_mode != 0 || !a.out || a.out_stride % 4 != 0 ||
+      ((uintptr_t)a.out & 15) != 0 || a.addend || a.mask || a.accum || a.drop_rate > 0.f || a.bnr_z || a.out_f8)
+    return 0;
+  const int groups = (a.M + 15) / 16, unr = 4;
+  const int waves = std::max(1, std::min((groups + unr - 1) / unr, option("cin8_waves", 2048)));
+  if (a.ca_real > 0 && a.ca_real <= 4) {
+    adp::set_kernel("igemm_fwd_cin8_f32_kernel<1, 4>");
+    hipLaunchKernelGGL((igemm_fwd_cin8_f32_kernel<1, 4>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  } else {
+    adp::set_kernel("igemm_fwd_cin8_f32_kernel<2, 4>");
+    hipLaunchKernelGGL((igemm_fwd_cin8_f32_kernel<2, 4>), dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  }
   return 1;
 }
 }  // namespace adp

@@ -1064,6 +1064,7 @@ void fill_fwd_args(const adp_conv_desc* d, const adp_conv_io* io, FwdArgs& a) {
   a.act_out = io->act_outA;
   // zero tails of the weights (the caller's real channel counts, adp_conv_desc v19): products with zero weight
   // columns / rows that a kernel may skip exactly
+  a.ca_real = d->CA_real;
   auto tail48 = [](int stride, int real) { return stride == 64 && real > 0 && real <= 48; };
   a.ztail = (tail48(d->CA_stride, d->CA_real) && (d->CB_stride == 0 || tail48(d->CB_stride, d->CB_real)) ? 1 : 0) |
             (tail48(d->Nout, d->Nout_real) && d->out_mode == 0 ? 2 : 0);
@@ -1161,7 +1162,7 @@ int launch_fwd(const adp_conv_desc* d, const adp_conv_io* io, hipStream_t s) {
   // f32: the LDS-DMA tap kernel with 32-channel K steps where every K step lies in one tap and one source
   if (std::is_same<T, float>::value && fast == 2 && !a.scA && !a.scB) {
     a.f32 = 1;
-    if (adp::launch_fwd_tap64(a, s)) {
+    if (adp::launch_fwd_cin8_f32(a, s) || adp::launch_fwd_tap64(a, s)) {
       adp::kernel_end();
       if (adp::check_launch("adp_conv_fwd")) return -2;
       return fold_stats(a, s);

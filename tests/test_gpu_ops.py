@@ -1934,6 +1934,45 @@ def test_cin8_input_layer_bn_stats(S, cout):
     assert bool(((s2[:cout].cpu().double() - (r * r).sum(0)).abs() <= 1e-2 * (r * r).sum(0) + 1e-3).all())
 
 
+@pytest.mark.parametrize("N,S,cin,cout,dil,hint", [(2, 32, 1, 44, 1, True), (2, 32, 3, 64, 1, True),
+                                                     (3, 13, 3, 24, 2, False), (1, 19, 1, 44, 1, False)])
+def test_cin8_f32_input_layer(N, S, cin, cout, dil, hint):
+    """f32 input-layer launch (igemm_fwd_cin8_f32_kernel: exact f32 MFMA, one channel quad per tap when the caller says
+    CA_real <= 4, else two) vs the f64 oracle at the f32 gate, BatchNorm sums vs a host reduction, pad channels stored
+    as zeros; and within f32 rounding of the generic register-staged kernel it replaces (option fwd_cin8_f32=0).
+    Ragged images leave partial 16-pixel groups."""
+    from adipose_amd._lib import lib
+    xs, kern, bias, l = make_case(N, S, [cin], cout, dil, False, seed=17)
+    W = torch.from_numpy(l.keras_to_packed(kern.numpy())).to(DEV).float().contiguous()
+    b = torch.zeros(l.cout_s, device=DEV)
+    b[:cout] = bias.to(DEV)
+    src = nhwc_pad(xs[0], l.cin_s[0], torch.float32)
+    res = {}
+    for on in (1, 0):
+        ops.set_option("fwd_cin8_f32", on)
+        try:
+            out = torch.full((N, S, S, l.cout_s), 7.0, device=DEV)
+            s1 = torch.zeros(l.cout_s, device=DEV)
+            s2 = torch.zeros(l.cout_s, device=DEV)
+            ops.conv_fwd(src, W, l.Nout, out=out, bias=b, relu=True, dil=dil, bn_stats=(s1, s2),
+                         real=(cin, 0, cout) if hint else None)
+            torch.cuda.synchronize()
+            res[on] = (out.clone(), s1.clone(), s2.clone(), lib().adp_last_kernel().decode())
+        finally:
+            ops.set_option("fwd_cin8_f32", None)
+    out, s1, s2, kname = res[1]
+    assert kname == f"igemm_fwd_cin8_f32_kernel<{1 if hint and cin <= 4 else 2}, 4>", kname
+    assert not res[0][3].startswith("igemm_fwd_cin8_f32"), res[0][3]
+    ref = oracle_fwd([xs[0]], kern, bias, dil, False, relu=True)
+    assert relerr(out[..., :cout], ref) < TOL[torch.float32]
+    assert relerr(out, res[0][0]) < 1e-6
+    if l.cout_s > cout:
+        assert out[..., cout:].abs().max().item() == 0.0
+    r = ref.reshape(-1, cout).double()
+    assert bool(((s1[:cout].cpu().double() - r.sum(0)).abs() <= 1e-4 * r.abs().sum(0) + 1e-4).all())
+    assert bool(((s2[:cout].cpu().double() - (r * r).sum(0)).abs() <= 1e-4 * (r * r).sum(0) + 1e-4).all())
+
+
 @pytest.mark.parametrize("N,S,cin,cout,dil,relu", [(2, 32, 3, 64, 1, True), (3, 13, 1, 44, 2, False),
                                                      (1, 10, 3, 24, 1, True), (5, 8, 3, 64, 1, False)])
 def test_cin8_pipelined_matches_plain(N, S, cin, cout, dil, relu):
