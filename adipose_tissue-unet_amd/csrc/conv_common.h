@@ -81,6 +81,13 @@ struct WgradArgs {
   int* claim;           // persistent halo weight gradient: dynamic tile claiming counters (nullptr: static lists)
   int claim_chunk;      // patches per claim
   int claim_full;       // every super-patch claimed, none static (option claim_full)
+  // f32 halo weight gradient, zero tails (adp_conv_desc CA_real / CB_real / Nout_real; 0 = unknown): zt_n > 0 ->
+  // combination c takes the blocks [zt_cstart[c], zt_cstart[c + 1]); zt_mode[c] > 0 -> its input chunk has <= 16 real
+  // channels, and waves 0 .. zt_mode[c] - 1 take its useful 16 x 16 blocks (one per wave), the others only stage
+  int ca_real, cb_real, nout_real;
+  int zt_n;
+  int zt_cstart[9];
+  int zt_mode[8];
 };
 
 // LDS-only workgroup barrier for epilogues: this wave's LDS traffic complete, then s_barrier. Unlike

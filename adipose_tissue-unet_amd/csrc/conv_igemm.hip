@@ -1241,6 +1241,7 @@ int launch_wgrad(const adp_conv_desc* d, const adp_conv_io* io, const void* dY, 
   a.dY = dY; a.dy_stride = dy_stride; a.dy_mode = d->out_mode == 1 ? 1 : 0; a.Cps = d->shuffle_c;
   a.Nout = d->Nout; a.dW = dW; a.dB = dB;
   a.M = d->N * d->Ho * d->Wo;
+  a.ca_real = d->CA_real; a.cb_real = d->CB_real; a.nout_real = d->Nout_real;
   ADP_REQUIRE(a.CAs % 8 == 0 && a.CBs % 8 == 0 && a.Nout % 8 == 0,
               "adp_conv_wgrad: channel strides and Nout must be multiples of 8");
   ADP_REQUIRE(d->out_mode != 2, "adp_conv_wgrad: split-store descriptors are dgrad-only");

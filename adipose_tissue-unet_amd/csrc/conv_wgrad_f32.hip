@@ -304,15 +304,28 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave >> 1, wc = wave & 1;
   const int tx_n = a.Wo / HF_PW, ty_n = a.Ho / HF_PH;
   const int Cin_s = a.CAs + a.CBs, nch = Cin_s / CI, nnb = (a.Nout + NB - 1) / NB, combos = nch * nnb;
-  const int T = a.Nimg * tx_n * ty_n, G = gridDim.x / combos;
+  const int T = a.Nimg * tx_n * ty_n;
   const int lin0 = xcd_remap(blockIdx.x, gridDim.x);
-  const int combo = lin0 % combos, lin = lin0 / combos;
+  int combo, lin, G;
+  if (a.zt_n) {   // zero tails: weighted block ranges per combination (the launcher's table)
+    combo = 0;
+    while (combo + 1 < a.zt_n && lin0 >= a.zt_cstart[combo + 1]) ++combo;
+    lin = lin0 - a.zt_cstart[combo];
+    G = a.zt_cstart[combo + 1] - a.zt_cstart[combo];
+  } else {
+    G = gridDim.x / combos;
+    combo = lin0 % combos;
+    lin = lin0 / combos;
+  }
   const int ch = combo % nch, nblk = combo / nch;
   const int nt = lin < T ? (T - lin + G - 1) / G : 0;
   if (nt == 0) return;   // (uniform)
+  // zero tails: a chunk with <= 16 real input channels has hm useful 16 x 16 blocks (output rows 16 w, input columns
+  // 0-15), one per wave 0 .. hm - 1 -- one wave per SIMD instead of two --, and the other waves only stage
+  const int hm = a.zt_n ? a.zt_mode[combo] : 0;
+  const bool idle = hm > 0 && wave >= hm;
   const bool inA = ch * CI < a.CAs;
   const int xcs = inA ? a.CAs : a.CBs;
   const int us = a.up >> 1;
@@ -380,6 +393,7 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   f32x4 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wn = hm ? wave : wave >> 1, wc = hm ? 0 : wave & 1;
   const int li = lane & 15, lg = lane >> 4;
   const int ncol = wn * 16 + li, ccol = wc * 16 + li;   // this lane's dY column (output channel), X column
   const uint32_t sbase = wf_lds(smem);
@@ -399,6 +413,19 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
     for (int i = 0; i < GD; ++i) issue_d(P0, i, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  if (idle) {   // (staging only: the same pieces, barriers and waits as the multiplying waves)
+    for (int k = 0; k < nt; ++k) {
+      const int buf = k & 1;
+      if (k + 1 < nt) {
+        const Patch Pn = patch(k + 1);
+#pragma unroll
+        for (int r = 0; r < HF_PH; ++r) issue_row(Pn, r, buf ^ 1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    return;
   }
   for (int k = 0; k < nt; ++k) {
     const int buf = k & 1;
@@ -469,11 +496,40 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
       a.srcA && (!a.CBs || a.srcB) &&
       (size_t)a.Nimg * a.Hs * a.Ws * std::max(a.CAs, a.CBs) * 4 < ((size_t)1 << 31) &&
       (size_t)a.M * a.dy_stride * 4 < ((size_t)1 << 31)) {
-    const int combos = (Cin_s / 32) * ((a.Nout + 63) / 64);
+    const int nch = Cin_s / 32, combos = nch * ((a.Nout + 63) / 64);
     const int tiles = a.Nimg * (a.Ho / HF_PH) * (a.Wo / HF_PW);
-    const int per = std::max(1, std::min(tiles, option("wgrad_f32_halo_grid", 256) / combos));
+    const int target = option("wgrad_f32_halo_grid", 256);
+    const int per = std::max(1, std::min(tiles, target / combos));
+    int grid = per * combos;
+    // zero tails (the caller's real channel counts; option wgrad_f32_zt): a combination whose input chunk holds
+    // <= 16 real channels runs its <= 4 useful 16 x 16 blocks one per SIMD, in about half the time per patch, and
+    // gets about half the blocks of a full one
+    a.zt_n = 0;
+    if (option("wgrad_f32_zt", 1) && combos <= 8 && (a.ca_real > 0 || a.cb_real > 0)) {
+      double w[8], tot = 0.0;
+      bool any = false;
+      for (int c = 0; c < combos; ++c) {
+        const int ch = c % nch, nb = c / nch;
+        const bool inA = ch * 32 < a.CAs;
+        const int rsrc = inA ? a.ca_real : a.cb_real, c0 = inA ? ch * 32 : ch * 32 - a.CAs;
+        const int rin = rsrc > 0 ? std::min(32, std::max(0, rsrc - c0)) : 32;
+        const int rows = a.nout_real > 0 ? std::min(64, std::max(0, a.nout_real - nb * 64)) : 64;
+        const int rb = (rows + 15) / 16;
+        a.zt_mode[c] = rin <= 16 && rb >= 1 ? rb : 0;
+        any = any || a.zt_mode[c] > 0;
+        w[c] = a.zt_mode[c] > 0 ? 0.5 : 1.0;
+        tot += w[c];
+      }
+      if (any) {
+        a.zt_n = combos;
+        a.zt_cstart[0] = 0;
+        for (int c = 0; c < combos; ++c)
+          a.zt_cstart[c + 1] = a.zt_cstart[c] + std::max(1, std::min(tiles, (int)(target * w[c] / tot + 0.5)));
+        grid = a.zt_cstart[combos];
+      }
+    }
     adp::set_kernel("igemm_wgrad_halo_f32_kernel");
-    hipLaunchKernelGGL(igemm_wgrad_halo_f32_kernel, dim3(per * combos), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(igemm_wgrad_halo_f32_kernel, dim3(grid), dim3(512), 0, s, a);
     adp::kernel_end();
     return 1;
   }

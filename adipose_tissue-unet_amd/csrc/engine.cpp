@@ -499,6 +499,9 @@ struct adp_handle {
     d.dil = l.dil;
     d.pad = l.dil;
     d.Nout = l.cout_s;
+    d.CA_real = l.cin[0];   // (hints as in conv())
+    d.CB_real = l.cin.size() > 1 ? l.cin[1] : 0;
+    d.Nout_real = l.cout;
     d.mask_scale = d.mask2_scale = 1.f;
     io.srcA = srcA;
     io.srcB = srcB;

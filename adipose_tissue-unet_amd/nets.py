@@ -378,7 +378,7 @@ class UNetEngine:
             ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, bnA=bnA, kh=1, kw=1, pad=0, shuffle_c=l.cout_s)
         else:
             ops.conv_wgrad(srcA, dZ, dW, l.Nout, dB=dB, srcB=srcB, bnA=bnA, bnB=bnB, up=l.up, kh=l.k, kw=l.k,
-                           dil=l.dil, bn_apply=bn_apply)
+                           dil=l.dil, bn_apply=bn_apply, real=l.real_fwd)
         self._grad_ready(l.name)
 
     def dgrad(self, l, dZ, out, *, Ho=None, Wo=None, addend=None, mask=None, mask_scale=1.0, split=False,

@@ -264,8 +264,10 @@ def _nbytes(t):
 
 
 def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up=False, stride=1, kh=3, kw=3,
-               dil=1, pad=None, Ho=None, Wo=None, shuffle_c=0, bn_apply=None):
+               dil=1, pad=None, Ho=None, Wo=None, shuffle_c=0, bn_apply=None, real=None):
     """dW (+)= X_tap^T dY (f32 accumulators, caller zeroes). shuffle_c>0: dY is a ConvT output.
+    real=(CA_real, CB_real, Nout_real): optional hints as in conv_fwd (the pad channels of the sources and of dY are
+    zeros); the f32 halo weight gradient then runs chunks of <= 16 real channels on fewer waves.
     bn_apply=(dA, z, scale, shift, mean, invstd, gamma, dgamma, dbeta, count): dY is first computed as
     bn_bwd_apply(dA, z, ...) and stored (adp_conv_wgrad_bn: fused into the weight-gradient launch where the
     halo kernel takes the shape, bit-identical to bn_bwd_apply + conv_wgrad). With bn_apply, dY may be None
@@ -292,6 +294,10 @@ def conv_wgrad(srcA, dY, dW, nout, *, dB=None, srcB=None, bnA=None, bnB=None, up
     d.upsample = 1 if up else 0
     d.Ho, d.Wo, d.stride, d.kh, d.kw, d.dil, d.pad = Ho, Wo, stride, kh, kw, dil, pad
     d.Nout = nout
+    if real is not None:
+        ca, cb, nr = (int(v) for v in real)
+        _check(0 <= ca <= CA and 0 <= cb <= CB and 0 <= nr <= nout, "real channel counts out of range")
+        d.CA_real, d.CB_real, d.Nout_real = ca, cb, nr
     if shuffle_c:
         d.out_mode, d.shuffle_c = 1, shuffle_c
         _check(tuple(dYs.shape[:3]) == (N, 2 * Ho, 2 * Wo), "convT dY shape mismatch")

@@ -119,6 +119,7 @@ def test_adipose_f32_zero_tail_skip_is_exact(adipose_weights):
     res = []
     for zt in (0, 1):
         ops.set_option("f32_ztail", zt)
+        ops.set_option("wgrad_f32_zt", zt)
         try:
             net = build_adipose("f32", adipose_weights, B, S)
             tr = Trainer(net, LossConfig(use_hard_mining=True))
@@ -131,6 +132,7 @@ def test_adipose_f32_zero_tail_skip_is_exact(adipose_weights):
             torch.cuda.synchronize()
         finally:
             ops.set_option("f32_ztail", None)
+            ops.set_option("wgrad_f32_zt", None)
         o = outs if isinstance(outs, dict) else dict(enumerate(outs))
         res.append(({k: v.clone() for k, v in o.items() if torch.is_tensor(v)},
                     {n: net.get_layer_grads(n) for n in adipose_weights}))
