@@ -88,6 +88,7 @@ struct WgradArgs {
   int zt_n;
   int zt_cstart[9];
   int zt_mode[8];
+  float* bias_part;     // f32 halo weight gradient: per-block bias-gradient rows (option wgrad_f32_bias)
 };
 
 // LDS-only workgroup barrier for epilogues: this wave's LDS traffic complete, then s_barrier. Unlike

@@ -276,7 +276,7 @@ ADP_DEV void hf_read(uint32_t abase, const uint32_t (&bbase)[3], float& A, float
 // multiplies); at the first step of each pixel row the row's share of the next patch's LDS-DMA goes out
 template <int S, typename RowIssue>
 ADP_DEV void hf_steps(uint32_t abase, const uint32_t (&bbase)[3], float (&fa)[2], float (&fb)[2][9], f32x4 (&acc)[9],
-                      const RowIssue& row_issue) {
+                      float& db, const RowIssue& row_issue) {
   constexpr int NS = HF_PH * HF_PW / 4, cur = S & 1;
   if constexpr (S % 8 == 0) row_issue(S / 8);
   if constexpr (S + 1 < NS) {
@@ -289,7 +289,8 @@ ADP_DEV void hf_steps(uint32_t abase, const uint32_t (&bbase)[3], float (&fa)[2]
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur], fb[cur][t], acc[t], 0, 0, 0);
   __builtin_amdgcn_s_setprio(0);
-  if constexpr (S + 1 < NS) hf_steps<S + 1>(abase, bbase, fa, fb, acc, row_issue);
+  db += fa[cur];   // (the bias gradient: every dY element of the patch passes one lane's A operand once)
+  if constexpr (S + 1 < NS) hf_steps<S + 1>(abase, bbase, fa, fb, acc, db, row_issue);
 }
 __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs a) {
   constexpr int NTH = 512, CI = 32, NB = 64;
@@ -393,6 +394,7 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   f32x4 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float db = 0.f;
   const int wn = hm ? wave : wave >> 1, wc = hm ? 0 : wave & 1;
   const int li = lane & 15, lg = lane >> 4;
   const int ncol = wn * 16 + li, ccol = wc * 16 + li;   // this lane's dY column (output channel), X column
@@ -436,9 +438,18 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
     const uint32_t bbase[3] = {hb + b_lane[0], hb + b_lane[1], hb + b_lane[2]};
     float fa[2], fb[2][9];
     hf_read<0>(abase, bbase, fa[0], fb[0]);
-    hf_steps<0>(abase, bbase, fa, fb, acc, [&](int r) { if (more) issue_row(Pn, r, buf ^ 1); });
+    hf_steps<0>(abase, bbase, fa, fb, acc, db, [&](int r) { if (more) issue_row(Pn, r, buf ^ 1); });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next patch landed
     __syncthreads();                                    // and nobody reads this stage any more
+  }
+  // bias gradient (a.bias_part: the launcher's per-block rows, summed in a fixed order by its slab reduce): the
+  // column-block-0 waves of the chunk-0 blocks hold each output channel's dY sum over the block's pixels in the four
+  // lane rows
+  if (a.bias_part && ch == 0 && wc == 0) {
+    db += __shfl_xor(db, 16, 64);
+    db += __shfl_xor(db, 32, 64);
+    const int n = nblk * NB + ncol;
+    if (lg == 0 && n < a.Nout) a.bias_part[(size_t)lin * a.Nout + n] = db;
   }
   // dW[n][tap * Cin_s + ch * CI + ccol] += acc[tap][r], n = nblk * NB + wn * 16 + 4 lg + r
   const int kc = ch * CI + ccol;
@@ -528,8 +539,27 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
         grid = a.zt_cstart[combos];
       }
     }
+    // the bias gradient in the same pass (option wgrad_f32_bias): per-block rows [G0][Nout] (G0 = the blocks of
+    // each chunk-0 combination), zeroed first (blocks without patches and idle waves write nothing), then the
+    // fixed-order slab reduce into dB -- instead of a channel-sum launch that reads dY once more
+    a.bias_part = nullptr;
+    int g0 = 0;
+    if (a.dB && a.Nout % 4 == 0 && option("wgrad_f32_bias", 1)) {
+      g0 = a.zt_n ? a.zt_cstart[1] - a.zt_cstart[0] : per;
+      bool same = true;   // (every chunk-0 combination must have g0 blocks: one row per block index)
+      for (int c = nch; a.zt_n && c < combos; c += nch) same = same && a.zt_cstart[c + 1] - a.zt_cstart[c] == g0;
+      if (same) a.bias_part = reduce_part(3, (size_t)g0 * a.Nout * sizeof(float), s);
+      if (a.bias_part && hipMemsetAsync(a.bias_part, 0, (size_t)g0 * a.Nout * sizeof(float), s) != hipSuccess)
+        a.bias_part = nullptr;
+    }
     adp::set_kernel("igemm_wgrad_halo_f32_kernel");
     hipLaunchKernelGGL(igemm_wgrad_halo_f32_kernel, dim3(grid), dim3(512), 0, s, a);
+    if (a.bias_part) {
+      adp::kernel_end();
+      slab_reduce(g0, (size_t)a.Nout / 4, a.bias_part, a.dB, s);
+      a.dB = nullptr;   // (done: the caller's channel-sum launch is skipped)
+      a.bias_part = nullptr;
+    }
     adp::kernel_end();
     return 1;
   }

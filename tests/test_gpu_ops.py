@@ -1145,13 +1145,15 @@ def test_f32_zero_tail_forms(case):
         assert res[1][0][..., nr:].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("reals,nreal", [([44], 44), ([44, 44], 44), ([40], 64), ([12], 20)],
-                         ids=["1src_44", "2src_44_44", "1src_40_n64", "1src_12_n20"])
-def test_f32_halo_wgrad_zero_tails(reals, nreal):
+@pytest.mark.parametrize("reals,nout,nreal", [([44], 64, 44), ([44, 44], 64, 44), ([40], 64, 64), ([12], 64, 20),
+                                               ([44], 128, 100)],
+                         ids=["1src_44", "2src_44_44", "1src_40_n64", "1src_12_n20", "1src_44_n128_100"])
+def test_f32_halo_wgrad_zero_tails(reals, nout, nreal):
     """f32 halo weight gradient with the real-channel hints (option wgrad_f32_zt): an input chunk with <= 16 real
-    channels runs its useful 16 x 16 blocks one per wave on fewer waves and gets fewer blocks. The weight gradient
-    equals the unhinted launch's to the f32 atomics' order (both add per-block partials with f32 atomics), the pad
-    rows and columns stay exactly zero, and both match a float64 reference."""
+    channels runs its useful 16 x 16 blocks one per wave on fewer waves and gets fewer blocks; and the bias gradient
+    summed in the same pass (option wgrad_f32_bias: per-block rows + the fixed-order slab reduce) instead of the
+    channel-sum launch. The weight gradient equals the unhinted launch's to the f32 atomics' order, the pad rows and
+    columns stay exactly zero, both match a float64 reference; the bias gradient to 1e-6 of the channel sum's."""
     from adipose_amd._lib import lib
     g = torch.Generator().manual_seed(101)
     N, S = 2, 64
@@ -1160,33 +1162,42 @@ def test_f32_halo_wgrad_zero_tails(reals, nreal):
         x = torch.zeros(N, S, S, 64)
         x[..., :r] = torch.randn(N, S, S, r, generator=g)
         xs.append(x.to(DEV))
-    dy = torch.zeros(N, S, S, 64)
+    dy = torch.zeros(N, S, S, nout)
     dy[..., :nreal] = torch.randn(N, S, S, nreal, generator=g)
     dy = dy.to(DEV)
     cin_s = 64 * len(reals)
     res = []
     for hint in (False, True):
-        dW = torch.zeros(64, ops.round_up(9 * cin_s, 32), device=DEV)
-        ops.conv_wgrad(xs[0], dy, dW, 64, srcB=xs[1] if len(xs) > 1 else None,
-                       real=(reals[0], reals[1] if len(reals) > 1 else 0, nreal) if hint else None)
-        torch.cuda.synchronize()
-        assert lib().adp_last_kernel().decode() == "igemm_wgrad_halo_f32_kernel"
-        res.append(dW.cpu())
+        dW = torch.zeros(nout, ops.round_up(9 * cin_s, 32), device=DEV)
+        dB = torch.zeros(nout, device=DEV)
+        ops.set_option("wgrad_f32_bias", 1 if hint else 0)
+        try:
+            ops.conv_wgrad(xs[0], dy, dW, nout, dB=dB, srcB=xs[1] if len(xs) > 1 else None,
+                           real=(reals[0], reals[1] if len(reals) > 1 else 0, nreal) if hint else None)
+            torch.cuda.synchronize()
+            kname = lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("wgrad_f32_bias", None)
+        assert kname == "igemm_wgrad_halo_f32_kernel", kname
+        res.append((dW.cpu(), dB.cpu()))
     # float64 reference: dW[n][t * cin_s + c] = sum_pixels dY[p][n] * X[p + off_t][c]
     x = torch.cat(xs, -1).cpu().double().permute(0, 3, 1, 2)
     xp = F.pad(x, (1, 1, 1, 1))
-    d64 = dy.cpu().double()
-    ref = torch.zeros(64, 9 * cin_s, dtype=torch.float64)
+    d64 = dy.cpu().double().reshape(-1, nout)
+    ref = torch.zeros(nout, 9 * cin_s, dtype=torch.float64)
     for t in range(9):
         ty, tx = t // 3, t % 3
         patch = xp[:, :, ty:ty + S, tx:tx + S].permute(0, 2, 3, 1).reshape(-1, cin_s)
-        ref[:, t * cin_s:(t + 1) * cin_s] = d64.reshape(-1, 64).T @ patch
-    for r_ in res:
-        assert relerr(r_[:, :9 * cin_s], ref) < 1e-5
-    assert relerr(res[1], res[0]) < 1e-6
-    assert res[1][nreal:].abs().max().item() == 0 if nreal < 64 else True
+        ref[:, t * cin_s:(t + 1) * cin_s] = d64.T @ patch
+    for w_, b_ in res:
+        assert relerr(w_[:, :9 * cin_s], ref) < 1e-5
+        assert relerr(b_, d64.sum(0)) < 1e-5
+    assert relerr(res[1][0], res[0][0]) < 1e-6
+    assert relerr(res[1][1], res[0][1]) < 1e-6
+    if nreal < nout:
+        assert res[1][0][nreal:].abs().max().item() == 0 and res[1][1][nreal:].abs().max().item() == 0
     pad_cols = [t * cin_s + 64 * p + c for t in range(9) for p, r in enumerate(reals) for c in range(r, 64)]
-    assert res[1][:, pad_cols].abs().max().item() == 0
+    assert res[1][0][:, pad_cols].abs().max().item() == 0
 
 
 HALOP_WIDE_CASES = [
