@@ -33,6 +33,10 @@ constexpr int WG_RSRC3 = 0x00020000;       // raw buffer descriptor word 3 (gfx9
 __device__ __forceinline__ void wg_buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, 0, 0, 0);
 }
+// (the same with a wave-uniform scalar offset added to the per-lane one)
+__device__ __forceinline__ void wg_buf_lds16s(__amdgpu_buffer_rsrc_t r, void* lds, unsigned off, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, off, soff, 0, 0);
+}
 __device__ __forceinline__ void wg_glds16(const void* p, void* lds) {
   __builtin_amdgcn_global_load_lds(p, (lds_void*)lds, 16, 0, 0);
 }
@@ -959,6 +963,546 @@ __global__ __launch_bounds__(NW * 64, 1) void igemm_wgrad_halop_kernel(WgradArgs
   }
 }
 
+// Round 6: the tap-pair form of the persistent halo weight gradient. The 8-wave form above gives
+// each wave one tap (64 x 64) and an eighth of tap 8: per patch row a wave reads 22 fragments (the whole dY^T tile, its
+// tap's halo rows, tap 8's share) for 18 MFMAs, and all eight waves read the same dY^T fragments -- the K loop alone ran
+// at 1.3-1.5 PF, bounded by LDS fragment reads and their waits, not by the MFMA pipe. Here the two waves of a SIMD
+// (w, w + 4) own the same 64 x 144 block of dW -- taps 2p and 2p + 1 and column block p of tap 8 (p = w & 3) -- and split
+// the patch rows between them (wave w + 4h takes rows h, h + 2, h + 4, h + 6). One dY^T fragment set (4) then feeds 36
+// MFMAs instead of 18: 26 reads per 36 MFMAs, 0.72 reads per MFMA against 1.22, and 104 fragment reads per CU and patch
+// row against 176. The LDS images, their swizzle, the LDS-DMA schedule and the block's (chunk, output block) work split
+// are those of the 8-wave form. Per row the reads of the next row are issued in two groups between the MFMA clusters
+// (G1 = the next dY^T set, double-buffered, + three of the four tap-2p halo fragments after the tap-2p MFMAs; G2 = the
+// last tap-2p fragment, the tap-2p+1 set and tap 8's fragment, double-buffered, after the tap-2p+1 MFMAs), so a row's
+// first MFMA waits only for reads issued a cluster earlier, and at most 15 reads are ever outstanding (the lgkmcnt
+// field). The two waves of a pair add their partial sums in LDS at the end (h = 0 + h = 1: fixed order,
+// deterministic) and the block's 64 x 576 partial leaves in 16-B pieces in one of the three output forms of the 8-wave
+// form (slab / dW += partial / f32 atomics). Static patch lists only, plain dY (no fused BatchNorm apply).
+// LSPR: the next patch's LDS-DMA groups are issued over the wave's first LSPR local rows (of 4).
+template <int LSPR, int PIPE>
+__global__ __launch_bounds__(512, 1) void igemm_wgrad_halopair_kernel(WgradArgs a) {
+  constexpr bool DB = PIPE == 1;
+  constexpr int NTH = 512, RB = 128;
+  // halo rows padded to HW = 36 pixels (the two extra columns are loaded and never read): rows pr and pr + 2 of a
+  // patch then start 72 LDS rows apart, a multiple of 8, so a wave's four rows share one swizzle and one address set
+  constexpr int PH = 8, PW = 32, HW = PW + 4, HROWS = (PH + 2) * HW;   // 360 halo pixels
+  constexpr int HCH = HROWS * 8, DCH = PH * PW * 8;                     // 16-B chunks per image
+  constexpr int GH = (HCH + NTH - 1) / NTH, GD = DCH / NTH;             // 6 halo + 4 dY groups per thread
+  constexpr int HBUF = HROWS * RB, DBUF = PH * PW * RB;
+  constexpr int STAGE = HBUF + DBUF;
+  constexpr int ES = 9 * 64 + 4;   // epilogue: the block's [64][576] f32 partial, row stride 580 (bank-conflict-free)
+  static_assert(64 * ES * 4 <= 2 * STAGE, "the epilogue image fits in the two stages");
+  static_assert(GD * NTH == DCH && GH + GD == 10 && LSPR >= 1 && LSPR <= 8, "shape");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // timing-only ablations (ablation build, option wgrad_debug): bit 0 no output, bit 1 no LDS-DMA after the prologue,
+  // bit 2 no patch barrier, bit 3 the MFMA clusters do not wait for their fragments
+  const int dbg = ADP_DBG(a);
+  // (the lane id is re-derived by v_mbcnt in a volatile statement wherever the loop needs it, so that neither it nor the
+  // thread id occupies a register across the loop)
+  auto lane_now = []() -> int {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+  };
+  const int p = wave & 3, h = wave >> 2;   // tap pair, row parity
+  prio_static<ADP_PRIO_WGRAD>(wave);
+  const int t0 = 2 * p, t1 = 2 * p + 1;
+  const int dy0 = t0 / 3, dx0 = t0 - 3 * (t0 / 3), dy1 = t1 / 3, dx1 = t1 - 3 * (t1 / 3);
+  const int tx_n = a.Wo / PW, ty_n = a.Ho / PH;
+  const int nch = (a.CAs + a.CBs) >> 6, combos = nch * (a.Nout >> 6);
+  const int T = a.Nimg * tx_n * ty_n, G = gridDim.x / combos;
+  const int lin0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int combo = lin0 % combos, lin = lin0 / combos;
+  const int ch = combo % nch, nblk = combo / nch;
+  const int nt = lin < T ? (T - lin + G - 1) / G : 0;
+  const bool inA = ch * 64 < a.CAs;
+  const int xcs = inA ? a.CAs : a.CBs;
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(inA ? a.srcA : a.srcB), 0, a.Nimg * a.Hs * a.Ws * xcs * 2, WG_RSRC3);
+  const __amdgpu_buffer_rsrc_t rsD =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dY, 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 2, WG_RSRC3);
+  const int us = a.up >> 1;
+  const int xc0 = (inA ? ch * 64 : ch * 64 - a.CAs) * 2;
+  struct Patch { int y0, x0, pbx, pbd; };
+  auto patch = [&](int t) {
+    Patch P;
+    const int px = t % tx_n, r = t / tx_n;
+    const int img = r / ty_n;
+    P.y0 = (r % ty_n) * PH;
+    P.x0 = px * PW;
+    P.pbx = (img * a.Hs + (P.y0 >> us)) * a.Ws + (P.x0 >> us);
+    P.pbd = (img * a.Ho + P.y0) * a.Wo + P.x0;
+    return P;
+  };
+  // LDS-DMA group gi of this thread (0 .. GH-1 halo, GH .. GH+GD-1 dY): its per-thread constants are rebuilt from an
+  // opaque copy of the thread id at each issue (a few VALU under the MFMAs) instead of 32 registers held across the loop
+  // LDS-DMA groups (round 6: per-group arithmetic cut to a few VALU). Thread t moves 16-B chunk t & 7 of LDS row
+  // r0 + 64 gi (r0 = t >> 3) of an image; that row's swizzle gsw(r0 + 64 gi) = gsw(r0), so the chunk's column on both
+  // sides is the same for every group. The halo rows' source-grid (y, x) relative to the patch are packed 10 bits a group
+  // in hpk (0x3ff: a row past the halo); a dY group's offset is one per-thread constant plus the patch and group part,
+  // which goes into the buffer instruction's scalar offset. The upsample (us = 1) halves the halo's source coordinates:
+  // (y0 + hy) >> 1 = (y0 >> 1) + ((hy + 2) >> 1) - 1 for the even patch origins.
+  uint32_t hpk[2] = {0u, 0u};
+#pragma unroll
+  for (int gi = 0; gi < GH; ++gi) {
+    const int hr = gi * 64 + (int)(threadIdx.x >> 3);
+    const uint32_t v = hr < HROWS ? (uint32_t)((((hr / HW) + us) >> us) << 6 | (((hr % HW) + us) >> us)) : 0x3ffu;
+    hpk[gi / 3] |= v << (10 * (gi % 3));
+  }
+  const int xcs2 = xcs * 2, dys2 = a.dy_stride * 2;
+  auto issue_g = [&](const Patch& P, int gi, int buf) {
+    const int l = lane_now();
+    const int cpos = 16 * ((l & 7) ^ (2 * ((l >> 4) & 3)));   // (gsw(r0) = 2 ((r0 >> 1) & 3), r0 = 8 wave + (l >> 3))
+    if (gi < GH) {
+      const uint32_t v = (hpk[gi / 3] >> (10 * (gi % 3))) & 0x3ffu;
+      if (gi < GH - 1 || v != 0x3ffu) {
+        const int hyS = (int)(v >> 6), hxS = (int)(v & 63u);
+        const bool ok = (unsigned)((P.y0 >> us) - 1 + hyS) < (unsigned)a.Hs && (unsigned)((P.x0 >> us) - 1 + hxS) < (unsigned)a.Ws;
+        const unsigned off = ok ? (unsigned)((hyS * a.Ws + hxS + (P.pbx - a.Ws - 1)) * xcs2 + xc0 + cpos) : WG_OOB;
+        wg_buf_lds16(rsX, smem + buf * STAGE + (size_t)(gi * NTH + wave * 64) * 16, off);
+      }
+    } else {
+      const int i = gi - GH;
+      const unsigned voff = (unsigned)(((wave >> 2) * a.Wo + 8 * (wave & 3) + (l >> 3)) * dys2 + nblk * 128 + cpos);
+      wg_buf_lds16s(rsD, smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16, voff, (P.pbd + 2 * i * a.Wo) * dys2);
+    }
+  };
+  // the groups of local row j: ceil(10 / LSPR) a row; each group's address arithmetic is fenced off from the next
+  // (sched_barrier), so that their temporaries are not all live at once
+  // (LSPR 1-4: ceil(10 / LSPR) groups a row over the first LSPR rows; 5, 6, 7: 4-3-3-0, 3-4-3-0, 3-3-4-0; 8: 3-4-3-0 with
+  //  the waves of rows 1, 3, .. issuing after their row's first cluster, the others before it)
+  auto issue_lrow = [&](const Patch& P, auto jc, int buf) {
+    constexpr int j = decltype(jc)::value, NG = GH + GD, PER = LSPR <= 4 ? (NG + LSPR - 1) / LSPR : 3;
+    constexpr int B0 = LSPR == 5 ? 4 : 3, B1 = LSPR == 6 || LSPR == 8 ? B0 + 4 : B0 + 3;
+    constexpr int lo = LSPR <= 4 ? j * PER : j == 0 ? 0 : j == 1 ? B0 : j == 2 ? B1 : NG;
+    constexpr int hi = LSPR <= 4 ? (j + 1) * PER : j == 0 ? B0 : j == 1 ? B1 : NG;
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi)
+      if (gi >= lo && gi < hi) {
+        issue_g(P, gi, buf);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  };
+
+  // fragment addresses (per lane byte offsets into a stage; the 8-wave PF form's addressing): local row i is patch row
+  // pr = h + 2i; the halo rows of (pr, tap) start at (pr + dy) HW + dx and dY rows at pr PW, so row i is the row-0
+  // address + i 2 HW RB (halo) or + i 2 PW RB (dY): the same swizzle, immediate offsets
+  auto xoff = [&](int C, int col0, int lz) -> uint32_t {
+    const int g_ = lz >> 4, i_ = lz & 15;
+    const int R = C + 16 * (g_ >> 1) + 4 * (g_ & 1) + (i_ >> 2);
+    const int col = col0 + 4 * (i_ & 3), chunk = col >> 3, inb = (col & 7) * 2;
+    return (uint32_t)(R * RB + ((chunk ^ gsw<RB>(R)) << 4) + inb);
+  };
+  const uint32_t sbase = lds_off(smem);
+  // one address per operand family (its cb = 0 column block): the image rows are 128-B aligned and a 16-column block is
+  // 2 of a row's 8 swizzled 16-B chunks, so column block cb of the same rows is at address ^ (cb << 5) (the XOR commutes
+  // with the swizzle). The XOR sits inside the read statement, so the column-block addresses are never held in
+  // registers (13 address registers would be, beside 144 accumulators and 72 fragment registers)
+  uint32_t da, ha0, ha1, h8;
+  auto addrs = [&](uint32_t hb) {
+    const int lz = lane_now();
+    da = hb + HBUF + xoff(h * PW, 0, lz);
+    ha0 = hb + xoff((h + dy0) * HW + dx0, 0, lz);
+    ha1 = hb + xoff((h + dy1) * HW + dx1, 0, lz);
+    h8 = hb + xoff((h + 2) * HW + 2, p * 16, lz);
+  };
+  // fragment = two ds_read_b64_tr_b16 at immediate offsets OFF, OFF + 8 RB from address ad ^ (cb << 5)
+  auto rd = [](uint32_t ad, auto cbc, auto off) -> bf16x8 {
+    constexpr int cb = decltype(cbc)::value, OFF = decltype(off)::value;
+    v4s16 lo, hi;
+    if constexpr (cb == 0) {
+      asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+                   : "=v"(lo), "=v"(hi) : "v"(ad), "n"(OFF), "n"(OFF + 8 * RB) : "memory");
+    } else {
+      uint32_t t;
+      asm volatile("v_xor_b32 %2, %4, %3\n\tds_read_b64_tr_b16 %0, %2 offset:%5\n\tds_read_b64_tr_b16 %1, %2 offset:%6"
+                   : "=v"(lo), "=v"(hi), "=&v"(t) : "v"(ad), "n"(cb << 5), "n"(OFF), "n"(OFF + 8 * RB) : "memory");
+    }
+    bf16x8 r;
+    const bf16* l = reinterpret_cast<const bf16*>(&lo);
+    const bf16* hh = reinterpret_cast<const bf16*>(&hi);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { r[e] = l[e]; r[4 + e] = hh[e]; }
+    return r;
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using C2 = std::integral_constant<int, 2>;
+  using C3 = std::integral_constant<int, 3>;
+  bf16x8 fd[4], fx0[4], fx1[4], f8;   // dY^T, tap 2p, tap 2p+1, tap 8 (one set each: 52 registers)
+  // per local row the MFMA clusters run tap 2p, tap 8, tap 2p+1, and the next row's fragments are read as each cluster
+  // frees its registers: after tap 2p the last tap-2p+1 fragment of this row (read a row late, see below) and the next
+  // tap-2p set (10 reads), after tap 8 the next tap-8 fragment (2), after tap 2p+1 the next dY^T set and tap-2p+1
+  // fragments 0-2 (14). At most 15 reads are ever outstanding (the lgkmcnt field); a row's first cluster waits for the
+  // dY^T reads issued at the end of the previous row (the other wave of the SIMD multiplies meanwhile)
+  auto load_a = [&](auto ic) {   // (after tap 2p) tap-2p+1 fragment 3 of row i - 1, tap-2p set of row i
+    constexpr int i = decltype(ic)::value & 3;
+    using HO = std::integral_constant<int, i * 2 * HW * RB>;
+    using HP = std::integral_constant<int, ((i + 3) & 3) * 2 * HW * RB>;
+    if constexpr (decltype(ic)::value > 0) fx1[3] = rd(ha1, C3{}, HP{});
+    fx0[0] = rd(ha0, C0{}, HO{});
+    fx0[1] = rd(ha0, C1{}, HO{});
+    fx0[2] = rd(ha0, C2{}, HO{});
+    fx0[3] = rd(ha0, C3{}, HO{});
+  };
+  auto load_b = [&](auto ic) {   // (after tap 8) tap-8 fragment of row i
+    constexpr int i = decltype(ic)::value & 3;
+    using HO = std::integral_constant<int, i * 2 * HW * RB>;
+    f8 = rd(h8, C0{}, HO{});
+  };
+  auto load_c = [&](auto ic) {   // (after tap 2p+1) dY^T set and tap-2p+1 fragments 0-2 of row i
+    constexpr int i = decltype(ic)::value & 3;
+    using DO = std::integral_constant<int, i * 2 * PW * RB>;
+    using HO = std::integral_constant<int, i * 2 * HW * RB>;
+    fd[0] = rd(da, C0{}, DO{});
+    fd[1] = rd(da, C1{}, DO{});
+    fd[2] = rd(da, C2{}, DO{});
+    fd[3] = rd(da, C3{}, DO{});
+    fx1[0] = rd(ha1, C0{}, HO{});
+    fx1[1] = rd(ha1, C1{}, HO{});
+    fx1[2] = rd(ha1, C2{}, HO{});
+  };
+  // DB: the dY^T set double-buffered by local row parity (fd for even rows, fe for odd ones), so the next row's set is
+  // read right after this row's tap-2p cluster: G1 = the next dY^T set + tap-2p fragments 0-2 (14 reads, after tap 2p),
+  // G1b = tap-2p fragment 3 + tap 8 (4, after tap 8), G2 = the tap-2p+1 set (8, after tap 2p+1); a row's first cluster
+  // then waits for reads issued two clusters earlier
+  bf16x8 fe[4];
+  auto db_g1 = [&](auto ic) {
+    constexpr int i = decltype(ic)::value & 3;
+    using DO = std::integral_constant<int, i * 2 * PW * RB>;
+    using HO = std::integral_constant<int, i * 2 * HW * RB>;
+    bf16x8* d = (i & 1) ? fe : fd;
+    d[0] = rd(da, C0{}, DO{});
+    d[1] = rd(da, C1{}, DO{});
+    d[2] = rd(da, C2{}, DO{});
+    d[3] = rd(da, C3{}, DO{});
+    fx0[0] = rd(ha0, C0{}, HO{});
+    fx0[1] = rd(ha0, C1{}, HO{});
+    fx0[2] = rd(ha0, C2{}, HO{});
+  };
+  auto db_g1b = [&](auto ic) {
+    constexpr int i = decltype(ic)::value & 3;
+    using HO = std::integral_constant<int, i * 2 * HW * RB>;
+    fx0[3] = rd(ha0, C3{}, HO{});
+    f8 = rd(h8, C0{}, HO{});
+  };
+  auto db_g2 = [&](auto ic) {
+    constexpr int i = decltype(ic)::value & 3;
+    using HO = std::integral_constant<int, i * 2 * HW * RB>;
+    fx1[0] = rd(ha1, C0{}, HO{});
+    fx1[1] = rd(ha1, C1{}, HO{});
+    fx1[2] = rd(ha1, C2{}, HO{});
+    fx1[3] = rd(ha1, C3{}, HO{});
+  };
+
+  // The MFMAs are inline asm accumulating in place ("+v": D = C, one register tuple per accumulator for the whole
+  // loop). With the builtin, hipcc rotated the accumulators through other registers (94 of 144 MFMAs had D != C), which
+  // at 144 accumulators and 52 fragment registers left no room and spilled. Hazards of the asm form: the A / B
+  // fragments are asm LDS reads this code waits for itself (no VALU writes them: tests/test_isa.py), an accumulator is
+  // read as C one cluster (>= 4 MFMAs) after the MFMA that wrote it, the zero-initialising moves are fenced off from the
+  // first MFMA (acc_fence), and the epilogue's first VALU reads of the last cluster's results come after s_nops.
+  auto mma = [](f32x4& c, const bf16x8& x, const bf16x8& y) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(x), "v"(y));
+  };
+  f32x4 acc0[4][4], acc1[4][4], acc8[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0[i][j] = acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+v"(acc0[i][j]), "+v"(acc1[i][j]));
+    }
+    acc8[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("" : "+v"(acc8[i]));
+  }
+  asm volatile("s_nop 4" ::: "memory");   // (acc_fence: VALU writes of the accumulators -> MFMA reads of them as C)
+
+  const bool any = nt > 0;
+  if (any) {
+    const Patch P0 = patch(lin);
+#pragma unroll
+    for (int gi = 0; gi < GH + GD; ++gi) issue_g(P0, gi, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    W64_BAR();
+    addrs(sbase);
+    if constexpr (PIPE == 2) {   // row 0's sets in the steady-state order (16, 2, 8 reads)
+      fx0[0] = rd(ha0, C0{}, std::integral_constant<int, 0>{});
+      fd[0] = rd(da, C0{}, std::integral_constant<int, 0>{});
+      fx0[1] = rd(ha0, C1{}, std::integral_constant<int, 0>{});
+      fd[1] = rd(da, C1{}, std::integral_constant<int, 0>{});
+      fx0[2] = rd(ha0, C2{}, std::integral_constant<int, 0>{});
+      fd[2] = rd(da, C2{}, std::integral_constant<int, 0>{});
+      fx0[3] = rd(ha0, C3{}, std::integral_constant<int, 0>{});
+      fd[3] = rd(da, C3{}, std::integral_constant<int, 0>{});
+      lgkm_wait<13>();
+      f8 = rd(h8, C0{}, std::integral_constant<int, 0>{});
+      lgkm_wait<7>();
+      db_g2(std::integral_constant<int, 0>{});
+    } else if constexpr (DB) {
+      db_g1(std::integral_constant<int, 0>{});
+      lgkm_wait<11>();   // (at most 15 reads in flight)
+      db_g1b(std::integral_constant<int, 0>{});
+      lgkm_wait<7>();
+      db_g2(std::integral_constant<int, 0>{});
+    } else {
+      load_a(std::integral_constant<int, 0>{});   // (the steady-state issue order; row 0's fx1[3] comes with A(1))
+      load_b(std::integral_constant<int, 0>{});
+      lgkm_wait<1>();   // (at most 15 reads in flight)
+      load_c(std::integral_constant<int, 0>{});
+    }
+  }
+  for (int k = 0; k < nt; ++k) {
+    const int buf = k & 1;
+    const bool more = k + 1 < nt;
+    const Patch Pn = patch(more ? lin + (k + 1) * G : lin);
+    auto row = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i < (LSPR <= 4 ? LSPR : 3)) {
+        if (more && !(dbg & 2) && (LSPR != 8 || h == 0)) issue_lrow(Pn, ic, buf ^ 1);
+      }
+      // issue order up to here: [A(i): fx1(i-1)[3] (not for row 0 of a patch: read before the patch barrier), fx0(i)]
+      // [B(i): f8(i)] [C(i): fd(i), fx1(i)[0..2]]; row i needs fd, fx0, f8: only fx1(i)[0..2] (6) may be younger
+      if (!(dbg & 8)) lgkm_wait<6>();
+      prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          mma(acc0[nb][cb], fd[nb], fx0[cb]);
+      prio_lo<ADP_PRIO_WGRAD>();
+      if constexpr (LSPR == 8 && i < 3) {
+        if (more && !(dbg & 2) && h == 1) issue_lrow(Pn, ic, buf ^ 1);
+      }
+      if constexpr (i == 3) {
+        lgkm_wait<0>();                                      // every read of this buffer but fx1(3)[3] has returned;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's pieces of the next patch have landed
+        fx1[3] = rd(ha1, C3{}, std::integral_constant<int, 3 * 2 * HW * RB>{});
+        lgkm_wait<0>();                                      // (and that one: the buffer is read out)
+        if (!(dbg & 4)) W64_BAR();
+        if (more) {                                          // the next patch's rows, from the other buffer
+          addrs(sbase + (buf ^ 1) * STAGE);
+          load_a(std::integral_constant<int, 0>{});
+        }
+      } else {
+        lgkm_wait<5>();   // (C(i) has had the tap-2p cluster: at most 15 reads in flight after A(i + 1))
+        load_a(std::integral_constant<int, i + 1>{});
+      }
+      prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) mma(acc8[nb], fd[nb], f8);
+      prio_lo<ADP_PRIO_WGRAD>();
+      if (i < 3 || more) {
+        lgkm_wait<13>();
+        load_b(std::integral_constant<int, i + 1>{});
+      }
+      // fx1(i) complete: younger are A(i + 1) minus its first fragment (8) and B(i + 1) (2)
+      if (dbg & 8) {
+      } else if (i < 3 || more) lgkm_wait<10>();
+      else lgkm_wait<0>();
+      prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          mma(acc1[nb][cb], fd[nb], fx1[cb]);
+      prio_lo<ADP_PRIO_WGRAD>();
+      if (i < 3 || more) {
+        lgkm_wait<1>();   // (A(i + 1) and B(i + 1) issued a cluster ago)
+        load_c(std::integral_constant<int, i + 1>{});
+      }
+    };
+    auto row_db = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i < (LSPR <= 4 ? LSPR : 3)) {
+        if (more && !(dbg & 2)) issue_lrow(Pn, ic, buf ^ 1);
+      }
+      const bf16x8* d = (i & 1) ? fe : fd;
+      // issue order: [G1(i)] [G1b(i)] [G2(i)]: row i's first clusters need G1 and G1b, G2 (8) may be younger
+      if (!(dbg & 8)) lgkm_wait<8>();
+      prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          mma(acc0[nb][cb], d[nb], fx0[cb]);
+      prio_lo<ADP_PRIO_WGRAD>();
+      lgkm_wait<0>();   // G2(i) too (issued a cluster ago): nothing of row i is in flight
+      if constexpr (i == 3) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's pieces of the next patch have landed
+        if (!(dbg & 4)) W64_BAR();
+        if (more) addrs(sbase + (buf ^ 1) * STAGE);        // the next patch's rows, from the other buffer
+      }
+      if (i < 3 || more) db_g1(std::integral_constant<int, i + 1>{});
+      prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) mma(acc8[nb], d[nb], f8);
+      prio_lo<ADP_PRIO_WGRAD>();
+      if (i < 3 || more) {
+        lgkm_wait<11>();
+        db_g1b(std::integral_constant<int, i + 1>{});
+      }
+      prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          mma(acc1[nb][cb], d[nb], fx1[cb]);
+      prio_lo<ADP_PRIO_WGRAD>();
+      if (i < 3 || more) {
+        lgkm_wait<7>();
+        db_g2(std::integral_constant<int, i + 1>{});
+      }
+    };
+    // PIPE 2: the next row's fragments read inside the clusters, each right after the MFMAs that free its registers
+    // (dY^T double-buffered): after tap 2p column block cb, its next-row fragment and the next dY^T block cb (4 reads),
+    // after tap 8 its next fragment (2), after tap 2p+1 column block cb its next fragment (2). Every fragment is read at
+    // least a cluster before its first MFMA. Row 3 needs no LDS reads (its fragments were read during row 2), so the
+    // patch barrier sits at its start and its clusters read the next patch's first row from the other buffer.
+    auto row_il = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      using NI = std::integral_constant<int, (i + 1) & 3>;
+      using DO = std::integral_constant<int, NI::value * 2 * PW * RB>;
+      using HO = std::integral_constant<int, NI::value * 2 * HW * RB>;
+      if constexpr (i < (LSPR <= 4 ? LSPR : 3)) {
+        if (more && !(dbg & 2)) issue_lrow(Pn, ic, buf ^ 1);
+      }
+      const bf16x8* cur = (i & 1) ? fe : fd;
+      bf16x8* nxt = (i & 1) ? fd : fe;
+      if constexpr (i == 3) {
+        lgkm_wait<0>();                                      // row 3's fragments have landed: the buffer is read out,
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // and this thread's pieces of the next patch have landed
+        if (!(dbg & 4)) W64_BAR();
+        if (more) addrs(sbase + (buf ^ 1) * STAGE);
+      } else if (!(dbg & 8)) {
+        lgkm_wait<10>();   // row i's dY^T and tap-2p sets (read during row i - 1's first cluster) have landed
+      }
+      const bool ld = i < 3 || more;
+      auto tap0_cb = [&](auto cbc) {
+        constexpr int cb = decltype(cbc)::value;
+        prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) mma(acc0[nb][cb], cur[nb], fx0[cb]);
+        prio_lo<ADP_PRIO_WGRAD>();
+        if (ld) {
+          if constexpr (cb > 0) lgkm_wait<11>();   // (at most 15 in flight; by cb = 1 this row's f8, by cb = 3 its fx1)
+          fx0[cb] = rd(ha0, cbc, HO{});
+          nxt[cb] = rd(da, cbc, DO{});
+        }
+      };
+      tap0_cb(C0{});
+      tap0_cb(C1{});
+      tap0_cb(C2{});
+      tap0_cb(C3{});
+      prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) mma(acc8[nb], cur[nb], f8);
+      prio_lo<ADP_PRIO_WGRAD>();
+      if (ld) {
+        lgkm_wait<13>();
+        f8 = rd(h8, C0{}, HO{});
+      }
+      auto tap1_cb = [&](auto cbc) {
+        constexpr int cb = decltype(cbc)::value;
+        prio_hi<ADP_PRIO_WGRAD>();
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) mma(acc1[nb][cb], cur[nb], fx1[cb]);
+        prio_lo<ADP_PRIO_WGRAD>();
+        if (ld) {
+          lgkm_wait<13>();
+          fx1[cb] = rd(ha1, cbc, HO{});
+        }
+      };
+      tap1_cb(C0{});
+      tap1_cb(C1{});
+      tap1_cb(C2{});
+      tap1_cb(C3{});
+    };
+    if constexpr (PIPE == 2) {
+      row_il(std::integral_constant<int, 0>{});
+      row_il(std::integral_constant<int, 1>{});
+      row_il(std::integral_constant<int, 2>{});
+      row_il(std::integral_constant<int, 3>{});
+    } else if constexpr (DB) {
+      row_db(std::integral_constant<int, 0>{});
+      row_db(std::integral_constant<int, 1>{});
+      row_db(std::integral_constant<int, 2>{});
+      row_db(std::integral_constant<int, 3>{});
+    } else {
+      row(std::integral_constant<int, 0>{});
+      row(std::integral_constant<int, 1>{});
+      row(std::integral_constant<int, 2>{});
+      row(std::integral_constant<int, 3>{});
+    }
+  }
+  // the last cluster's results (tap 2p+1, column block 3: its last four MFMAs) before any VALU reads them
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc1[0][3]), "+v"(acc1[1][3]), "+v"(acc1[2][3]), "+v"(acc1[3][3]));
+  if (!any && !a.part) return;   // (a slab gets its zeros)
+  if (dbg & 1) {
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) asm volatile("" ::"v"(acc0[nb][cb]), "v"(acc1[nb][cb]));
+      asm volatile("" ::"v"(acc8[nb]));
+    }
+    return;
+  }
+  // epilogue: waves h = 1 put their partial in the [64][ES] image, waves h = 0 add it to theirs (h0 + h1) and put the
+  // sum back, then the whole block writes the 64 x 576 partial out in 16-B pieces. (Every LDS read of the loop has
+  // returned before the last patch barrier, and no LDS-DMA is in flight after it.)
+  float* img = reinterpret_cast<float*>(smem);
+  const int lane = lane_now(), tid = wave * 64 + lane;
+  const int col = lane & 15, rq = (lane >> 4) * 4;
+  auto each = [&](auto fn) {   // (tile, element) -> image index, for the 36 tiles of this pair
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rowi = (nb * 16 + rq + r) * ES + cb * 16 + col;
+          fn(acc0[nb][cb][r], rowi + t0 * 64);
+          fn(acc1[nb][cb][r], rowi + t1 * 64);
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) fn(acc8[nb][r], (nb * 16 + rq + r) * ES + 8 * 64 + p * 16 + col);
+    }
+  };
+  if (h == 1) each([&](float v, int ix) { img[ix] = v; });
+  __syncthreads();
+  if (h == 0) each([&](float v, int ix) { img[ix] = v + img[ix]; });
+  __syncthreads();
+  const int cin = a.CAs + a.CBs;
+  float* dW = a.part ? a.part + ((size_t)lin * a.Nout + (size_t)nblk * 64) * a.Kpad : a.dW + (size_t)nblk * 64 * a.Kpad;
+#pragma unroll 2
+  for (int j = 0; j < 64 * 144 / NTH; ++j) {
+    const int idx = j * NTH + tid, n = idx / 144, r = idx - 144 * (idx / 144), tap = r >> 4, c4 = r & 15;
+    const float4 v = *reinterpret_cast<const float4*>(img + n * ES + tap * 64 + c4 * 4);
+    float* d = dW + (size_t)n * a.Kpad + tap * cin + ch * 64 + c4 * 4;
+    if (a.part) {
+      *reinterpret_cast<float4*>(d) = v;
+    } else if (a.part_rmw) {
+      float4 o = *reinterpret_cast<float4*>(d);
+      o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+      *reinterpret_cast<float4*>(d) = o;
+    } else {
+      atomicAdd(d, v.x); atomicAdd(d + 1, v.y); atomicAdd(d + 2, v.z); atomicAdd(d + 3, v.w);
+    }
+  }
+}
+
+
+template __global__ void igemm_wgrad_halopair_kernel<4, 0>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<4, 1>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<4, 2>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<6, 0>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<8, 0>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<6, 1>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<6, 2>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<2, 0>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<2, 1>(WgradArgs);
+
 // Weight gradient of the input layers (one 8-channel source, 3x3 stride 1, 64 outputs; K = 72): an
 // HBM-bound pass over dY (128 B per pixel) and X (16 B per pixel). Persistent, one block per CU, a
 // 3-stage LDS-DMA ring of 8 x 32 patches (34 x 10 halo of 16-B pixels + the 256 x 64 dY tile); wave w
@@ -1550,6 +2094,22 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
         adp::set_kernel("igemm_wgrad_halop_kernel<8, true, 4, true, false>");
         hipLaunchKernelGGL((igemm_wgrad_halop_kernel<8, true, 4>), dim3(grid), dim3(512), 0, s, a);
       }
+    } else if (stat_inst && option("wgrad_halop_pair", 1)) {
+      // (round 6, default: the tap-pair form -- two waves of a SIMD own taps 2p, 2p + 1 and a quarter of tap 8 and split
+      //  the patch rows; option wgrad_halop_pair = 0 keeps the one-tap-per-wave forms below)
+      // (options wgrad_pair_spread: the LDS-DMA schedule LSPR; wgrad_pair_pipe: the fragment-read schedule PIPE)
+      const int spr = option("wgrad_pair_spread", 6), pipe = option("wgrad_pair_pipe", 0);
+#define ADP_PAIR(L, D)                                                                                              \
+  if (spr == L && pipe == D) {                                                                                      \
+    adp::set_kernel("igemm_wgrad_halopair_kernel<" #L ", " #D ">");                                                \
+    hipLaunchKernelGGL((igemm_wgrad_halopair_kernel<L, D>), dim3(grid), dim3(512), 0, s, a);                       \
+  } else
+      ADP_PAIR(6, 0) ADP_PAIR(6, 2) ADP_PAIR(6, 1) ADP_PAIR(8, 0) ADP_PAIR(4, 0) ADP_PAIR(4, 1) ADP_PAIR(4, 2) ADP_PAIR(2, 0)
+      ADP_PAIR(2, 1) {
+        set_error("wgrad_pair_spread 2 / 4 / 6 / 8, wgrad_pair_pipe 0 / 1 / 2");
+        return -1;
+      }
+#undef ADP_PAIR
     } else if (option("wgrad_halop_waves", 8) == 9) {
       adp::set_kernel("igemm_wgrad_halop_kernel<9, false, 8, true, false>");
       hipLaunchKernelGGL(igemm_wgrad_halop_kernel<9>, dim3(grid), dim3(576), 0, s, a);

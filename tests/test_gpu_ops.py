@@ -1601,14 +1601,18 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     dW = torch.zeros((l.Npad, l.Kpad), device=DEV)
     try:
         ops.conv_wgrad(xd[0], dzd, dW, l.Nout, srcB=srcB)
-        # default: the row-pipelined static-list form (round 5)
-        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false, true>"
+        # default: the tap-pair form (round 6)
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halopair_kernel<6, 0>"
         torch.cuda.synchronize()
         dW2 = torch.zeros_like(dW)   # fixed-order slab reduce (option wgrad_det): a second run gives the same bits
         ops.conv_wgrad(xd[0], dzd, dW2, l.Nout, srcB=srcB)
         torch.cuda.synchronize()
         assert torch.equal(dW, dW2)
-        ops.set_option("wgrad_halop_pf", 0)   # the unpipelined row loop: the same per-block sums
+        ops.set_option("wgrad_halop_pair", 0)   # the one-tap-per-wave forms: the row-pipelined one (round 5) ...
+        dWpf = torch.zeros_like(dW)
+        ops.conv_wgrad(xd[0], dzd, dWpf, l.Nout, srcB=srcB)
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false, true>"
+        ops.set_option("wgrad_halop_pf", 0)   # ... and the unpipelined row loop: the same per-block sums
         dWn = torch.zeros_like(dW)
         ops.conv_wgrad(xd[0], dzd, dWn, l.Nout, srcB=srcB)
         assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false, false>"
@@ -1634,8 +1638,11 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
         ops.set_option("wgrad_halop_waves", None)
         ops.set_option("wgrad_halop_spread", None)
         ops.set_option("wgrad_halop_pf", None)
+        ops.set_option("wgrad_halop_pair", None)
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
-    assert torch.equal(dW, dWn) and torch.equal(dW, dWp8)   # (same per-block sums, same fixed-order reduce)
+    assert torch.equal(dWpf, dWn) and torch.equal(dWpf, dWp8)   # (same per-block sums, same fixed-order reduce)
+    # the tap-pair form sums the even and the odd patch rows separately, then adds the two: another f32 order
+    assert relerr(dW.cpu(), dWpf.cpu()) < 1e-5
     assert relerr(dW.cpu(), ref.cpu()) < 1e-4 and relerr(dW9.cpu(), ref.cpu()) < 1e-4
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
@@ -1675,7 +1682,7 @@ def test_wgrad_deferred_reductions():
     ops.wgrad_defer(True)
     try:
         run(d_h)
-        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halop_kernel<8, false, 4, false, true>"
+        assert _lib.lib().adp_last_kernel().decode() == "igemm_wgrad_halopair_kernel<6, 0>"
         run(d_h2)
         run(d_h2)
         run(d_t, "wgrad_halop", dB=d_b)
@@ -1840,7 +1847,7 @@ def test_halo_kernels_claimed_match_static(case, grid):
         for o_ in ("halo_persist_grid", "wgrad_halop_grid", wopt, "claim_full", wopt + "_chunk"):
             ops.set_option(o_, None)
     k0 = res[0][2]
-    assert k0.startswith("igemm_wgrad_halop_kernel" if kind.startswith("wgrad") else "igemm_fwd_halop_kernel"), k0
+    assert k0.startswith("igemm_wgrad_halop" if kind.startswith("wgrad") else "igemm_fwd_halop_kernel"), k0
     for ex, fl, kn in res[1:]:
         if not kind.startswith("wgrad") and kind != "bnr":
             assert kn.split("<")[1].rstrip(">").split(", ")[6] == "true", kn   # the claimed form ran (DYN)
@@ -1877,7 +1884,7 @@ def test_wgrad_persistent_halo_upsample(N, Hs, Ws, parts, cout):
         torch.cuda.synchronize()
     finally:
         ops.set_option("wgrad_halop", None)
-    assert kname.startswith("igemm_wgrad_halop_kernel"), kname
+    assert kname == "igemm_wgrad_halopair_kernel<6, 0>", kname
     assert relerr(torch.from_numpy(l.packed_to_keras(dW.cpu().numpy())), kr.grad) < 2e-2
     assert relerr(dW.cpu(), ref.cpu()) < 1e-4
 

@@ -200,3 +200,102 @@ def test_reported_kernel_names_exist(code_objects):
         if not any(re.fullmatch(rx, n) for n in names):
             missing.append((f, p))
     assert not missing, missing
+
+
+def _ds_paths_ok(ins, start):
+    """From an LDS read at index `start` (the kernels' fragment reads are inline asm, which hipcc does not count): on every
+    control-flow path, its destination registers are neither read nor written -- no copy, spill or reuse -- before an
+    s_waitcnt lgkmcnt(N) with N <= the LDS instructions issued after the read on that path (LDS operations return in
+    order; scalar loads also count in lgkmcnt but only make such a wait stricter)."""
+    addr_idx = {a: i for i, (a, _, _) in enumerate(ins)}
+    dst = _regs(ins[start][2].split(",")[0])
+    stack = [(start + 1, 0)]
+    seen = set()
+    while stack:
+        i, young = stack.pop()
+        while i < len(ins):
+            if (i, young) in seen:
+                break
+            seen.add((i, young))
+            addr, op, opnd = ins[i]
+            if op == "s_waitcnt":
+                m = re.search(r"lgkmcnt\((\d+)\)", opnd)
+                if (m and int(m.group(1)) <= young) or opnd.strip() == "0":
+                    break
+            elif op == "s_endpgm":
+                break
+            elif dst & _regs(opnd):
+                return [(hex(addr), op, opnd)]
+            if op.startswith("ds_"):
+                young += 1
+            if op == "s_branch" or op.startswith("s_cbranch"):
+                tgt = addr + 4 + 4 * int(opnd.split()[0])
+                if tgt in addr_idx:
+                    stack.append((addr_idx[tgt], young))
+                if op == "s_branch":
+                    break
+            i += 1
+    return []
+
+
+@pytest.mark.parametrize("obj", ["conv_wgrad_tap64.hip.o", "conv_fwd_halo.hip.o", "conv_fwd_tap64p.hip.o",
+                                 "conv_fwd_tap64.hip.o"])
+def test_asm_lds_reads_untouched_until_waited(code_objects, obj):
+    """The hot K loops read their MFMA fragments with inline-asm ds_read_b64_tr_b16 / ds_read_b128 (the builtins would make
+    hipcc drain every LDS-DMA in flight first). hipcc treats an asm load's destination as written at the statement, so
+    under register pressure it may copy or spill the register before the data lands (round 6: the first build of the
+    tap-pair weight gradient spilled and moved fragment registers right after their reads; silent garbage, no fault).
+    Every LDS read's destination must stay untouched until a wait that retires it."""
+    co = code_objects.get(obj)
+    assert co is not None
+    bad = []
+    n = 0
+    for fn, ins in _disasm(co).items():
+        for i, (addr, op, opnd) in enumerate(ins):
+            if op.startswith("ds_read"):
+                n += 1
+                p = _ds_paths_ok(ins, i)
+                if p:
+                    bad.append((_demangle([fn])[0][:80], hex(addr), op, opnd, p[0]))
+    assert n > 0
+    assert not bad, bad[:5]
+
+
+def test_pair_wgrad_mfma_operands_come_from_lds():
+    """The tap-pair weight gradient's MFMAs are inline asm (accumulating in place), so hipcc pads no hazard in front of
+    them: every A / B operand register must have been written last by one of the kernel's LDS reads (never by a VALU
+    copy, which would need wait states before an MFMA reads it), and every accumulator is used in place (D = C)."""
+    co = None
+    for f in os.listdir(BUILD):
+        if f == "conv_wgrad_tap64.hip.o":
+            tmp = tempfile.mkdtemp()
+            co = _code_object(os.path.join(BUILD, f), tmp)
+    assert co is not None
+    checked = 0
+    bad = []
+    for fn, ins in _disasm(co).items():
+        if "halopair" not in fn:
+            continue
+        for i, (addr, op, opnd) in enumerate(ins):
+            if not op.startswith("v_mfma"):
+                continue
+            parts = [p.strip() for p in opnd.split(",")]
+            if parts[0] != parts[3]:
+                bad.append((hex(addr), "D != C", opnd))
+            for src in (parts[1], parts[2]):
+                regs = _regs(src)
+                j = i - 1
+                while j >= 0:
+                    _, op2, opnd2 = ins[j]
+                    if op2.startswith("v_mfma") or op2.startswith("s_") or not opnd2:
+                        j -= 1
+                        continue
+                    d = _regs(opnd2.split(",")[0])
+                    if d & regs:
+                        if not op2.startswith("ds_read"):
+                            bad.append((hex(addr), op2, opnd2))
+                        break
+                    j -= 1
+            checked += 1
+    assert checked >= 144
+    assert not bad, bad[:5]
