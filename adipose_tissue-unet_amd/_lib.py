@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 
 class AdpError(RuntimeError):
@@ -88,6 +88,8 @@ _SIGS = {
     "adp_bn_fold_reset": [_P],
     "adp_wgrad_defer": [_I, _P],
     "adp_wgrad_flush": [_P],
+    "adp_wgrad_release": [_P],
+    "adp_wgrad_arena_chunks": [_P],
     "adp_debug_grad_flat": [_P, _I, _P, _S],
     "adp_bn_apply": [_I, _S, _I, _P, _P, _P, _P, _P],
     "adp_bn_bwd_reduce":[_I, _S, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P],

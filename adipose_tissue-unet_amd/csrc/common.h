@@ -153,6 +153,8 @@ void* scratch(int slot, size_t bytes);
 // deferred weight-gradient slab reductions of a stream (adp_wgrad_defer / adp_wgrad_flush; conv_wgrad_tap64.hip)
 int wgrad_defer(hipStream_t s, int on);
 int wgrad_flush(hipStream_t s);
+int wgrad_release(hipStream_t s);
+int wgrad_arena_chunks(hipStream_t s);
 int stat_fold(int C, float* dst0, float* dst1, hipStream_t s);   // elementwise.hip
 // the same over replica channels [c0, c0 + C) into dst0[0..C) (and dst1 unless nullptr)
 int stat_fold_at(int c0, int C, float* dst0, float* dst1, hipStream_t s);

@@ -297,6 +297,9 @@ __global__ __launch_bounds__(512, 1) void igemm_fwd_halop_kernel(FwdArgs a) {
   constexpr int NTH = 512, NF = BN / 16;
   constexpr int HCH = NCH * HROWS * 8;                      // 16-B halo chunks (all input chunks)
   constexpr int GH = (HCH + NTH - 1) / NTH;                 // halo chunks per thread
+  // (BNL applies the next patch's chunk j between the MFMAs of tap 3 + j, taps 3..8: six chunks at most, or later
+  //  chunks would reach LDS without the BatchNorm-ReLU -- round-5 ADVICE)
+  static_assert(!BNL || GH <= 6, "BN-on-load: at most six halo chunks per thread");
   constexpr int HBUF = HCH * 16;
   constexpr int GW = 9 * NCH * BN * 8 / NTH;                // resident weight chunks per thread
   constexpr int WTAP = NCH * BN * ROWB;

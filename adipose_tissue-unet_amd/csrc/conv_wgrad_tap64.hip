@@ -992,12 +992,13 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halopair_kernel(WgradArgs 
   constexpr int STAGE = HBUF + DBUF;
   constexpr int ES = 9 * 64 + 4;   // epilogue: the block's [64][576] f32 partial, row stride 580 (bank-conflict-free)
   static_assert(64 * ES * 4 <= 2 * STAGE, "the epilogue image fits in the two stages");
-  static_assert(GD * NTH == DCH && GH + GD == 10 && LSPR >= 1 && LSPR <= 8, "shape");
+  static_assert(GD * NTH == DCH && GH + GD == 10 && LSPR >= 1 && LSPR <= 9, "shape");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // timing-only ablations (ablation build, option wgrad_debug): bit 0 no output, bit 1 no LDS-DMA after the prologue,
-  // bit 2 no patch barrier, bit 3 the MFMA clusters do not wait for their fragments
+  // bit 2 no patch barrier, bit 3 the MFMA clusters do not wait for their fragments, bit 4 no wait for the next patch's
+  // LDS-DMA before the barrier
   const int dbg = ADP_DBG(a);
   // (the lane id is re-derived by v_mbcnt in a volatile statement wherever the loop needs it, so that neither it nor the
   // thread id occupies a register across the loop)
@@ -1086,6 +1087,19 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halopair_kernel(WgradArgs 
       }
   };
 
+  // LSPR 9: one group at each MFMA-cluster boundary of rows 0-2 (row start, after tap 2p, after tap 8; two at row 0's
+  // start), so that no two pieces are issued back to back
+  auto issue_slot = [&](const Patch& P, auto jc, auto bc, int buf) {
+    constexpr int sl = 3 * decltype(jc)::value + decltype(bc)::value;
+    constexpr int lo = sl == 0 ? 0 : sl + 1, hi = sl + 2;
+    if constexpr (decltype(jc)::value < 3) {
+#pragma unroll
+      for (int gi = lo; gi < hi; ++gi) {
+        issue_g(P, gi, buf);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
   // fragment addresses (per lane byte offsets into a stage; the 8-wave PF form's addressing): local row i is patch row
   // pr = h + 2i; the halo rows of (pr, tap) start at (pr + dy) HW + dx and dY rows at pr PW, so row i is the row-0
   // address + i 2 HW RB (halo) or + i 2 PW RB (dY): the same swizzle, immediate offsets
@@ -1259,7 +1273,9 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halopair_kernel(WgradArgs 
     const Patch Pn = patch(more ? lin + (k + 1) * G : lin);
     auto row = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      if constexpr (i < (LSPR <= 4 ? LSPR : 3)) {
+      if constexpr (LSPR == 9) {
+        if (more && !(dbg & 2)) issue_slot(Pn, ic, C0{}, buf ^ 1);
+      } else if constexpr (i < (LSPR <= 4 ? LSPR : 3)) {
         if (more && !(dbg & 2) && (LSPR != 8 || h == 0)) issue_lrow(Pn, ic, buf ^ 1);
       }
       // issue order up to here: [A(i): fx1(i-1)[3] (not for row 0 of a patch: read before the patch barrier), fx0(i)]
@@ -1275,9 +1291,12 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halopair_kernel(WgradArgs 
       if constexpr (LSPR == 8 && i < 3) {
         if (more && !(dbg & 2) && h == 1) issue_lrow(Pn, ic, buf ^ 1);
       }
+      if constexpr (LSPR == 9) {
+        if (more && !(dbg & 2)) issue_slot(Pn, ic, C1{}, buf ^ 1);
+      }
       if constexpr (i == 3) {
         lgkm_wait<0>();                                      // every read of this buffer but fx1(3)[3] has returned;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's pieces of the next patch have landed
+        if (!(dbg & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's next-patch pieces landed
         fx1[3] = rd(ha1, C3{}, std::integral_constant<int, 3 * 2 * HW * RB>{});
         lgkm_wait<0>();                                      // (and that one: the buffer is read out)
         if (!(dbg & 4)) W64_BAR();
@@ -1293,6 +1312,9 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halopair_kernel(WgradArgs 
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) mma(acc8[nb], fd[nb], f8);
       prio_lo<ADP_PRIO_WGRAD>();
+      if constexpr (LSPR == 9) {
+        if (more && !(dbg & 2)) issue_slot(Pn, ic, C2{}, buf ^ 1);
+      }
       if (i < 3 || more) {
         lgkm_wait<13>();
         load_b(std::integral_constant<int, i + 1>{});
@@ -1493,15 +1515,13 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halopair_kernel(WgradArgs 
 }
 
 
-template __global__ void igemm_wgrad_halopair_kernel<4, 0>(WgradArgs);
-template __global__ void igemm_wgrad_halopair_kernel<4, 1>(WgradArgs);
-template __global__ void igemm_wgrad_halopair_kernel<4, 2>(WgradArgs);
+
 template __global__ void igemm_wgrad_halopair_kernel<6, 0>(WgradArgs);
-template __global__ void igemm_wgrad_halopair_kernel<8, 0>(WgradArgs);
 template __global__ void igemm_wgrad_halopair_kernel<6, 1>(WgradArgs);
 template __global__ void igemm_wgrad_halopair_kernel<6, 2>(WgradArgs);
-template __global__ void igemm_wgrad_halopair_kernel<2, 0>(WgradArgs);
-template __global__ void igemm_wgrad_halopair_kernel<2, 1>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<4, 0>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<8, 0>(WgradArgs);
+template __global__ void igemm_wgrad_halopair_kernel<9, 0>(WgradArgs);
 
 // Weight gradient of the input layers (one 8-channel source, 3x3 stride 1, 64 outputs; K = 72): an
 // HBM-bound pass over dY (128 B per pixel) and X (16 B per pixel). Persistent, one block per CU, a
@@ -1899,7 +1919,8 @@ namespace adp {
 // kernel (up to SEG_MAX segments per launch), in the same fixed order: bit-identical gradients.
 struct Deferred {
   bool on = false;
-  std::vector<std::pair<char*, size_t>> chunks;   // (base, bytes), reused across steps
+  bool fallback = false;                            // the last reduce_part came from scratch: reduce it at once
+  std::vector<std::pair<char*, size_t>> chunks;   // (base, bytes) on the key's device, reused across steps
   size_t ci = 0, used = 0;                          // current chunk, bytes used in it
   size_t pending = 0;                               // slab bytes recorded since the last launch of the tables
   std::vector<SegTable> tables;                     // (built as the segments are recorded)
@@ -1909,17 +1930,26 @@ static void launch_tables(std::vector<SegTable>& tables, hipStream_t s) {
     if (t.n > 0) hipLaunchKernelGGL(wgrad_slab_reduce_batched_kernel, dim3((unsigned)t.blk0[t.n]), dim3(256), 0, s, t);
   tables.clear();
 }
+// keyed by (device, stream) like every other piece of library state (round-5 ADVICE): the default stream is handle 0
+// on every device, and an arena chunk must live on the device whose launches write it
+using DefKey = std::pair<int, hipStream_t>;
 static std::mutex g_def_mu;
-static std::map<hipStream_t, Deferred>& deferred_map() {
-  static std::map<hipStream_t, Deferred> m;
+static std::map<DefKey, Deferred>& deferred_map() {
+  static std::map<DefKey, Deferred> m;
   return m;
+}
+static DefKey def_key(hipStream_t s) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return {dev, s};
 }
 float* reduce_part(int slot, size_t bytes, hipStream_t s) {
   {
     std::lock_guard<std::mutex> lk(g_def_mu);
-    auto it = deferred_map().find(s);
+    auto it = deferred_map().find(def_key(s));
     if (it != deferred_map().end() && it->second.on) {
       Deferred& d = it->second;
+      d.fallback = false;
       bytes = (bytes + 255) / 256 * 256;
       // (option wgrad_defer_mb: once the recorded slabs would pass this many MB, the recorded reductions are
       //  launched first and the arena starts over: the slabs are re-read while they still sit in the MALL, and the
@@ -1931,15 +1961,21 @@ float* reduce_part(int slot, size_t bytes, hipStream_t s) {
         d.used = 0;
         d.pending = 0;
       }
-      d.pending += bytes;
       while (d.ci < d.chunks.size() && d.used + bytes > d.chunks[d.ci].second) { ++d.ci; d.used = 0; }
-      if (d.ci == d.chunks.size()) {   // (first steps only: a new chunk, never freed while the process runs)
+      if (d.ci == d.chunks.size()) {   // (first steps only: a new chunk, kept until adp_wgrad_release)
         const size_t sz = std::max(bytes, (size_t)256 << 20);
         void* p = nullptr;
-        if (hipMalloc(&p, sz) != hipSuccess) { set_error("adp_wgrad_defer: arena allocation failed"); return nullptr; }
+        if (hipMalloc(&p, sz) != hipSuccess) {
+          // no arena: this launch's slabs go to the scratch slot and its reduction runs at once (slab_reduce), still
+          // in a fixed order (round-5 ADVICE: it fell back to the f32 atomics and left a stale error)
+          (void)hipGetLastError();
+          d.fallback = true;
+          return static_cast<float*>(scratch(slot, bytes));
+        }
         d.chunks.push_back({static_cast<char*>(p), sz});
         d.used = 0;
       }
+      d.pending += bytes;
       float* r = reinterpret_cast<float*>(d.chunks[d.ci].first + d.used);
       d.used += bytes;
       return r;
@@ -1950,8 +1986,8 @@ float* reduce_part(int slot, size_t bytes, hipStream_t s) {
 void slab_reduce(int G, size_t n4, const float* part, float* dst, hipStream_t s) {
   {
     std::lock_guard<std::mutex> lk(g_def_mu);
-    auto it = deferred_map().find(s);
-    if (it != deferred_map().end() && it->second.on) {
+    auto it = deferred_map().find(def_key(s));
+    if (it != deferred_map().end() && it->second.on && !it->second.fallback) {
       Deferred& d = it->second;
       // segments of one launch run concurrently: a destination already in the open table (the same gradient
       // accumulated twice) starts a new table, launched after it
@@ -1975,13 +2011,14 @@ void slab_reduce(int G, size_t n4, const float* part, float* dst, hipStream_t s)
       t.blk0[j + 1] = t.blk0[j] + (int)((n4 + 31) / 32);
       return;
     }
+    if (it != deferred_map().end()) it->second.fallback = false;
   }
   hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)((n4 + 31) / 32)), dim3(256), 0, s, G, n4,
                      reinterpret_cast<const float4*>(part), reinterpret_cast<float4*>(dst));
 }
 int wgrad_defer(hipStream_t s, int on) {
   std::lock_guard<std::mutex> lk(g_def_mu);
-  Deferred& d = deferred_map()[s];
+  Deferred& d = deferred_map()[def_key(s)];
   if (!on && !d.tables.empty()) { set_error("adp_wgrad_defer: reductions pending (adp_wgrad_flush first)"); return -1; }
   d.on = on != 0 && option("wgrad_defer", 1);   // (option wgrad_defer = 0: every reduction launched at once)
   return 0;
@@ -1992,7 +2029,7 @@ int wgrad_flush(hipStream_t s) {
   std::vector<SegTable> tables;
   {
     std::lock_guard<std::mutex> lk(g_def_mu);
-    Deferred& d = deferred_map()[s];
+    Deferred& d = deferred_map()[def_key(s)];
     tables.swap(d.tables);
     d.on = false;
     d.ci = 0;
@@ -2001,6 +2038,28 @@ int wgrad_flush(hipStream_t s) {
   }
   launch_tables(tables, s);
   return 0;
+}
+// free the arena of (current device, stream s) and forget the stream (an arena per stream that ever
+// deferred, never freed; a destroyed stream's reused handle inherited it). Synchronises s first; an error with
+// reductions pending (flush first).
+int wgrad_release(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_def_mu);
+  auto it = deferred_map().find(def_key(s));
+  if (it == deferred_map().end()) return 0;
+  if (!it->second.tables.empty()) { set_error("adp_wgrad_release: reductions pending (adp_wgrad_flush first)"); return -1; }
+  if (!it->second.chunks.empty() && hipStreamSynchronize(s) != hipSuccess) {
+    set_error("adp_wgrad_release: stream synchronisation failed");
+    return -1;
+  }
+  for (auto& c : it->second.chunks) (void)hipFree(c.first);
+  deferred_map().erase(it);
+  return 0;
+}
+// (test hook) the number of arena chunks of (current device, stream s)
+int wgrad_arena_chunks(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_def_mu);
+  auto it = deferred_map().find(def_key(s));
+  return it == deferred_map().end() ? 0 : (int)it->second.chunks.size();
 }
 // shapes of the persistent halo weight-gradient kernel
 static bool halop_ok(const WgradArgs& a) {
@@ -2104,9 +2163,8 @@ int launch_wgrad_tap64(WgradArgs& a, hipStream_t s) {
     adp::set_kernel("igemm_wgrad_halopair_kernel<" #L ", " #D ">");                                                \
     hipLaunchKernelGGL((igemm_wgrad_halopair_kernel<L, D>), dim3(grid), dim3(512), 0, s, a);                       \
   } else
-      ADP_PAIR(6, 0) ADP_PAIR(6, 2) ADP_PAIR(6, 1) ADP_PAIR(8, 0) ADP_PAIR(4, 0) ADP_PAIR(4, 1) ADP_PAIR(4, 2) ADP_PAIR(2, 0)
-      ADP_PAIR(2, 1) {
-        set_error("wgrad_pair_spread 2 / 4 / 6 / 8, wgrad_pair_pipe 0 / 1 / 2");
+      ADP_PAIR(6, 0) ADP_PAIR(6, 1) ADP_PAIR(6, 2) ADP_PAIR(4, 0) ADP_PAIR(8, 0) ADP_PAIR(9, 0) {
+        set_error("wgrad_pair_spread / wgrad_pair_pipe: (6, 0 / 1 / 2), (4, 0), (8, 0) or (9, 0)");
         return -1;
       }
 #undef ADP_PAIR

@@ -1120,6 +1120,8 @@ extern "C" int adp_wgrad_flush(adp_stream_t st) {
   adp::wgrad_flush((hipStream_t)st);
   return adp::check_launch("adp_wgrad_flush");
 }
+extern "C" int adp_wgrad_release(adp_stream_t st) { return adp::wgrad_release((hipStream_t)st) ? -1 : 0; }
+extern "C" int adp_wgrad_arena_chunks(adp_stream_t st) { return adp::wgrad_arena_chunks((hipStream_t)st); }
 
 extern "C" int adp_bn_finalize_fold(int C, float count, float* sum, float* sq, const float* gamma, const float* beta,
                                     float eps, float momentum, float* scale, float* shift, float* mean, float* invstd,

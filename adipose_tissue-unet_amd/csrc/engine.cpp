@@ -759,6 +759,7 @@ struct adp_handle {
       bev.push_back(e);
     }
     pend.assign(buckets.size(), {});
+    dp_queue.clear();
     for (size_t b = 0; b < buckets.size(); ++b) {
       buckets[b].launched = false;
       for (int id : buckets[b].layers)
@@ -767,13 +768,23 @@ struct adp_handle {
     dp_active = true;
     return 0;
   }
-  int dp_launch(int bi, hipStream_t s) {
-    Bucket& bk = buckets[bi];
-    bk.launched = true;
-    if (deferring) {   // the bucket's gradients are final only after the recorded reductions ran
+  // ready buckets are queued and go out dp_launch_group (option, default 2) at a time behind ONE flush of the deferred
+  // weight-gradient reductions (trainer.GradBuckets.launch_group, round 6); dp_finish sends the rest
+  std::vector<int> dp_queue;
+  int dp_launch_queued(hipStream_t s) {
+    if (dp_queue.empty()) return 0;
+    if (deferring) {   // the buckets' gradients are final only after the recorded reductions ran
       CL(adp_wgrad_flush(s));
       CL(adp_wgrad_defer(1, s));
     }
+    std::vector<int> q;
+    q.swap(dp_queue);
+    for (int bi : q) CL(dp_launch(bi, s));
+    return 0;
+  }
+  int dp_launch(int bi, hipStream_t s) {
+    Bucket& bk = buckets[bi];
+    bk.launched = true;
     CK(hipEventRecord(bev[bi], s));
     CK(hipStreamWaitEvent(cstream, bev[bi], 0));
     if (adp::option("dp_snapshot", 0)) {   // test hook: what the all-reduce is about to read
@@ -794,7 +805,10 @@ struct adp_handle {
     if (it == bucket_of.end()) return 0;
     const int bi = it->second;
     pend[bi].erase(id);
-    if (pend[bi].empty() && !buckets[bi].launched) return dp_launch(bi, s);
+    if (pend[bi].empty() && !buckets[bi].launched &&
+        std::find(dp_queue.begin(), dp_queue.end(), bi) == dp_queue.end())
+      dp_queue.push_back(bi);
+    if ((int)dp_queue.size() >= std::max(1, adp::option("dp_launch_group", 2))) return dp_launch_queued(s);
     return 0;
   }
   // error path between dp_begin and dp_finish: buckets already issued may still read G on the communication
@@ -802,6 +816,7 @@ struct adp_handle {
   void dp_abort(hipStream_t s) {
     if (!dp_active) return;
     dp_active = false;
+    dp_queue.clear();
     bool any = false;
     for (auto& b : buckets) any = any || b.launched;
     if (any && hipEventRecord(comm_done, cstream) == hipSuccess) (void)hipStreamWaitEvent(s, comm_done, 0);
@@ -809,7 +824,9 @@ struct adp_handle {
   int dp_finish(hipStream_t s) {
     if (!dp_active) return 0;
     for (size_t b = 0; b < buckets.size(); ++b)   // buckets whose layers never reported (frozen only)
-      if (!buckets[b].launched) CL(dp_launch((int)b, s));
+      if (!buckets[b].launched && std::find(dp_queue.begin(), dp_queue.end(), (int)b) == dp_queue.end())
+        dp_queue.push_back((int)b);
+    CL(dp_launch_queued(s));
     CK(hipEventRecord(comm_done, cstream));
     CK(hipStreamWaitEvent(s, comm_done, 0));
     dp_active = false;

@@ -509,6 +509,18 @@ def wgrad_flush():
     call("adp_wgrad_flush", stream_ptr())
 
 
+def wgrad_release(stream=None):
+    """adp_wgrad_release: free the deferral arena of (current device, stream) and forget the stream (synchronises it;
+    AdpError with reductions pending). stream: a torch.cuda.Stream, default the current one."""
+    call("adp_wgrad_release", stream_ptr() if stream is None else stream.cuda_stream)
+
+
+def wgrad_arena_chunks(stream=None):
+    """The number of deferral-arena chunks of (current device, stream) (adp_wgrad_arena_chunks; test hook)."""
+    from . import _lib
+    return int(_lib.lib().adp_wgrad_arena_chunks(stream_ptr() if stream is None else stream.cuda_stream))
+
+
 def bn_fold_reset():
     """Drop a deferred BatchNorm fold left pending by a failed step and re-zero the accumulator replicas
     (adp_bn_fold_reset, stream-ordered; a no-op when nothing is pending)."""

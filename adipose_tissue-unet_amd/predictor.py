@@ -249,12 +249,17 @@ class BandCanvas:
             return False
         if (self.y0, self.y1) != (0, self.H):
             raise ValueError("rank 0's canvas must cover the whole frame")
+        # every band's receive is posted at once (round 6), so the transfers overlap; the adds still run in rank order
+        # (waiting on rank q while the later bands keep arriving): the sum's association stays the sharding's
+        posted = []
         for q in range(1, n):
             y0, y1 = int(bands[q][0]), int(bands[q][1])
             if y1 <= y0:
                 continue
             tmp = torch.empty((2, y1 - y0, self.W), dtype=torch.float32, device="cpu" if host else self.buf.device)
-            dist.recv(tmp, dist.get_global_rank(group, q), group=group)
+            posted.append((y0, y1, tmp, dist.irecv(tmp, dist.get_global_rank(group, q), group=group)))
+        for y0, y1, tmp, work in posted:
+            work.wait()
             tmp = tmp.to(self.buf.device)
             for k in range(2):
                 dst = self.buf[k, y0:y1]
@@ -268,6 +273,16 @@ class BandCanvas:
         out = torch.empty_like(self.acc)
         ops.blend_finalize(self.acc, self.ws, out, floor_)
         return out
+
+
+def _bcast_frame(frame, shape, dev, group):
+    """Rank 0's finished (H, W) map to every rank of `group` (frame = None on the receiving ranks)."""
+    import torch.distributed as dist
+    host = _p2p_cpu(group)
+    buf = frame if frame is not None else torch.empty(shape, dtype=torch.float32, device=dev)
+    tb = buf.cpu() if host else buf
+    dist.broadcast(tb, dist.get_global_rank(group, 0), group=group)
+    return tb.to(dev) if host else tb
 
 
 def _gpu_reconstruct(blender, tiles, positions, output_shape):
@@ -330,7 +345,12 @@ class SlidingWindowInference:
         return positions[r * per:(r + 1) * per]
 
     def predict_with_sliding_window(self, image, model, mean, std, use_tta=False, tta_mode="basic",
-                                    return_device=False):
+                                    return_device=False, broadcast=False):
+        """The blended probability map of `image` (full_evaluation_enhanced.py:286-329).
+
+        With a process group (rank-sharded tiles, round 5): the bands are reduced to rank 0, which returns the map;
+        the other ranks return None unless broadcast=True, which sends rank 0's finished map to every rank (one
+        H x W f32 broadcast) so that every rank returns it, as the single-process call does."""
         if not hasattr(model, "predict_views"):
             raise TypeError("GPU sliding window needs a HIP predictor (AdiposeUNet / HipUnetPredictor)")
         dev = model.net.device if hasattr(model, "net") else torch.device("cuda")
@@ -357,6 +377,11 @@ class SlidingWindowInference:
             for (y, x), p in zip(chunk, probs):
                 canvas.add(p, wmap, y, x)
         if self.group is not None and not canvas.reduce_to_root(self.group, bands):
-            return None   # (the blended frame lives on rank 0 only)
-        out = canvas.finalize(self.blender.floor)
+            if not broadcast:
+                return None   # (the blended frame lives on rank 0 only)
+            out = _bcast_frame(None, (h, w), dev, self.group)
+        else:
+            out = canvas.finalize(self.blender.floor)
+            if self.group is not None and broadcast:
+                _bcast_frame(out, (h, w), dev, self.group)
         return out if return_device else out.cpu().numpy()

@@ -87,7 +87,7 @@ class GradBuckets:
     blocks that find no free CU run after the others, so an overlapped bucket can cost as much as an exposed one
     (profiles/r03_contention_probe.txt); the switch is there to measure both on a multi-GPU node."""
 
-    def __init__(self, net, bucket_bytes=16 << 20, group=None, overlap=True):
+    def __init__(self, net, bucket_bytes=16 << 20, group=None, overlap=True, launch_group=2):
         self.group = group
         self.overlap = overlap
         self.world = dist.get_world_size(group)
@@ -95,11 +95,19 @@ class GradBuckets:
         self.ps = net.ps
         self.net = net
         self.works = []
+        # buckets whose layers are done wait until launch_group of them are ready (or the backward ends) and go out
+        # together behind ONE flush of the deferred weight-gradient reductions (round 6): with a flush per bucket the
+        # backward's batched reductions were split into as many launches as buckets
+        self.launch_group = max(1, int(launch_group))
+        self.queued = []
+        self.launches = 0   # (flush + launch points of the last backward)
 
     def begin(self, frozen=()):
         self.pending = [set(b[0]) - set(frozen) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works = []
+        self.queued = []
+        self.launches = 0
 
     def ready(self, lname):
         if not self.overlap:
@@ -107,17 +115,29 @@ class GradBuckets:
         for i, p in enumerate(self.pending):
             if lname in p:
                 p.discard(lname)
-                if not p and not self.launched[i]:
-                    self._launch(i)
+                if not p and not self.launched[i] and i not in self.queued:
+                    self.queued.append(i)
+        if len(self.queued) >= self.launch_group:
+            self._launch_queued()
 
-    def _launch(self, i):
-        _, lo, hi = self.buckets[i]
-        self.launched[i] = True
-        if getattr(self.net, "_deferring", False):   # the bucket's gradients are final after the recorded reductions
+    def _launch_queued(self):
+        if not self.queued:
+            return
+        self.launches += 1
+        if getattr(self.net, "_deferring", False):   # the buckets' gradients are final after the recorded reductions
             ops.wgrad_flush()
             ops.wgrad_defer(True)
-        self.works.append(dist.all_reduce(self.ps.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                          async_op=True))
+        for i in self.queued:
+            _, lo, hi = self.buckets[i]
+            self.launched[i] = True
+            self.works.append(dist.all_reduce(self.ps.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True))
+        self.queued = []
+
+    def _launch(self, i):
+        if not self.launched[i] and i not in self.queued:
+            self.queued.append(i)
+        self._launch_queued()
 
     def abort(self):
         """Error path of a backward: the buckets already issued may still read the gradient buffer on the RCCL
@@ -130,8 +150,9 @@ class GradBuckets:
         # every gradient is final here: reduce any bucket a ready-hook did not launch (a layer that never
         # reported, or frozen-only buckets, whose zero gradients are harmless to sum)
         for i, done in enumerate(self.launched):
-            if not done:
-                self._launch(i)
+            if not done and i not in self.queued:
+                self.queued.append(i)
+        self._launch_queued()
         for w in self.works:
             w.wait()  # current stream waits on the RCCL stream
         self.works = []

@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 19 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 20 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
@@ -42,7 +42,8 @@ extern "C" {
                               v16: adp_bn_fold_reset, adp_debug_grad_flat;
                               v17: adp_wgrad_defer / adp_wgrad_flush
                               v18: adp_conv_io.act_outA;
-                              v19: adp_conv_desc.CA_real / CB_real / Nout_real (zero-weight hints) */
+                              v19: adp_conv_desc.CA_real / CB_real / Nout_real (zero-weight hints);
+                              v20: adp_wgrad_release / adp_wgrad_arena_chunks (deferral arenas per (device, stream)) */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -249,6 +250,11 @@ int adp_bn_fold_reset(adp_stream_t s);
  * them (the optimizer, a gradient all-reduce). adp_wgrad_defer(0, s) with reductions pending is an error. */
 int adp_wgrad_defer(int on, adp_stream_t s);
 int adp_wgrad_flush(adp_stream_t s);
+/* The deferral arena of (current device, stream s) -- chunks of >= 256 MiB allocated by the first deferred steps and reused
+ * afterwards -- freed, and the stream forgotten (v20). Synchronises s; an error with reductions pending. Call it before
+ * destroying a stream that deferred. adp_wgrad_arena_chunks: the number of arena chunks of (device, s) (test hook). */
+int adp_wgrad_release(adp_stream_t s);
+int adp_wgrad_arena_chunks(adp_stream_t s);
 /* a = relu(z*scale + shift), the post-BatchNorm activation, materialised once per layer */
 int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* scale, const float* shift,
                  void* out, adp_stream_t s);

@@ -89,7 +89,7 @@ def _buckets_fn(rank, world, overlap=True):
     launched_before_finish = sum(gb.launched)
     gb.finish()
     return {"before": before, "after": net.ps.grad.clone(), "nbuckets": len(gb.buckets),
-            "launched_before_finish": launched_before_finish}
+            "launched_before_finish": launched_before_finish, "launches": gb.launches}
 
 
 def _buckets_after_fn(rank, world):
@@ -107,6 +107,8 @@ def test_grad_buckets_sum_allreduce(fn):
         assert res[0]["launched_before_finish"] == 0
     else:
         assert res[0]["launched_before_finish"] > 0
+        # ready buckets go out two at a time behind one flush (launch_group = 2), the rest at finish()
+        assert res[0]["launches"] <= (res[0]["nbuckets"] + 1) // 2 + 1
     for r in range(WORLD):
         np.testing.assert_allclose(res[r]["after"], total, rtol=0, atol=1e-5)
 
@@ -216,3 +218,19 @@ def test_band_reduce_to_root_matches_one_canvas(world):
     np.testing.assert_allclose(res[0]["ws"], ref.ws.numpy(), rtol=0, atol=2e-6)
     for r in range(1, world):
         assert not res[r]["root"] and 0 < res[r]["rows"] < H
+
+
+def _bcast_fn(rank, world):
+    import _adipose_pkg  # noqa: F401
+    from adipose_amd.predictor import _bcast_frame
+    frame = torch.arange(12, dtype=torch.float32).reshape(3, 4) + 0.5 if rank == 0 else None
+    return {"out": _bcast_frame(frame, (3, 4), "cpu", dist.group.WORLD)}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sliding_window_broadcast_frame(world):
+    """predict_with_sliding_window(broadcast=True): rank 0's finished map reaches every rank (predictor._bcast_frame)."""
+    res = run_ranks(_bcast_fn, world)
+    ref = torch.arange(12, dtype=torch.float32).reshape(3, 4) + 0.5
+    for r in range(world):
+        np.testing.assert_array_equal(np.asarray(res[r]["out"]), ref.numpy())

@@ -172,7 +172,10 @@ def _sw_fn(rank, world):
                                              tta_mode="basic")
     finally:
         P.BandCanvas.__init__ = orig
-    return {"out": out, "mine": len(sw.shard(pos)), "all": len(pos), "rows": rows}
+    # broadcast=True: every rank returns rank 0's map (round 6, opt-in)
+    outb = sw.predict_with_sliding_window(_sw_image(), _sw_predictor(), 127.0, 50.0, use_tta=True, tta_mode="basic",
+                                          broadcast=True)
+    return {"out": out, "outb": outb, "mine": len(sw.shard(pos)), "all": len(pos), "rows": rows}
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -185,6 +188,8 @@ def test_dp_sliding_window_bands_match_one_rank(world):
     # the bands are summed in a different association (rank partial sums), so allow f32 rounding
     np.testing.assert_allclose(res[0]["out"], ref, rtol=0, atol=2e-6)
     assert res[0]["rows"] == [320]
+    for r in range(world):
+        np.testing.assert_array_equal(res[r]["outb"], res[0]["out"])
     for r in range(1, world):
         assert res[r]["out"] is None   # (the frame lives on rank 0)
         assert len(res[r]["rows"]) == 1 and res[r]["rows"][0] < 320, res[r]["rows"]   # a band, not the frame

@@ -1647,6 +1647,40 @@ def test_wgrad_persistent_halo(N, H, W, parts, cout):
     assert relerr(dWs.cpu(), ref.cpu()) < 1e-4
 
 
+def test_wgrad_defer_arena_release():
+    """adp_wgrad_release (ABI 20, round-5 ADVICE): deferral arenas are per (device, stream); a stream that deferred holds
+    an arena until released, release frees it (and refuses while reductions are pending), a second stream gets its own,
+    and a deferral after a release allocates again and still gives the immediate-mode bits."""
+    N, H, W, cout = 2, 64, 64, 64
+    _, kern, bias, l = make_case(N, H, [64], cout, 1, False, seed=25)
+    g = torch.Generator().manual_seed(26)
+    x = torch.randn(N, H, W, 64, generator=g).to(DEV, torch.bfloat16)
+    dz = nhwc_pad(rb(torch.randn(N, H, W, cout, generator=g), torch.bfloat16), l.cout_s, torch.bfloat16)
+    ref = torch.zeros((l.Npad, l.Kpad), device=DEV)
+    ops.conv_wgrad(x, dz, ref, l.Nout)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(device=DEV)
+    outs = []
+    for st in (torch.cuda.current_stream(), side, torch.cuda.current_stream()):
+        with torch.cuda.stream(st):
+            d = torch.zeros_like(ref)
+            ops.wgrad_defer(True)
+            ops.conv_wgrad(x, dz, d, l.Nout)
+            with pytest.raises(ops.AdpError):
+                ops.wgrad_release()   # reductions pending
+            ops.wgrad_flush()
+            assert ops.wgrad_arena_chunks() >= 1
+            outs.append(d)
+    torch.cuda.synchronize()
+    assert ops.wgrad_arena_chunks(side) >= 1
+    ops.wgrad_release(side)
+    assert ops.wgrad_arena_chunks(side) == 0
+    ops.wgrad_release()
+    assert ops.wgrad_arena_chunks() == 0
+    for d in outs:
+        assert torch.equal(d, ref)
+
+
 def test_wgrad_deferred_reductions():
     """adp_wgrad_defer / adp_wgrad_flush: between them the slab reductions of the deterministic weight-gradient
     launches are only recorded (dW untouched), the flush runs them all in one batched launch with the arithmetic of
