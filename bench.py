@@ -114,6 +114,42 @@ def cpu_baseline(args, min_seconds=10.0, max_steps=60):
                       f"({n * B / dt:.3f} {S}^2 tiles/s); torch CPU, {threads} threads ({tdesc})"}
 
 
+def gpu_same_workload(dev, min_seconds=3.0):
+    """The CPU baseline's own workload on the GPU (round-5 VERDICT item 6): the product path's adipose_v3 (reference
+    topology) f32 train step at BASELINE configs[0] (256x256 gray, B=2, OHEM + deep-supervision losses, Adam), so the
+    baseline compares the same network and precision, not the headline's unet_bn bf16. Same 1024^2-equivalent unit."""
+    import numpy as np
+    import torch
+
+    from adipose_amd.data import synthetic_batch, to_gray
+    from adipose_amd.nets import AdiposeV3Net
+    from adipose_amd.trainer import LossConfig, Trainer
+
+    S, B = 256, 2
+    net = AdiposeV3Net(B, S, dtype="f32", device=dev, seed=865)
+    tr = Trainer(net, LossConfig(), lr=1e-4)
+    xs, ys = synthetic_batch(B, S, channels=3, seed=865)
+    xs = to_gray(xs.astype(np.float32))
+    x = torch.from_numpy((xs - xs.mean()) / (xs.std() + 1e-10)).to(dev).contiguous()
+    y = torch.from_numpy(ys).to(dev).contiguous()
+    for _ in range(3):
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+    n, t0 = 0, time.perf_counter()
+    while n < 10 or time.perf_counter() - t0 < min_seconds:
+        for _ in range(10):
+            tr.train_step(x, y)
+        n += 10
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del tr, net
+    torch.cuda.empty_cache()
+    return {"value": round(n * B * (S / 1024.0) ** 2 / dt, 4), "unit": "1024^2 tiles/s (train, 1024^2-equivalent)",
+            "ms_per_step": round(dt / n * 1e3, 3),
+            "workload": "adipose_v3 (reference topology) 256x256x1 f32 B=2 (BASELINE configs[0]) on this GPU, "
+                        f"{n} steps after 3 warm-up"}
+
+
 def workload_label(args):
     """What this run trains, and which BASELINE.json config it is (if any)."""
     if args.preset == "unet_bn":
@@ -164,10 +200,10 @@ def dice_leg(args):
 
     a = argparse.Namespace(preset=args.preset, levels=args.levels, size=args.size, batch=args.batch, dtype=args.dtype,
                            pool=128, val=64, lr=1e-3, max_steps=1 << 30, max_seconds=args.dice_seconds,
-                           eval_every=400, target=0.9, fp8=args.preset == "unet_bn", hard=True)
+                           eval_every=400, target=0.9, fp8=args.preset == "unet_bn", hard=True, f32_eval=True)
     r = converge(a, log=lambda m: print(m, file=sys.stderr, flush=True))
-    out = {k: r.get(k) for k in ("dice_val", "dice_val_thr", "best_dice_val", "steps", "train_seconds", "fp8", "build",
-                                  "data")}
+    out = {k: r.get(k) for k in ("dice_val", "best_dice_val", "dice_val_thr", "steps", "train_seconds", "fp8", "f32",
+                                  "build", "data")}
     out["curve"] = [(c["step"], c["dice_val"]) for c in r["curve"]]
     out["same_build"] = True   # (measured by this process on the library it benched)
     return out
@@ -293,9 +329,19 @@ def main():
             cpu = cpu_baseline(args)
         except Exception as e:  # report, never fake
             cpu = {"value": None, "error": repr(e)}
+        try:   # the like-for-like comparison: the CPU baseline's own network and precision on this GPU
+            del tr, net, x, y
+            torch.cuda.empty_cache()
+            tr = net = x = y = None
+            g = gpu_same_workload(dev)
+            cpu["gpu_same_workload"] = g
+            if cpu.get("value"):
+                cpu["gpu_over_cpu_same_workload"] = round(g["value"] / cpu["value"], 1)
+        except Exception as e:  # report, never fake
+            cpu["gpu_same_workload"] = {"value": None, "error": repr(e)}
     dice = None
     if world == 1 and not args.no_dice:
-        del tr, net, x, y
+        tr = net = x = y = None
         torch.cuda.empty_cache()
         try:
             dice = dice_leg(args)

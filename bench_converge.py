@@ -202,8 +202,35 @@ def converge(args, log=log):
             raise SystemExit("--fp8: the fp8 forward is the unet_bn preset's (BASELINE configs[4])")
         d8 = evaluate(fp8=True)
         line["fp8"] = {"dice_val": round(d8[0], 5), "dice_val_thr": round(d8[1], 5),
-                       "delta_dice_val": round(d8[0] - final["dice_val"], 6),
-                       "delta_dice_val_thr": round(d8[1] - final["dice_val_thr"], 6)}
+                       "delta_dice_val": round(d8[0] - final["dice_val"], 7),
+                       "delta_dice_val_thr": round(d8[1] - final["dice_val_thr"], 7)}
+    if getattr(args, "f32_eval", False) and args.dtype == "bf16":
+        # the same trained weights (f32 masters) and BatchNorm running statistics in an f32 twin of the network:
+        # the bf16 forward's Dice against the reference precision's on the same val tiles (round-5 VERDICT item 8)
+        if args.preset == "unet_bn":
+            twin = UNetBN(B, S, levels=args.levels, base=64, in_ch=3, dtype="f32", device=dev, seed=865)
+        else:
+            twin = AdiposeV3Net(B, S, dtype="f32", device=dev, seed=865)
+        if twin.ps.flat.numel() != net.ps.flat.numel():
+            line["f32"] = {"error": "the f32 twin packs its weights differently"}
+        else:
+            twin.ps.flat.copy_(net.ps.flat)
+            for k, (rm, rv) in getattr(net, "running", {}).items():
+                twin.running[k][0].copy_(rm)
+                twin.running[k][1].copy_(rv)
+            keep = net
+            net = twin
+            try:
+                d32 = evaluate()
+            finally:
+                net = keep
+            line["f32"] = {"dice_val": round(d32[0], 5), "dice_val_thr": round(d32[1], 5),
+                           "delta_bf16_minus_f32": round(final["dice_val"] - d32[0], 7),
+                           "delta_bf16_minus_f32_thr": round(final["dice_val_thr"] - d32[1], 7)}
+            if args.fp8:
+                line["fp8"]["delta_vs_f32"] = round(line["fp8"]["dice_val"] - d32[0], 7)
+        del twin
+        torch.cuda.empty_cache()
     return line
 
 
