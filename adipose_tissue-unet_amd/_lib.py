@@ -89,6 +89,7 @@ _SIGS = {
     "adp_wgrad_defer": [_I, _P],
     "adp_wgrad_flush": [_P],
     "adp_wgrad_release": [_P],
+    "adp_get_option": [C.c_char_p],
     "adp_wgrad_arena_chunks": [_P],
     "adp_debug_grad_flat": [_P, _I, _P, _S],
     "adp_bn_apply": [_I, _S, _I, _P, _P, _P, _P, _P],

@@ -104,6 +104,15 @@ extern "C" int adp_set_option(const char* name, int value) {
   return 0;
 }
 
+// the current value of an option (its default when unset: INT_MIN); also the library's report channel for test
+// hooks ("tap64_ksplit_last": the split-K factor of the last tap64 launch)
+extern "C" int adp_get_option(const char* name) {
+  if (!name) return INT_MIN;
+  std::lock_guard<std::mutex> lk(adp::g_opt_mu);
+  auto it = adp::opts().find(name);
+  return it == adp::opts().end() ? INT_MIN : it->second;
+}
+
 extern "C" const char* adp_last_error(void) { return adp::g_err.c_str(); }
 extern "C" const char* adp_last_kernel(void) { return adp::g_kernel; }
 extern "C" int adp_abi_version(void) { return ADP_ABI_VERSION; }

@@ -53,6 +53,12 @@ struct FwdArgs {
   int ca_real;           // adp_conv_desc.CA_real (0 = unknown)
   int ztail;             // zero tails of the weights (adp_conv_desc CA_real / CB_real / Nout_real): bit 0 every source a
                          // 64-channel stride with <= 48 real channels, bit 1 Nout == 64 with <= 48 real columns
+  // tap64 split-K (round 6, option tap64_ksplit): ksplit > 1 blocks per output tile, each a contiguous K range; the
+  // partial accumulators go to kpart, the tile's last block (counter kcnt[tile], re-zeroed by it) sums them in split
+  // order and runs the epilogue
+  int ksplit;
+  float* kpart;
+  int* kcnt;
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]

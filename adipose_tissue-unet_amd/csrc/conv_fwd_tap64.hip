@@ -22,9 +22,12 @@
 // h4 and h4+4 of the row: the bf16 read pattern, conflict-free under the swizzle), so the k order inside
 // the instruction cancels out of the dot product.
 // The per-output-channel weight scale is applied in the epilogue (FwdArgs::wscale).
+#include <algorithm>
 #include <type_traits>
 
 #include "conv_common.h"
+
+extern "C" int adp_set_option(const char* name, int value);   // (abi.cpp)
 
 namespace {
 
@@ -106,7 +109,10 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   // (wc = w >> 2); a wave skips the MFMAs of a 32-column group wholly past Nout (option f32_skip)
   const bool SPLIT = F32 && WM == 4 && WN == 2 && a.f32_skip;   // (f32_skip = 0: the bf16 forms' wave layout)
   const int wr = SPLIT ? (wave & 3) : wave / WN, wc = SPLIT ? (wave >> 2) : wave % WN;
-  const int lin = xcd_remap(blockIdx.x, a.nblocks);
+  // split-K (FwdArgs::ksplit): block -> (tile, K range); the ranges are contiguous runs of K steps
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  const int lin0 = xcd_remap(blockIdx.x, a.nblocks);
+  const int ksid = lin0 % nsplit, lin = lin0 / nsplit;
   const int tn = lin % a.ntile_n, tm = lin / a.ntile_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int wcu = SPLIT ? (__builtin_amdgcn_readfirstlane(wave) >> 2) : 0;
@@ -117,7 +123,9 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   const int HWo = a.Ho * a.Wo, Hv = a.Hs * upv, Wv = a.Ws * upv;
   const int Cin_s = a.CAs + a.CBs;
   const int Wrows = (a.Nout + 63) / 64 * 64;
-  const int nk = a.K / KSTEP;
+  const int nk_all = a.K / KSTEP;
+  const int kb = (int)((long long)ksid * nk_all / nsplit);
+  const int nk = (int)((long long)(ksid + 1) * nk_all / nsplit) - kb;
 
   // ---- per-thread staging rows: quarter h, instruction i -> quarter row q = i*(NTH/8) + tid/8
   int ry[2][GA], rx[2][GA], rn[2][GA], rc[2][GA], pb[2][GA];   // pb: pixel of tap (0,0) (up == 1)
@@ -162,7 +170,9 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
   // run channel-chunk-fastest inside a tap, taps row-major). cs = pixel stride in bytes, cb = byte offset
   // of the step's first channel inside its source's pixel, dpix = pixel delta of the tap (up == 1).
   struct Kt { int oy, ox, cs, cb, srcb, dpix, kt; const unsigned char* base; };
-  int it_ci = 0, it_ty = 0, it_tx = 0, it_kt = 0;   // iterator state: the NEXT step kinfo() returns
+  // iterator state: the NEXT step kinfo() returns (split-K: the block's first step kb)
+  const int spt = Cin_s / KSTEP;
+  int it_ci = (kb % spt) * KSTEP, it_ty = (kb / spt) / a.kw, it_tx = (kb / spt) % a.kw, it_kt = kb;
   auto kinfo = [&]() {
     Kt r;
     r.oy = it_ty * a.dil; r.ox = it_tx * a.dil; r.kt = it_kt;
@@ -378,6 +388,47 @@ __global__ __launch_bounds__(WM * WN * 64, (tap64_occ<WM, WN, TM>())) void igemm
     mma(fa, fb0, 1, 0);
   }
   T64_BAR();   // the epilogue reuses the stages
+
+  if (nsplit > 1) {
+    // split-K: this K range's accumulators to the tile's partial slab (accumulator i of thread t of split k at
+    // [(k NACC + i) NTH + t]: coalesced 16-B stores), then the tile's counter; the last of its nsplit blocks re-zeroes
+    // the counter, reads every split's partial in split order (its own too: the sum's order does not depend on which
+    // block came last) and runs the epilogue below. Release / acquire at agent scope: the blocks sit on any XCD.
+    constexpr int NACC = 2 * MIQ * 4;
+    float4* part = reinterpret_cast<float4*>(a.kpart) + (size_t)lin * nsplit * NACC * NTH;
+#pragma unroll
+    for (int i = 0; i < 2 * MIQ; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = acc[i][j];
+        part[(size_t)(ksid * NACC + i * 4 + j) * NTH + tid] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    __syncthreads();   // (every wave's stores complete: its vmcnt is drained by the barrier's fence)
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(a.kcnt + lin, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == nsplit - 1;
+      if (last) __hip_atomic_store(a.kcnt + lin, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    const int last = flag[0];
+    __syncthreads();   // (the flag is read before the epilogue reuses the LDS)
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+    for (int i = 0; i < 2 * MIQ; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < nsplit; ++k) {
+          const float4 v = part[(size_t)(k * NACC + i * 4 + j) * NTH + tid];
+          if (k == 0) sum = f32x4{v.x, v.y, v.z, v.w};
+          else sum += f32x4{v.x, v.y, v.z, v.w};
+        }
+        acc[i][j] = sum;
+      }
+  }
 
   if (ADP_DBG(a) & 16) {   // timing-only ablation (option fwd_debug bit 4): no epilogue at all
 #pragma unroll
@@ -596,6 +647,31 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
   constexpr int BM = WM * TM, BN = WN * 64;
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
+  // split-K (round 6, option tap64_ksplit): a launch whose tiles occupy at most tap64_ksplit_max
+  // (96) of the chip's 256 (occupancy 1) or 512 (occupancy 2) block slots -- the f32 path's 32^2 level at BASELINE
+  // configs[0]: 48 tiles -- gets up to 8 blocks per tile, each at least 6 K steps; not the zero-tail forms (their loop
+  // runs K steps in pairs) or the mid-step-barrier loop
+  a.ksplit = 0;
+  {
+    const int tiles = a.nblocks, nk = a.K / (a.f8 ? 128 : (a.f32 ? 32 : 64));
+    const int occ = tap64_occ<WM, WN, TM>();
+    if (adp::option("tap64_ksplit", 1) && tiles <= adp::CLAIM_INTS &&
+        tiles * occ <= adp::option("tap64_ksplit_max", 96) && !(a.f32 && a.ztail)) {
+      const int sp = std::min(std::min(8, (256 * occ) / tiles), nk / 6);
+      if (sp >= 2) {
+        int* cnt = adp::claim_slot();
+        float* part = static_cast<float*>(adp::scratch(7, (size_t)tiles * sp * BM * BN * sizeof(float)));
+        if (cnt && part) {
+          a.ksplit = sp;
+          a.kcnt = cnt;
+          a.kpart = part;
+          a.kpipe = 0;
+          a.nblocks = tiles * sp;
+        }
+      }
+    }
+  }
+  ::adp_set_option("tap64_ksplit_last", a.ksplit);   // (test hook, adp_get_option)
   const dim3 g(a.nblocks), b(WM * WN * 64);
   // buffer-resource loads need every operand below 2 GiB (32-bit offsets, T64_OOB reserved)
   const int es = a.f8 ? 1 : (a.f32 ? 4 : 2);

@@ -509,6 +509,13 @@ def wgrad_flush():
     call("adp_wgrad_flush", stream_ptr())
 
 
+def get_option(name):
+    """adp_get_option: the value set for `name`, None when unset (the built-in default applies)."""
+    from . import _lib
+    v = int(_lib.lib().adp_get_option(name.encode()))
+    return None if v == -(2 ** 31) else v
+
+
 def wgrad_release(stream=None):
     """adp_wgrad_release: free the deferral arena of (current device, stream) and forget the stream (synchronises it;
     AdpError with reductions pending). stream: a torch.cuda.Stream, default the current one."""

@@ -43,7 +43,7 @@ extern "C" {
                               v17: adp_wgrad_defer / adp_wgrad_flush
                               v18: adp_conv_io.act_outA;
                               v19: adp_conv_desc.CA_real / CB_real / Nout_real (zero-weight hints);
-                              v20: adp_wgrad_release / adp_wgrad_arena_chunks (deferral arenas per (device, stream)) */
+                              v20: adp_wgrad_release / adp_wgrad_arena_chunks (deferral arenas per (device, stream)), adp_get_option */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -134,6 +134,9 @@ const char* adp_source_hash(void);
  * "wgrad_cin8_bna" (1: the input layer's fused BN-backward weight gradient when dY = NULL), "tap64_kpipe" (0:
  * mid-step barrier in the tap64 K loop); "wgrad_debug" / "fwd_debug" are timing-only ablations (results invalid). */
 int adp_set_option(const char* name, int value);
+/* The value adp_set_option gave `name`, INT_MIN when unset (v20; "tap64_ksplit_last" reports the split-K factor of the
+ * last tap64 launch: 0 = none). */
+int adp_get_option(const char* name);
 /* Per-launch timing of the conv kernels (bench roofline; no reference counterpart). mode 1: clear the record
  * and start recording a HIP event pair around the MAIN kernel of every adp_conv_fwd / adp_conv_wgrad(_bn)
  * launch (the kernel adp_last_kernel names; statistic folds, split reduces, bias sums and BatchNorm applies

@@ -4,6 +4,8 @@ f32 launches run the exact-f32 MFMA path: tolerance 1e-4 relative to the output 
 bf16 launches are compared with the oracle evaluated on bf16-rounded operands (f32 accumulate):
 tolerance 2e-2 relative to the output scale.
 """
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -23,6 +25,17 @@ def nhwc_pad(x, cs, dt):
     out = torch.zeros((N, H, W, cs), dtype=dt, device=DEV)
     out[..., :C] = x.to(DEV, dt)
     return out
+
+
+@pytest.fixture(autouse=True)
+def _no_split_k():
+    """The kernel-level tests here compare kernel forms bit for bit on small problems, which the tap64 launcher's
+    split-K (round 6) would otherwise take: it is off in this module except where a test turns it on
+    (test_tap64_split_k); the network and config tests run with the default."""
+    from adipose_amd import ops
+    ops.set_option("tap64_ksplit", 0)
+    yield
+    ops.set_option("tap64_ksplit", None)
 
 
 def relerr(a, b):
@@ -2483,3 +2496,70 @@ def test_f32_tap_kernel_matches_generic(case):
         res.append([out.clone()] + [e.clone() for e in extra])
     for a, b in zip(*res):
         assert relerr(a, b) < 1e-5, (name, relerr(a, b))
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("epi", ["bias_relu", "mask_addend", "accum", "stats", "bnr"])
+@pytest.mark.parametrize("dil", [1, 4])
+def test_tap64_split_k(dt, epi, dil):
+    """Split-K on the tap64 kernel (round 6, option tap64_ksplit): a launch whose tiles fill under a
+    quarter of the CUs -- the 32^2 bottleneck of BASELINE configs[0] (adipose_v3 at 256^2: M = 2048) -- runs several
+    blocks per tile over contiguous K ranges; the tile's last block sums the partials in split order and runs the
+    epilogue. Against the oracle conv (plain product) and against the unsplit launch (every epilogue: bias + ReLU,
+    mask + addend, f32 accumulate, BatchNorm statistics, the BN-backward reduction), and two runs give the same bits."""
+    if dt == "f32" and epi == "bnr":
+        pytest.skip("the BN-backward reduction epilogue is a bf16 data-gradient form")
+    torch_dt = torch.float32 if dt == "f32" else torch.bfloat16
+    N, H, W_ = 2, 32, 32
+    cin = cout = 352 if dt == "f32" else 384
+    g = torch.Generator().manual_seed(71)
+    x = torch.randn(N, H, W_, cin, generator=g)
+    Wm = torch.randn(cout, 9 * cin, generator=g) * (1.0 / math.sqrt(9 * cin))
+    npad = (cout + 63) // 64 * 64   # (the packed layout's rows: a multiple of 64, the pad rows zero)
+    xd, Wd = x.to(DEV, torch_dt), torch.cat([Wm, torch.zeros(npad - cout, 9 * cin)]).to(DEV, torch_dt)
+    bias = torch.randn(cout, generator=g).to(DEV)
+    mask = torch.randn(N, H, W_, cout, generator=g).to(DEV, torch_dt)
+    addend = torch.randn(N, H, W_, cout, generator=g).to(DEV, torch_dt)
+    z = torch.randn(N, H, W_, cout, generator=g).to(DEV, torch.bfloat16)
+    vec = [(torch.rand(cout, generator=g) + 0.5).to(DEV) for _ in range(4)]
+
+    def run(split):
+        ops.set_option("tap64_ksplit", split)   # (the module fixture turns it off around every test)
+        try:
+            out = torch.zeros(N, H, W_, cout, dtype=torch_dt, device=DEV)
+            side = [torch.zeros(cout, device=DEV), torch.zeros(cout, device=DEV)]
+            acc = torch.ones(N, H, W_, cout, device=DEV)
+            kw = dict(out=out, dil=dil)
+            if epi == "bias_relu":
+                ops.conv_fwd(xd, Wd, cout, bias=bias, relu=True, **kw)
+            elif epi == "mask_addend":
+                ops.conv_fwd(xd, Wd, cout, mask=mask, addend=addend, **kw)
+            elif epi == "accum":
+                ops.conv_fwd(xd, Wd, cout, accum=acc, **kw)
+            elif epi == "stats":
+                ops.conv_fwd(xd, Wd, cout, bias=bias, bn_stats=(side[0], side[1]), **kw)
+            else:
+                ops.conv_fwd(xd, Wd, cout, bn_reduce=(z, vec[0], vec[1] - 1.0, vec[2] - 1.0, vec[3], side[1], side[0]),
+                             **kw)
+            ks = ops.get_option("tap64_ksplit_last")
+            kn = _lib.lib().adp_last_kernel().decode()
+            torch.cuda.synchronize()
+            return out.float().cpu(), acc.cpu(), [t.cpu() for t in side], ks, kn
+        finally:
+            ops.set_option("tap64_ksplit", 0)
+
+    from adipose_amd import _lib
+    o1, a1, s1, ks1, kn1 = run(1)
+    o1b, a1b, s1b, _, _ = run(1)
+    o0, a0, s0, ks0, kn0 = run(0)
+    assert kn1.startswith("igemm_fwd_tap64_kernel") and kn0 == kn1, (kn0, kn1)
+    assert ks1 >= 2 and ks0 == 0, (ks1, ks0)
+    assert torch.equal(o1, o1b) and torch.equal(a1, a1b) and all(torch.equal(p, q) for p, q in zip(s1, s1b))
+    tol = 1e-5 if dt == "f32" else 2e-2   # (bf16: the stored outputs round the two f32 sums; a flip is one bf16 ulp)
+    assert relerr(o1, o0) < tol and relerr(a1, a0) < tol   # (bf16 accum: the rounded output is what it adds)
+    for p, q in zip(s1, s0):
+        assert relerr(p, q) < (1e-5 if dt == "f32" else 1e-2)
+    if epi == "bias_relu" and dt == "f32":   # the oracle: 'same' dilated conv of the packed weights
+        wk = Wm.view(cout, 3, 3, cin).permute(0, 3, 1, 2)
+        ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), wk, bias.cpu(), padding=dil, dilation=dil).relu()
+        assert relerr(o1, ref.permute(0, 2, 3, 1)) < 1e-4
