@@ -648,7 +648,7 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
   a.ntile_n = (a.Nout + BN - 1) / BN;
   a.nblocks = ((a.M + BM - 1) / BM) * a.ntile_n;
   // split-K (round 6, option tap64_ksplit): a launch whose tiles occupy at most tap64_ksplit_max
-  // (96) of the chip's 256 (occupancy 1) or 512 (occupancy 2) block slots -- the f32 path's 32^2 level at BASELINE
+  // (192) of the chip's 256 (occupancy 1) or 512 (occupancy 2) block slots -- the f32 path's 32^2 level at BASELINE
   // configs[0]: 48 tiles -- gets up to 8 blocks per tile, each at least 6 K steps; not the zero-tail forms (their loop
   // runs K steps in pairs) or the mid-step-barrier loop
   a.ksplit = 0;
@@ -656,7 +656,7 @@ void launch_cfg(FwdArgs& a, hipStream_t s) {
     const int tiles = a.nblocks, nk = a.K / (a.f8 ? 128 : (a.f32 ? 32 : 64));
     const int occ = tap64_occ<WM, WN, TM>();
     if (adp::option("tap64_ksplit", 1) && tiles <= adp::CLAIM_INTS &&
-        tiles * occ <= adp::option("tap64_ksplit_max", 96) && !(a.f32 && a.ztail)) {
+        tiles * occ <= adp::option("tap64_ksplit_max", 192) && !(a.f32 && a.ztail)) {
       const int sp = std::min(std::min(8, (256 * occ) / tiles), nk / 6);
       if (sp >= 2) {
         int* cnt = adp::claim_slot();
