@@ -257,30 +257,36 @@ ADP_DEV float wf_rdo(uint32_t addr) {
   asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
   return r;
 }
+// halo geometry of the dilated form (below): the 32 patch columns in SPLIT segments of 32 / SPLIT, each segment with
+// its own two halo columns; SPLIT 1 is the dilation-1 layout (34 halo columns)
+template <int SPLIT>
+constexpr int hf_hw() { return HF_PW + 2 * SPLIT; }
+template <int SPLIT>
+constexpr int hf_col(int c) { return c + 2 * (c / (HF_PW / SPLIT)); }
 // k step S of a patch (pixel row S / 8, pixels 4 (S % 8) .. + 3): dY^T element and the 9 tap-shifted halo elements
-template <int S>
+template <int S, int SPLIT>
 ADP_DEV void hf_read(uint32_t abase, const uint32_t (&bbase)[3], float& A, float (&B)[9]) {
-  constexpr int r = S / 8, xs = S % 8;
+  constexpr int r = S / 8, xs = S % 8, HW = hf_hw<SPLIT>(), hc = hf_col<SPLIT>(4 * xs);
   A = wf_rdo<(r * HF_PW + 4 * xs) * 256>(abase);
-  B[0] = wf_rdo<((r + 0) * HF_HW + 4 * xs) * 128>(bbase[0]);
-  B[1] = wf_rdo<((r + 0) * HF_HW + 4 * xs) * 128>(bbase[1]);
-  B[2] = wf_rdo<((r + 0) * HF_HW + 4 * xs) * 128>(bbase[2]);
-  B[3] = wf_rdo<((r + 1) * HF_HW + 4 * xs) * 128>(bbase[0]);
-  B[4] = wf_rdo<((r + 1) * HF_HW + 4 * xs) * 128>(bbase[1]);
-  B[5] = wf_rdo<((r + 1) * HF_HW + 4 * xs) * 128>(bbase[2]);
-  B[6] = wf_rdo<((r + 2) * HF_HW + 4 * xs) * 128>(bbase[0]);
-  B[7] = wf_rdo<((r + 2) * HF_HW + 4 * xs) * 128>(bbase[1]);
-  B[8] = wf_rdo<((r + 2) * HF_HW + 4 * xs) * 128>(bbase[2]);
+  B[0] = wf_rdo<((r + 0) * HW + hc) * 128>(bbase[0]);
+  B[1] = wf_rdo<((r + 0) * HW + hc) * 128>(bbase[1]);
+  B[2] = wf_rdo<((r + 0) * HW + hc) * 128>(bbase[2]);
+  B[3] = wf_rdo<((r + 1) * HW + hc) * 128>(bbase[0]);
+  B[4] = wf_rdo<((r + 1) * HW + hc) * 128>(bbase[1]);
+  B[5] = wf_rdo<((r + 1) * HW + hc) * 128>(bbase[2]);
+  B[6] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[0]);
+  B[7] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[1]);
+  B[8] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[2]);
 }
 // the 32 k steps of a patch, software-pipelined one step deep (the reads of step S + 1 in flight while step S
 // multiplies); at the first step of each pixel row the row's share of the next patch's LDS-DMA goes out
-template <int S, typename RowIssue>
+template <int S, int SPLIT = 1, typename RowIssue>
 ADP_DEV void hf_steps(uint32_t abase, const uint32_t (&bbase)[3], float (&fa)[2], float (&fb)[2][9], f32x4 (&acc)[9],
                       float& db, const RowIssue& row_issue) {
   constexpr int NS = HF_PH * HF_PW / 4, cur = S & 1;
   if constexpr (S % 8 == 0) row_issue(S / 8);
   if constexpr (S + 1 < NS) {
-    hf_read<S + 1>(abase, bbase, fa[cur ^ 1], fb[cur ^ 1]);
+    hf_read<S + 1, SPLIT>(abase, bbase, fa[cur ^ 1], fb[cur ^ 1]);
     wf_lgkm<10>();
   } else {
     wf_lgkm<0>();
@@ -290,7 +296,7 @@ ADP_DEV void hf_steps(uint32_t abase, const uint32_t (&bbase)[3], float (&fa)[2]
   for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur], fb[cur][t], acc[t], 0, 0, 0);
   __builtin_amdgcn_s_setprio(0);
   db += fa[cur];   // (the bias gradient: every dY element of the patch passes one lane's A operand once)
-  if constexpr (S + 1 < NS) hf_steps<S + 1>(abase, bbase, fa, fb, acc, db, row_issue);
+  if constexpr (S + 1 < NS) hf_steps<S + 1, SPLIT>(abase, bbase, fa, fb, acc, db, row_issue);
 }
 __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs a) {
   constexpr int NTH = 512, CI = 32, NB = 64;
@@ -437,7 +443,7 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
     const uint32_t abase = hb + HBUF + a_lane;
     const uint32_t bbase[3] = {hb + b_lane[0], hb + b_lane[1], hb + b_lane[2]};
     float fa[2], fb[2][9];
-    hf_read<0>(abase, bbase, fa[0], fb[0]);
+    hf_read<0, 1>(abase, bbase, fa[0], fb[0]);
     hf_steps<0>(abase, bbase, fa, fb, acc, db, [&](int r) { if (more) issue_row(Pn, r, buf ^ 1); });
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next patch landed
     __syncthreads();                                    // and nobody reads this stage any more
@@ -461,6 +467,179 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
       if (n < a.Nout) atomicAdd(a.dW + (size_t)n * a.Kpad + t * Cin_s + kc, acc[t][r]);
     }
 }
+
+// Dilated form of the halo weight gradient (3x3, stride 1, dilation d > 1, 'same'; adipose_v3's bottleneck
+// dilate2..dilate6 at d = 2 .. 32, which ran on the register-staged kernel at ~85 TF). A dilation-d conv is d x d
+// independent dilation-1 convs on the sub-lattices y = a (mod d), x = b (mod d), so a patch is 4 sub-lattice rows
+// (image rows y0 + d r) by 32 output columns, and its halo the same 6 x 34 layout as above: output (r, c) reads halo
+// (r + ty, c + tx). Where a sub-lattice row is narrower than 32 (Wo / d < 32) the 32 columns are SPLIT segments of
+// Wo / d columns on SPLIT neighbouring sub-lattices b0 .. b0 + SPLIT - 1, each with its own two halo columns (32 + 2
+// SPLIT halo columns; the k loop's fragment addresses stay compile-time: hf_col). The pieces are the same 16-B LDS-DMA
+// gathers of whole 128-B channel chunks (a strided pixel costs what a neighbouring one does).
+// Work: the (channel chunk, output block) x patch items of a layer are cut into gridDim.x contiguous ranges, one per
+// block, so the 66 combinations of a 352 -> 352 layer fill every CU (the dilation-1 form gives each combination a
+// whole number of blocks: 198 of 256 there); a block flushes its accumulators with f32 atomics where its range
+// changes combination, as the dilation-1 form does at its end.
+// (a device function: the builtin inside a kernel template fails the host pass's substitution)
+__device__ __forceinline__ void hf_buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, off, 0, 0, 0);
+}
+template <int SPLIT>
+__global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_dil_kernel(WgradArgs a) {
+  constexpr int NTH = 512, CI = 32, NB = 64;
+  constexpr int HW = hf_hw<SPLIT>(), SEGW = HF_PW / SPLIT, HROWS = (HF_PH + 2) * HW;
+  constexpr int HRB = CI * 4, DRB = NB * 4, NPIX = HF_PH * HF_PW;
+  constexpr int HBUF = HROWS * HRB, DBUF = NPIX * DRB, STAGE = HBUF + DBUF;
+  constexpr int HCH = HROWS * (HRB / 16), DCH = NPIX * (DRB / 16);
+  constexpr int GH = (HCH + NTH - 1) / NTH, GD = DCH / NTH, GT = GH + GD;
+  static_assert(GD * NTH == DCH && GT <= 3 * HF_PH, "pieces: at most three per patch row");
+  static_assert(2 * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int d = a.dil;
+  const int nxq = a.Wo / d / SEGW, nbg = d / SPLIT, nyq = a.Ho / d / HF_PH;
+  const int T = a.Nimg * d * nyq * nbg * nxq;   // patches per combination
+  const int Cin_s = a.CAs + a.CBs, nch = Cin_s / CI, nnb = (a.Nout + NB - 1) / NB, combos = nch * nnb;
+  const int G = gridDim.x, blk = xcd_remap(blockIdx.x, G);
+  const long long I = (long long)combos * T;
+  const int it0 = (int)(I * blk / G), it1 = (int)(I * (blk + 1) / G);
+  if (it0 >= it1) return;   // (uniform)
+  const size_t npx = (size_t)a.Nimg * a.Hs * a.Ws;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a.srcA, 0, npx * a.CAs * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.CBs ? a.srcB : a.srcA), 0, npx * a.CBs * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsD =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dY, 0, a.Nimg * a.Ho * a.Wo * a.dy_stride * 4, 0x00020000);
+  constexpr unsigned OOB = 0x80000000u;
+  // per-thread parts of the gathers: halo piece -> image row / column offset from the patch origin and byte offset
+  // inside the 32-channel chunk; dY piece -> pixel offset and channel inside the 64-channel block
+  int hy[GH], hx[GH], hl[GH];
+#pragma unroll
+  for (int i = 0; i < GH; ++i) {
+    const int idx = i * NTH + tid, hr = idx >> 3, pos = idx & 7;
+    const int hrow = hr / HW, hcol = hr % HW, sg = hcol / (SEGW + 2), hc = hcol % (SEGW + 2);
+    hy[i] = d * (hrow - 1);
+    hx[i] = sg + d * (hc - 1);
+    hl[i] = 16 * (pos ^ (4 * (hr & 1)));
+  }
+  int dpix[GD], dq[GD];
+#pragma unroll
+  for (int i = 0; i < GD; ++i) {
+    const int idx = i * NTH + tid, pr = idx >> 4, q = (idx & 15) ^ (4 * (pr & 1));
+    const int r = pr >> 5, c = pr & 31;
+    dpix[i] = d * r * a.Wo + c / SEGW + d * (c % SEGW);
+    dq[i] = 4 * q;
+  }
+  struct Cmb { int ch, nb, xcs, xc0; bool inA; };
+  auto cmb = [&](int c) {
+    Cmb C;
+    C.ch = c % nch;
+    C.nb = c / nch;
+    C.inA = C.ch * CI < a.CAs;
+    C.xcs = C.inA ? a.CAs : a.CBs;
+    C.xc0 = (C.inA ? C.ch * CI : C.ch * CI - a.CAs) * 4;
+    return C;
+  };
+  struct Patch { int img, y0, x0, pbd; };
+  auto patch = [&](int t) {   // t -> (img, sub-lattice row a, patch row, column group b0, patch column)
+    Patch P;
+    const int px = t % nxq, t1 = t / nxq, bg = t1 % nbg, t2 = t1 / nbg, yq = t2 % nyq, t3 = t2 / nyq;
+    P.img = t3 / d;
+    P.y0 = t3 % d + d * yq * HF_PH;
+    P.x0 = bg * SPLIT + d * px * SEGW;
+    P.pbd = (P.img * a.Ho + P.y0) * a.Wo + P.x0;
+    return P;
+  };
+  auto issue_h = [&](const Patch& P, const Cmb& C, int i, int buf) {
+    const int idx = i * NTH + tid;
+    if (i < GH - 1 || idx < HCH) {
+      const int gy = P.y0 + hy[i], gx = P.x0 + hx[i];
+      const bool ok = (unsigned)gy < (unsigned)a.Hs && (unsigned)gx < (unsigned)a.Ws;
+      const unsigned off = ok ? (unsigned)(((P.img * a.Hs + gy) * a.Ws + gx) * C.xcs * 4 + C.xc0 + hl[i]) : OOB;
+      hf_buf_lds16(C.inA ? rsA : rsB, smem + buf * STAGE + (size_t)(i * NTH + wave * 64) * 16, off);
+    }
+  };
+  auto issue_d = [&](const Patch& P, const Cmb& C, int i, int buf) {
+    const int cc = C.nb * NB + dq[i];
+    const unsigned off = cc < a.Nout ? (unsigned)((P.pbd + dpix[i]) * a.dy_stride * 4 + cc * 4) : OOB;
+    hf_buf_lds16(rsD, smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16, off);
+  };
+  auto issue_row = [&](const Patch& P, const Cmb& C, int r, int buf) {   // the pieces that ride on patch row r
+#pragma unroll
+    for (int g = 0; g < GT; ++g)
+      if (g * HF_PH / GT == r) {
+        if (g < GH) issue_h(P, C, g, buf);
+        else issue_d(P, C, g - GH, buf);
+      }
+  };
+
+  f32x4 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float db = 0.f;
+  const int wn = wave >> 1, wc = wave & 1;
+  const int li = lane & 15, lg = lane >> 4;
+  const int ncol = wn * 16 + li, ccol = wc * 16 + li;
+  const uint32_t sbase = wf_lds(smem);
+  const uint32_t a_lane = lg * DRB + ((((ncol >> 2) ^ (4 * (lg & 1))) << 4) | ((ncol & 3) << 2));
+  uint32_t b_lane[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+    b_lane[dx] = (lg + dx) * HRB + ((((ccol >> 2) ^ (4 * ((lg + dx) & 1))) << 4) | ((ccol & 3) << 2));
+
+  {
+    const Cmb C0 = cmb(it0 / T);
+    const Patch P0 = patch(it0 % T);
+#pragma unroll
+    for (int i = 0; i < GH; ++i) issue_h(P0, C0, i, 0);
+#pragma unroll
+    for (int i = 0; i < GD; ++i) issue_d(P0, C0, i, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int it = it0; it < it1; ++it) {
+    const int buf = (it - it0) & 1;
+    const bool more = it + 1 < it1;
+    const int itn = more ? it + 1 : it;
+    const Cmb Cn = cmb(itn / T);
+    const Patch Pn = patch(itn % T);
+    const uint32_t hb = sbase + buf * STAGE;
+    const uint32_t abase = hb + HBUF + a_lane;
+    const uint32_t bbase[3] = {hb + b_lane[0], hb + b_lane[1], hb + b_lane[2]};
+    float fa[2], fb[2][9];
+    hf_read<0, SPLIT>(abase, bbase, fa[0], fb[0]);
+    hf_steps<0, SPLIT>(abase, bbase, fa, fb, acc, db, [&](int r) { if (more) issue_row(Pn, Cn, r, buf ^ 1); });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next item landed
+    __syncthreads();                                    // and nobody reads this stage any more
+    if (more && (it + 1) % T != 0) continue;
+    // the block's last item of this combination: bias row (block blk of the launcher's [G][Nout] rows) and dW atomics
+    const Cmb C = cmb(it / T);
+    if (a.bias_part && C.ch == 0 && wc == 0) {
+      float s = db;
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const int n = C.nb * NB + ncol;
+      if (lg == 0 && n < a.Nout) a.bias_part[(size_t)blk * a.Nout + n] = s;
+    }
+    const int kc = C.ch * CI + ccol;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = C.nb * NB + wn * 16 + 4 * lg + r;
+        if (n < a.Nout) atomicAdd(a.dW + (size_t)n * a.Kpad + t * Cin_s + kc, acc[t][r]);
+        acc[t][r] = 0.f;
+      }
+    db = 0.f;
+  }
+}
+
+template __global__ void igemm_wgrad_halo_f32_dil_kernel<1>(WgradArgs);
+template __global__ void igemm_wgrad_halo_f32_dil_kernel<2>(WgradArgs);
+template __global__ void igemm_wgrad_halo_f32_dil_kernel<4>(WgradArgs);
+template __global__ void igemm_wgrad_halo_f32_dil_kernel<8>(WgradArgs);
 
 template <int WN, int WK>
 void launch_f32cfg(WgradArgs& a, hipStream_t s) {
@@ -562,6 +741,42 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
     }
     adp::kernel_end();
     return 1;
+  }
+  // the dilated halo form (option wgrad_f32_dil): the same layers at dilation d > 1 whose sub-lattices tile into
+  // 4-row patches and whose rows into 32 / SPLIT-column segments (SPLIT <= 8, d a multiple of SPLIT)
+  if (option("wgrad_f32_dil", 1) && a.kh == 3 && a.kw == 3 && a.dil > 1 && a.pad == a.dil && a.stride == 1 &&
+      a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Ho % a.dil == 0 && a.Wo % a.dil == 0 &&
+      (a.Ho / a.dil) % HF_PH == 0 && a.CAs % 32 == 0 && a.CBs % 32 == 0 && a.Nout % 32 == 0 && a.dy_mode == 0 &&
+      a.K == 9 * Cin_s && a.Kpad >= a.K && a.dy_stride % 4 == 0 && a.dy_stride >= a.Nout && a.srcA &&
+      (!a.CBs || a.srcB) && (size_t)a.Nimg * a.Hs * a.Ws * std::max(a.CAs, a.CBs) * 4 < ((size_t)1 << 31) &&
+      (size_t)a.M * a.dy_stride * 4 < ((size_t)1 << 31)) {
+    const int wq = a.Wo / a.dil;
+    const int split = wq >= HF_PW ? (wq % HF_PW == 0 ? 1 : 0) : (HF_PW % wq == 0 ? HF_PW / wq : 0);
+    if (split >= 1 && split <= 8 && a.dil % split == 0) {
+      const int combos = Cin_s / 32 * ((a.Nout + 63) / 64);
+      const long long items = (long long)combos * a.Nimg * (a.Ho / HF_PH) * (a.Wo / HF_PW);
+      const int grid = (int)std::max(1LL, std::min<long long>(items, option("wgrad_f32_dil_grid", 256)));
+      a.zt_n = 0;
+      a.bias_part = nullptr;
+      if (a.dB && a.Nout % 4 == 0 && option("wgrad_f32_bias", 1)) {
+        a.bias_part = reduce_part(3, (size_t)grid * a.Nout * sizeof(float), s);
+        if (a.bias_part && hipMemsetAsync(a.bias_part, 0, (size_t)grid * a.Nout * sizeof(float), s) != hipSuccess)
+          a.bias_part = nullptr;
+      }
+      adp::set_kernel("igemm_wgrad_halo_f32_dil_kernel<%d>", split);
+      if (split == 1) hipLaunchKernelGGL((igemm_wgrad_halo_f32_dil_kernel<1>), dim3(grid), dim3(512), 0, s, a);
+      else if (split == 2) hipLaunchKernelGGL((igemm_wgrad_halo_f32_dil_kernel<2>), dim3(grid), dim3(512), 0, s, a);
+      else if (split == 4) hipLaunchKernelGGL((igemm_wgrad_halo_f32_dil_kernel<4>), dim3(grid), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((igemm_wgrad_halo_f32_dil_kernel<8>), dim3(grid), dim3(512), 0, s, a);
+      if (a.bias_part) {
+        adp::kernel_end();
+        slab_reduce(grid, (size_t)a.Nout / 4, a.bias_part, a.dB, s);
+        a.dB = nullptr;
+        a.bias_part = nullptr;
+      }
+      adp::kernel_end();
+      return 1;
+    }
   }
   if (!option("wgrad_f32", 0)) return 0;
   if (a.CAs % 4 != 0 || a.CBs % 4 != 0 || a.K != a.kh * a.kw * Cin_s || a.Kpad % 4 != 0 || a.Kpad < a.K ||

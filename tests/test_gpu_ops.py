@@ -1804,6 +1804,53 @@ def test_wgrad_f32_halo(case):
     assert relerr(res[0][0], res[1][0]) < 1e-5
 
 
+F32_DIL_WGRAD_CASES = [
+    # name, dilation, N, H, W, Cin, Nout: sub-lattices of Wo / d >= 32 columns (SPLIT 1) and narrower (2, 4, 8 segments)
+    ("d2_64_64", 2, 1, 32, 64, 64, 64),
+    ("d4_96_96_ragged_n", 4, 2, 16, 128, 96, 96),
+    ("d8_split2", 8, 1, 32, 128, 64, 64),
+    ("d16_split4", 16, 1, 128, 128, 64, 64),
+    ("d16_split8", 16, 1, 64, 64, 32, 96),
+    ("d32_352_352_bottleneck", 32, 2, 128, 128, 352, 352),
+]
+
+
+@pytest.mark.parametrize("case", F32_DIL_WGRAD_CASES, ids=[c[0] for c in F32_DIL_WGRAD_CASES])
+def test_wgrad_f32_halo_dilated(case):
+    """Dilated halo form of the f32 weight gradient (igemm_wgrad_halo_f32_dil_kernel<SPLIT>: sub-lattice patches,
+    work ranges across combinations, the bias gradient in the same pass) vs autograd of the fp32 oracle conv at the
+    same dilation (<= 1e-4 of the largest element) and vs the register-staged f32 kernel (option wgrad_f32_dil=0)
+    on the same operands (<= 1e-5): adipose_v3's bottleneck dilations 2 .. 32, the last at its real 128^2 x 352
+    shape."""
+    name, dil, N, H, W_, cin, cout = case
+    g = torch.Generator().manual_seed(67)
+    x = torch.randn(N, H, W_, cin, generator=g)
+    dZ = torch.randn(N, H, W_, cout, generator=g)
+    kern = (torch.randn(3, 3, cin, cout, generator=g) * 0.05).requires_grad_(True)
+    (R.conv2d_same(x, kern, None, dilation=dil, relu=False) * dZ).sum().backward()
+    xd = x.to(DEV).contiguous()
+    dzd = dZ.to(DEV).contiguous()
+    K = 9 * cin
+    res = []
+    for on in (1, 0):
+        dW = torch.zeros(((cout + 63) // 64 * 64, K), device=DEV)
+        dB = torch.zeros(cout, device=DEV)
+        ops.set_option("wgrad_f32_dil", on)
+        try:
+            ops.conv_wgrad(xd, dzd, dW, cout, dB=dB, dil=dil)
+            torch.cuda.synchronize()
+            kname = _lib.lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("wgrad_f32_dil", None)
+        res.append((dW[:cout].cpu(), dB.cpu(), kname))
+    assert res[0][2].startswith("igemm_wgrad_halo_f32_dil_kernel<"), res[0][2]
+    assert not res[1][2].startswith("igemm_wgrad_halo_f32_dil_kernel"), res[1][2]
+    got = res[0][0].view(cout, 3, 3, cin).permute(1, 2, 3, 0)
+    assert relerr(got, kern.grad) < 1e-4, relerr(got, kern.grad)
+    assert relerr(res[0][0], res[1][0]) < 1e-5
+    assert relerr(res[0][1], dZ.sum((0, 1, 2))) < 1e-5 and relerr(res[0][1], res[1][1]) < 1e-5
+
+
 CLAIM_HALO_CASES = [
     # name, source channels, Nout, forward kwargs kind
     ("fwd_1ch_relu", [64], 64, "relu"),
