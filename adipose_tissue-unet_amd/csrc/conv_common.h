@@ -62,6 +62,7 @@ struct FwdArgs {
 };
 
 // weight-gradient launch arguments: dW[n][k] += sum_m dY[m][n] * X(k)[m]
+constexpr int ZT_MAX = 40;   // combinations the f32 halo weight gradient's zero-tail table holds
 struct WgradArgs {
   const void* srcA; const void* srcB;
   const float* scA; const float* shA; const float* scB; const float* shB;
@@ -92,8 +93,10 @@ struct WgradArgs {
   // channels, and waves 0 .. zt_mode[c] - 1 take its useful 16 x 16 blocks (one per wave), the others only stage
   int ca_real, cb_real, nout_real;
   int zt_n;
-  int zt_cstart[9];
-  int zt_mode[8];
+  // (zt_mode[c] >= 16: row tails -- the output block holds zt_mode[c] - 16 <= 2 real 16-row blocks and waves 0 ..
+  // 2 (zt_mode[c] - 16) - 1 take them with both input column blocks; round 6)
+  int zt_cstart[ZT_MAX + 1];
+  int zt_mode[ZT_MAX];
   float* bias_part;     // f32 halo weight gradient: per-block bias-gradient rows (option wgrad_f32_bias)
 };
 

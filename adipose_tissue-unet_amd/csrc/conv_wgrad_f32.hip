@@ -331,8 +331,11 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   if (nt == 0) return;   // (uniform)
   // zero tails: a chunk with <= 16 real input channels has hm useful 16 x 16 blocks (output rows 16 w, input columns
   // 0-15), one per wave 0 .. hm - 1 -- one wave per SIMD instead of two --, and the other waves only stage
-  const int hm = a.zt_n ? a.zt_mode[combo] : 0;
-  const bool idle = hm > 0 && wave >= hm;
+  // row tails (zt_mode >= 16): an output block with <= 2 real 16-row blocks takes them on waves 0 .. 2 rb - 1 (both
+  // column blocks), one wave per SIMD as well
+  const int zm = a.zt_n ? a.zt_mode[combo] : 0, hm = zm & 15;
+  const bool rt = zm >= 16;
+  const bool idle = hm > 0 && wave >= (rt ? 2 * hm : hm);
   const bool inA = ch * CI < a.CAs;
   const int xcs = inA ? a.CAs : a.CBs;
   const int us = a.up >> 1;
@@ -401,7 +404,8 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db = 0.f;
-  const int wn = hm ? wave : wave >> 1, wc = hm ? 0 : wave & 1;
+  const bool zc = hm && !rt;   // (chunk tails: one 16-column block, a 16-row block per wave)
+  const int wn = zc ? wave : wave >> 1, wc = zc ? 0 : wave & 1;
   const int li = lane & 15, lg = lane >> 4;
   const int ncol = wn * 16 + li, ccol = wc * 16 + li;   // this lane's dY column (output channel), X column
   const uint32_t sbase = wf_lds(smem);
@@ -692,11 +696,16 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
     const int per = std::max(1, std::min(tiles, target / combos));
     int grid = per * combos;
     // zero tails (the caller's real channel counts; option wgrad_f32_zt): a combination whose input chunk holds
-    // <= 16 real channels runs its <= 4 useful 16 x 16 blocks one per SIMD, in about half the time per patch, and
-    // gets about half the blocks of a full one
+    // <= 16 real channels runs its <= 4 useful 16 x 16 blocks one per SIMD, and since round 6 one whose output
+    // block holds <= 2 real 16-row blocks runs them on 2 rb waves (row tails, option wgrad_f32_rt); either takes
+    // ~60 % of a full patch's time (option wgrad_f32_zt_w, percent; 50 and 70 measured slower,
+    // profiles/r06f_f32_wgrad_probe.log) and gets blocks in proportion
     a.zt_n = 0;
-    if (option("wgrad_f32_zt", 1) && combos <= 8 && (a.ca_real > 0 || a.cb_real > 0)) {
-      double w[8], tot = 0.0;
+    if (option("wgrad_f32_zt", 1) && combos <= std::min(ZT_MAX, option("wgrad_f32_zt_max", ZT_MAX)) &&
+        (a.ca_real > 0 || a.cb_real > 0 || a.nout_real > 0)) {
+      const bool rows_too = option("wgrad_f32_rt", 1) && a.nout_real > 0;
+      const double wt = option("wgrad_f32_zt_w", 60) / 100.0;
+      double w[ZT_MAX], tot = 0.0;
       bool any = false;
       for (int c = 0; c < combos; ++c) {
         const int ch = c % nch, nb = c / nch;
@@ -705,16 +714,32 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
         const int rin = rsrc > 0 ? std::min(32, std::max(0, rsrc - c0)) : 32;
         const int rows = a.nout_real > 0 ? std::min(64, std::max(0, a.nout_real - nb * 64)) : 64;
         const int rb = (rows + 15) / 16;
-        a.zt_mode[c] = rin <= 16 && rb >= 1 ? rb : 0;
+        a.zt_mode[c] = rin <= 16 && rb >= 1 ? rb : rows_too && rb >= 1 && rb <= 2 ? 16 + rb : 0;
         any = any || a.zt_mode[c] > 0;
-        w[c] = a.zt_mode[c] > 0 ? 0.5 : 1.0;
+        w[c] = a.zt_mode[c] > 0 ? wt : 1.0;
         tot += w[c];
       }
       if (any) {
+        // blocks per combination: one each, then greedily to the combination with the longest weighted time
+        // w ceil(tiles / n) until the target is reached (never more blocks than the target: a second round of
+        // blocks would double the launch)
+        (void)tot;
+        int n[ZT_MAX], used = combos;
+        for (int c = 0; c < combos; ++c) n[c] = 1;
+        while (used < target) {
+          int best = -1;
+          double bt = 0.0;
+          for (int c = 0; c < combos; ++c) {
+            const double t = w[c] * ((tiles + n[c] - 1) / n[c]);
+            if (n[c] < tiles && t > bt) { bt = t; best = c; }
+          }
+          if (best < 0) break;
+          ++n[best];
+          ++used;
+        }
         a.zt_n = combos;
         a.zt_cstart[0] = 0;
-        for (int c = 0; c < combos; ++c)
-          a.zt_cstart[c + 1] = a.zt_cstart[c] + std::max(1, std::min(tiles, (int)(target * w[c] / tot + 0.5)));
+        for (int c = 0; c < combos; ++c) a.zt_cstart[c + 1] = a.zt_cstart[c] + n[c];
         grid = a.zt_cstart[combos];
       }
     }
@@ -724,10 +749,14 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
     a.bias_part = nullptr;
     int g0 = 0;
     if (a.dB && a.Nout % 4 == 0 && option("wgrad_f32_bias", 1)) {
-      g0 = a.zt_n ? a.zt_cstart[1] - a.zt_cstart[0] : per;
-      bool same = true;   // (every chunk-0 combination must have g0 blocks: one row per block index)
-      for (int c = nch; a.zt_n && c < combos; c += nch) same = same && a.zt_cstart[c + 1] - a.zt_cstart[c] == g0;
-      if (same) a.bias_part = reduce_part(3, (size_t)g0 * a.Nout * sizeof(float), s);
+      // (one row per block index of the chunk-0 combinations; a combination with fewer blocks leaves its other
+      // rows zero)
+      g0 = per;
+      if (a.zt_n) {
+        g0 = 0;
+        for (int c = 0; c < combos; c += nch) g0 = std::max(g0, a.zt_cstart[c + 1] - a.zt_cstart[c]);
+      }
+      a.bias_part = reduce_part(3, (size_t)g0 * a.Nout * sizeof(float), s);
       if (a.bias_part && hipMemsetAsync(a.bias_part, 0, (size_t)g0 * a.Nout * sizeof(float), s) != hipSuccess)
         a.bias_part = nullptr;
     }

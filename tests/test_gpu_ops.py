@@ -1159,13 +1159,16 @@ def test_f32_zero_tail_forms(case):
 
 
 @pytest.mark.parametrize("reals,nout,nreal", [([44], 64, 44), ([44, 44], 64, 44), ([40], 64, 64), ([12], 64, 20),
-                                               ([44], 128, 100)],
-                         ids=["1src_44", "2src_44_44", "1src_40_n64", "1src_12_n20", "1src_44_n128_100"])
+                                               ([44], 128, 100), ([44], 128, 88), ([64, 44], 192, 136)],
+                         ids=["1src_44", "2src_44_44", "1src_40_n64", "1src_12_n20", "1src_44_n128_100",
+                              "1src_44_n128_88_row_tail", "2src_64_44_n192_136_12_combos"])
 def test_f32_halo_wgrad_zero_tails(reals, nout, nreal):
     """f32 halo weight gradient with the real-channel hints (option wgrad_f32_zt): an input chunk with <= 16 real
     channels runs its useful 16 x 16 blocks one per wave on fewer waves and gets fewer blocks; and the bias gradient
     summed in the same pass (option wgrad_f32_bias: per-block rows + the fixed-order slab reduce) instead of the
-    channel-sum launch. The weight gradient equals the unhinted launch's to the f32 atomics' order, the pad rows and
+    channel-sum launch. Round 6: row tails (an output block with <= 2 real 16-row blocks on 2 rb waves) and tables of
+    up to 40 combinations (12 here) with greedily balanced block counts.
+    The weight gradient equals the unhinted launch's to the f32 atomics' order, the pad rows and
     columns stay exactly zero, both match a float64 reference; the bias gradient to 1e-6 of the channel sum's."""
     from adipose_amd._lib import lib
     g = torch.Generator().manual_seed(101)
