@@ -145,7 +145,7 @@ double* stat_scratch_fold(int C, const float* sum, hipStream_t s);
 int bn_fold_reset(hipStream_t s);   // adp_bn_fold_reset
 // dynamic tile claiming: a zeroed slot of CLAIM_INTS counters for one persistent launch (a ring of CLAIM_SLOTS per
 // device, handed out in turn; a launch leaves its slot zeroed again), or nullptr (error set)
-constexpr int CLAIM_SLOTS = 64, CLAIM_INTS = 64;
+constexpr int CLAIM_SLOTS = 64, CLAIM_INTS = 512;
 int* claim_slot();
 // per-device growable scratch (slot 0: weight-gradient split partials / slabs, 1: dz of the unfused BN-backward
 // weight gradient, 2: metrics, 3: bias-gradient block sums); growing synchronises the device
