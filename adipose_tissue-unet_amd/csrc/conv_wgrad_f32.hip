@@ -645,6 +645,87 @@ template __global__ void igemm_wgrad_halo_f32_dil_kernel<2>(WgradArgs);
 template __global__ void igemm_wgrad_halo_f32_dil_kernel<4>(WgradArgs);
 template __global__ void igemm_wgrad_halo_f32_dil_kernel<8>(WgradArgs);
 
+// f32 weight gradient of a one-real-channel input layer (adipose_v3's down1_conv1: the gray tile in an 8-channel
+// stride, <= 64 output channels): dW[n][t * 8] = sum_p dY[p][n] X[p + off_t][0] and dB[n] = sum_p dY[p][n]. The
+// products are 2 M x 64 x 10 per 1024^2 tile -- nothing -- and dY is 256 B a pixel: the launch streams dY once. The
+// generic register-staged kernel tiled K = 72 in 64-wide blocks and ran at ~1.5 TB/s. Here one v_mfma_f32_16x16x4_f32
+// per 4 pixels and 16 channels: A = the tap-shifted input (row i = tap i < 9, row 9 = ones for the bias, k = pixel),
+// B = dY (k = pixel, column j = channel 4 j + q of block q: one float4 load per lane and 4 pixels, 1 KB per wave
+// instruction). 8 waves a block, each a strided run of 4-pixel steps; the waves' sums are added in LDS in wave order
+// and each block writes one slab (dW layout, zero pad columns) and one bias row, summed in a fixed order by the slab
+// reduce: deterministic.
+__global__ __launch_bounds__(512) void wgrad_in1_f32_kernel(WgradArgs a, float* part, float* bpart) {
+  constexpr int NW = 8, UNR = 8;
+  __shared__ float red[NW][64 * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = gridDim.x, blk = blockIdx.x;
+  const int per = ((a.M + G - 1) / G + 4 * NW - 1) / (4 * NW) * (4 * NW);
+  const int p0 = blk * per, p1 = min(a.M, p0 + per);
+  const int i = lane & 15, kq = lane >> 4;
+  const int ty = i / 3 - 1, tx = i % 3 - 1;
+  const int HW = a.Ho * a.Wo;
+  const float* X = reinterpret_cast<const float*>(a.srcA);
+  const float4* dy4 = reinterpret_cast<const float4*>(a.dY);
+  const int ds4 = a.dy_stride / 4;
+  f32x4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int pb = p0 + 4 * wave; pb < p1; pb += 4 * NW * UNR) {
+    float av[UNR];
+    float4 bv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int p = pb + u * 4 * NW + kq;
+      const bool in = p < p1;
+      bv[u] = in ? dy4[(size_t)p * ds4 + i] : float4{0.f, 0.f, 0.f, 0.f};
+      float v = 0.f;
+      if (in && i < 10) {
+        if (i == 9) {
+          v = 1.f;
+        } else {
+          const int n = p / HW, rem = p - n * HW, y = rem / a.Wo, x = rem - y * a.Wo;
+          const int yy = y + ty, xx = x + tx;
+          if ((unsigned)yy < (unsigned)a.Hs && (unsigned)xx < (unsigned)a.Ws)
+            v = X[((size_t)(n * a.Hs + yy) * a.Ws + xx) * a.CAs];
+        }
+      }
+      av[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u].x, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u].y, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u].z, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u].w, acc[3], 0, 0, 0);
+    }
+  }
+  // D[i][j] of block q at lane j + 16 (i >> 2), register i & 3: tap / ones row i, channel n = 4 j + q
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][(4 * (lane & 15) + q) * 16 + 4 * (lane >> 4) + r] = acc[q][r];
+  __syncthreads();
+  // slab: [Nout][Kpad] (tap t at column 8 t, the other columns zero), bias row [Nout]
+  float* slab = part + (size_t)blk * a.Nout * a.Kpad;
+  for (int e = tid; e < a.Nout * a.Kpad; e += 512) {
+    const int n = e / a.Kpad, c = e - n * a.Kpad;
+    float v = 0.f;
+    if ((c & 7) == 0 && c < 72) {
+      const int t = c >> 3;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[w][n * 16 + t];
+    }
+    slab[e] = v;
+  }
+  if (bpart)
+    for (int n = tid; n < a.Nout; n += 512) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[w][n * 16 + 9];
+      bpart[(size_t)blk * a.Nout + n] = v;
+    }
+}
+
 template <int WN, int WK>
 void launch_f32cfg(WgradArgs& a, hipStream_t s) {
   constexpr int TN = WN * 64, TK = WK * 64;
@@ -682,6 +763,26 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
   // (profiles/r03_wgrad_f32_ab.txt)
   if (a.scA || a.scB || a.bna_dA) return 0;
   const int Cin_s = a.CAs + a.CBs;
+  // one real input channel (the caller's hint) in a stride of 8, <= 64 outputs (option wgrad_f32_in1)
+  if (option("wgrad_f32_in1", 1) && a.ca_real == 1 && a.CAs == 8 && a.CBs == 0 && a.kh == 3 && a.kw == 3 &&
+      a.dil == 1 && a.pad == 1 && a.stride == 1 && a.up == 1 && a.Ho == a.Hs && a.Wo == a.Ws && a.Nout <= 64 &&
+      a.Nout % 4 == 0 && a.dy_mode == 0 && a.K == 72 && a.Kpad >= 72 && a.Kpad % 4 == 0 && a.dy_stride % 4 == 0 &&
+      a.dy_stride >= 64 && a.srcA && a.M > 0) {
+    const int G = std::max(1, std::min(option("wgrad_f32_in1_grid", 256), (a.M + 31) / 32));
+    float* part = reduce_part(0, (size_t)G * a.Nout * a.Kpad * sizeof(float), s);
+    float* bpart = a.dB ? reduce_part(3, (size_t)G * a.Nout * sizeof(float), s) : nullptr;
+    if (part && (bpart || !a.dB)) {
+      adp::set_kernel("wgrad_in1_f32_kernel");
+      hipLaunchKernelGGL(wgrad_in1_f32_kernel, dim3(G), dim3(512), 0, s, a, part, bpart);
+      adp::kernel_end();
+      slab_reduce(G, (size_t)a.Nout * a.Kpad / 4, part, a.dW, s);
+      if (bpart) {
+        slab_reduce(G, (size_t)a.Nout / 4, bpart, a.dB, s);
+        a.dB = nullptr;   // (done: the caller's channel-sum launch is skipped)
+      }
+      return 1;
+    }
+  }
   // the persistent halo form (option wgrad_f32_halo): 3x3 stride-1 'same' layers of 32-channel multiples
   if (option("wgrad_f32_halo", 1) && a.kh == 3 && a.kw == 3 && a.dil == 1 && a.pad == 1 && a.stride == 1 &&
       (a.up == 1 || a.up == 2) && a.Ho == a.Hs * a.up && a.Wo == a.Ws * a.up && a.Ho % HF_PH == 0 &&

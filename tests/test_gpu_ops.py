@@ -1807,6 +1807,51 @@ def test_wgrad_f32_halo(case):
     assert relerr(res[0][0], res[1][0]) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 96, 44, 64), (1, 40, 56, 48, 64), (2, 32, 32, 64, 64)],
+                         ids=["n2_64x96_44of64", "ragged_40x56_48", "n2_32x32_64"])
+def test_wgrad_f32_input_layer(shape):
+    """f32 weight gradient of the one-real-channel input layer (wgrad_in1_f32_kernel: adipose_v3's down1_conv1, the
+    gray tile in an 8-channel stride): dW at columns 8 t and dB against a float64 reference (1e-5 of the largest
+    element), against the generic register-staged kernel (option wgrad_f32_in1=0, 1e-5), pad columns exactly zero,
+    and two runs bit-identical (per-block slabs summed in a fixed order)."""
+    from adipose_amd._lib import lib
+    N, H, W_, nreal, nst = shape
+    g = torch.Generator().manual_seed(131)
+    x = torch.zeros(N, H, W_, 8)
+    x[..., 0] = torch.randn(N, H, W_, generator=g)
+    dy = torch.zeros(N, H, W_, nst)
+    dy[..., :nreal] = torch.randn(N, H, W_, nreal, generator=g)
+    xd, dyd = x.to(DEV), dy.to(DEV)
+
+    def run(on):
+        dW = torch.zeros(nst, 96, device=DEV)
+        dB = torch.zeros(nst, device=DEV)
+        ops.set_option("wgrad_f32_in1", on)
+        try:
+            ops.conv_wgrad(xd, dyd, dW, nst, dB=dB, real=(1, 0, nreal))
+            torch.cuda.synchronize()
+            kn = lib().adp_last_kernel().decode()
+        finally:
+            ops.set_option("wgrad_f32_in1", None)
+        return dW.cpu(), dB.cpu(), kn
+
+    w1, b1, k1 = run(1)
+    w1b, b1b, _ = run(1)
+    w0, b0, k0 = run(0)
+    assert k1 == "wgrad_in1_f32_kernel" and k0 != k1, (k1, k0)
+    assert torch.equal(w1, w1b) and torch.equal(b1, b1b)
+    xp = F.pad(x[..., 0].double(), (1, 1, 1, 1))
+    d64 = dy.double().reshape(-1, nst)
+    ref = torch.zeros(nst, 96, dtype=torch.float64)
+    for t in range(9):
+        ty, tx = t // 3, t % 3
+        ref[:, 8 * t] = d64.T @ xp[:, ty:ty + H, tx:tx + W_].reshape(-1)
+    assert relerr(w1, ref) < 1e-5 and relerr(b1, d64.sum(0)) < 1e-5
+    assert relerr(w1, w0) < 1e-5 and relerr(b1, b0) < 1e-5
+    pad = [c for c in range(96) if c % 8 or c >= 72]
+    assert w1[:, pad].abs().max().item() == 0
+
+
 F32_DIL_WGRAD_CASES = [
     # name, dilation, N, H, W, Cin, Nout: sub-lattices of Wo / d >= 32 columns (SPLIT 1) and narrower (2, 4, 8 segments)
     ("d2_64_64", 2, 1, 32, 64, 64, 64),
