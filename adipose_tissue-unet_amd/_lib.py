@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("ADP_LIB_PATH") or os.path.join(PKG_DIR, "libadipose_h
 F32 = 0
 BF16 = 1
 FP8 = 2   # OCP e4m3fn (torch.float8_e4m3fn storage), forward launches only
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 
 class AdpError(RuntimeError):
@@ -65,6 +65,7 @@ _SIGS = {
     "adp_abi_version": [],
     "adp_set_option": [C.c_char_p, _I],
     "adp_timing": [_I],
+    "adp_timing_filter": [C.c_char_p],
     "adp_timing_read": [_I, C.c_char_p, _I, C.POINTER(C.c_float), C.POINTER(C.c_int)],
     "adp_conv_fwd": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P],
     "adp_conv_wgrad": [_I, C.POINTER(ConvDesc), C.POINTER(ConvIO), _P, _I, _P, _P, _P],

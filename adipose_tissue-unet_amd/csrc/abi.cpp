@@ -26,6 +26,8 @@ struct TimedLaunch {
 };
 static std::mutex g_time_mu;
 static bool g_timing = false;
+static std::string g_time_filter;   // (adp_timing_filter: only launches of this kernel name; empty = all)
+static bool g_time_open = false;    // a recorded launch waits for its end mark
 static std::vector<TimedLaunch> g_timed;
 static std::vector<hipEvent_t> g_event_pool;
 static hipEvent_t pool_event() {
@@ -45,16 +47,21 @@ void set_kernel(const char* fmt, ...) {
   vsnprintf(g_kernel, sizeof(g_kernel), fmt, ap);
   va_end(ap);
   std::lock_guard<std::mutex> lk(g_time_mu);
-  if (!g_timing) return;
+  g_time_open = false;
+  if (!g_timing || (!g_time_filter.empty() && g_time_filter != g_kernel)) return;
   TimedLaunch t{};
   std::snprintf(t.name, sizeof(t.name), "%s", g_kernel);
   t.e0 = pool_event();
   t.e1 = nullptr;
-  if (t.e0 && hipEventRecord(t.e0, g_launch_stream) == hipSuccess) g_timed.push_back(t);
+  if (t.e0 && hipEventRecord(t.e0, g_launch_stream) == hipSuccess) {
+    g_timed.push_back(t);
+    g_time_open = true;
+  }
 }
 void kernel_end() {
   std::lock_guard<std::mutex> lk(g_time_mu);
-  if (!g_timing || g_timed.empty() || g_timed.back().e1) return;
+  if (!g_timing || !g_time_open || g_timed.empty() || g_timed.back().e1) return;
+  g_time_open = false;
   hipEvent_t e = pool_event();
   if (e && hipEventRecord(e, g_launch_stream) == hipSuccess) g_timed.back().e1 = e;
 }
@@ -131,6 +138,11 @@ extern "C" int adp_timing(int mode) {
   return 0;
 }
 
+extern "C" int adp_timing_filter(const char* name) {
+  std::lock_guard<std::mutex> lk(adp::g_time_mu);
+  adp::g_time_filter = name ? name : "";
+  return 0;
+}
 extern "C" int adp_timing_read(int max, char* names, int name_len, float* ms, int* n) {
   if (!n || (max > 0 && (!names || !ms || name_len < 2))) { adp::set_error("adp_timing_read: bad arguments"); return -1; }
   std::lock_guard<std::mutex> lk(adp::g_time_mu);

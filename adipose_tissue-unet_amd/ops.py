@@ -33,12 +33,16 @@ class LaunchTimer:
 
     NAME_LEN = 160
 
-    def __init__(self):
+    def __init__(self, only=None):
+        """only: a kernel name (as adp_last_kernel reports it): record that kernel's launches alone
+        (adp_timing_filter), so the other launches of a timed region carry no event pair."""
         self.recs = []
+        self.only = only
 
     def wrap(self, dcode, flops, fn, nbytes=0.0):
         fn()
-        self.recs.append((dcode, flops, nbytes))
+        if self.only is None or lib().adp_last_kernel().decode() == self.only:
+            self.recs.append((dcode, flops, nbytes))
 
     def summary(self):
         """(kernel name, dtype code) -> (launches, total flops, total ms, total algorithmic bytes)
@@ -70,7 +74,12 @@ def set_launch_timer(t):
     """Start (t = a LaunchTimer) or stop (None) recording; the record is read by t.summary()."""
     global _timer
     _timer = t
-    call("adp_timing", 1 if t is not None else 0)
+    if t is not None:
+        call("adp_timing_filter", t.only.encode() if t.only else None)
+        call("adp_timing", 1)
+    else:
+        call("adp_timing", 0)
+        call("adp_timing_filter", None)
 
 
 def _timed(dcode, flops, fn, nbytes=0.0):

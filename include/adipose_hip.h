@@ -29,7 +29,7 @@ extern "C" {
 #define ADP_DTYPE_F32 0
 #define ADP_DTYPE_BF16 1
 #define ADP_DTYPE_FP8 2 /* OCP e4m3fn, inference (forward) launches only */
-#define ADP_ABI_VERSION 20 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
+#define ADP_ABI_VERSION 21 /* v4: adp_threshold_hist; v5: adp_maxpool2_bwd_bnr; v6: adp_aug_*, adp_percentile_normalize;
                               v7: handle engine adp_create / adp_forward / adp_*_param / adp_destroy;
                               v8: adp_train_step / adp_set_comm / adp_comm_*, adp_auc_metrics, adp_distance_transform, adp_boundary_metrics, adp_pack_weights_batch,
                               adp_bn_apply_maxpool2, adp_head_sigmoid_bwd_bnr;
@@ -43,7 +43,8 @@ extern "C" {
                               v17: adp_wgrad_defer / adp_wgrad_flush
                               v18: adp_conv_io.act_outA;
                               v19: adp_conv_desc.CA_real / CB_real / Nout_real (zero-weight hints);
-                              v20: adp_wgrad_release / adp_wgrad_arena_chunks (deferral arenas per (device, stream)), adp_get_option */
+                              v20: adp_wgrad_release / adp_wgrad_arena_chunks (deferral arenas per (device, stream)), adp_get_option;
+                              v21: adp_timing_filter */
 
 typedef void* adp_stream_t; /* hipStream_t */
 
@@ -143,6 +144,10 @@ int adp_get_option(const char* name);
  * around it are excluded, so each pair times exactly one kernel of rocprofv3's list); 0: stop recording (the
  * record is kept); 2: stop and clear. */
 int adp_timing(int mode);
+/* Restricts the recording to launches whose kernel name (adp_last_kernel) equals `name` (NULL or "": every
+ * launch): the bench times only its dominant kernel inside the timed region, where each event pair costs the
+ * step time. */
+int adp_timing_filter(const char* name);
 /* Reads the record (synchronises on its events): *n = number of timed launches; for i < max: names[i *
  * name_len] = kernel name, ms[i] = its duration (-1 if its end was not marked). max = 0 only counts. */
 int adp_timing_read(int max, char* names, int name_len, float* ms, int* n);

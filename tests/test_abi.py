@@ -26,7 +26,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_error_plumbing():
     lib = _lib.lib()
-    assert lib.adp_abi_version() == _lib.ABI_VERSION == 20
+    assert lib.adp_abi_version() == _lib.ABI_VERSION == 21
     assert isinstance(lib.adp_last_error(), bytes)
 
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Cost of the bench's per-launch event timing (ops.LaunchTimer: a HIP event pair around the main kernel of every conv
+"""Cost of the bench's per-launch event timing (arm events: every conv launch; dom: the dominant kernel's only) (ops.LaunchTimer: a HIP event pair around the main kernel of every conv
 launch) on the unet_bn bench step: alternating blocks of steps with and without it, in one process."""
 import os
 import sys
@@ -25,22 +25,26 @@ def main():
     y = torch.from_numpy(ys).to(dev)
     for _ in range(3):
         tr.train_step(x, y)
-    res = {"events": [], "plain": []}
-    for _ in range(4):
-        for arm in ("plain", "events"):
-            timer = ops.LaunchTimer() if arm == "events" else None
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    nst = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    res = {"events": [], "plain": [], "dom": []}
+    for _ in range(rounds):
+        for arm in ("plain", "events", "dom"):
+            timer = (ops.LaunchTimer() if arm == "events" else
+                     ops.LaunchTimer(only="igemm_wgrad_halopair_kernel<6, 0>") if arm == "dom" else None)
             torch.cuda.synchronize()
             ops.set_launch_timer(timer)
             t0 = time.perf_counter()
-            for _ in range(8):
+            for _ in range(nst):
                 tr.train_step(x, y)
             torch.cuda.synchronize()
-            res[arm].append((time.perf_counter() - t0) / 8 * 1e3)
+            res[arm].append((time.perf_counter() - t0) / nst * 1e3)
             ops.set_launch_timer(None)
             if timer is not None:
                 timer.summary()
     for k, v in res.items():
-        print(k, "ms/step", [round(t, 3) for t in v], "min", round(min(v), 3), flush=True)
+        print(k, "ms/step", [round(t, 3) for t in v], "min", round(min(v), 3), "median",
+              round(sorted(v)[len(v) // 2], 3), flush=True)
 
 
 if __name__ == "__main__":
