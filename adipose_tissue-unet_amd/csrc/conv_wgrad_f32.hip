@@ -257,47 +257,54 @@ ADP_DEV float wf_rdo(uint32_t addr) {
   asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
   return r;
 }
+// (a device function: the builtin inside a kernel template fails the host pass's substitution)
+__device__ __forceinline__ void hf_buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds, unsigned off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, off, 0, 0, 0);
+}
 // halo geometry of the dilated form (below): the 32 patch columns in SPLIT segments of 32 / SPLIT, each segment with
 // its own two halo columns; SPLIT 1 is the dilation-1 layout (34 halo columns)
 template <int SPLIT>
 constexpr int hf_hw() { return HF_PW + 2 * SPLIT; }
 template <int SPLIT>
 constexpr int hf_col(int c) { return c + 2 * (c / (HF_PW / SPLIT)); }
-// k step S of a patch (pixel row S / 8, pixels 4 (S % 8) .. + 3): dY^T element and the 9 tap-shifted halo elements
-template <int S, int SPLIT>
+// k step S of a patch (pixel row S / 8, pixels 4 (S % 8) .. + 3): dY^T element and the tap-shifted halo elements of
+// the taps in TM (all 9 by default; the tap-split waves of the T3 form take 5 or 4)
+#define HF_B(t) \
+  if constexpr ((TM >> (t)) & 1) B[t] = wf_rdo<((r + (t) / 3) * HW + hc) * 128>(bbase[(t) % 3]);
+template <int S, int SPLIT, int TM = 0x1FF>
 ADP_DEV void hf_read(uint32_t abase, const uint32_t (&bbase)[3], float& A, float (&B)[9]) {
   constexpr int r = S / 8, xs = S % 8, HW = hf_hw<SPLIT>(), hc = hf_col<SPLIT>(4 * xs);
   A = wf_rdo<(r * HF_PW + 4 * xs) * 256>(abase);
-  B[0] = wf_rdo<((r + 0) * HW + hc) * 128>(bbase[0]);
-  B[1] = wf_rdo<((r + 0) * HW + hc) * 128>(bbase[1]);
-  B[2] = wf_rdo<((r + 0) * HW + hc) * 128>(bbase[2]);
-  B[3] = wf_rdo<((r + 1) * HW + hc) * 128>(bbase[0]);
-  B[4] = wf_rdo<((r + 1) * HW + hc) * 128>(bbase[1]);
-  B[5] = wf_rdo<((r + 1) * HW + hc) * 128>(bbase[2]);
-  B[6] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[0]);
-  B[7] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[1]);
-  B[8] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[2]);
+  HF_B(0) HF_B(1) HF_B(2) HF_B(3) HF_B(4) HF_B(5) HF_B(6) HF_B(7) HF_B(8)
 }
+#undef HF_B
 // the 32 k steps of a patch, software-pipelined one step deep (the reads of step S + 1 in flight while step S
 // multiplies); at the first step of each pixel row the row's share of the next patch's LDS-DMA goes out
-template <int S, int SPLIT = 1, typename RowIssue>
+#define HF_M(t) \
+  if constexpr ((TM >> (t)) & 1) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur], fb[cur][t], acc[t], 0, 0, 0);
+template <int S, int SPLIT = 1, int TM = 0x1FF, typename RowIssue>
 ADP_DEV void hf_steps(uint32_t abase, const uint32_t (&bbase)[3], float (&fa)[2], float (&fb)[2][9], f32x4 (&acc)[9],
                       float& db, const RowIssue& row_issue) {
-  constexpr int NS = HF_PH * HF_PW / 4, cur = S & 1;
+  constexpr int NS = HF_PH * HF_PW / 4, cur = S & 1, NRD = 1 + __builtin_popcount(TM);
   if constexpr (S % 8 == 0) row_issue(S / 8);
   if constexpr (S + 1 < NS) {
-    hf_read<S + 1, SPLIT>(abase, bbase, fa[cur ^ 1], fb[cur ^ 1]);
-    wf_lgkm<10>();
+    hf_read<S + 1, SPLIT, TM>(abase, bbase, fa[cur ^ 1], fb[cur ^ 1]);
+    wf_lgkm<NRD>();
   } else {
     wf_lgkm<0>();
   }
   __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur], fb[cur][t], acc[t], 0, 0, 0);
+  HF_M(0) HF_M(1) HF_M(2) HF_M(3) HF_M(4) HF_M(5) HF_M(6) HF_M(7) HF_M(8)
   __builtin_amdgcn_s_setprio(0);
   db += fa[cur];   // (the bias gradient: every dY element of the patch passes one lane's A operand once)
-  if constexpr (S + 1 < NS) hf_steps<S + 1, SPLIT>(abase, bbase, fa, fb, acc, db, row_issue);
+  if constexpr (S + 1 < NS) hf_steps<S + 1, SPLIT, TM>(abase, bbase, fa, fb, acc, db, row_issue);
 }
+#undef HF_M
+// T3 (round 6): output blocks with 3 real 16-row blocks (adipose_v3's level-0 44 outputs) leave rows 48-63 to the
+// waves 6 and 7, i.e. SIMDs 2 and 3 idle half the time while SIMDs 0 and 1 run two full waves. In the T3 form the
+// third row block is split by taps: waves 4 / 5 take its taps 0-4, waves 6 / 7 taps 5-8, so the SIMDs run 14, 14, 13
+// and 13 tap blocks per k step instead of 18, 18, 9 and 9.
+template <bool T3>
 __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs a) {
   constexpr int NTH = 512, CI = 32, NB = 64;
   constexpr int HRB = CI * 4, DRB = NB * 4;                    // LDS row bytes: halo pixel, dY pixel
@@ -334,8 +341,8 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   // row tails (zt_mode >= 16): an output block with <= 2 real 16-row blocks takes them on waves 0 .. 2 rb - 1 (both
   // column blocks), one wave per SIMD as well
   const int zm = a.zt_n ? a.zt_mode[combo] : 0, hm = zm & 15;
-  const bool rt = zm >= 16;
-  const bool idle = hm > 0 && wave >= (rt ? 2 * hm : hm);
+  const bool rt = (zm & 16) != 0, t3 = T3 && (zm & 32) != 0;   // (row tails; T3: the tap-split third row block)
+  const bool idle = hm > 0 && !t3 && wave >= (rt ? 2 * hm : hm);
   const bool inA = ch * CI < a.CAs;
   const int xcs = inA ? a.CAs : a.CBs;
   const int us = a.up >> 1;
@@ -381,14 +388,12 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
       const bool ok = (unsigned)gy < (unsigned)(a.Hs << us) && (unsigned)gx < (unsigned)(a.Ws << us);
       const unsigned off =
           ok ? (unsigned)(((P.img * a.Hs + (gy >> us)) * a.Ws + (gx >> us)) * xcs * 4 + hoff[i]) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsX, (lds_void*)(smem + buf * STAGE + (size_t)(i * NTH + wave * 64) * 16),
-                                               16, off, 0, 0, 0);
+      hf_buf_lds16(rsX, smem + buf * STAGE + (size_t)(i * NTH + wave * 64) * 16, off);
     }
   };
   auto issue_d = [&](const Patch& P, int i, int buf) {
     const unsigned off = dok[i] ? (unsigned)((P.pbd + dpix[i]) * a.dy_stride * 4 + doff[i]) : OOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        rsD, (lds_void*)(smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16), 16, off, 0, 0, 0);
+    hf_buf_lds16(rsD, smem + buf * STAGE + HBUF + (size_t)(i * NTH + wave * 64) * 16, off);
   };
   // the next patch's pieces, two per patch row (halo first)
   auto issue_row = [&](const Patch& P, int r, int buf) {
@@ -404,8 +409,11 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db = 0.f;
-  const bool zc = hm && !rt;   // (chunk tails: one 16-column block, a 16-row block per wave)
-  const int wn = zc ? wave : wave >> 1, wc = zc ? 0 : wave & 1;
+  const bool zc = hm && !rt && !t3;   // (chunk tails: one 16-column block, a 16-row block per wave)
+  const int wn = zc ? wave : (t3 ? min(wave >> 1, 2) : wave >> 1), wc = zc ? 0 : wave & 1;
+  // T3: waves 4 / 5 the taps 0-4 of row block 2, waves 6 / 7 its taps 5-8 (tap masks 0x01F / 0x1E0)
+  const int tsel = t3 ? (wave < 4 ? 0 : wave < 6 ? 1 : 2) : 0;
+  const int tmask = tsel == 0 ? 0x1FF : tsel == 1 ? 0x01F : 0x1E0;
   const int li = lane & 15, lg = lane >> 4;
   const int ncol = wn * 16 + li, ccol = wc * 16 + li;   // this lane's dY column (output channel), X column
   const uint32_t sbase = wf_lds(smem);
@@ -447,8 +455,17 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
     const uint32_t abase = hb + HBUF + a_lane;
     const uint32_t bbase[3] = {hb + b_lane[0], hb + b_lane[1], hb + b_lane[2]};
     float fa[2], fb[2][9];
-    hf_read<0, 1>(abase, bbase, fa[0], fb[0]);
-    hf_steps<0>(abase, bbase, fa, fb, acc, db, [&](int r) { if (more) issue_row(Pn, r, buf ^ 1); });
+    auto row_issue = [&](int r) { if (more) issue_row(Pn, r, buf ^ 1); };
+    if (!T3 || tsel == 0) {
+      hf_read<0, 1>(abase, bbase, fa[0], fb[0]);
+      hf_steps<0>(abase, bbase, fa, fb, acc, db, row_issue);
+    } else if (tsel == 1) {
+      hf_read<0, 1, 0x01F>(abase, bbase, fa[0], fb[0]);
+      hf_steps<0, 1, 0x01F>(abase, bbase, fa, fb, acc, db, row_issue);
+    } else {
+      hf_read<0, 1, 0x1E0>(abase, bbase, fa[0], fb[0]);
+      hf_steps<0, 1, 0x1E0>(abase, bbase, fa, fb, acc, db, row_issue);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next patch landed
     __syncthreads();                                    // and nobody reads this stage any more
   }
@@ -461,16 +478,18 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
     const int n = nblk * NB + ncol;
     if (lg == 0 && n < a.Nout) a.bias_part[(size_t)lin * a.Nout + n] = db;
   }
-  // dW[n][tap * Cin_s + ch * CI + ccol] += acc[tap][r], n = nblk * NB + wn * 16 + 4 lg + r
+  // dW[n][tap * Cin_s + ch * CI + ccol] += acc[tap][r], n = nblk * NB + wn * 16 + 4 lg + r (the wave's taps)
   const int kc = ch * CI + ccol;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = nblk * NB + wn * 16 + 4 * lg + r;
-      if (n < a.Nout) atomicAdd(a.dW + (size_t)n * a.Kpad + t * Cin_s + kc, acc[t][r]);
+      if (n < a.Nout && ((tmask >> t) & 1)) atomicAdd(a.dW + (size_t)n * a.Kpad + t * Cin_s + kc, acc[t][r]);
     }
 }
+template __global__ void igemm_wgrad_halo_f32_kernel<false>(WgradArgs);
+template __global__ void igemm_wgrad_halo_f32_kernel<true>(WgradArgs);
 
 // Dilated form of the halo weight gradient (3x3, stride 1, dilation d > 1, 'same'; adipose_v3's bottleneck
 // dilate2..dilate6 at d = 2 .. 32, which ran on the register-staged kernel at ~85 TF). A dilation-d conv is d x d
@@ -484,10 +503,6 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
 // block, so the 66 combinations of a 352 -> 352 layer fill every CU (the dilation-1 form gives each combination a
 // whole number of blocks: 198 of 256 there); a block flushes its accumulators with f32 atomics where its range
 // changes combination, as the dilation-1 form does at its end.
-// (a device function: the builtin inside a kernel template fails the host pass's substitution)
-__device__ __forceinline__ void hf_buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds, unsigned off) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds, 16, off, 0, 0, 0);
-}
 template <int SPLIT>
 __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_dil_kernel(WgradArgs a) {
   constexpr int NTH = 512, CI = 32, NB = 64;
@@ -802,10 +817,12 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
     // ~60 % of a full patch's time (option wgrad_f32_zt_w, percent; 50 and 70 measured slower,
     // profiles/r06f_f32_wgrad_probe.log) and gets blocks in proportion
     a.zt_n = 0;
+    bool t3 = false;   // (a combination in the tap-split form: the T3 instance)
     if (option("wgrad_f32_zt", 1) && combos <= std::min(ZT_MAX, option("wgrad_f32_zt_max", ZT_MAX)) &&
         (a.ca_real > 0 || a.cb_real > 0 || a.nout_real > 0)) {
       const bool rows_too = option("wgrad_f32_rt", 1) && a.nout_real > 0;
-      const double wt = option("wgrad_f32_zt_w", 60) / 100.0;
+      const bool t3_ok = option("wgrad_f32_t3", 1) && a.nout_real > 0;
+      const double wt = option("wgrad_f32_zt_w", 60) / 100.0, w3 = option("wgrad_f32_t3_w", 85) / 100.0;
       double w[ZT_MAX], tot = 0.0;
       bool any = false;
       for (int c = 0; c < combos; ++c) {
@@ -815,9 +832,10 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
         const int rin = rsrc > 0 ? std::min(32, std::max(0, rsrc - c0)) : 32;
         const int rows = a.nout_real > 0 ? std::min(64, std::max(0, a.nout_real - nb * 64)) : 64;
         const int rb = (rows + 15) / 16;
-        a.zt_mode[c] = rin <= 16 && rb >= 1 ? rb : rows_too && rb >= 1 && rb <= 2 ? 16 + rb : 0;
+        a.zt_mode[c] = rin <= 16 && rb >= 1 ? rb : rows_too && rb >= 1 && rb <= 2 ? 16 + rb : t3_ok && rb == 3 ? 32 + 3 : 0;
         any = any || a.zt_mode[c] > 0;
-        w[c] = a.zt_mode[c] > 0 ? wt : 1.0;
+        t3 = t3 || a.zt_mode[c] >= 32;
+        w[c] = a.zt_mode[c] >= 32 ? w3 : a.zt_mode[c] > 0 ? wt : 1.0;
         tot += w[c];
       }
       if (any) {
@@ -861,8 +879,10 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
       if (a.bias_part && hipMemsetAsync(a.bias_part, 0, (size_t)g0 * a.Nout * sizeof(float), s) != hipSuccess)
         a.bias_part = nullptr;
     }
-    adp::set_kernel("igemm_wgrad_halo_f32_kernel");
-    hipLaunchKernelGGL(igemm_wgrad_halo_f32_kernel, dim3(grid), dim3(512), 0, s, a);
+    t3 = t3 && a.zt_n;
+    adp::set_kernel(t3 ? "igemm_wgrad_halo_f32_kernel<true>" : "igemm_wgrad_halo_f32_kernel<false>");
+    if (t3) hipLaunchKernelGGL((igemm_wgrad_halo_f32_kernel<true>), dim3(grid), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((igemm_wgrad_halo_f32_kernel<false>), dim3(grid), dim3(512), 0, s, a);
     if (a.bias_part) {
       adp::kernel_end();
       slab_reduce(g0, (size_t)a.Nout / 4, a.bias_part, a.dB, s);
