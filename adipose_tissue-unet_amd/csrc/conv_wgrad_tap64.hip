@@ -1870,6 +1870,11 @@ void launch_wcfg(WgradArgs& a, hipStream_t s, int target_blocks, int min_chunk) 
   a.ntile_k = (a.K + TK - 1) / TK;
   a.ntile_n = (a.Nout + TN - 1) / TN;
   const int tiles = a.ntile_k * a.ntile_n;
+  // a one-tile launch (unet_bn's dec0_up ConvTranspose weight gradient: 128 x 256 over 1 M pixels) splits at most
+  // wgrad_blocks_1tile (256) ways: one round of one-block-per-CU blocks and half the slabs of the 512-way split,
+  // 0.225 -> 0.181 ms (profiles/r06o_convt_wgrad.log); multi-tile launches keep the larger targets (256 for all of
+  // them cost adipose_v3's bf16 step 3.5 %, profiles/r06p_v3_bf16_ab.log)
+  if (tiles == 1) target_blocks = std::min(target_blocks, adp::option("wgrad_blocks_1tile", 256));
   int splits = (target_blocks + tiles - 1) / tiles;
   const int maxsplit = (a.M + min_chunk - 1) / min_chunk;
   splits = std::max(1, std::min(splits, maxsplit));
