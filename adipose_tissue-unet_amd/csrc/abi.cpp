@@ -35,7 +35,10 @@ static hipEvent_t pool_event() {
   if (!g_event_pool.empty()) {
     e = g_event_pool.back();
     g_event_pool.pop_back();
-  } else if (hipEventCreate(&e) != hipSuccess) {
+  } else if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess &&
+             hipEventCreate(&e) != hipSuccess) {
+    // (timing-only events: no system-scope cache write-back / invalidate when they complete, which both delayed
+    //  the next kernel and inflated the measured duration; adp_timing_read reads them after a device sync)
     e = nullptr;
   }
   return e;
