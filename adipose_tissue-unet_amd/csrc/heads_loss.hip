@@ -120,7 +120,7 @@ void launch_head_fwd(size_t M, int Cs, int Cin, const T* x, const float* W, cons
 // BNR (x = the pre-BN map z, sc/sh its BatchNorm): also the BatchNorm-backward reduction of that layer
 // over the stored dx (adp_bn_bwd_reduce fused): dbeta += sum db, dgamma += sum db*(z-mean)*invstd,
 // db = dx*(z*sc+sh > 0)
-template <typename T, int NOUT, bool BNR = false>
+template <typename T, int NOUT, bool BNR = false, bool FAST = false>
 __global__ __launch_bounds__(TPB) void head_bwd_kernel(size_t M, int Cs, int Cin, const T* x, const float* W, const float* sc,
                                 const float* sh, const float* p, const float* dp, const T* addend,
                                 const T* mask, float ms, T* dx, float* dW, float* db, const float* bmean = nullptr,
@@ -158,11 +158,14 @@ __global__ __launch_bounds__(TPB) void head_bwd_kernel(size_t M, int Cs, int Cin
     float f[8], o[8], a[8], mk[8];
     grp_to_f(gx, f);
     Grp<T> gt;
-    if (addend) { grp_load(gt, addend + m * Cs + g * 8); grp_to_f(gt, a); }
-    if (mask) { grp_load(gt, mask + m * Cs + g * 8); grp_to_f(gt, mk); }
+    // FAST (round 6, the unet_bn BNR head: BatchNorm coefficients present, no addend or mask -- compile-time, so the
+    // loop has no per-element selects)
+    const bool has_add = !FAST && addend, has_mask = !FAST && mask;
+    if (has_add) { grp_load(gt, addend + m * Cs + g * 8); grp_to_f(gt, a); }
+    if (has_mask) { grp_load(gt, mask + m * Cs + g * 8); grp_to_f(gt, mk); }
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = sc ? fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f) : f[j];
+    for (int j = 0; j < 8; ++j) v[j] = (FAST || sc) ? fmaxf(fmaf(f[j], s_[j], h_[j]), 0.f) : f[j];
     if constexpr (BNR) {   // the activation as adp_bn_apply materializes it (rounded to T)
       Grp<T> gv;
       grp_from_f(gv, v);
@@ -171,8 +174,8 @@ __global__ __launch_bounds__(TPB) void head_bwd_kernel(size_t M, int Cs, int Cin
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       acc[j] = fmaf(dz, v[j], acc[j]);
-      float d = dz * wd[j] + (addend ? a[j] : 0.f);
-      if (mask) d = mk[j] > 0.f ? d * ms : 0.f;
+      float d = dz * wd[j] + (has_add ? a[j] : 0.f);
+      if (has_mask) d = mk[j] > 0.f ? d * ms : 0.f;
       o[j] = d;
     }
     Grp<T> gr;
@@ -564,12 +567,19 @@ extern "C" int adp_head_sigmoid_bwd_bnr(int dtype, size_t M, int Cs, int Cin, co
   const int lanes = TPB / (Cs / 8);
   // every block resident at once (measured at level 0: 233 us with 2 blocks per CU, 286 us with 4096)
   DTYPE_SWITCH(dtype, T, {
-    const int cap = adp::option("head_bwd_blocks",
-                                adp::resident_grid(reinterpret_cast<const void*>(&head_bwd_kernel<T, 1, true>), TPB));
+    const bool fast = adp::option("head_bwd_fast", 1) != 0;   // (sc / sh are required above)
+    const void* kf = fast ? reinterpret_cast<const void*>(&head_bwd_kernel<T, 1, true, true>)
+                          : reinterpret_cast<const void*>(&head_bwd_kernel<T, 1, true>);
+    const int cap = adp::option("head_bwd_blocks", adp::resident_grid(kf, TPB));
     const int blocks = (int)std::min<size_t>((M + lanes - 1) / lanes, (size_t)cap);
-    hipLaunchKernelGGL((head_bwd_kernel<T, 1, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, Cs, Cin,
-                       (const T*)z, W, sc, sh, p, dp, (const T*)nullptr, (const T*)nullptr, 1.f, (T*)dx, dW, db, mean,
-                       invstd, stat);
+    if (fast)
+      hipLaunchKernelGGL((head_bwd_kernel<T, 1, true, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, Cs, Cin,
+                         (const T*)z, W, sc, sh, p, dp, (const T*)nullptr, (const T*)nullptr, 1.f, (T*)dx, dW, db, mean,
+                         invstd, stat);
+    else
+      hipLaunchKernelGGL((head_bwd_kernel<T, 1, true>), dim3(blocks), dim3(TPB), 0, (hipStream_t)st, M, Cs, Cin,
+                         (const T*)z, W, sc, sh, p, dp, (const T*)nullptr, (const T*)nullptr, 1.f, (T*)dx, dW, db, mean,
+                         invstd, stat);
   });
   if (adp::check_launch("adp_head_sigmoid_bwd_bnr")) return -2;
   if (adp::stat_fold_at(0, Cs, dbeta, dgamma, (hipStream_t)st)) return -2;
