@@ -2432,6 +2432,22 @@ def test_head_bn_on_load_and_fused_bn_reduce(dt):
     torch.testing.assert_close(gb2, gb1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dg2, dg1, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db2, db1, rtol=1e-4, atol=1e-3)
+    # the compile-time form (round 6, option head_bwd_fast) against the run-time-flag form: every output bit for bit
+    outs = []
+    for fast in (1, 0):
+        dx3 = torch.empty_like(z)
+        gw3, gb3 = torch.zeros(cin, device=DEV), torch.zeros(1, device=DEV)
+        dg3, db3 = torch.zeros(Cs, device=DEV), torch.zeros(Cs, device=DEV)
+        ops.set_option("head_bwd_fast", fast)
+        try:
+            ops.head_bwd(z, W, p1, dp, gw3, gb3, cin=cin, softmax2=False, dx=dx3, bn=(sc, sh),
+                         bn_reduce=(mean, inv, dg3, db3))
+            torch.cuda.synchronize()
+        finally:
+            ops.set_option("head_bwd_fast", None)
+        outs.append((dx3, gw3, gb3, dg3, db3))
+    assert all(torch.equal(u, v) for u, v in zip(*outs))
+    assert torch.equal(outs[0][0], dx2)
 
 
 @pytest.mark.parametrize("dt", DTS)
