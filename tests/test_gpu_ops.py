@@ -2432,7 +2432,8 @@ def test_head_bn_on_load_and_fused_bn_reduce(dt):
     torch.testing.assert_close(gb2, gb1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dg2, dg1, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db2, db1, rtol=1e-4, atol=1e-3)
-    # the compile-time form (round 6, option head_bwd_fast) against the run-time-flag form: every output bit for bit
+    # the compile-time form (round 6, option head_bwd_fast) against the run-time-flag form: dx bit for bit, the sums
+    # (per-block f64 replicas; the two forms may be resident with different block counts) to f32 rounding
     outs = []
     for fast in (1, 0):
         dx3 = torch.empty_like(z)
@@ -2446,8 +2447,9 @@ def test_head_bn_on_load_and_fused_bn_reduce(dt):
         finally:
             ops.set_option("head_bwd_fast", None)
         outs.append((dx3, gw3, gb3, dg3, db3))
-    assert all(torch.equal(u, v) for u, v in zip(*outs))
-    assert torch.equal(outs[0][0], dx2)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][0], dx2)
+    for u, v in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(u, v, rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.parametrize("dt", DTS)
