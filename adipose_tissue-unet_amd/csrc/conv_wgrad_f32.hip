@@ -822,7 +822,10 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
         (a.ca_real > 0 || a.cb_real > 0 || a.nout_real > 0)) {
       const bool rows_too = option("wgrad_f32_rt", 1) && a.nout_real > 0;
       const bool t3_ok = option("wgrad_f32_t3", 1) && a.nout_real > 0;
+      // (per-mode weights, profiles/r06ab_probe.log: chunk tails 60 %, row tails 55 % -- the level-1 layers ran 2-4 %
+      //  faster at 55 than at 60, the level-0 chunk tails 5 % slower --, the T3 split 85 %)
       const double wt = option("wgrad_f32_zt_w", 60) / 100.0, w3 = option("wgrad_f32_t3_w", 85) / 100.0;
+      const double wr = option("wgrad_f32_rt_w", 55) / 100.0;
       double w[ZT_MAX], tot = 0.0;
       bool any = false;
       for (int c = 0; c < combos; ++c) {
@@ -835,7 +838,7 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
         a.zt_mode[c] = rin <= 16 && rb >= 1 ? rb : rows_too && rb >= 1 && rb <= 2 ? 16 + rb : t3_ok && rb == 3 ? 32 + 3 : 0;
         any = any || a.zt_mode[c] > 0;
         t3 = t3 || a.zt_mode[c] >= 32;
-        w[c] = a.zt_mode[c] >= 32 ? w3 : a.zt_mode[c] > 0 ? wt : 1.0;
+        w[c] = a.zt_mode[c] >= 32 ? w3 : a.zt_mode[c] >= 16 ? wr : a.zt_mode[c] > 0 ? wt : 1.0;
         tot += w[c];
       }
       if (any) {
