@@ -300,6 +300,37 @@ ADP_DEV void hf_steps(uint32_t abase, const uint32_t (&bbase)[3], float (&fa)[2]
   if constexpr (S + 1 < NS) hf_steps<S + 1, SPLIT, TM>(abase, bbase, fa, fb, acc, db, row_issue);
 }
 #undef HF_M
+// Z3 (round 6): the multi-row wave of a chunk tail with 3 row blocks -- taps 7 and 8 (halo row r + 2, columns + 1 and
+// + 2) of all three 16-row blocks: three dY^T elements and two halo elements per k step, six MFMAs into acc[0..5]
+template <int S>
+ADP_DEV void hf_read_mr(const uint32_t (&abase)[3], const uint32_t (&bbase)[3], float (&A)[3], float (&B)[2]) {
+  constexpr int r = S / 8, xs = S % 8, HW = hf_hw<1>(), hc = hf_col<1>(4 * xs);
+  A[0] = wf_rdo<(r * HF_PW + 4 * xs) * 256>(abase[0]);
+  A[1] = wf_rdo<(r * HF_PW + 4 * xs) * 256>(abase[1]);
+  A[2] = wf_rdo<(r * HF_PW + 4 * xs) * 256>(abase[2]);
+  B[0] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[1]);
+  B[1] = wf_rdo<((r + 2) * HW + hc) * 128>(bbase[2]);
+}
+template <int S, typename RowIssue>
+ADP_DEV void hf_steps_mr(const uint32_t (&abase)[3], const uint32_t (&bbase)[3], float (&fa)[2][3], float (&fb)[2][2],
+                         f32x4 (&acc)[9], const RowIssue& row_issue) {
+  constexpr int NS = HF_PH * HF_PW / 4, cur = S & 1;
+  if constexpr (S % 8 == 0) row_issue(S / 8);
+  if constexpr (S + 1 < NS) {
+    hf_read_mr<S + 1>(abase, bbase, fa[cur ^ 1], fb[cur ^ 1]);
+    wf_lgkm<5>();
+  } else {
+    wf_lgkm<0>();
+  }
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int rr = 0; rr < 3; ++rr) {
+    acc[2 * rr] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur][rr], fb[cur][0], acc[2 * rr], 0, 0, 0);
+    acc[2 * rr + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur][rr], fb[cur][1], acc[2 * rr + 1], 0, 0, 0);
+  }
+  __builtin_amdgcn_s_setprio(0);
+  if constexpr (S + 1 < NS) hf_steps_mr<S + 1>(abase, bbase, fa, fb, acc, row_issue);
+}
 // T3 (round 6): output blocks with 3 real 16-row blocks (adipose_v3's level-0 44 outputs) leave rows 48-63 to the
 // waves 6 and 7, i.e. SIMDs 2 and 3 idle half the time while SIMDs 0 and 1 run two full waves. In the T3 form the
 // third row block is split by taps: waves 4 / 5 take its taps 0-4, waves 6 / 7 taps 5-8, so the SIMDs run 14, 14, 13
@@ -342,7 +373,10 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   // column blocks), one wave per SIMD as well
   const int zm = a.zt_n ? a.zt_mode[combo] : 0, hm = zm & 15;
   const bool rt = (zm & 16) != 0, t3 = T3 && (zm & 32) != 0;   // (row tails; T3: the tap-split third row block)
-  const bool idle = hm > 0 && !t3 && wave >= (rt ? 2 * hm : hm);
+  // Z3 (T3 instance): a chunk tail with 3 row blocks -- waves 0-2 take taps 0-6 of row block w, wave 3 taps 7-8 of all
+  // three (SIMD loads 7, 7, 7, 6 tap blocks instead of 9, 9, 9, 0), waves 4-7 stage
+  const bool z3 = T3 && (zm & 64) != 0;
+  const bool idle = hm > 0 && !t3 && wave >= (z3 ? 4 : rt ? 2 * hm : hm);
   const bool inA = ch * CI < a.CAs;
   const int xcs = inA ? a.CAs : a.CBs;
   const int us = a.up >> 1;
@@ -410,10 +444,11 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db = 0.f;
   const bool zc = hm && !rt && !t3;   // (chunk tails: one 16-column block, a 16-row block per wave)
-  const int wn = zc ? wave : (t3 ? min(wave >> 1, 2) : wave >> 1), wc = zc ? 0 : wave & 1;
-  // T3: waves 4 / 5 the taps 0-4 of row block 2, waves 6 / 7 its taps 5-8 (tap masks 0x01F / 0x1E0)
-  const int tsel = t3 ? (wave < 4 ? 0 : wave < 6 ? 1 : 2) : 0;
-  const int tmask = tsel == 0 ? 0x1FF : tsel == 1 ? 0x01F : 0x1E0;
+  const int wn = zc ? (z3 && wave == 3 ? 0 : wave) : (t3 ? min(wave >> 1, 2) : wave >> 1), wc = zc ? 0 : wave & 1;
+  // T3: waves 4 / 5 the taps 0-4 of row block 2, waves 6 / 7 its taps 5-8 (tap masks 0x01F / 0x1E0); Z3: waves 0-2
+  // taps 0-6 (0x07F), wave 3 the multi-row taps 7-8 (tsel 4)
+  const int tsel = t3 ? (wave < 4 ? 0 : wave < 6 ? 1 : 2) : z3 ? (wave < 3 ? 3 : 4) : 0;
+  const int tmask = tsel == 0 ? 0x1FF : tsel == 1 ? 0x01F : tsel == 2 ? 0x1E0 : tsel == 3 ? 0x07F : 0x180;
   const int li = lane & 15, lg = lane >> 4;
   const int ncol = wn * 16 + li, ccol = wc * 16 + li;   // this lane's dY column (output channel), X column
   const uint32_t sbase = wf_lds(smem);
@@ -424,6 +459,12 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
 #pragma unroll
   for (int dx = 0; dx < 3; ++dx)
     b_lane[dx] = (lg + dx) * HRB + ((((ccol >> 2) ^ (4 * ((lg + dx) & 1))) << 4) | ((ccol & 3) << 2));
+  uint32_t a_lane_mr[3];   // (Z3's multi-row wave: the dY^T columns of row blocks 0-2)
+#pragma unroll
+  for (int rr = 0; rr < 3; ++rr) {
+    const int nc = rr * 16 + li;
+    a_lane_mr[rr] = lg * DRB + ((((nc >> 2) ^ (4 * (lg & 1))) << 4) | ((nc & 3) << 2));
+  }
 
   {
     const Patch P0 = patch(0);
@@ -462,9 +503,17 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
     } else if (tsel == 1) {
       hf_read<0, 1, 0x01F>(abase, bbase, fa[0], fb[0]);
       hf_steps<0, 1, 0x01F>(abase, bbase, fa, fb, acc, db, row_issue);
-    } else {
+    } else if (tsel == 2) {
       hf_read<0, 1, 0x1E0>(abase, bbase, fa[0], fb[0]);
       hf_steps<0, 1, 0x1E0>(abase, bbase, fa, fb, acc, db, row_issue);
+    } else if (tsel == 3) {
+      hf_read<0, 1, 0x07F>(abase, bbase, fa[0], fb[0]);
+      hf_steps<0, 1, 0x07F>(abase, bbase, fa, fb, acc, db, row_issue);
+    } else {
+      const uint32_t ab3[3] = {hb + HBUF + a_lane_mr[0], hb + HBUF + a_lane_mr[1], hb + HBUF + a_lane_mr[2]};
+      float fa3[2][3], fb2[2][2];
+      hf_read_mr<0>(ab3, bbase, fa3[0], fb2[0]);
+      hf_steps_mr<0>(ab3, bbase, fa3, fb2, acc, row_issue);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next patch landed
     __syncthreads();                                    // and nobody reads this stage any more
@@ -472,7 +521,7 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   // bias gradient (a.bias_part: the launcher's per-block rows, summed in a fixed order by its slab reduce): the
   // column-block-0 waves of the chunk-0 blocks hold each output channel's dY sum over the block's pixels in the four
   // lane rows
-  if (a.bias_part && ch == 0 && wc == 0) {
+  if (a.bias_part && ch == 0 && wc == 0 && tsel != 4) {   // (Z3's multi-row wave sums no bias)
     db += __shfl_xor(db, 16, 64);
     db += __shfl_xor(db, 32, 64);
     const int n = nblk * NB + ncol;
@@ -480,6 +529,18 @@ __global__ __launch_bounds__(512, 1) void igemm_wgrad_halo_f32_kernel(WgradArgs 
   }
   // dW[n][tap * Cin_s + ch * CI + ccol] += acc[tap][r], n = nblk * NB + wn * 16 + 4 lg + r (the wave's taps)
   const int kc = ch * CI + ccol;
+  if (T3 && tsel == 4) {   // Z3's multi-row wave: acc[2 rb + (tap - 7)] of row block rb
+#pragma unroll
+    for (int rb = 0; rb < 3; ++rb)
+#pragma unroll
+      for (int t = 7; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = nblk * NB + rb * 16 + 4 * lg + r;
+          if (n < a.Nout) atomicAdd(a.dW + (size_t)n * a.Kpad + t * Cin_s + kc, acc[2 * rb + t - 7][r]);
+        }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -825,7 +886,8 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
       // (per-mode weights, profiles/r06ab_probe.log: chunk tails 60 %, row tails 55 % -- the level-1 layers ran 2-4 %
       //  faster at 55 than at 60, the level-0 chunk tails 5 % slower --, the T3 split 85 %)
       const double wt = option("wgrad_f32_zt_w", 60) / 100.0, w3 = option("wgrad_f32_t3_w", 85) / 100.0;
-      const double wr = option("wgrad_f32_rt_w", 55) / 100.0;
+      const double wr = option("wgrad_f32_rt_w", 55) / 100.0, wz3 = option("wgrad_f32_z3_w", 47) / 100.0;
+      const bool z3_ok = option("wgrad_f32_z3", 1) != 0;
       double w[ZT_MAX], tot = 0.0;
       bool any = false;
       for (int c = 0; c < combos; ++c) {
@@ -835,10 +897,14 @@ int launch_wgrad_f32(WgradArgs& a, hipStream_t s) {
         const int rin = rsrc > 0 ? std::min(32, std::max(0, rsrc - c0)) : 32;
         const int rows = a.nout_real > 0 ? std::min(64, std::max(0, a.nout_real - nb * 64)) : 64;
         const int rb = (rows + 15) / 16;
-        a.zt_mode[c] = rin <= 16 && rb >= 1 ? rb : rows_too && rb >= 1 && rb <= 2 ? 16 + rb : t3_ok && rb == 3 ? 32 + 3 : 0;
+        a.zt_mode[c] = rin <= 16 && rb == 3 && z3_ok ? 64 + 3
+                       : rin <= 16 && rb >= 1         ? rb
+                       : rows_too && rb >= 1 && rb <= 2 ? 16 + rb
+                       : t3_ok && rb == 3             ? 32 + 3
+                                                      : 0;
         any = any || a.zt_mode[c] > 0;
         t3 = t3 || a.zt_mode[c] >= 32;
-        w[c] = a.zt_mode[c] >= 32 ? w3 : a.zt_mode[c] >= 16 ? wr : a.zt_mode[c] > 0 ? wt : 1.0;
+        w[c] = a.zt_mode[c] >= 64 ? wz3 : a.zt_mode[c] >= 32 ? w3 : a.zt_mode[c] >= 16 ? wr : a.zt_mode[c] > 0 ? wt : 1.0;
         tot += w[c];
       }
       if (any) {
