@@ -37,8 +37,10 @@ def parse():
     p.add_argument("--cpad", type=lambda v: tuple(int(x) for x in v.split(",")), default=None, help="adipose_v3 channel-stride granule (default 64 for bf16)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-dice", action="store_true", help="skip the Dice@val leg (profiling runs)")
-    p.add_argument("--dice-seconds", type=float, default=45.0,
-                   help="Dice@val leg: training time of a fresh network on the hard synthetic task (eval excluded)")
+    p.add_argument("--dice-steps", type=int, default=2000,
+                   help="Dice@val leg: training steps (a fixed count, so the value is one number per build on any box)")
+    p.add_argument("--dice-seconds", type=float, default=90.0,
+                   help="Dice@val leg: time cap on the training (the step count normally ends it first)")
     p.add_argument("--opt", action="append", default=[], help="name=value native option (A/B experiments only)")
     p.add_argument("--allreduce", default="overlap", choices=["overlap", "after"],
                    help="N > 1: gradient buckets all-reduced as the backward completes them (default) or all after it")
@@ -191,7 +193,8 @@ def committed_traffic(kernel, workload, build):
 
 def dice_leg(args):
     """Dice@val of THIS build, measured in this process after the timed steps (round-4 VERDICT item 5): a fresh
-    network of the benched workload (seed 865) trains for --dice-seconds on a pool of 128 distinct tiles of the
+    network of the benched workload (seed 865) trains --dice-steps steps (2000; round 6: a step count instead of 45 s,
+    so that boxes of different speed report the same value for one build) on a pool of 128 distinct tiles of the
     hard synthetic task (data.synthetic_tile_hard; x 8 dihedral views) and is validated on its 64-tile seeded val
     stream as the reference monitors val_main_out_dice_coef (train_adipose_unet_v3.py:1267, :1316-1324; Keras
     dice_coef, src/utils/model.py:93-98, mean over val batches), plus the thresholded per-tile Dice of
@@ -200,7 +203,7 @@ def dice_leg(args):
     from bench_converge import converge
 
     a = argparse.Namespace(preset=args.preset, levels=args.levels, size=args.size, batch=args.batch, dtype=args.dtype,
-                           pool=128, val=64, lr=1e-3, max_steps=1 << 30, max_seconds=args.dice_seconds,
+                           pool=128, val=64, lr=1e-3, max_steps=args.dice_steps, max_seconds=args.dice_seconds,
                            eval_every=400, target=0.9, fp8=args.preset == "unet_bn", hard=True, f32_eval=True)
     r = converge(a, log=lambda m: print(m, file=sys.stderr, flush=True))
     out = {k: r.get(k) for k in ("dice_val", "best_dice_val", "dice_val_thr", "steps", "train_seconds", "fp8", "f32",
