@@ -719,6 +719,9 @@ inline int bn_blocks(size_t M, int C, int U, int cap) {
   const size_t b = (M + (size_t)U * lanes - 1) / ((size_t)U * lanes);
   return (int)std::max<size_t>(1, std::min<size_t>(b, (size_t)adp::option("bn_cap", cap)));
 }
+// (round 6: default 4 pixels a thread for the BatchNorm apply / backward-apply passes, -0.10 and -0.37 % on the
+//  unet_bn step in two round-robin sweeps, profiles/r06x_bn_sweep.log, r06af_option_sweep.log; elementwise, so the
+//  values are the same bits at any unroll)
 #define BN_UNROLL_SWITCH(U, dflt, ...)                \
   do {                                                \
     const int u_ = adp::option("bn_unroll", dflt);    \
@@ -1156,7 +1159,7 @@ extern "C" int adp_bn_bwd_apply(int dtype, size_t M, int C, const void* dA, cons
                                 const float* dgamma, const float* dbeta, float count, void* dz,
                                 adp_stream_t st) {
   ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && count > 0, "adp_bn_bwd_apply: bad arguments (C % 8 == 0, C <= 2048)");
-  BN_UNROLL_SWITCH(U, 2, DTYPE_SWITCH(dtype, T,
+  BN_UNROLL_SWITCH(U, 4, DTYPE_SWITCH(dtype, T,
                hipLaunchKernelGGL((bn_bwd_apply_kernel<T, U>), dim3(bn_blocks(M, C, U, 32768)), dim3(TPB), 0, (hipStream_t)st,
                                   M, C, (const T*)dA, (const T*)z, sc, sh, mean, invstd, gamma, dgamma, dbeta,
                                   1.f / count, (T*)dz)));
@@ -1171,7 +1174,7 @@ extern "C" int adp_bn_bwd_apply_head(int dtype, size_t M, int C, int Cin, const 
   ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && Cin <= C && Cin % 8 == 0 && count > 0 && W && p && dp &&
                   ((uintptr_t)W & 15) == 0,
               "adp_bn_bwd_apply_head: bad arguments (C % 8 == 0, C <= 2048, Cin <= C, Cin % 8 == 0, W 16-B aligned)");
-  BN_UNROLL_SWITCH(U, 2, DTYPE_SWITCH(dtype, T,
+  BN_UNROLL_SWITCH(U, 4, DTYPE_SWITCH(dtype, T,
                hipLaunchKernelGGL((bn_bwd_apply_head_kernel<T, U>), dim3(bn_blocks(M, C, U, 32768)), dim3(TPB), 0,
                                   (hipStream_t)st, M, C, Cin, (const T*)z, W, p, dp, sc, sh, mean, invstd, gamma,
                                   dgamma, dbeta, 1.f / count, (T*)dz)));
@@ -1181,7 +1184,7 @@ extern "C" int adp_bn_bwd_apply_head(int dtype, size_t M, int C, int Cin, const 
 extern "C" int adp_bn_apply(int dtype, size_t M, int C, const void* z, const float* sc, const float* sh, void* out,
                             adp_stream_t st) {
   ADP_REQUIRE(C % 8 == 0 && C / 8 <= TPB && sc && sh, "adp_bn_apply: bad arguments (C % 8 == 0, C <= 2048)");
-  BN_UNROLL_SWITCH(U, 1, DTYPE_SWITCH(dtype, T,
+  BN_UNROLL_SWITCH(U, 4, DTYPE_SWITCH(dtype, T,
                hipLaunchKernelGGL((bn_apply_kernel<T, U>), dim3(bn_blocks(M, C, U, 65536)), dim3(TPB), 0, (hipStream_t)st, M,
                                   C, (const T*)z, sc, sh, (T*)out)));
   return adp::check_launch("adp_bn_apply");
